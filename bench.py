@@ -1,0 +1,291 @@
+"""rankops benchmark — forward samples/s of the CTR interaction engine on MI355X.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`, one process per GPU
+(torchrun for N > 1); rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json metric "forward samples/sec at batch 4096 (DCN, DIN, BST)"): the
+headline is configs[2], DIN forward with behaviour seq_len 50, emb_dim 32, batch 4096 per GPU,
+wechat-sized tables, eval mode, inputs resident in HBM.  A step is one forward of one batch,
+captured once in a hipGraph and replayed.  The H2 attention MLP is in 'frozen' mode (drawn once
+with the reference's calls, kept on the device); the per-call redraw is reported separately
+under models.din_per_call (eager, it has host work).  Multi-GPU is replicas (the forward has
+no exchange step): every rank runs its own batch, `value` = all ranks' samples / max time.
+
+Extra keys: `models` (N=1, rank 0) times DCN@4096, DeepFM configs[1] and BST configs[3] the
+same way; `roofline` prices the dominant kernel with HIP events around its own launches on the
+stream it runs on; `cpu_baseline` times the oracle (CPU restatement, per-call draws included)
+on a bounded sample of the same workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(REPO, "implementation-of-rank-algorithm-for-mainstream-recommender-systems_amd")
+for _p in (PKG_DIR, REPO, os.path.join(REPO, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_FP32_MFMA = 157.3e12  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_HBM = 8.0e12          # MI355X_MICROARCH.md: HBM3E peak BW (spec)
+
+METRIC = "forward samples/sec at batch 4096 (DCN, DIN, BST) on 1/2/4/8 MI355X"
+
+# Algorithmic work per sample
+DIN_ATT_FLOP = 2 * 50 * (128 * 64 + 64 * 32 + 32)  # 1,028,200: att-MLP of din_attention, T=50, H=32
+DEEPFM_GATHER_BYTES = 30 * (8 + 128 + 4) + 30 * 128 + 8  # 8,048 B: gather+FM kernel
+BST_BLOCK_FLOP = 14_680_064
+DCN_FLOP = 379_236
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--no-extras", action="store_true", help="skip the per-model extras")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--models", default="dcn,deepfm,bst,din_per_call")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(world, value: float) -> float:
+    if world == 1:
+        return value
+    import torch.distributed as dist
+    t = torch.tensor([value], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ------------------------------------------------------------------ workloads
+
+def workload(name: str, batch: int, seed: int):
+    """(model, inputs, call, cfg) for a benchmark workload, built directly on the GPU."""
+    import helpers as H
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if name in ("din", "din_per_call"):
+        cfg = {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32,
+               "interaction_weights": "frozen" if name == "din" else "per_call"}
+        model_name = "din"
+    elif name == "dcn":
+        cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+        model_name = "dcn"
+    elif name == "deepfm":
+        cfg = {"dim": 32, "fields": {f"field_{i:02d}": 1_000_000 for i in range(30)}}
+        model_name = "deepfm"
+    elif name == "bst":
+        cfg = {"vocab": H.WECHAT_VOCAB, "T": 64, "dim": 128, "heads": 4, "max_len": 64}
+        model_name = "bst"
+    else:
+        raise ValueError(name)
+    with torch.device(dev):
+        model = H.build(model_name, cfg, seed=42)
+    model = model.to(dev).eval()
+    inp = H.to_device(H.make_inputs(model_name, cfg, batch, seed=1000 + seed), dev)
+    return model, inp, (lambda: H.call_model(model, model_name, inp)), cfg, model_name
+
+
+def graph_of(fn):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.no_grad():
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        out = fn()
+    return g, out
+
+
+def time_replays(run, steps, warmup, world):
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def kernel_avg_ms(launch, iters=50):
+    """Average duration of one launch, HIP events on the stream the kernel runs on."""
+    st = torch.cuda.current_stream()
+    for _ in range(5):
+        launch()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(st)
+    for _ in range(iters):
+        launch()
+    end.record(st)
+    end.synchronize()
+    return start.elapsed_time(end) / iters
+
+
+# ------------------------------------------------------------------ dominant-kernel launchers
+
+def din_attention_launcher(model, inp):
+    """Re-launch exactly the forward's rk_din_attention call (same buffers, same stream)."""
+    from rankops import ops
+    from rankops.din import SEQ_KEY
+    B = inp["target"]["feedid"].shape[0]
+    dev = inp["target"]["feedid"].device
+    H = model.embeddings["feedid"].embedding_dim
+    width = 16 + 34 + 2 * H
+    row = torch.randn(B, width, device=dev)
+    seq = inp["sequence"][SEQ_KEY].contiguous()
+    lens = inp["sequence"][f"{SEQ_KEY}_length"]
+    w = model.att_weights.get(dev)
+
+    def launch():
+        ops.din_attention(ops._lib.fptr(row, 50), width, model.embeddings[SEQ_KEY].weight, seq, lens, seq.shape[1], H,
+                          w, model.use_softmax, ops._lib.fptr(row, 50 + H), width, B, dev)
+    return launch
+
+
+def load_traffic(kernel: str, workload_name: str):
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(f"{workload_name}:{kernel}")
+    except (OSError, ValueError):
+        return None
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+
+def cpu_baseline(name, model, cfg, batch, budget_s):
+    """The oracle (CPU restatement of the reference forward, per-call draws included) on this
+    host, on a bounded sample: repeated forwards of batch `batch` until ~budget_s."""
+    import helpers as H
+    n = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(n)
+    p = H.cpu_params(model)
+    cfg_cpu = dict(cfg)
+    inp = H.make_inputs(name, cfg_cpu, batch, seed=2000)
+    with torch.no_grad():
+        H.call_oracle(name, cfg_cpu, p, inp)  # warm-up
+        t0 = time.perf_counter()
+        iters = 0
+        while True:
+            H.call_oracle(name, cfg_cpu, p, inp)
+            iters += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or iters >= 200:
+                break
+    return {"value": round(iters * batch / el, 1), "unit": "samples/s", "cores": n, "kind": "port",
+            "sample": f"{iters} oracle forwards of batch {batch} ({el:.1f} s, per-call H2 draws included, "
+                      f"fp32, torch {torch.__version__} CPU)"}
+
+
+# ------------------------------------------------------------------ main
+
+def bench_one(name, batch, steps, warmup, world, rank):
+    model, inp, fn, cfg, model_name = workload(name, batch, rank)
+    if name == "din_per_call":  # eager: per-call CPU draws + H2D are part of every forward
+        def run():
+            with torch.no_grad():
+                fn()
+        t = time_replays(run, max(5, steps // 5), 2, 1)
+        return {"samples_per_s": round(batch * max(5, steps // 5) / t, 1), "mode": "eager, per-call H2 draws",
+                "ms_per_step": round(1e3 * t / max(5, steps // 5), 4)}, model, inp, cfg, model_name
+    g, _ = graph_of(fn)
+    t = time_replays(g.replay, steps, warmup, world)
+    t = max_over_ranks(world, t)
+    return {"samples_per_s": round(world * batch * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4)}, \
+        model, inp, cfg, model_name
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import rankops
+    rankops.load_library()
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    head, model, inp, cfg, model_name = bench_one("din", args.batch, args.steps, args.warmup, world, rank)
+    result = {
+        "metric": METRIC,
+        "value": head["samples_per_s"],
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded wechat-shaped ids, log1p(Poisson(2)) dense, random-init weights)",
+        "config": {"workload": "configs[2]: DIN forward, seq_len 50, emb_dim 32, batch 4096 per GPU",
+                   "model": "DIN", "global_batch": world * args.batch, "seq_len": 50, "emb_dim": 32,
+                   "tables": "wechat_algo_data1 sizes (feedid 106445 rows)", "mode": "eval, hipGraph replay",
+                   "interaction_weights": "frozen", "parallelism": f"replicas x{world}"},
+    }
+    if rank == 0:
+        launch = din_attention_launcher(model, inp)
+        ms = kernel_avg_ms(launch)
+        flop = DIN_ATT_FLOP * args.batch
+        achieved = flop / (ms * 1e-3)
+        result["roofline"] = {"kernel": "din_attention_kernel<32>", "bound": "mfma",
+                              "achieved": round(achieved / 1e12, 3), "peak": PEAK_FP32_MFMA / 1e12,
+                              "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
+                              "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
+                              "traffic": load_traffic("din_attention_kernel", "din")}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = {}
+        for name in [m for m in args.models.split(",") if m]:
+            batch = 2048 if name == "bst" else args.batch
+            r, m2, inp2, cfg2, mn2 = bench_one(name, batch, args.steps, args.warmup, 1, 0)
+            if name == "bst":
+                r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
+            extras[name] = r
+            del m2, inp2
+            torch.cuda.empty_cache()
+        result["models"] = extras
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(model_name, model.cpu(), cfg, args.batch, args.cpu_seconds)
+        result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+// AFM forward, fully fused (reference: AFM.forward, afm.py:92-119).
+//
+//   dense_logit = dense . w_d + b_d                                     afm.py:94
+//   pair[p]     = e_i * e_j   for i < j in field order                  afm.py:101-108
+//   score[p]    = h . relu(W_a pair[p] + b_a) + b_h                     afm.py:110
+//   w           = softmax_p(score)                                      afm.py:111
+//   logit       = dense_logit + p_w . sum_p w[p] pair[p] + p_b          afm.py:113-117
+//
+// One wave per sample.  The field embeddings of the wave's sample are staged in LDS; lane a
+// owns attention units a, a+64, ... (their W_a rows live in registers) and accumulates its
+// share of every pair score; one wave reduction per pair finishes the score.
+#include "common.h"
+
+namespace rk {
+
+constexpr int kAfmMaxFields = 16;
+constexpr int kAfmMaxDim = 64;
+constexpr int kAfmMaxUnitsPerLane = 4;  // attention factor <= 256
+constexpr int kAfmMaxPairs = kAfmMaxFields * (kAfmMaxFields - 1) / 2;
+
+struct AfmFields {
+  rk_segment s[kAfmMaxFields];
+};
+
+template <int D, int UPL>
+__global__ __launch_bounds__(256) void afm_kernel(AfmFields fields, int F, int64_t batch,
+                                                  const float* __restrict__ dense, int64_t ld_dense, int nd,
+                                                  const float* __restrict__ dense_w, const float* __restrict__ dense_b,
+                                                  const float* __restrict__ att_w, const float* __restrict__ att_b,
+                                                  int A, const float* __restrict__ att_h,
+                                                  const float* __restrict__ att_hb, const float* __restrict__ p_w,
+                                                  const float* __restrict__ p_b, float* __restrict__ logit_out,
+                                                  float* __restrict__ prob_out, uint32_t* flags) {
+  __shared__ float emb[4][kAfmMaxFields * D];
+  __shared__ float score[4][kAfmMaxPairs];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* e = emb[wave];
+  float* sc = score[wave];
+
+  // lane-resident attention weights
+  float wa[UPL][D];
+  float ba[UPL], ha[UPL];
+#pragma unroll
+  for (int u = 0; u < UPL; ++u) {
+    const int a = lane + 64 * u;
+    const bool on = a < A;
+#pragma unroll
+    for (int d = 0; d < D; ++d) wa[u][d] = on ? att_w[(int64_t)a * D + d] : 0.f;
+    ba[u] = on ? att_b[a] : 0.f;
+    ha[u] = on ? att_h[a] : 0.f;
+  }
+  const int P = F * (F - 1) / 2;
+
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < batch; b += (int64_t)gridDim.x * 4) {
+    for (int i = lane; i < F * D; i += 64) {
+      const int f = i / D, d = i % D;
+      const float* row = segment_row(fields.s[f], b, flags);
+      e[i] = row ? row[d] : 0.f;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+
+    int p = 0;
+    for (int i = 0; i < F; ++i)
+      for (int j = i + 1; j < F; ++j, ++p) {
+        float pr[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) pr[d] = e[i * D + d] * e[j * D + d];
+        float part = 0.f;
+#pragma unroll
+        for (int u = 0; u < UPL; ++u) {
+          float z = ba[u];
+          // nn.Linear(D, A): sum_d pair[d] * W[a][d] + b[a]
+          float acc = 0.f;
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc = fmaf(pr[d], wa[u][d], acc);
+          z = acc + z;
+          z = z < 0.f ? 0.f : z;
+          part = fmaf(z, ha[u], part);
+        }
+        part = wave_sum(part) + att_hb[0];
+        if (lane == 0) sc[p] = part;
+      }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+
+    // softmax over pairs (every lane computes the same weights)
+    float mx = -INFINITY;
+    for (int q = 0; q < P; ++q) mx = fmaxf(mx, sc[q]);
+    float den = 0.f;
+    for (int q = 0; q < P; ++q) den += expf(sc[q] - mx);
+
+    // weighted pair sum: lane d < D owns component d
+    float ws = 0.f;
+    if (lane < D) {
+      int q = 0;
+      for (int i = 0; i < F; ++i)
+        for (int j = i + 1; j < F; ++j, ++q) {
+          const float w = expf(sc[q] - mx) / den;
+          ws += (e[i * D + lane] * e[j * D + lane]) * w;
+        }
+    }
+    float afm = wave_sum(lane < D ? ws * p_w[lane] : 0.f) + p_b[0];
+    float dl = 0.f;
+    for (int k = lane; k < nd; k += 64) dl = fmaf(dense[b * ld_dense + k], dense_w[k], dl);
+    dl = wave_sum(dl) + dense_b[0];
+    if (lane == 0) {
+      const float t = dl + afm;
+      logit_out[b] = t;
+      prob_out[b] = 1.0f / (1.0f + expf(-t));
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                          const float* dense, int64_t ld_dense, int32_t num_dense, const float* dense_w,
+                          const float* dense_b, const float* att_w, const float* att_b, int32_t att_factor,
+                          const float* att_h, const float* att_hb, const float* p_w, const float* p_b, float* logit,
+                          float* prob, void* stream) {
+  if (!fields || num_fields < 2 || num_fields > kAfmMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_afm_forward: %d fields (need 2..%d)", num_fields, kAfmMaxFields);
+  if (att_factor <= 0 || att_factor > 64 * kAfmMaxUnitsPerLane)
+    return fail(RK_ERR_UNSUPPORTED, "rk_afm_forward: attention factor %d > %d", att_factor, 64 * kAfmMaxUnitsPerLane);
+  if (!att_w || !att_b || !att_h || !att_hb || !p_w || !p_b || !logit || !prob ||
+      (num_dense > 0 && (!dense || !dense_w)) || !dense_b)
+    return fail(RK_ERR_INVALID, "rk_afm_forward: null pointer");
+  AfmFields t;
+  for (int f = 0; f < num_fields; ++f) {
+    if (!fields[f].src || fields[f].dim != dim) return fail(RK_ERR_INVALID, "rk_afm_forward: field %d dim mismatch", f);
+    t.s[f] = fields[f];
+  }
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_afm_forward: negative batch");
+  const unsigned blocks = (unsigned)std::min<int64_t>((batch + 3) / 4, (int64_t)num_cus() * 8);
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* fl = device_flags();
+  const int upl = (att_factor + 63) / 64;
+#define RK_AFM_LAUNCH(DD, UU)                                                                                    \
+  afm_kernel<DD, UU><<<blocks, 256, 0, st>>>(t, num_fields, batch, dense, ld_dense, num_dense, dense_w, dense_b, \
+                                             att_w, att_b, att_factor, att_h, att_hb, p_w, p_b, logit, prob, fl)
+#define RK_AFM_CASE(DD)              \
+  case DD:                           \
+    if (upl == 1)                    \
+      RK_AFM_LAUNCH(DD, 1);          \
+    else if (upl == 2)               \
+      RK_AFM_LAUNCH(DD, 2);          \
+    else                             \
+      RK_AFM_LAUNCH(DD, 4);          \
+    break;
+  switch (dim) {
+    RK_AFM_CASE(4)
+    RK_AFM_CASE(8)
+    RK_AFM_CASE(16)
+    RK_AFM_CASE(32)
+    default:
+      return fail(RK_ERR_UNSUPPORTED, "rk_afm_forward: embedding dim %d not in {4,8,16,32}", dim);
+  }
+#undef RK_AFM_CASE
+#undef RK_AFM_LAUNCH
+  return check_launch("rk_afm_forward");
+}

@@ -1,0 +1,87 @@
+// Shared device/host helpers for the rankops HIP library (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/rankops.h"
+
+#define RK_API extern "C" __attribute__((visibility("default")))
+
+namespace rk {
+
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---- host-side error plumbing (runtime.cpp) ----
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+// Device flag word of the current device (allocated by rk_init; may be null).
+uint32_t* device_flags();
+// Number of CUs on the current device (cached).
+int num_cus();
+
+// ---- device helpers ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Sum over the 32 lanes of each half-wave (lanes l and l^32 are not combined).
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ void flag_oob(uint32_t* flags) {
+  if (flags) atomicOr(flags, RK_FLAG_INDEX_OOB);
+}
+
+// Reads table row `idx` (bounds-checked): returns nullptr for an out-of-range index.
+__device__ __forceinline__ const float* table_row(const rk_segment& s, int64_t b,
+                                                  uint32_t* flags) {
+  const int64_t r = s.idx[b * s.idx_stride];
+  if (r < 0 || r >= s.rows) {
+    flag_oob(flags);
+    return nullptr;
+  }
+  return s.src + r * s.src_ld;
+}
+
+// Row of a segment for sample b (table or dense); nullptr if OOB.
+__device__ __forceinline__ const float* segment_row(const rk_segment& s, int64_t b,
+                                                    uint32_t* flags) {
+  if (s.idx) return table_row(s, b, flags);
+  return s.src + b * s.src_ld;
+}
+
+// FP32-input MFMA, 32x32x2: lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
+// accumulator register r of lane l is D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int acc_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+// Segment table passed by value as a kernel argument.
+struct SegTable {
+  rk_segment s[RK_MAX_SEGMENTS];
+};
+
+}  // namespace rk

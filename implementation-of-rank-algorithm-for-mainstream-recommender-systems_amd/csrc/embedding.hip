@@ -1,0 +1,384 @@
+// Embedding gather + concat, DCN cross network, DeepFM FM, DIN l2 term, BN folding.
+//
+// Reference semantics (file:line in the reference snapshot):
+//   concat:  nn.Embedding(idx) per field, torch.cat([dense, emb...], 1)    dcn.py:163-169
+//   cross:   x_{l+1} = x0 * (x_l @ w_l) + b_l^T + x_l                       dcn.py:47-49
+//   FM:      fm1 = sum_f w_f[idx_f]; fm2 = 0.5*sum_d((sum_f e)^2 - sum_f e^2) deepfm.py:122-140
+//   l2:      lambda * mean_b ||[cat_emb, target, att]_b||_2                 din.py:318-322
+#include "common.h"
+
+namespace rk {
+
+// ------------------------------------------------------------------------------------
+// Generic concat gather: out[b, col] for every column covered by a segment.
+// Columns are handled in units of V floats (V = 4 when every segment is 16-B clean).
+// ------------------------------------------------------------------------------------
+constexpr int kConcatThreads = 256;
+constexpr int kConcatMaxUnits = 4096;
+
+template <int V>
+__global__ __launch_bounds__(kConcatThreads) void concat_gather_kernel(
+    SegTable segs, int nseg, int64_t batch, int width_units, int rows_per_block, float* __restrict__ out,
+    int64_t ld_out, uint32_t* flags) {
+  __shared__ uint8_t col_seg[kConcatMaxUnits];
+  __shared__ uint16_t col_off[kConcatMaxUnits];
+  for (int c = threadIdx.x; c < width_units; c += kConcatThreads) {
+    uint8_t s_hit = 255;
+    uint16_t off = 0;
+    for (int s = 0; s < nseg; ++s) {
+      const int lo = segs.s[s].out_col / V, hi = (segs.s[s].out_col + segs.s[s].dim) / V;
+      if (c >= lo && c < hi) {
+        s_hit = (uint8_t)s;
+        off = (uint16_t)(c - lo);
+      }
+    }
+    col_seg[c] = s_hit;
+    col_off[c] = off;
+  }
+  __syncthreads();
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  if (r0 >= batch) return;
+  const int rows = (int)min<int64_t>(rows_per_block, batch - r0);
+  const int total = rows * width_units;
+  for (int e = threadIdx.x; e < total; e += kConcatThreads) {
+    const int rr = e / width_units;
+    const int c = e - rr * width_units;
+    const int s = col_seg[c];
+    if (s == 255) continue;
+    const int64_t b = r0 + rr;
+    const rk_segment& sg = segs.s[s];
+    const float* row = segment_row(sg, b, flags);
+    float* dst = out + b * ld_out + (int64_t)c * V;
+    if constexpr (V == 4) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row) v = *reinterpret_cast<const f32x4*>(row + (int64_t)col_off[c] * 4);
+      *reinterpret_cast<f32x4*>(dst) = v;
+    } else {
+      *dst = row ? row[col_off[c]] : 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// DCN: one wave per sample row; lane c owns column c (width <= 256, 4 columns/lane).
+// ------------------------------------------------------------------------------------
+constexpr int kCrossMaxPerLane = 4;
+
+__global__ __launch_bounds__(256) void dcn_cross_kernel(SegTable segs, int nseg, int64_t batch, int width,
+                                                        const float* __restrict__ cross_w,
+                                                        const float* __restrict__ cross_b, int num_layers,
+                                                        const float* __restrict__ head_w, float* __restrict__ x0_out,
+                                                        int64_t ld_x0, const float* __restrict__ xl_in,
+                                                        int64_t ld_xl_in, float* __restrict__ xl_out,
+                                                        int64_t ld_xl_out, float* __restrict__ partial,
+                                                        uint32_t* flags) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  int seg_of[kCrossMaxPerLane], off_of[kCrossMaxPerLane];
+#pragma unroll
+  for (int j = 0; j < kCrossMaxPerLane; ++j) {
+    const int c = lane + 64 * j;
+    seg_of[j] = -1;
+    off_of[j] = 0;
+    for (int s = 0; s < nseg; ++s)
+      if (c < width && c >= segs.s[s].out_col && c < segs.s[s].out_col + segs.s[s].dim) {
+        seg_of[j] = s;
+        off_of[j] = c - segs.s[s].out_col;
+      }
+  }
+  for (int64_t b = wave; b < batch; b += nwaves) {
+    float x0[kCrossMaxPerLane], xl[kCrossMaxPerLane];
+#pragma unroll
+    for (int j = 0; j < kCrossMaxPerLane; ++j) {
+      float v = 0.f;
+      if (seg_of[j] >= 0) {
+        const float* row = segment_row(segs.s[seg_of[j]], b, flags);
+        if (row) v = row[off_of[j]];
+      }
+      x0[j] = v;
+      const int c = lane + 64 * j;
+      xl[j] = (xl_in && c < width) ? xl_in[b * ld_xl_in + c] : v;
+      if (x0_out && c < width) x0_out[b * ld_x0 + c] = v;
+    }
+    for (int l = 0; l < num_layers; ++l) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < kCrossMaxPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) d = fmaf(xl[j], cross_w[(int64_t)l * width + c], d);
+      }
+      d = wave_sum(d);
+#pragma unroll
+      for (int j = 0; j < kCrossMaxPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) {
+          float t = x0[j] * d;                      // torch.mul(x0, xl_wl)
+          t = t + cross_b[(int64_t)l * width + c];  // + bl.t()
+          xl[j] = t + xl[j];                        // + xl
+        }
+      }
+    }
+    if (xl_out) {
+#pragma unroll
+      for (int j = 0; j < kCrossMaxPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) xl_out[b * ld_xl_out + c] = xl[j];
+      }
+    }
+    if (partial) {
+      float p = 0.f;
+#pragma unroll
+      for (int j = 0; j < kCrossMaxPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) p = fmaf(xl[j], head_w[c], p);
+      }
+      p = wave_sum(p);
+      if (lane == 0) partial[b] = p;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// DeepFM FM: a workgroup of 4 waves owns a block of samples; lane = (sample, float4 quad of
+// the embedding); wave w sums fields w, w+4, ...; partials are combined through LDS.
+// ------------------------------------------------------------------------------------
+constexpr int kFmMaxFields = 32;
+struct FmTables {
+  rk_segment second[kFmMaxFields];
+  rk_segment first[kFmMaxFields];
+};
+
+template <int G>  // lanes per sample = dim / 4
+__global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64_t batch, float* __restrict__ deep_in,
+                                                        int64_t ld_deep, float* __restrict__ fm1,
+                                                        float* __restrict__ fm2, uint32_t* flags) {
+  constexpr int SPW = 64 / G;  // samples per block
+  __shared__ float red[4][9][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane % G;
+  const int64_t b = (int64_t)blockIdx.x * SPW + lane / G;
+  const bool live = b < batch;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
+  float fo = 0.f;
+  if (live) {
+#pragma unroll 4
+    for (int f = wave; f < F; f += 4) {
+      const rk_segment& sg = t.second[f];
+      const float* row = segment_row(sg, b, flags);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row) v = *reinterpret_cast<const f32x4*>(row + 4 * q);
+      *reinterpret_cast<f32x4*>(deep_in + b * ld_deep + sg.out_col + 4 * q) = v;
+      s += v;
+      sq += v * v;
+      if (q == 0) {
+        const float* w = segment_row(t.first[f], b, flags);
+        fo += w ? w[0] : 0.f;
+      }
+    }
+  }
+  red[wave][0][lane] = s.x;
+  red[wave][1][lane] = s.y;
+  red[wave][2][lane] = s.z;
+  red[wave][3][lane] = s.w;
+  red[wave][4][lane] = sq.x;
+  red[wave][5][lane] = sq.y;
+  red[wave][6][lane] = sq.z;
+  red[wave][7][lane] = sq.w;
+  red[wave][8][lane] = fo;
+  __syncthreads();
+  if (wave != 0) return;
+  float S[4], Q[4], FO = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    S[c] = 0.f;
+    Q[c] = 0.f;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      S[c] += red[w][c][lane];
+      Q[c] += red[w][4 + c][lane];
+    }
+    FO += red[w][8][lane];
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) part += S[c] * S[c] - Q[c];
+  // reduce over the G lanes of this sample
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
+  if (live && q == 0) {
+    fm2[b] = 0.5f * part;
+    fm1[b] = FO;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// DIN l2 term: scale * mean_r ||x[r, col0:col0+ncols]||_2 — one deterministic workgroup.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void row_l2norm_mean_kernel(const float* __restrict__ x, int64_t ld, int64_t rows,
+                                                               int col0, int ncols, float scale,
+                                                               float* __restrict__ out) {
+  __shared__ float part[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int64_t r = wave; r < rows; r += 16) {
+    float ss = 0.f;
+    for (int c = lane; c < ncols; c += 64) {
+      const float v = x[r * ld + col0 + c];
+      ss = fmaf(v, v, ss);
+    }
+    ss = wave_sum(ss);
+    acc += sqrtf(ss);
+  }
+  if (lane == 0) part[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    out[0] = scale * (t / (float)rows);
+  }
+}
+
+__global__ void bn_fold_kernel(const float* __restrict__ mean, const float* __restrict__ var,
+                               const float* __restrict__ weight, const float* __restrict__ bias, float eps, int n,
+                               float* __restrict__ scale, float* __restrict__ shift) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float invstd = 1.0f / sqrtf(var[i] + eps);
+  const float a = weight ? invstd * weight[i] : invstd;
+  scale[i] = a;
+  shift[i] = (bias ? bias[i] : 0.f) - mean[i] * a;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static int check_segments(const rk_segment* segs, int nseg, const char* what) {
+  if (!segs || nseg <= 0 || nseg > RK_MAX_SEGMENTS) return fail(RK_ERR_INVALID, "%s: bad segment count %d", what, nseg);
+  for (int i = 0; i < nseg; ++i) {
+    const rk_segment& s = segs[i];
+    if (!s.src || s.dim <= 0 || s.out_col < 0)
+      return fail(RK_ERR_INVALID, "%s: segment %d invalid (src=%p dim=%d col=%d)", what, i, s.src, s.dim, s.out_col);
+    if (s.idx && s.rows <= 0) return fail(RK_ERR_INVALID, "%s: segment %d has no rows", what, i);
+  }
+  return RK_OK;
+}
+
+}  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_concat_gather(const rk_segment* segs, int32_t nseg, int64_t batch, float* out, int64_t ld_out,
+                            void* stream) {
+  if (int e = check_segments(segs, nseg, "rk_concat_gather")) return e;
+  if (batch < 0 || !out) return fail(RK_ERR_INVALID, "rk_concat_gather: bad batch/out");
+  if (batch == 0) return RK_OK;
+  SegTable t;
+  int width = 0;
+  bool vec = aligned16(out) && (ld_out % 4 == 0);
+  for (int i = 0; i < nseg; ++i) {
+    t.s[i] = segs[i];
+    width = std::max(width, segs[i].out_col + segs[i].dim);
+    vec = vec && segs[i].dim % 4 == 0 && segs[i].out_col % 4 == 0 && segs[i].src_ld % 4 == 0 && aligned16(segs[i].src);
+  }
+  if (width > ld_out) return fail(RK_ERR_INVALID, "rk_concat_gather: width %d exceeds ld_out %lld", width, (long long)ld_out);
+  const int V = vec ? 4 : 1;
+  const int units = (width + V - 1) / V;
+  if (units > kConcatMaxUnits) return fail(RK_ERR_UNSUPPORTED, "rk_concat_gather: width %d too large", width);
+  int rows_per_block = std::max(1, 4096 / units);
+  const int64_t blocks = (batch + rows_per_block - 1) / rows_per_block;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_concat_gather: batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  if (vec)
+    concat_gather_kernel<4><<<(unsigned)blocks, kConcatThreads, 0, st>>>(t, nseg, batch, units, rows_per_block, out,
+                                                                          ld_out, device_flags());
+  else
+    concat_gather_kernel<1><<<(unsigned)blocks, kConcatThreads, 0, st>>>(t, nseg, batch, units, rows_per_block, out,
+                                                                          ld_out, device_flags());
+  return check_launch("rk_concat_gather");
+}
+
+RK_API int rk_dcn_cross(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t width, const float* cross_w,
+                        const float* cross_b, int32_t num_layers, const float* head_w, float* x0, int64_t ld_x0,
+                        const float* xl_in, int64_t ld_xl_in, float* xl_out, int64_t ld_xl_out,
+                        float* cross_partial, void* stream) {
+  if (int e = check_segments(segs, nseg, "rk_dcn_cross")) return e;
+  if (width <= 0 || width > 64 * kCrossMaxPerLane)
+    return fail(RK_ERR_UNSUPPORTED, "rk_dcn_cross: width %d outside [1, %d]", width, 64 * kCrossMaxPerLane);
+  if (num_layers < 0 || (num_layers > 0 && (!cross_w || !cross_b)) || (x0 && ld_x0 < width) ||
+      (xl_in && ld_xl_in < width) || (xl_out && ld_xl_out < width) || (cross_partial && !head_w))
+    return fail(RK_ERR_INVALID, "rk_dcn_cross: bad arguments");
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_dcn_cross: negative batch");
+  SegTable t;
+  for (int i = 0; i < nseg; ++i) t.s[i] = segs[i];
+  const int64_t waves = std::min<int64_t>(batch, (int64_t)num_cus() * 32);
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  dcn_cross_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(t, nseg, batch, width, cross_w, cross_b, num_layers,
+                                                            head_w, x0, ld_x0, xl_in, ld_xl_in, xl_out, ld_xl_out,
+                                                            cross_partial, device_flags());
+  return check_launch("rk_dcn_cross");
+}
+
+RK_API int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_order, int32_t num_fields,
+                        int32_t dim, int64_t batch, float* deep_in, int64_t ld_deep, float* fm1, float* fm2,
+                        void* stream) {
+  if (num_fields <= 0 || num_fields > kFmMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: %d fields (max %d)", num_fields, kFmMaxFields);
+  if (int e = check_segments(second_order, num_fields, "rk_fm_gather(second)")) return e;
+  if (int e = check_segments(first_order, num_fields, "rk_fm_gather(first)")) return e;
+  if (!deep_in || !fm1 || !fm2 || ld_deep % 4 != 0 || !aligned16(deep_in))
+    return fail(RK_ERR_INVALID, "rk_fm_gather: outputs must be non-null, 16-B aligned, ld %% 4 == 0");
+  if (dim % 4 != 0 || dim < 4 || dim > 256)
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim %d must be a multiple of 4 in [4, 256]", dim);
+  const int G = dim / 4;
+  if (G & (G - 1)) return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim/4 = %d must be a power of two", G);
+  FmTables t;
+  for (int f = 0; f < num_fields; ++f) {
+    const rk_segment& s = second_order[f];
+    if (s.dim != dim || s.out_col % 4 || s.src_ld % 4 || !aligned16(s.src) || s.out_col + dim > ld_deep)
+      return fail(RK_ERR_INVALID, "rk_fm_gather: field %d layout not 16-B clean", f);
+    if (first_order[f].dim != 1) return fail(RK_ERR_INVALID, "rk_fm_gather: first-order field %d dim != 1", f);
+    t.second[f] = s;
+    t.first[f] = first_order[f];
+  }
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_fm_gather: negative batch");
+  const int spw = 64 / G;
+  const int64_t blocks = (batch + spw - 1) / spw;
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* fl = device_flags();
+#define RK_FM_CASE(GG) \
+  case GG:             \
+    fm_gather_kernel<GG><<<(unsigned)blocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl); \
+    break;
+  switch (G) {
+    RK_FM_CASE(1)
+    RK_FM_CASE(2)
+    RK_FM_CASE(4)
+    RK_FM_CASE(8)
+    RK_FM_CASE(16)
+    RK_FM_CASE(32)
+    RK_FM_CASE(64)
+    default:
+      return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim %d", dim);
+  }
+#undef RK_FM_CASE
+  return check_launch("rk_fm_gather");
+}
+
+RK_API int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols, float scale,
+                              float* out_scalar, void* stream) {
+  if (!x || !out_scalar || rows <= 0 || ncols <= 0 || col0 < 0 || col0 + ncols > ld)
+    return fail(RK_ERR_INVALID, "rk_row_l2norm_mean: bad arguments");
+  row_l2norm_mean_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(x, ld, rows, col0, ncols, scale, out_scalar);
+  return check_launch("rk_row_l2norm_mean");
+}
+
+RK_API int rk_bn_fold(const float* mean, const float* var, const float* weight, const float* bias, float eps,
+                      int32_t n, float* scale, float* shift, void* stream) {
+  if (!mean || !var || !scale || !shift || n <= 0) return fail(RK_ERR_INVALID, "rk_bn_fold: bad arguments");
+  bn_fold_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(mean, var, weight, bias, eps, n, scale, shift);
+  return check_launch("rk_bn_fold");
+}

@@ -1,0 +1,205 @@
+"""ctypes binding of the rankops C ABI (include/rankops.h).
+
+This is the reference-side FFI a maintainer adds next to the reference's `nn.Module`
+bodies: plain device pointers, sizes and the current HIP stream go in, nothing torch-typed
+crosses the boundary.  The shared library is `librankops.so`, built in-tree by
+`csrc/Makefile` (hipcc, gfx950).  There is no fallback: if the library is missing or fails
+to load, every rankops op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int32, c_int64, c_uint32, c_void_p
+
+import torch  # noqa: F401  -- must be loaded first: librankops binds to torch's HIP runtime
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RANKOPS_LIB", os.path.join(_HERE, "librankops.so"))
+
+RK_OK = 0
+RK_FLAG_INDEX_OOB = 1
+RK_ACT_NONE, RK_ACT_RELU, RK_ACT_LEAKY, RK_ACT_DICE, RK_ACT_PRELU = 0, 1, 2, 3, 4
+RK_MAX_SEGMENTS = 64
+ABI_VERSION = 1
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [
+        ("src", c_void_p),
+        ("idx", c_void_p),
+        ("idx_stride", c_int64),
+        ("src_ld", c_int64),
+        ("rows", c_int64),
+        ("dim", c_int32),
+        ("out_col", c_int32),
+    ]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [
+        ("bias", c_void_p),
+        ("residual", c_void_p),
+        ("ld_residual", c_int64),
+        ("residual_periodic", c_void_p),
+        ("residual_period", c_int32),
+        ("pre_scale", c_void_p),
+        ("pre_shift", c_void_p),
+        ("act", c_int32),
+        ("slope", c_float),
+        ("act_scale", c_void_p),
+        ("act_shift", c_void_p),
+        ("act_alpha", c_void_p),
+        ("act_alpha_len", c_int32),
+        ("post_scale", c_void_p),
+        ("post_shift", c_void_p),
+        ("ln_gamma", c_void_p),
+        ("ln_beta", c_void_p),
+        ("ln_eps", c_float),
+        ("has_ln", c_int32),
+        ("pool_out", c_void_p),
+        ("ld_pool", c_int64),
+        ("pool_rows", c_int32),
+        ("pool_mean", c_int32),
+        ("pool_len", c_void_p),
+        ("head_w", c_void_p),
+        ("head_b", c_void_p),
+        ("head_partial", c_void_p),
+        ("fm1", c_void_p),
+        ("fm2", c_void_p),
+        ("final_w", c_void_p),
+        ("final_b", c_void_p),
+        ("head_logit", c_void_p),
+        ("head_prob", c_void_p),
+        ("head_aux", c_void_p),
+    ]
+
+
+_SEG_P = POINTER(Segment)
+_EPI_P = POINTER(Epilogue)
+
+# name -> (restype, argtypes); the exact set declared in include/rankops.h
+SIGNATURES = {
+    "rk_abi_version": (c_int32, []),
+    "rk_last_error": (c_char_p, []),
+    "rk_init": (ctypes.c_int, [c_int32]),
+    "rk_error_flags": (ctypes.c_int, [c_int32, POINTER(c_uint32), c_int32]),
+    "rk_concat_gather": (ctypes.c_int, [_SEG_P, c_int32, c_int64, c_void_p, c_int64, c_void_p]),
+    "rk_dcn_cross": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p,
+         c_int64, c_void_p, c_int64, c_void_p, c_void_p],
+    ),
+    "rk_fm_gather": (
+        ctypes.c_int,
+        [_SEG_P, _SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+    ),
+    "rk_din_attention": (
+        ctypes.c_int,
+        [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p],
+    ),
+    "rk_row_l2norm_mean": (
+        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_void_p, c_void_p]),
+    "rk_afm_forward": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "rk_bst_attention": (
+        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_linear": (
+        ctypes.c_int,
+        [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, _EPI_P, c_void_p,
+         c_int64, c_void_p],
+    ),
+    "rk_bn_fold": (
+        ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+_load_error = None
+_initialised = set()
+
+
+class RankOpsError(RuntimeError):
+    pass
+
+
+def _hip_runtimes_mapped():
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return paths
+
+
+def load():
+    """Loads librankops.so (once) and declares every C-ABI prototype."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise RankOpsError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f"rankops: native library not found at {LIB_PATH}; build it with "
+                       f"`make -C csrc` or __graft_entry__.build()")
+        raise RankOpsError(_load_error)
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rk_abi_version() != ABI_VERSION:
+        raise RankOpsError(f"rankops: ABI mismatch ({lib.rk_abi_version()} != {ABI_VERSION})")
+    runtimes = _hip_runtimes_mapped()
+    if len(runtimes) > 1:
+        raise RankOpsError(f"rankops: two HIP runtimes mapped in one process: {sorted(runtimes)}")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().rk_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str):
+    if rc != RK_OK:
+        raise RankOpsError(f"{what} failed (code {rc}): {last_error()}")
+
+
+def ensure_device(device: torch.device):
+    """Initialises the library's per-device state (flag word) once per device."""
+    lib = load()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _initialised:
+        check(lib.rk_init(idx), "rk_init")
+        _initialised.add(idx)
+    return idx
+
+
+def error_flags(device=None, reset=True) -> int:
+    """Reads the device flag word (synchronises).  Bit 0: an embedding index was out of range."""
+    lib = load()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    idx = ensure_device(dev)
+    out = c_uint32(0)
+    check(lib.rk_error_flags(idx, ctypes.byref(out), 1 if reset else 0), "rk_error_flags")
+    return int(out.value)
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def fptr(t: torch.Tensor, offset_elems: int = 0):
+    return t.data_ptr() + offset_elems * t.element_size()

@@ -1,0 +1,180 @@
+"""BST (Behavior Sequence Transformer) on the rankops engine — drop-in for algorithm/BST/bst.py.
+
+`BSTModel(vocab_dir, hidden_units=[512,256,128], dropout_rate=0.1, batch_norm=True, d_model=16,
+nhead=4, num_transformer_blocks=1, max_seq_length=50, pooling_method='sum')` keeps the
+reference constructor, creation order, state_dict keys (`embeddings.*`,
+`transformer_blocks.N.{position_embedding,w_q,w_k,w_v,w_o,norm1,norm2,ffn.0,ffn.3}.*`,
+`dnn.N.*`; bst.py:162-214) and `forward(dense, category, seq_feedid, seq_length) ->
+(probabilities, logits)` (bst.py:216-247).  The reference hard-codes the transformer width to
+16 (bst.py:188,192,201); here `d_model` sets it (default 16 = the reference) so the
+benchmark's d_model=128 runs through the same class.
+
+Per transformer block (bst.py:66-91):
+  rk_linear   [Q|K] = (x + pos) W_{q,k}^T + b          (positions added in the A-tile loader)
+  rk_linear   V = x W_v^T + b_v
+  rk_bst_attention   masked softmax(QK^T/sqrt(d_h)) V per head (-inf mask, NaN for empty rows)
+  rk_linear   out1 = LN1((x + pos) + ctx W_o^T + b_o)    (residual + LayerNorm in the epilogue)
+  rk_linear   f = LeakyReLU(out1 W_1^T + b_1)
+  rk_linear   out = LN2(out1 + f W_2^T + b_2); the last block sums (or averages) the T rows of
+              each sample straight into the DNN input row (bst.py:238-241)
+then rk_concat_gather for [dense | category] and the DNN on rk_linear with the final Linear +
+sigmoid fused.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common import Layer, Packed, check_eval, table_rows
+
+FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
+
+
+def load_vocabulary(vocab_file):
+    import os
+    if not os.path.exists(vocab_file):
+        return []
+    with open(vocab_file, 'r') as f:
+        return [line.strip() for line in f]
+
+
+class BSTTransformer(nn.Module):
+    """Transformer block with the reference's parameters (bst.py:42-64)."""
+
+    def __init__(self, d_model, nhead, max_len, dropout=0.1):
+        super().__init__()
+        self.d_model = d_model
+        self.nhead = nhead
+        self.position_embedding = nn.Embedding(max_len, d_model)
+        self.w_q = nn.Linear(d_model, d_model)
+        self.w_k = nn.Linear(d_model, d_model)
+        self.w_v = nn.Linear(d_model, d_model)
+        self.w_o = nn.Linear(d_model, d_model)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.dropout = nn.Dropout(dropout)
+        self.ffn = nn.Sequential(
+            nn.Linear(d_model, d_model),
+            nn.LeakyReLU(negative_slope=0.01),
+            nn.Dropout(dropout),
+            nn.Linear(d_model, d_model),
+        )
+        self._wqk = Packed()
+        self._bqk = Packed()
+
+    def run(self, x: torch.Tensor, B: int, T: int, seq_length: torch.Tensor, out: torch.Tensor = None,
+            pool_out_ptr: int = None, ld_pool: int = 0, pool_mean: bool = False):
+        """x: [B*T, d] (queries = keys = values).  Writes the block output to `out`, or pools it
+        per sample into pool_out_ptr when given."""
+        d = self.d_model
+        dev = x.device
+        pos = self.position_embedding.weight
+        if T > pos.shape[0]:
+            raise IndexError(f"BSTTransformer: sequence length {T} exceeds max_len {pos.shape[0]}")
+        qkv = torch.empty(B * T, 3 * d, device=dev, dtype=torch.float32)
+        wqk = self._wqk(self.w_q.weight, self.w_k.weight)
+        bqk = self._bqk(self.w_q.bias, self.w_k.bias)
+        ops.linear(x, wqk, None, x_periodic=pos, x_period=T, y_ptr=qkv.data_ptr(), ldy=3 * d,
+                   epilogue=ops.make_epilogue(bias=bqk))
+        ops.linear(x, self.w_v.weight, None, y_ptr=ops._lib.fptr(qkv, 2 * d), ldy=3 * d,
+                   epilogue=ops.make_epilogue(bias=self.w_v.bias))
+        ctx = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+        ops.bst_attention(qkv, B, T, d, self.nhead, seq_length, ctx)
+        out1 = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+        ops.linear(ctx, self.w_o.weight, out1, epilogue=ops.make_epilogue(
+            bias=self.w_o.bias, residual=x, ld_residual=x.stride(0), residual_periodic=pos, residual_period=T,
+            has_ln=1, ln_gamma=self.norm1.weight, ln_beta=self.norm1.bias, ln_eps=self.norm1.eps))
+        f1 = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+        ops.linear(out1, self.ffn[0].weight, f1, epilogue=ops.make_epilogue(
+            bias=self.ffn[0].bias, act="leaky", slope=self.ffn[1].negative_slope))
+        ep = dict(bias=self.ffn[3].bias, residual=out1, ld_residual=out1.stride(0), has_ln=1,
+                  ln_gamma=self.norm2.weight, ln_beta=self.norm2.bias, ln_eps=self.norm2.eps)
+        if pool_out_ptr is not None:
+            ep.update(pool_out=pool_out_ptr, ld_pool=ld_pool, pool_rows=T, pool_mean=1 if pool_mean else 0,
+                      pool_len=seq_length)
+        ops.linear(f1, self.ffn[3].weight, out, epilogue=ops.make_epilogue(**ep))
+        return out
+
+
+class BSTModel(nn.Module):
+    def __init__(self, vocab_dir, hidden_units=[512, 256, 128], dropout_rate=0.1, batch_norm=True, d_model=16,
+                 nhead=4, num_transformer_blocks=1, max_seq_length=50, pooling_method='sum', *,
+                 vocab_sizes=None):
+        super().__init__()
+        self.vocab_sizes = {f: table_rows(vocab_dir, f, vocab_sizes) for f in FIELDS}
+        self.num_dense_features = 16
+        self.d_model = d_model
+        self.embeddings = nn.ModuleDict({
+            'userid': nn.Embedding(self.vocab_sizes['userid'], 16),
+            'device': nn.Embedding(self.vocab_sizes['device'], 2),
+            'authorid': nn.Embedding(self.vocab_sizes['authorid'], 4),
+            'bgm_song_id': nn.Embedding(self.vocab_sizes['bgm_song_id'], 4),
+            'bgm_singer_id': nn.Embedding(self.vocab_sizes['bgm_singer_id'], 4),
+            'manual_tag_list': nn.Embedding(self.vocab_sizes['manual_tag_list'], 4),
+            'feedid': nn.Embedding(self.vocab_sizes['feedid'], d_model),
+        })
+        self.transformer_blocks = nn.ModuleList([
+            BSTTransformer(d_model=d_model, nhead=nhead, max_len=max_seq_length + 1, dropout=dropout_rate)
+            for _ in range(num_transformer_blocks)
+        ])
+        self.batch_norm = batch_norm
+        self.dropout_rate = dropout_rate
+        self.pooling_method = pooling_method
+        category_emb_dim = 16 + 2 + 4 + 4 + 4 + 4
+        layers = []
+        self._tail = []
+        width = self.num_dense_features + category_emb_dim + d_model
+        for h in hidden_units:
+            lin = nn.Linear(width, h)
+            layers.append(lin)
+            bn = None
+            if batch_norm:
+                bn = nn.BatchNorm1d(h)
+                layers.append(bn)
+            act = nn.LeakyReLU(negative_slope=0.01)
+            layers.append(act)
+            if dropout_rate > 0:
+                layers.append(nn.Dropout(dropout_rate))
+            self._tail.append(Layer(lin, pre_bn=bn, act="leaky", slope=act.negative_slope))
+            width = h
+        layers.append(nn.Linear(width, 1))
+        self.dnn = nn.Sequential(*layers)
+
+    def forward(self, dense, category, seq_feedid, seq_length):
+        check_eval(self)
+        dense = ops.as_f32(dense, "dense")
+        seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
+        seq_length = ops.as_index(seq_length, "seq_length")
+        B, T = seq_feedid.shape
+        dev = dense.device
+        d = self.d_model
+        # DNN input row: [dense | category embeddings | pooled transformer output]
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col = self.num_dense_features
+        for name, emb in self.embeddings.items():
+            if name in category:
+                idx = ops.as_index(category[name], f"category[{name!r}]")
+                segs.append(ops.table_segment(emb.weight, idx, col))
+                col += emb.embedding_dim
+        width = col + d
+        row = torch.empty(B, width, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, row)
+        # behaviour sequence: x[b*T + t] = feedid_table[seq_feedid[b, t]]
+        x = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+        flat = seq_feedid.view(-1)
+        ops.concat_gather([ops.table_segment(self.embeddings['feedid'].weight, flat, 0)], B * T, x)
+        nblk = len(self.transformer_blocks)
+        for i, blk in enumerate(self.transformer_blocks):
+            if i == nblk - 1:
+                blk.run(x, B, T, seq_length, pool_out_ptr=ops._lib.fptr(row, col), ld_pool=width,
+                        pool_mean=self.pooling_method != 'sum')
+            else:
+                x = blk.run(x, B, T, seq_length, out=torch.empty_like(x))
+        if nblk == 0:
+            raise NotImplementedError("BSTModel with zero transformer blocks")
+        logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        from .common import run_tail
+        run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
+        return probs, logits

@@ -1,0 +1,238 @@
+"""Plumbing shared by the drop-in models: vocab sizes, per-call random weights (H2),
+BatchNorm folding, packed-weight caches and the fused MLP tail."""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+WECHAT_VOCAB_FILES = {
+    "userid": "userid.txt",
+    "feedid": "feedid.txt",
+    "device": "device.txt",
+    "authorid": "authorid.txt",
+    "bgm_song_id": "bgm_song_id.txt",
+    "bgm_singer_id": "bgm_singer_id.txt",
+    "manual_tag_list": "manual_tag_id.txt",
+}
+
+DENSE_FEATURES = [
+    "videoplayseconds", "u_read_comment_7d_sum", "u_like_7d_sum",
+    "u_click_avatar_7d_sum", "u_forward_7d_sum", "u_comment_7d_sum",
+    "u_follow_7d_sum", "u_favorite_7d_sum", "i_read_comment_7d_sum",
+    "i_like_7d_sum", "i_click_avatar_7d_sum", "i_forward_7d_sum",
+    "i_comment_7d_sum", "i_follow_7d_sum", "i_favorite_7d_sum",
+    "c_user_author_read_comment_7d_sum",
+]
+
+
+def load_vocabulary(vocab_dir: str, filename: str):
+    """Vocabulary file -> list of stripped lines; a missing file is an empty vocabulary
+    (dcn.py:154-159)."""
+    path = os.path.join(vocab_dir, filename)
+    if not os.path.exists(path):
+        return []
+    with open(path, "r") as f:
+        return [line.strip() for line in f]
+
+
+def table_rows(vocab_dir, field: str, vocab_sizes: Optional[dict] = None) -> int:
+    """Embedding rows of a field: len(vocab)+1 (dcn.py:118-126); `vocab_sizes` overrides the
+    vocabulary length per field (used for synthetic configs without vocabulary files)."""
+    if vocab_sizes is not None and field in vocab_sizes:
+        return int(vocab_sizes[field]) + 1
+    return len(load_vocabulary(vocab_dir, WECHAT_VOCAB_FILES[field])) + 1
+
+
+# ---------------------------------------------------------------- per-call random weights (H2)
+# The reference re-creates these layers inside forward() from the default CPU generator on
+# every call; the draw order below is the reference's construction order.
+
+def draw_cross_layers(dim: int, num_layers: int):
+    """cross_layer(): w ~ xavier_normal_ on a (d, 1) tensor, b = 0, per layer (dcn.py:37-41)."""
+    ws, bs = [], []
+    for _ in range(num_layers):
+        w = torch.zeros(dim, 1)
+        b = torch.zeros(dim, 1)
+        nn.init.xavier_normal_(w)
+        nn.init.zeros_(b)
+        ws.append(w.reshape(dim))
+        bs.append(b.reshape(dim))
+    if not ws:
+        return torch.zeros(0, dim), torch.zeros(0, dim)
+    return torch.stack(ws), torch.stack(bs)
+
+
+def draw_din_attention(embedding_dim: int):
+    """din_attention(): Linear(4H,64), Linear(64,32), Linear(32,1) in order (din.py:61-67)."""
+    l1 = nn.Linear(4 * embedding_dim, 64)
+    l2 = nn.Linear(64, 32)
+    l3 = nn.Linear(32, 1)
+    return [t.detach() for t in (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)]
+
+
+def draw_residual_units(dim: int, internal_dim: int, num_units: int):
+    """residual_unit(): Linear(d, I) then Linear(I, d), per unit (deepcrossing.py:37-39)."""
+    units = []
+    for _ in range(num_units):
+        a = nn.Linear(dim, internal_dim)
+        b = nn.Linear(internal_dim, dim)
+        units.append([t.detach() for t in (a.weight, a.bias, b.weight, b.bias)])
+    return units
+
+
+class InteractionWeights:
+    """Holds the H2 weights for one model.  mode 'per_call' redraws them on every forward
+    exactly like the reference; 'frozen' draws them once (on the first forward, with the same
+    generator calls) and keeps them resident on the device."""
+
+    MODES = ("per_call", "frozen")
+
+    def __init__(self, mode: str, draw):
+        if mode not in self.MODES:
+            raise ValueError(f"interaction_weights must be one of {self.MODES}, got {mode!r}")
+        self.mode = mode
+        self._draw = draw
+        self._cached = None
+
+    def get(self, device):
+        if self.mode == "frozen" and self._cached is not None and self._cached[0] == device:
+            return self._cached[1]
+        host = self._draw()
+        dev = _to_device(host, device)
+        if self.mode == "frozen":
+            self._cached = (device, dev)
+        return dev
+
+
+def _to_device(obj, device):
+    if isinstance(obj, torch.Tensor):
+        return obj.to(device).contiguous()
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_device(o, device) for o in obj)
+    return obj
+
+
+# ---------------------------------------------------------------- caches keyed on tensor versions
+
+def _key(tensors):
+    return tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)
+
+
+class FoldedBN:
+    """BatchNorm1d (eval) as a per-channel affine z*scale + shift, recomputed on the device only
+    when a running stat or affine parameter changed."""
+
+    def __init__(self):
+        self._key = None
+        self._val = None
+
+    def __call__(self, bn: nn.BatchNorm1d):
+        t = (bn.running_mean, bn.running_var, bn.weight, bn.bias)
+        k = _key(t) + (bn.eps,)
+        if k != self._key:
+            dev = bn.running_mean.device
+            scale = torch.empty(bn.num_features, device=dev, dtype=torch.float32)
+            shift = torch.empty_like(scale)
+            ops.bn_fold(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps, scale, shift)
+            self._key, self._val = k, (scale, shift)
+        return self._val
+
+
+class Packed:
+    """Row-concatenation of parameters (e.g. [W_q; W_k]) cached on parameter versions."""
+
+    def __init__(self):
+        self._key = None
+        self._val = None
+
+    def __call__(self, *tensors):
+        k = _key(tensors)
+        if k != self._key:
+            self._key, self._val = k, torch.cat([t.detach() for t in tensors], 0).contiguous()
+        return self._val
+
+
+_CONST = {}
+
+
+def const(device, value: float):
+    key = (str(device), value)
+    if key not in _CONST:
+        _CONST[key] = torch.full((1,), value, device=device, dtype=torch.float32)
+    return _CONST[key]
+
+
+# ---------------------------------------------------------------- fused MLP tail
+
+@dataclass
+class Layer:
+    linear: nn.Linear
+    pre_bn: Optional[nn.BatchNorm1d] = None   # BatchNorm before the activation
+    act: str = "none"
+    slope: float = 0.0
+    act_module: Optional[nn.Module] = None    # Dice (alpha + its BatchNorm1d(affine=False)) / PReLU
+    post_bn: Optional[nn.BatchNorm1d] = None  # BatchNorm after the activation (DIN)
+    fold_pre: Optional[FoldedBN] = None
+    fold_dice: Optional[FoldedBN] = None
+    fold_post: Optional[FoldedBN] = None
+
+    def __post_init__(self):
+        self.fold_pre, self.fold_dice, self.fold_post = FoldedBN(), FoldedBN(), FoldedBN()
+
+    def epilogue_kwargs(self):
+        kw = dict(bias=self.linear.bias, act=self.act, slope=self.slope)
+        if self.pre_bn is not None:
+            kw["pre_scale"], kw["pre_shift"] = self.fold_pre(self.pre_bn)
+        if self.act == "dice":
+            kw["act_scale"], kw["act_shift"] = self.fold_dice(self.act_module.bn)
+            kw["act_alpha"], kw["act_alpha_len"] = self.act_module.alpha, self.act_module.alpha.numel()
+        elif self.act == "prelu":
+            kw["act_alpha"], kw["act_alpha_len"] = self.act_module.weight, self.act_module.weight.numel()
+        if self.post_bn is not None:
+            kw["post_scale"], kw["post_shift"] = self.fold_post(self.post_bn)
+        return kw
+
+
+def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit: torch.Tensor,
+             prob: torch.Tensor):
+    """Runs the hidden layers and the final Linear(N, 1) + sigmoid.  The head is fused into
+    the last hidden layer's epilogue when its width fits one workgroup (N <= 256)."""
+    h = x
+    B = x.shape[0]
+    dev = x.device
+    head_w = head.weight
+    for i, layer in enumerate(layers):
+        last = i == len(layers) - 1
+        lin = layer.linear
+        kw = layer.epilogue_kwargs()
+        if last and lin.out_features <= 256:
+            ep = ops.make_epilogue(head_w=head_w, head_b=head.bias, head_logit=logit, head_prob=prob,
+                                   **head_kwargs, **kw)
+            ops.linear(h, lin.weight, None, epilogue=ep)
+            return
+        y = torch.empty(B, lin.out_features, device=dev, dtype=torch.float32)
+        ops.linear(h, lin.weight, y, epilogue=ops.make_epilogue(**kw))
+        h = y
+    # head on its own: z = h . w + b as an N=1 GEMM, then the unit head epilogue
+    ep = ops.make_epilogue(bias=head.bias, head_w=const(dev, 1.0), head_b=const(dev, 0.0), head_logit=logit,
+                           head_prob=prob, **head_kwargs)
+    ops.linear(h, head_w, None, epilogue=ep)
+
+
+def check_eval(module: nn.Module):
+    if module.training:
+        raise NotImplementedError(
+            f"{type(module).__name__}: the rankops engine implements the eval-mode forward "
+            f"(BatchNorm running stats, Dropout identity); call .eval() first. "
+            f"Training (backward) is the next row of the build plan (DESIGN.md).")
+
+
+def sqrt_f32(x: float) -> float:
+    return float(torch.tensor(math.sqrt(x), dtype=torch.float32))

@@ -1,0 +1,98 @@
+"""Deep Crossing on the rankops engine — drop-in for algorithm/DeepCrossing/deepcrossing.py.
+
+`DeepCrossingModel(vocab_dir, residual_internal_dim=128, residual_network_num=1)` keeps the
+reference constructor, state_dict keys (`embeddings.*`, `output_layer.*`; the residual units
+have none, deepcrossing.py:106-137) and `forward(dense, category) -> (probability, logit)`
+(deepcrossing.py:146-163).
+
+Launches: rk_concat_gather -> x0 [B, 50]; per residual unit two rk_linear calls
+(Linear+ReLU, then Linear + residual + ReLU), the last one also evaluating output_layer and
+the sigmoid in its epilogue.  The residual units' Linear layers are drawn per call from the
+CPU generator like the reference (deepcrossing.py:37-39) or frozen.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common import InteractionWeights, check_eval, const, draw_residual_units, load_vocabulary, table_rows
+
+
+def residual_unit(input_tensor, internal_dim, index, weights=None):
+    """Reference residual_unit (deepcrossing.py:25-42): ReLU(x + Linear2(ReLU(Linear1(x))))."""
+    x = ops.as_f32(input_tensor, "input_tensor")
+    B, d = x.shape
+    if weights is None:
+        weights = [t.to(x.device) for t in draw_residual_units(d, internal_dim, 1)[0]]
+    w1, b1, w2, b2 = weights
+    h = torch.empty(B, internal_dim, device=x.device, dtype=torch.float32)
+    ops.linear(x, w1, h, epilogue=ops.make_epilogue(bias=b1, act="relu"))
+    out = torch.empty(B, d, device=x.device, dtype=torch.float32)
+    ops.linear(h, w2, out, epilogue=ops.make_epilogue(bias=b2, residual=x, ld_residual=x.stride(0), act="relu"))
+    return out
+
+
+class DeepCrossingModel(nn.Module):
+    def __init__(self, vocab_dir, residual_internal_dim=128, residual_network_num=1, *, vocab_sizes=None,
+                 interaction_weights="per_call"):
+        super().__init__()
+        fields = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
+        self.vocab_sizes = {f: table_rows(vocab_dir, f, vocab_sizes) for f in fields}
+        self.num_dense_features = 16
+        self.embeddings = nn.ModuleDict({
+            "userid": nn.Embedding(self.vocab_sizes["userid"], 16),
+            "device": nn.Embedding(self.vocab_sizes["device"], 2),
+            "authorid": nn.Embedding(self.vocab_sizes["authorid"], 4),
+            "bgm_song_id": nn.Embedding(self.vocab_sizes["bgm_song_id"], 4),
+            "bgm_singer_id": nn.Embedding(self.vocab_sizes["bgm_singer_id"], 4),
+            "manual_tag_list": nn.Embedding(self.vocab_sizes["manual_tag_list"], 4),
+        })
+        self.input_dim = self.num_dense_features + 16 + 2 + 4 + 4 + 4 + 4
+        self.residual_internal_dim = residual_internal_dim
+        self.residual_network_num = residual_network_num
+        self.output_layer = nn.Linear(self.input_dim, 1)
+        self.residual_weights = InteractionWeights(
+            interaction_weights,
+            lambda: draw_residual_units(self.input_dim, self.residual_internal_dim, self.residual_network_num))
+
+    def _load_vocabulary(self, vocab_dir, filename):
+        return load_vocabulary(vocab_dir, filename)
+
+    def forward(self, dense, category):
+        check_eval(self)
+        dense = ops.as_f32(dense, "dense")
+        B = dense.shape[0]
+        dev = dense.device
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col = self.num_dense_features
+        for name, emb in self.embeddings.items():
+            if name not in category:
+                raise KeyError(f"DeepCrossingModel.forward: category feature {name!r} missing")
+            idx = ops.as_index(category[name], f"category[{name!r}]")
+            segs.append(ops.table_segment(emb.weight, idx, col))
+            col += emb.embedding_dim
+        x = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, x)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head = dict(head_w=self.output_layer.weight, head_b=self.output_layer.bias, head_logit=logit,
+                    head_prob=prob)
+        units = self.residual_weights.get(dev)
+        I = self.residual_internal_dim
+        for i, (w1, b1, w2, b2) in enumerate(units):
+            last = i == len(units) - 1
+            h = torch.empty(B, I, device=dev, dtype=torch.float32)
+            ops.linear(x, w1, h, epilogue=ops.make_epilogue(bias=b1, act="relu"))
+            res = dict(bias=b2, residual=x, ld_residual=x.stride(0), act="relu")
+            if last:
+                ops.linear(h, w2, None, epilogue=ops.make_epilogue(**res, **head))
+            else:
+                y = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
+                ops.linear(h, w2, y, epilogue=ops.make_epilogue(**res))
+                x = y
+        if not units:
+            ep = ops.make_epilogue(bias=self.output_layer.bias, head_w=const(dev, 1.0), head_b=const(dev, 0.0),
+                                   head_logit=logit, head_prob=prob)
+            ops.linear(x, self.output_layer.weight, None, epilogue=ep)
+        return prob, logit

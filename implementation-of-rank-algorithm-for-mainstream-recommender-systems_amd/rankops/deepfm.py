@@ -1,0 +1,90 @@
+"""DeepFM on the rankops engine — drop-in for algorithm/DeepFM/deepfm.py.
+
+`DeepFM(vocab_dir, embedding_dim=8, hidden_units=None, dropout_rate=0.1, batch_norm=True)`
+keeps the reference constructor, creation order and state_dict keys
+(`first_order_embeddings.*`, `second_order_embeddings.*`, `deep_layers.N.*`,
+`deep_output_layer.*`, `final_layer.*`; deepfm.py:73-112) and
+`forward(category) -> (probability, total_logit, fm1, fm2, deep_logit)` (deepfm.py:121-151).
+
+Beyond the reference's six wechat fields the constructor takes `vocab_sizes={field: rows-1}`
+(any field names, dict order = field order) so the 30-field benchmark configuration runs
+through the same class; with the default wechat vocabulary it is the reference model.
+
+Launches: rk_fm_gather (both embedding orders, fm1, fm2 and the deep input in one pass), then
+the deep layers on rk_linear with BatchNorm folded into the epilogue; the last one also
+evaluates deep_output_layer, final_layer(3->1) and the sigmoid.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common import Layer, check_eval, load_vocabulary, run_tail, table_rows
+
+WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
+
+
+class DeepFM(nn.Module):
+    def __init__(self, vocab_dir, embedding_dim=8, hidden_units=None, dropout_rate=0.1, batch_norm=True, *,
+                 vocab_sizes=None):
+        super().__init__()
+        if hidden_units is None:
+            hidden_units = [512, 256, 128]
+        if vocab_sizes is not None and any(f not in WECHAT_FIELDS for f in vocab_sizes):
+            self.vocab_sizes = {f: int(n) + 1 for f, n in vocab_sizes.items()}
+        else:
+            self.vocab_sizes = {f: table_rows(vocab_dir, f, vocab_sizes) for f in WECHAT_FIELDS}
+        self.num_categories = len(self.vocab_sizes)
+        self.embedding_dim = embedding_dim
+        self.first_order_embeddings = nn.ModuleDict(
+            {col: nn.Embedding(n, 1) for col, n in self.vocab_sizes.items()})
+        self.second_order_embeddings = nn.ModuleDict(
+            {col: nn.Embedding(n, embedding_dim) for col, n in self.vocab_sizes.items()})
+        self.deep_layers = nn.ModuleList()
+        width = self.num_categories * embedding_dim
+        self._tail = []
+        for unit in hidden_units:
+            lin = nn.Linear(width, unit)
+            self.deep_layers.append(lin)
+            bn = None
+            if batch_norm:
+                bn = nn.BatchNorm1d(unit)
+                self.deep_layers.append(bn)
+            self.deep_layers.append(nn.ReLU())
+            if dropout_rate > 0:
+                self.deep_layers.append(nn.Dropout(dropout_rate))
+            self._tail.append(Layer(lin, pre_bn=bn, act="relu"))
+            width = unit
+        self.deep_output_layer = nn.Linear(width, 1)
+        self.final_layer = nn.Linear(3, 1)
+
+    def _load_vocabulary(self, vocab_dir, filename):
+        return load_vocabulary(vocab_dir, filename)
+
+    def forward(self, category):
+        check_eval(self)
+        names = [c for c in self.second_order_embeddings if c in category]
+        if len(names) != self.num_categories:
+            missing = [c for c in self.second_order_embeddings if c not in category]
+            raise KeyError(f"DeepFM.forward: category features missing: {missing}")
+        D = self.embedding_dim
+        first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
+        B = first.shape[0]
+        dev = first.device
+        second_segs, first_segs = [], []
+        for f, name in enumerate(names):
+            idx = ops.as_index(category[name], f"category[{name!r}]")
+            second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
+            first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
+        deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        ops.fm_gather(second_segs, first_segs, D, B, deep_in, fm1, fm2)
+        deep = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        total = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head_kwargs = dict(fm1=fm1, fm2=fm2, final_w=self.final_layer.weight, final_b=self.final_layer.bias,
+                           head_aux=deep)
+        run_tail(deep_in, self._tail, self.deep_output_layer, head_kwargs, total, prob)
+        return prob, total, fm1, fm2, deep

@@ -1,0 +1,157 @@
+"""DIN (Deep Interest Network) on the rankops engine — drop-in for algorithm/DIN/din.py.
+
+`DIN(vocab_dir, hidden_units=None, activation='dice', dropout_rate=0.1, batch_norm=True,
+use_softmax=False, l2_lambda=0.2, mini_batch_aware_regularization=True)` keeps the reference
+constructor, creation order, state_dict keys (`embeddings.*`, `fcn.N.*` incl. Dice's
+`alpha`/`bn.running_*`, `output_layer.*`; din.py:225-285) and
+`forward(dense, category, sequence, target) -> (probability, logit, l2_reg)` (din.py:294-323).
+
+`embedding_dim` (keyword, default 16 = the reference) widens the target/history embeddings
+for the benchmark configuration (H = 32).
+
+Launches: rk_concat_gather builds [dense | category | target] in one row buffer, the
+rk_din_attention kernel (din.py:42-84) writes the attention output straight into the same
+row, rk_row_l2norm_mean gives the l2 term (din.py:318-322), and the fcn stack runs on
+rk_linear with Dice + BatchNorm in the epilogue and the output layer + sigmoid fused last.
+The attention MLP is drawn per call like the reference (din.py:61-67) or frozen.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common import InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
+    table_rows
+
+FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
+SEQ_KEY = "his_read_comment_7d_seq"
+
+
+class Dice(nn.Module):
+    """Dice activation (din.py:26-36).  Same parameters/buffers as the reference; its eval-mode
+    math runs inside the rk_linear epilogue."""
+
+    def __init__(self, num_features, eps=1e-9):
+        super().__init__()
+        self.eps = eps
+        self.alpha = nn.Parameter(torch.zeros(num_features))
+        self.bn = nn.BatchNorm1d(num_features, affine=False)
+
+    def forward(self, x):
+        raise RuntimeError("Dice runs fused inside the rankops fcn epilogue; call DIN.forward")
+
+
+def din_attention(query, keys_table, seq, keys_length, is_softmax=False, weights=None):
+    """Reference din_attention (din.py:42-84) with the history given as (table, index) —
+    the gather happens inside the kernel.  `weights` = (W1, b1, W2, b2, W3, b3) device tensors;
+    when None they are drawn from the CPU generator like the reference."""
+    query = ops.as_f32(query, "query")
+    seq = ops.as_index(seq, "keys index")
+    keys_length = ops.as_index(keys_length, "keys_length")
+    B, H = query.shape
+    T = seq.shape[1]
+    if weights is None:
+        weights = [t.to(query.device) for t in draw_din_attention(H)]
+    out = torch.empty(B, H, device=query.device, dtype=torch.float32)
+    ops.din_attention(query.data_ptr(), query.stride(0), keys_table, seq.contiguous(), keys_length, T, H, weights,
+                      is_softmax, out.data_ptr(), out.stride(0), B, query.device)
+    return out
+
+
+class DIN(nn.Module):
+    def __init__(self, vocab_dir, hidden_units=None, activation='dice', dropout_rate=0.1, batch_norm=True,
+                 use_softmax=False, l2_lambda=0.2, mini_batch_aware_regularization=True, *, vocab_sizes=None,
+                 embedding_dim=16, interaction_weights="per_call"):
+        super().__init__()
+        if hidden_units is None:
+            hidden_units = [512, 256, 128]
+        self.activation = activation
+        self.dropout_rate = dropout_rate
+        self.batch_norm = batch_norm
+        self.use_softmax = use_softmax
+        self.l2_lambda = l2_lambda
+        self.mini_batch_aware_regularization = mini_batch_aware_regularization
+        self.vocab_sizes = {f: table_rows(vocab_dir, f, vocab_sizes) for f in FIELDS}
+        self.num_dense_features = 16
+        self.embeddings = nn.ModuleDict({
+            "userid": nn.Embedding(self.vocab_sizes["userid"], 16),
+            "device": nn.Embedding(self.vocab_sizes["device"], 2),
+            "authorid": nn.Embedding(self.vocab_sizes["authorid"], 4),
+            "bgm_song_id": nn.Embedding(self.vocab_sizes["bgm_song_id"], 4),
+            "bgm_singer_id": nn.Embedding(self.vocab_sizes["bgm_singer_id"], 4),
+            "manual_tag_list": nn.Embedding(self.vocab_sizes["manual_tag_list"], 4),
+            "feedid": nn.Embedding(self.vocab_sizes["feedid"], embedding_dim),
+            SEQ_KEY: nn.Embedding(self.vocab_sizes["feedid"], embedding_dim),
+        })
+        width = self.num_dense_features
+        for key in ("userid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"):
+            width += self.embeddings[key].embedding_dim
+        width += self.embeddings["feedid"].embedding_dim + self.embeddings[SEQ_KEY].embedding_dim
+        self.fcn = nn.ModuleList()
+        self._tail = []
+        for unit in hidden_units:
+            lin = nn.Linear(width, unit)
+            self.fcn.append(lin)
+            if activation == 'dice':
+                act = Dice(unit)
+                kind = "dice"
+            else:
+                act = nn.PReLU()
+                kind = "prelu"
+            self.fcn.append(act)
+            bn = None
+            if batch_norm:
+                bn = nn.BatchNorm1d(unit)
+                self.fcn.append(bn)
+            if dropout_rate > 0:
+                self.fcn.append(nn.Dropout(dropout_rate))
+            self._tail.append(Layer(lin, act=kind, act_module=act, post_bn=bn))
+            width = unit
+        self.output_layer = nn.Linear(width, 1)
+        self.att_weights = InteractionWeights(
+            interaction_weights, lambda: draw_din_attention(self.embeddings[SEQ_KEY].embedding_dim))
+
+    def _load_vocabulary(self, vocab_dir, filename):
+        return load_vocabulary(vocab_dir, filename)
+
+    def forward(self, dense, category, sequence, target):
+        check_eval(self)
+        dense_cols = [ops.as_f32(v, f"dense[{k!r}]") for k, v in dense.items()]
+        B = dense_cols[0].shape[0]
+        dev = dense_cols[0].device
+        segs = [ops.dense_segment(v, 1, i) for i, v in enumerate(dense_cols)]
+        col = len(dense_cols)
+        cat_col0 = col
+        for name, emb in self.embeddings.items():
+            if name in category:
+                idx = ops.as_index(category[name], f"category[{name!r}]")
+                segs.append(ops.table_segment(emb.weight, idx, col))
+                col += emb.embedding_dim
+        cat_dim = col - cat_col0
+        tgt_emb = self.embeddings["feedid"]
+        H = tgt_emb.embedding_dim
+        tgt_idx = ops.as_index(target["feedid"], "target['feedid']")
+        segs.append(ops.table_segment(tgt_emb.weight, tgt_idx, col))
+        q_col = col
+        att_col = q_col + H
+        width = att_col + self.embeddings[SEQ_KEY].embedding_dim
+        row = torch.empty(B, width, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, row)
+
+        seq = ops.as_index(sequence[SEQ_KEY], f"sequence[{SEQ_KEY!r}]").contiguous()
+        seq_len = ops.as_index(sequence[f"{SEQ_KEY}_length"], "sequence length")
+        T = seq.shape[1]
+        w = self.att_weights.get(dev)
+        ops.din_attention(ops._lib.fptr(row, q_col), width, self.embeddings[SEQ_KEY].weight, seq, seq_len, T, H, w,
+                          self.use_softmax, ops._lib.fptr(row, att_col), width, B, dev)
+
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        run_tail(row, self._tail, self.output_layer, {}, logit, prob)
+
+        l2_reg = 0.0
+        if self.mini_batch_aware_regularization and self.l2_lambda > 0:
+            l2_reg = torch.empty((), device=dev, dtype=torch.float32)
+            ops.row_l2norm_mean(row, cat_col0, width - cat_col0, float(self.l2_lambda), l2_reg)
+        return prob, logit, l2_reg

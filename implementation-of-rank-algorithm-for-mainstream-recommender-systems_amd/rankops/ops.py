@@ -1,0 +1,181 @@
+"""Thin Python wrappers over the rankops C ABI.
+
+Each wrapper validates devices/dtypes/shapes, turns tensors into device pointers and launches
+on the current HIP stream of the tensors' device.  Outputs are allocated from PyTorch's
+caching allocator, so every wrapper is safe inside `torch.cuda.graph` capture.  There is no
+CPU path: a CPU tensor is an error (the CPU restatement in oracle/ is test-only).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import Epilogue, Segment, check, fptr, ptr
+
+ACT = {"none": _lib.RK_ACT_NONE, "relu": _lib.RK_ACT_RELU, "leaky": _lib.RK_ACT_LEAKY,
+       "dice": _lib.RK_ACT_DICE, "prelu": _lib.RK_ACT_PRELU}
+
+
+def require_gpu(t: torch.Tensor, what: str):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"rankops: {what} must be a tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"rankops: {what} is on {t.device}; the rankops forward runs only on a ROCm GPU "
+            f"(move the model and inputs with .to('cuda'))")
+    return t
+
+
+def as_index(t: torch.Tensor, what: str) -> torch.Tensor:
+    require_gpu(t, what)
+    if t.dtype != torch.int64:
+        if t.dtype in (torch.int32, torch.int16, torch.uint8, torch.int8):
+            t = t.long()
+        else:
+            raise TypeError(f"rankops: {what} must be an integer tensor, got {t.dtype}")
+    return t
+
+
+def as_f32(t: torch.Tensor, what: str) -> torch.Tensor:
+    require_gpu(t, what)
+    if t.dtype != torch.float32:
+        raise TypeError(f"rankops: {what} must be float32, got {t.dtype}")
+    return t
+
+
+def table_segment(weight: torch.Tensor, idx: torch.Tensor, out_col: int, idx_stride: int = None) -> Segment:
+    """Embedding-table segment: rows weight[idx[b]] -> out[b, out_col:out_col+dim]."""
+    if weight.dim() != 2 or weight.stride(1) != 1:
+        raise ValueError("rankops: embedding weight must be 2-D with unit column stride")
+    if idx_stride is None:
+        if idx.dim() != 1:
+            raise ValueError(f"rankops: expected a 1-D index tensor, got shape {tuple(idx.shape)}")
+        idx_stride = idx.stride(0)
+    return Segment(weight.data_ptr(), idx.data_ptr(), idx_stride, weight.stride(0), weight.shape[0],
+                   weight.shape[1], out_col)
+
+
+def dense_segment(src: torch.Tensor, dim: int, out_col: int, col_offset: int = 0) -> Segment:
+    """Dense segment: src[b, col_offset:col_offset+dim] -> out[b, out_col:+dim] (src is [B] or [B, *])."""
+    if src.dim() == 1:
+        if dim != 1:
+            raise ValueError("rankops: a 1-D dense source has dim 1")
+        ld = src.stride(0)
+    else:
+        if src.stride(-1) != 1:
+            raise ValueError("rankops: dense source must have unit column stride")
+        ld = src.stride(0)
+    return Segment(fptr(src, col_offset), None, 0, ld, 0, dim, out_col)
+
+
+def _seg_array(segs):
+    arr = (Segment * len(segs))(*segs)
+    return arr
+
+
+def concat_gather(segs, batch: int, out: torch.Tensor):
+    lib = _lib.load()
+    _lib.ensure_device(out.device)
+    arr = _seg_array(segs)
+    check(lib.rk_concat_gather(arr, len(segs), batch, ptr(out), out.stride(0), _lib.stream_of(out)),
+          "rk_concat_gather")
+    return out
+
+
+def dcn_cross(segs, batch, width, cross_w, cross_b, num_layers, head_w_ptr, x0, partial, device,
+              xl_in=None, xl_out=None):
+    lib = _lib.load()
+    _lib.ensure_device(device)
+    arr = _seg_array(segs)
+    check(lib.rk_dcn_cross(arr, len(segs), batch, width, ptr(cross_w), ptr(cross_b), num_layers, head_w_ptr,
+                           ptr(x0), x0.stride(0) if x0 is not None else 0,
+                           ptr(xl_in), xl_in.stride(0) if xl_in is not None else 0,
+                           ptr(xl_out), xl_out.stride(0) if xl_out is not None else 0,
+                           ptr(partial), torch.cuda.current_stream(device).cuda_stream), "rk_dcn_cross")
+
+
+def fm_gather(second, first, dim, batch, deep_in, fm1, fm2):
+    lib = _lib.load()
+    _lib.ensure_device(deep_in.device)
+    a2, a1 = _seg_array(second), _seg_array(first)
+    check(lib.rk_fm_gather(a2, a1, len(second), dim, batch, ptr(deep_in), deep_in.stride(0), ptr(fm1), ptr(fm2),
+                           _lib.stream_of(deep_in)), "rk_fm_gather")
+
+
+def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, use_softmax, out_ptr, ld_out,
+                  batch, device):
+    lib = _lib.load()
+    _lib.ensure_device(device)
+    w1, b1, w2, b2, w3, b3 = weights
+    check(lib.rk_din_attention(query_ptr, ld_query, ptr(key_table), key_table.shape[0], key_table.stride(0),
+                               ptr(seq), seq.stride(0), T, ptr(seq_len), batch, H, ptr(w1), ptr(b1), ptr(w2),
+                               ptr(b2), ptr(w3), ptr(b3), 1 if use_softmax else 0, out_ptr, ld_out,
+                               torch.cuda.current_stream(device).cuda_stream), "rk_din_attention")
+
+
+def row_l2norm_mean(x: torch.Tensor, col0: int, ncols: int, scale: float, out: torch.Tensor):
+    lib = _lib.load()
+    check(lib.rk_row_l2norm_mean(ptr(x), x.stride(0), x.shape[0], col0, ncols, scale, ptr(out),
+                                 _lib.stream_of(x)), "rk_row_l2norm_mean")
+    return out
+
+
+def afm_forward(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h, att_hb, p_w, p_b, logit, prob):
+    lib = _lib.load()
+    _lib.ensure_device(logit.device)
+    arr = _seg_array(fields)
+    nd = dense.shape[1] if dense is not None else 0
+    check(lib.rk_afm_forward(arr, len(fields), dim, batch, ptr(dense), dense.stride(0) if dense is not None else 0,
+                             nd, ptr(dense_w), ptr(dense_b), ptr(att_w), ptr(att_b), att_w.shape[0], ptr(att_h),
+                             ptr(att_hb), ptr(p_w), ptr(p_b), ptr(logit), ptr(prob), _lib.stream_of(logit)),
+          "rk_afm_forward")
+
+
+def bst_attention(qkv, batch, T, d_model, heads, seq_len, ctx):
+    lib = _lib.load()
+    check(lib.rk_bst_attention(ptr(qkv), qkv.stride(0), batch, T, d_model, heads, ptr(seq_len), ptr(ctx),
+                               ctx.stride(0), _lib.stream_of(qkv)), "rk_bst_attention")
+
+
+def bn_fold(mean, var, weight, bias, eps, scale, shift):
+    lib = _lib.load()
+    check(lib.rk_bn_fold(ptr(mean), ptr(var), ptr(weight), ptr(bias), float(eps), mean.numel(), ptr(scale),
+                         ptr(shift), _lib.stream_of(mean)), "rk_bn_fold")
+
+
+_EPI_PTR_FIELDS = {f for f, t in Epilogue._fields_ if t is ctypes.c_void_p}
+
+
+def make_epilogue(**kw) -> Epilogue:
+    ep = Epilogue()
+    for k, v in kw.items():
+        if v is None:
+            continue
+        if k == "act" and isinstance(v, str):
+            v = ACT[v]
+        if k in _EPI_PTR_FIELDS and isinstance(v, torch.Tensor):
+            v = v.data_ptr()
+        setattr(ep, k, v)
+    return ep
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M: int = None, K: int = None,
+           x_ptr: int = None, ldx: int = None, x_periodic: torch.Tensor = None, x_period: int = 0,
+           y_ptr: int = None, ldy: int = None, epilogue: Epilogue = None):
+    """y = epilogue(x . weight^T) on FP32 MFMA.  weight is [N, K] (nn.Linear layout)."""
+    lib = _lib.load()
+    N = weight.shape[0]
+    K = weight.shape[1] if K is None else K
+    M = x.shape[0] if M is None else M
+    if weight.stride(1) != 1:
+        raise ValueError("rankops.linear: weight needs unit column stride")
+    xp = x.data_ptr() if x_ptr is None else x_ptr
+    lx = x.stride(0) if ldx is None else ldx
+    if y_ptr is None and out is not None:
+        y_ptr, ldy = out.data_ptr(), out.stride(0) if ldy is None else ldy
+    ep = epilogue if epilogue is not None else Epilogue()
+    check(lib.rk_linear(xp, lx, ptr(x_periodic), x_period, weight.data_ptr(), weight.stride(0), M, N, K,
+                        ctypes.byref(ep), y_ptr, ldy or 0, _lib.stream_of(x)), "rk_linear")
+    return out

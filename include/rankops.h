@@ -1,0 +1,178 @@
+/*
+ * rankops.h — C ABI of the MI355X (gfx950) CTR feature-interaction engine.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t passed
+ * as `void*` (NULL = the default stream).  Nothing here knows about torch: the
+ * Python host layer (the rankops Python package) binds these with ctypes, exactly as the
+ * reference's `nn.Module.forward()` bodies would bind them.
+ * All work is enqueued asynchronously on `stream`; no entry point allocates
+ * device memory or synchronises, so every forward can be captured in a hipGraph.
+ *
+ * Return value: RK_OK (0) or an RK_ERR_* code; rk_last_error() gives the text.
+ * Out-of-range embedding indices never fault: the row is read as zeros and
+ * RK_FLAG_INDEX_OOB is raised in the device flag word (rk_error_flags), the
+ * analogue of nn.Embedding's IndexError / device assert.
+ *
+ * Reference interfaces replaced (file:line in the reference snapshot):
+ *   rk_concat_gather   nn.Embedding lookups + torch.cat       dcn.py:163-169, deepcrossing.py:148-155,
+ *                                                            din.py:296-305,310, bst.py:218-224,243
+ *   rk_dcn_cross       cross_layer() loop + output_layer part dcn.py:25-50,171-173,177-178
+ *   rk_fm_gather       DeepFM first/second-order FM + concat deepfm.py:122-142
+ *   rk_linear          nn.Linear (+BatchNorm1d eval, ReLU/LeakyReLU/Dice/PReLU, residual,
+ *                      LayerNorm, sum/mean pooling, final Linear(*,1)+sigmoid) dcn.py:144-152,175-180;
+ *                      deepfm.py:100-112,143-151; din.py:26-36,272-285,312-316; deepcrossing.py:25-42,161-162;
+ *                      bst.py:59-64,73-75,86-90,203-214,238-247
+ *   rk_din_attention   din_attention()                       din.py:42-84
+ *   rk_row_l2norm_mean DIN mini-batch-aware l2 term          din.py:318-322
+ *   rk_afm_forward     AFM.forward()                         afm.py:92-119
+ *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84
+ *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
+ */
+#ifndef RANKOPS_H
+#define RANKOPS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RK_ABI_VERSION 1
+
+#define RK_OK 0
+#define RK_ERR_INVALID 1     /* bad argument (shape, null pointer, limit) */
+#define RK_ERR_LAUNCH 2      /* hipLaunch / hipGetLastError failure */
+#define RK_ERR_RUNTIME 3     /* other HIP runtime failure */
+#define RK_ERR_UNSUPPORTED 4 /* shape outside the implemented envelope */
+
+#define RK_FLAG_INDEX_OOB 1u /* an embedding index was < 0 or >= table rows */
+
+#define RK_ACT_NONE 0
+#define RK_ACT_RELU 1
+#define RK_ACT_LEAKY 2 /* LeakyReLU(slope) */
+#define RK_ACT_DICE 3  /* Dice: a*(1-p)*x + p*x, p = sigmoid(x*act_scale + act_shift) */
+#define RK_ACT_PRELU 4 /* PReLU(act_alpha) */
+
+#define RK_MAX_SEGMENTS 64
+
+/* One column block of a concatenated feature row.
+ * Table segment (idx != NULL): out[b, out_col:out_col+dim] = src[idx[b*idx_stride]*src_ld : +dim]
+ * Dense segment (idx == NULL): out[b, out_col:out_col+dim] = src[b*src_ld : +dim]           */
+typedef struct rk_segment {
+  const float* src;
+  const int64_t* idx;
+  int64_t idx_stride;
+  int64_t src_ld;
+  int64_t rows; /* table rows (bounds check); ignored for dense segments */
+  int32_t dim;
+  int32_t out_col;
+} rk_segment;
+
+/* Fused GEMM epilogue, applied in this order to z = x.W^T:
+ *   z += bias[n]; z += residual[m, n] (+ residual_periodic[m % period, n]);
+ *   z = z*pre_scale[n] + pre_shift[n];   (BatchNorm1d eval before the activation)
+ *   z = act(z);
+ *   z = z*post_scale[n] + post_shift[n]; (BatchNorm1d eval after the activation: DIN)
+ * then the optional row epilogues (need the whole row in one workgroup, N <= 256):
+ *   LayerNorm over n (ln_gamma/ln_beta, ln_eps);
+ *   pool: pool_out[g, n] = sum over rows m of group g (pool_rows consecutive rows),
+ *         divided by pool_len[g] when pool_mean;
+ *   head: logit[m] = sum_n z[m,n]*head_w[n] + head_b[0] (+ head_partial[m]);
+ *         DeepFM combine when fm1 != NULL: head_aux[m] = logit (deep logit),
+ *         logit = final_w[0]*fm1[m] + final_w[1]*fm2[m] + final_w[2]*deep + final_b[0];
+ *         head_prob[m] = sigmoid(logit).
+ * y may be NULL when only row-epilogue outputs are wanted.                              */
+typedef struct rk_epilogue {
+  const float* bias;
+  const float* residual;
+  int64_t ld_residual;
+  const float* residual_periodic;
+  int32_t residual_period;
+  const float* pre_scale;
+  const float* pre_shift;
+  int32_t act;
+  float slope;
+  const float* act_scale;
+  const float* act_shift;
+  const float* act_alpha;
+  int32_t act_alpha_len;
+  const float* post_scale;
+  const float* post_shift;
+  const float* ln_gamma;
+  const float* ln_beta;
+  float ln_eps;
+  int32_t has_ln;
+  float* pool_out;
+  int64_t ld_pool;
+  int32_t pool_rows;
+  int32_t pool_mean;
+  const int64_t* pool_len;
+  const float* head_w;
+  const float* head_b;
+  const float* head_partial;
+  const float* fm1;
+  const float* fm2;
+  const float* final_w;
+  const float* final_b;
+  float* head_logit;
+  float* head_prob;
+  float* head_aux;
+} rk_epilogue;
+
+/* ---- runtime ---- */
+int32_t rk_abi_version(void);
+const char* rk_last_error(void);
+int rk_init(int32_t device);
+/* Reads (and optionally clears) the device flag word; synchronises the device. */
+int rk_error_flags(int32_t device, uint32_t* flags, int32_t reset);
+
+/* ---- embedding gather / interaction kernels ---- */
+int rk_concat_gather(const rk_segment* segs, int32_t nseg, int64_t batch, float* out,
+                     int64_t ld_out, void* stream);
+
+/* x0 = concat(segs); x_0 = xl_in (or x0 when NULL); x_{l+1} = x0*(x_l.w_l) + b_l + x_l.
+ * Optional outputs: x0 (the gathered row), xl_out (x_L), cross_partial = x_L.head_w.      */
+int rk_dcn_cross(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t width,
+                 const float* cross_w, const float* cross_b, int32_t num_layers,
+                 const float* head_w, float* x0, int64_t ld_x0, const float* xl_in,
+                 int64_t ld_xl_in, float* xl_out, int64_t ld_xl_out, float* cross_partial,
+                 void* stream);
+
+int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_order,
+                 int32_t num_fields, int32_t dim, int64_t batch, float* deep_in,
+                 int64_t ld_deep, float* fm1, float* fm2, void* stream);
+
+int rk_din_attention(const float* query, int64_t ld_query, const float* key_table,
+                     int64_t key_rows, int64_t ld_key, const int64_t* seq, int64_t ld_seq,
+                     int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
+                     const float* w1, const float* b1, const float* w2, const float* b2,
+                     const float* w3, const float* b3, int32_t use_softmax, float* out,
+                     int64_t ld_out, void* stream);
+
+int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols,
+                       float scale, float* out_scalar, void* stream);
+
+int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                   const float* dense, int64_t ld_dense, int32_t num_dense,
+                   const float* dense_w, const float* dense_b, const float* att_w,
+                   const float* att_b, int32_t att_factor, const float* att_h,
+                   const float* att_hb, const float* p_w, const float* p_b, float* logit,
+                   float* prob, void* stream);
+
+int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T,
+                     int32_t d_model, int32_t heads, const int64_t* seq_len, float* ctx,
+                     int64_t ld_ctx, void* stream);
+
+/* ---- dense layers ---- */
+int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_period,
+              const float* w, int64_t ldw, int64_t M, int32_t N, int32_t K,
+              const rk_epilogue* ep, float* y, int64_t ldy, void* stream);
+
+int rk_bn_fold(const float* mean, const float* var, const float* weight, const float* bias,
+               float eps, int32_t n, float* scale, float* shift, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RANKOPS_H */

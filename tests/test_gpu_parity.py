@@ -1,0 +1,229 @@
+"""GPU parity: every rankops model (HIP path, through the C ABI) against the CPU oracle on
+the same seeded inputs and weights.  Tolerance (north star): logits and probabilities within
+atol 1e-4 + rtol 1e-4 in fp32; indices are used bit-exactly (same rows gathered)."""
+import pytest
+import torch
+
+import helpers as H
+import rankops
+
+ATOL = 1e-4
+RTOL = 1e-4
+
+FIELDS30 = {f"field_{i:02d}": 1000 + 37 * i for i in range(30)}
+
+CASES = [
+    ("dcn", {}),
+    ("dcn", {"cross": 3}),
+    ("dcn", {"cross": 0}),
+    ("dcn", {"hidden": [64, 300]}),  # last hidden width > 256: head runs as its own GEMM
+    ("deepfm", {}),
+    ("deepfm", {"dim": 32, "fields": FIELDS30}),
+    ("deepfm", {"batch_norm": False}),
+    ("din", {"T": 50}),
+    ("din", {"T": 50, "softmax": True}),
+    ("din", {"T": 50, "dim": 32}),
+    ("din", {"T": 50, "dim": 32, "softmax": True}),
+    ("din", {"T": 7, "activation": "prelu", "batch_norm": False, "l2": 0.0}),
+    ("din", {"T": 77}),  # more than two 32-position tiles
+    ("afm", {}),
+    ("afm", {"dim": 32, "att": 64}),
+    ("afm", {"dim": 16, "att": 200}),
+    ("deepcrossing", {}),
+    ("deepcrossing", {"units": 3, "internal": 64}),
+    ("bst", {"T": 50}),
+    ("bst", {"T": 50, "pooling": "mean"}),
+    ("bst", {"T": 64, "dim": 128, "max_len": 64, "heads": 4}),
+    ("bst", {"T": 20, "blocks": 2, "batch_norm": False}),
+    ("bst", {"T": 1}),
+]
+
+
+def _ids(case):
+    name, cfg = case
+    return name + ("-" + "-".join(f"{k}{v}" for k, v in cfg.items() if k != "fields") if cfg else "")
+
+
+def _compare(out, ref, what):
+    out, ref = H.as_tuple(out), H.as_tuple(ref)
+    assert len(out) == len(ref), what
+    for i, (o, r) in enumerate(zip(out, ref)):
+        if not isinstance(r, torch.Tensor):
+            assert o == r, f"{what}[{i}]"
+            continue
+        assert o.device.type == "cuda", f"{what}[{i}] not produced on the GPU"
+        assert tuple(o.shape) == tuple(r.shape), f"{what}[{i}] shape {tuple(o.shape)} vs {tuple(r.shape)}"
+        torch.testing.assert_close(o.detach().cpu(), r, atol=ATOL, rtol=RTOL, equal_nan=True,
+                                   msg=lambda m: f"{what}[{i}]: {m}")
+
+
+def run_pair(name, cfg, B, seed=123, inputs=None, model=None):
+    model = model if model is not None else H.build(name, cfg)
+    p = H.cpu_params(model)
+    inp = inputs if inputs is not None else H.make_inputs(name, cfg, B)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        ref = H.call_oracle(name, cfg, p, inp)
+    model = model.cuda()
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        out = H.call_model(model, name, H.to_device(inp, "cuda"))
+    torch.cuda.synchronize()
+    return out, ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=_ids)
+def test_model_parity(case):
+    name, cfg = case
+    out, ref = run_pair(name, cfg, B=300)
+    _compare(out, ref, _ids(case))
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dcn", "deepcrossing", "din"])
+def test_frozen_interaction_weights(name):
+    """'frozen' draws the H2 weights once with the reference's calls; the first forward equals
+    the reference's first call and later forwards reuse the same weights."""
+    cfg = {"interaction_weights": "frozen", "T": 20}
+    model = H.build(name, cfg).cuda()
+    inp = H.to_device(H.make_inputs(name, cfg, 128), "cuda")
+    torch.manual_seed(5)
+    with torch.no_grad():
+        a = H.call_model(model, name, inp)
+        torch.manual_seed(99)
+        b = H.call_model(model, name, inp)
+    for x, y in zip(H.as_tuple(a), H.as_tuple(b)):
+        assert torch.equal(x, y)
+    p = H.cpu_params(model)
+    torch.manual_seed(5)
+    ref = H.call_oracle(name, cfg, p, H.to_device(inp, "cpu"))
+    _compare(a, ref, f"{name}-frozen")
+
+
+@pytest.mark.gpu
+def test_wechat_scale_tables():
+    """Full wechat vocabulary sizes at batch 4096: DCN and DIN."""
+    for name, cfg in (("dcn", {"vocab": H.WECHAT_VOCAB}), ("din", {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32})):
+        out, ref = run_pair(name, cfg, B=4096)
+        _compare(out, ref, name + "-wechat")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("softmax", [False, True])
+def test_din_edge_lengths(softmax):
+    """Length 0 (softmax -> uniform weights over T, din.py:74-77; plain -> zeros), T=1, len=T."""
+    cfg = {"T": 9, "softmax": softmax}
+    inp = H.make_inputs("din", cfg, 64)
+    lens = inp["sequence"]["his_read_comment_7d_seq_length"]
+    lens[:8] = 0
+    lens[8:16] = 9
+    lens[16:24] = 1
+    out, ref = run_pair("din", cfg, B=64, inputs=inp)
+    _compare(out, ref, f"din-edge-softmax{softmax}")
+    cfg1 = {"T": 1, "softmax": softmax}
+    out, ref = run_pair("din", cfg1, B=32)
+    _compare(out, ref, "din-T1")
+
+
+@pytest.mark.gpu
+def test_bst_empty_sequence_is_nan_like_reference():
+    """A length-0 row is all -inf in the reference softmax -> NaN output (bst.py:80-82)."""
+    cfg = {"T": 12}
+    inp = H.make_inputs("bst", cfg, 32)
+    inp["seq_length"][:4] = 0
+    out, ref = run_pair("bst", cfg, B=32, inputs=inp)
+    assert torch.isnan(ref[1][:4]).all()
+    _compare(out, ref, "bst-empty")
+
+
+@pytest.mark.gpu
+def test_out_of_range_index_is_flagged():
+    cfg = {}
+    model = H.build("dcn", {"interaction_weights": "frozen"}).cuda()
+    inp = H.to_device(H.make_inputs("dcn", cfg, 64), "cuda")
+    rankops.error_flags(reset=True)
+    with torch.no_grad():
+        H.call_model(model, "dcn", inp)
+    assert rankops.error_flags() == 0
+    inp["category"]["userid"][3] = model.vocab_sizes["userid"] + 5
+    with torch.no_grad():
+        H.call_model(model, "dcn", inp)
+    assert rankops.error_flags(reset=True) & 1
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+def test_graph_capture_replay_matches_eager():
+    """The forward has no host sync or allocation outside the caching allocator, so it captures
+    into a hipGraph; replay must equal the eager result."""
+    for name, cfg in (("deepfm", {"dim": 32, "fields": FIELDS30}), ("din", {"T": 50, "dim": 32,
+                      "interaction_weights": "frozen"}), ("bst", {"T": 64, "dim": 128, "max_len": 64})):
+        model = H.build(name, cfg).cuda()
+        inp = H.to_device(H.make_inputs(name, cfg, 512), "cuda")
+        with torch.no_grad():
+            eager = H.as_tuple(H.call_model(model, name, inp))
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    H.call_model(model, name, inp)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                static = H.as_tuple(H.call_model(model, name, inp))
+            g.replay()
+            torch.cuda.synchronize()
+        for e, r in zip(eager, static):
+            if isinstance(e, torch.Tensor):
+                assert torch.equal(e, r), name
+
+
+@pytest.mark.gpu
+def test_cpu_inputs_raise():
+    model = H.build("dcn", {}).cuda()
+    inp = H.make_inputs("dcn", {}, 8)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        H.call_model(model, "dcn", inp)
+
+
+@pytest.mark.gpu
+def test_training_mode_raises():
+    model = H.build("deepfm", {}).cuda().train()
+    inp = H.to_device(H.make_inputs("deepfm", {}, 8), "cuda")
+    with pytest.raises(NotImplementedError):
+        H.call_model(model, "deepfm", inp)
+
+
+@pytest.mark.gpu
+def test_standalone_reference_functions():
+    """cross_layer, residual_unit and din_attention as module-level functions (dcn.py:25,
+    deepcrossing.py:25, din.py:42) draw per call like the reference."""
+    from oracle import reference_forward as ref
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.randn(40, 50, generator=g)
+    xl = torch.randn(40, 50, generator=g)
+    torch.manual_seed(11)
+    w, b = ref.draw_cross(50, 1)[0]
+    expect = ref.dcn_cross_layer(x0, xl, w, b)
+    torch.manual_seed(11)
+    got = rankops.cross_layer(x0.cuda(), xl.cuda(), 0)
+    torch.testing.assert_close(got.cpu(), expect, atol=ATOL, rtol=RTOL)
+
+    torch.manual_seed(12)
+    expect = ref.residual_unit(x0, *ref.draw_residual(50, 32))
+    torch.manual_seed(12)
+    got = rankops.residual_unit(x0.cuda(), 32, 0)
+    torch.testing.assert_close(got.cpu(), expect, atol=ATOL, rtol=RTOL)
+
+    table = torch.randn(90, 16, generator=g)
+    seq = torch.randint(0, 90, (40, 13), generator=g)
+    lens = torch.randint(0, 14, (40,), generator=g)
+    q = torch.randn(40, 16, generator=g)
+    for sm in (False, True):
+        torch.manual_seed(13)
+        expect = ref.din_attention(q, table[seq], lens, sm)
+        torch.manual_seed(13)
+        got = rankops.din_attention(q.cuda(), table.cuda(), seq.cuda(), lens.cuda(), sm)
+        torch.testing.assert_close(got.cpu(), expect, atol=ATOL, rtol=RTOL)
