@@ -191,7 +191,8 @@ RK_API int rk_din_attention(const float* query, int64_t ld_query, const float* k
     return fail(RK_ERR_UNSUPPORTED, "rk_din_attention: key table rows must be 16-B aligned");
   if (batch == 0) return RK_OK;
   const int64_t want = (batch + 3) / 4;
-  const unsigned blocks = (unsigned)std::min<int64_t>(want, (int64_t)num_cus() * 4);
+  // persistent: W1/W2 are staged in LDS once per workgroup, which then walks many samples
+  const unsigned blocks = (unsigned)std::min<int64_t>(want, (int64_t)num_cus() * 2);
   hipStream_t st = (hipStream_t)stream;
   uint32_t* fl = device_flags();
 #define RK_DIN_CASE(HH)                                                                                         \

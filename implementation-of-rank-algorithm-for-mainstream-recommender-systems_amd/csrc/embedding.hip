@@ -163,18 +163,33 @@ __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64
   f32x4 s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
   float fo = 0.f;
   if (live) {
-#pragma unroll 4
-    for (int f = wave; f < F; f += 4) {
-      const rk_segment& sg = t.second[f];
-      const float* row = segment_row(sg, b, flags);
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row) v = *reinterpret_cast<const f32x4*>(row + 4 * q);
-      *reinterpret_cast<f32x4*>(deep_in + b * ld_deep + sg.out_col + 4 * q) = v;
-      s += v;
-      sq += v * v;
-      if (q == 0) {
-        const float* w = segment_row(t.first[f], b, flags);
-        fo += w ? w[0] : 0.f;
+    // wave w owns fields w, w+4, ... (<= 8).  All index loads are issued first, then all row
+    // loads, then the stores: no store sits between two dependent loads, so every lane keeps
+    // up to 8 row fetches in flight.
+    constexpr int FPW = kFmMaxFields / 4;
+    const float* rp[FPW];
+    const float* wp[FPW];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const int f = wave + 4 * j;
+      rp[j] = f < F ? segment_row(t.second[f], b, flags) : nullptr;
+      wp[j] = (f < F && q == 0) ? segment_row(t.first[f], b, flags) : nullptr;
+    }
+    f32x4 v[FPW];
+    float w1[FPW];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      v[j] = rp[j] ? *reinterpret_cast<const f32x4*>(rp[j] + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      w1[j] = wp[j] ? wp[j][0] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const int f = wave + 4 * j;
+      if (f < F) {
+        *reinterpret_cast<f32x4*>(deep_in + b * ld_deep + t.second[f].out_col + 4 * q) = v[j];
+        s += v[j];
+        sq += v[j] * v[j];
+        fo += w1[j];
       }
     }
   }
@@ -219,28 +234,34 @@ __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64
 // ------------------------------------------------------------------------------------
 // DIN l2 term: scale * mean_r ||x[r, col0:col0+ncols]||_2 — one deterministic workgroup.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void row_l2norm_mean_kernel(const float* __restrict__ x, int64_t ld, int64_t rows,
-                                                               int col0, int ncols, float scale,
-                                                               float* __restrict__ out) {
-  __shared__ float part[16];
+// Stage 1: block b sums the norms of rows b, b+G, ... (wave-strided, fixed order) into part[b].
+constexpr int kL2Blocks = 512;
+__global__ __launch_bounds__(256) void row_l2norm_partial_kernel(const float* __restrict__ x, int64_t ld,
+                                                                 int64_t rows, int col0, int ncols,
+                                                                 float* __restrict__ part) {
+  __shared__ float wsum[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc = 0.f;
-  for (int64_t r = wave; r < rows; r += 16) {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
     float ss = 0.f;
     for (int c = lane; c < ncols; c += 64) {
       const float v = x[r * ld + col0 + c];
       ss = fmaf(v, v, ss);
     }
-    ss = wave_sum(ss);
-    acc += sqrtf(ss);
+    acc += sqrtf(wave_sum(ss));
   }
-  if (lane == 0) part[wave] = acc;
+  if (lane == 0) wsum[wave] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int w = 0; w < 16; ++w) t += part[w];
-    out[0] = scale * (t / (float)rows);
-  }
+  if (threadIdx.x == 0) part[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+// Stage 2: one wave adds the block partials in a fixed tree order.
+__global__ __launch_bounds__(64) void row_l2norm_final_kernel(const float* __restrict__ part, int nparts,
+                                                              int64_t rows, float scale, float* __restrict__ out) {
+  float t = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 64) t += part[i];
+  t = wave_sum(t);
+  if (threadIdx.x == 0) out[0] = scale * (t / (float)rows);
 }
 
 __global__ void bn_fold_kernel(const float* __restrict__ mean, const float* __restrict__ var,
@@ -288,7 +309,10 @@ RK_API int rk_concat_gather(const rk_segment* segs, int32_t nseg, int64_t batch,
   const int V = vec ? 4 : 1;
   const int units = (width + V - 1) / V;
   if (units > kConcatMaxUnits) return fail(RK_ERR_UNSUPPORTED, "rk_concat_gather: width %d too large", width);
-  int rows_per_block = std::max(1, 4096 / units);
+  // enough blocks to cover every CU several times, each still moving >= ~1 KB
+  const int64_t want_blocks = 4 * (int64_t)num_cus();
+  int rows_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(4096 / units, (batch + want_blocks - 1) / want_blocks));
+  rows_per_block = std::max(rows_per_block, std::max(1, 256 / units));
   const int64_t blocks = (batch + rows_per_block - 1) / rows_per_block;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_concat_gather: batch too large");
   hipStream_t st = (hipStream_t)stream;
@@ -369,10 +393,13 @@ RK_API int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_
 }
 
 RK_API int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols, float scale,
-                              float* out_scalar, void* stream) {
-  if (!x || !out_scalar || rows <= 0 || ncols <= 0 || col0 < 0 || col0 + ncols > ld)
+                              float* workspace, float* out_scalar, void* stream) {
+  if (!x || !out_scalar || !workspace || rows <= 0 || ncols <= 0 || col0 < 0 || col0 + ncols > ld)
     return fail(RK_ERR_INVALID, "rk_row_l2norm_mean: bad arguments");
-  row_l2norm_mean_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(x, ld, rows, col0, ncols, scale, out_scalar);
+  const int blocks = (int)std::min<int64_t>(kL2Blocks, (rows + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+  row_l2norm_partial_kernel<<<blocks, 256, 0, st>>>(x, ld, rows, col0, ncols, workspace);
+  row_l2norm_final_kernel<<<1, 64, 0, st>>>(workspace, blocks, rows, scale, out_scalar);
   return check_launch("rk_row_l2norm_mean");
 }
 

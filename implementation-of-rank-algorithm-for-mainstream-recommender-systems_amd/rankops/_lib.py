@@ -75,8 +75,30 @@ class Epilogue(ctypes.Structure):
     ]
 
 
+class MlpLayer(ctypes.Structure):
+    _fields_ = [
+        ("w", c_void_p),
+        ("ldw", c_int64),
+        ("n", c_int32),
+        ("act", c_int32),
+        ("slope", c_float),
+        ("residual", c_int32),
+        ("bias", c_void_p),
+        ("pre_scale", c_void_p),
+        ("pre_shift", c_void_p),
+        ("act_scale", c_void_p),
+        ("act_shift", c_void_p),
+        ("act_alpha", c_void_p),
+        ("act_alpha_len", c_int32),
+        ("post_scale", c_void_p),
+        ("post_shift", c_void_p),
+    ]
+
+
+RK_MLP_MAX_LAYERS = 8
 _SEG_P = POINTER(Segment)
 _EPI_P = POINTER(Epilogue)
+_MLP_P = POINTER(MlpLayer)
 
 # name -> (restype, argtypes); the exact set declared in include/rankops.h
 SIGNATURES = {
@@ -100,7 +122,7 @@ SIGNATURES = {
          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p],
     ),
     "rk_row_l2norm_mean": (
-        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_void_p, c_void_p]),
+        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
     "rk_afm_forward": (
         ctypes.c_int,
         [_SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -113,6 +135,10 @@ SIGNATURES = {
         [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, _EPI_P, c_void_p,
          c_int64, c_void_p],
     ),
+    "rk_mlp_packed_size": (ctypes.c_int, [c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
+    "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
+    "rk_mlp_forward": (
+        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
     "rk_bn_fold": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),
 }

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import DENSE_FEATURES, check_eval
+from .common import DENSE_FEATURES, EngineModule, check_eval
 
 
 def create_feature_columns(vocabulary_dir):
@@ -41,7 +41,7 @@ def create_feature_columns(vocabulary_dir):
     return feature_columns, label_columns
 
 
-class AFM(nn.Module):
+class AFM(EngineModule):
     def __init__(self, feature_columns, embedding_dim, attention_factor):
         super().__init__()
         self.feature_columns = feature_columns

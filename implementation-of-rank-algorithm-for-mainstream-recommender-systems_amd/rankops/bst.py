@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import Layer, Packed, check_eval, table_rows
+from .common import EngineModule, Layer, Packed, check_eval, run_tail, table_rows
 
 FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
 
@@ -39,7 +39,7 @@ def load_vocabulary(vocab_file):
         return [line.strip() for line in f]
 
 
-class BSTTransformer(nn.Module):
+class BSTTransformer(EngineModule):
     """Transformer block with the reference's parameters (bst.py:42-64)."""
 
     def __init__(self, d_model, nhead, max_len, dropout=0.1):
@@ -97,7 +97,7 @@ class BSTTransformer(nn.Module):
         return out
 
 
-class BSTModel(nn.Module):
+class BSTModel(EngineModule):
     def __init__(self, vocab_dir, hidden_units=[512, 256, 128], dropout_rate=0.1, batch_norm=True, d_model=16,
                  nhead=4, num_transformer_blocks=1, max_seq_length=50, pooling_method='sum', *,
                  vocab_sizes=None):
@@ -175,6 +175,5 @@ class BSTModel(nn.Module):
             raise NotImplementedError("BSTModel with zero transformer blocks")
         logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
         probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        from .common import run_tail
         run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
         return probs, logits

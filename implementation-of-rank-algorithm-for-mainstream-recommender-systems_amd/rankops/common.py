@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -121,8 +122,21 @@ def _to_device(obj, device):
 
 # ---------------------------------------------------------------- caches keyed on tensor versions
 
+_GENERATION = [0]
+
+
+class EngineModule(nn.Module):
+    """Base of the drop-in models: any `.to()/.cuda()/.cpu()/.float()` (nn.Module._apply)
+    invalidates every derived-tensor cache (folded BatchNorm, packed weights), so a storage that
+    lands at a previously used address can never revive a stale cache entry."""
+
+    def _apply(self, fn, *args, **kwargs):
+        _GENERATION[0] += 1
+        return super()._apply(fn, *args, **kwargs)
+
+
 def _key(tensors):
-    return tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)
+    return (_GENERATION[0],) + tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)
 
 
 class FoldedBN:
@@ -200,14 +214,58 @@ class Layer:
         return kw
 
 
+FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
+
+
+def _pad64(v: int) -> int:
+    return (v + 63) // 64 * 64
+
+
+def fused_mlp_fits(k0: int, widths) -> bool:
+    if len(widths) == 0 or len(widths) > 8 or max(widths) > 512 or _pad64(k0) > 1024:
+        return False
+    need0 = max([_pad64(k0)] + [_pad64(n) for i, n in enumerate(widths) if i % 2 == 1])
+    need1 = max([64] + [_pad64(n) for i, n in enumerate(widths) if i % 2 == 0])
+    return 16 * (need0 + 4 + need1 + 4) * 4 <= 160 * 1024
+
+
+class PackedWeights:
+    """rk_mlp_pack_weight images, held weakly per weight tensor object and rebuilt when its
+    storage or version changes (load_state_dict, .to(), optimizer steps).  Keying on the
+    object — not the address — keeps a freed model's packed image from being served to a new
+    tensor that reuses its memory."""
+
+    def __init__(self):
+        self._d = {}  # id(tensor) -> (weakref, key, packed); the weakref callback drops the entry
+
+    def __call__(self, w: torch.Tensor) -> torch.Tensor:
+        key = (_GENERATION[0], w.data_ptr(), w._version, tuple(w.shape), w.device)
+        hit = self._d.get(id(w))
+        if hit is None or hit[0]() is not w or hit[1] != key:
+            d, i = self._d, id(w)
+            ref = weakref.ref(w, lambda _r, d=d, i=i: d.pop(i, None) if d.get(i, (None,))[0] is _r else None)
+            hit = (ref, key, ops.pack_mlp_weight(w))
+            self._d[i] = hit
+        return hit[2]
+
+
+PACKED = PackedWeights()
+
+
 def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit: torch.Tensor,
              prob: torch.Tensor):
-    """Runs the hidden layers and the final Linear(N, 1) + sigmoid.  The head is fused into
-    the last hidden layer's epilogue when its width fits one workgroup (N <= 256)."""
+    """Runs the hidden layers and the final Linear(N, 1) + sigmoid.  Normally one fused
+    rk_mlp_forward launch; otherwise per-layer rk_linear with the head fused into the last
+    layer's epilogue when its width fits one workgroup (N <= 256)."""
     h = x
     B = x.shape[0]
     dev = x.device
     head_w = head.weight
+    if FUSED_MLP and fused_mlp_fits(x.shape[1], [l.linear.out_features for l in layers]):
+        mls = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs()) for l in layers]
+        ep = ops.make_epilogue(head_w=head_w, head_b=head.bias, head_logit=logit, head_prob=prob, **head_kwargs)
+        ops.mlp_forward(x, mls, ep)
+        return
     for i, layer in enumerate(layers):
         last = i == len(layers) - 1
         lin = layer.linear

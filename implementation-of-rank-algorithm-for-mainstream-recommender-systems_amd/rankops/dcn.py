@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import InteractionWeights, Layer, check_eval, draw_cross_layers, load_vocabulary, run_tail, \
+from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_cross_layers, load_vocabulary, run_tail, \
     table_rows
 
 
@@ -38,7 +38,7 @@ def cross_layer(x0: torch.Tensor, xl: torch.Tensor, index: int) -> torch.Tensor:
     return out
 
 
-class DCNModel(nn.Module):
+class DCNModel(EngineModule):
     def __init__(self, vocab_dir, hidden_units=[512, 256, 128], num_cross_layer=1, *, vocab_sizes=None,
                  interaction_weights="per_call"):
         super().__init__()

@@ -16,7 +16,9 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import InteractionWeights, check_eval, const, draw_residual_units, load_vocabulary, table_rows
+from . import common
+from .common import InteractionWeights, check_eval, const, draw_residual_units, fused_mlp_fits, load_vocabulary, \
+    table_rows
 
 
 def residual_unit(input_tensor, internal_dim, index, weights=None):
@@ -33,7 +35,7 @@ def residual_unit(input_tensor, internal_dim, index, weights=None):
     return out
 
 
-class DeepCrossingModel(nn.Module):
+class DeepCrossingModel(common.EngineModule):
     def __init__(self, vocab_dir, residual_internal_dim=128, residual_network_num=1, *, vocab_sizes=None,
                  interaction_weights="per_call"):
         super().__init__()
@@ -80,6 +82,15 @@ class DeepCrossingModel(nn.Module):
                     head_prob=prob)
         units = self.residual_weights.get(dev)
         I = self.residual_internal_dim
+        widths = [w for _ in units for w in (I, self.input_dim)]
+        if units and common.FUSED_MLP and fused_mlp_fits(self.input_dim, widths):
+            # all residual units + output_layer + sigmoid in one launch
+            layers = []
+            for w1, b1, w2, b2 in units:
+                layers.append(ops.make_mlp_layer(w1, common.PACKED(w1), bias=b1, act="relu"))
+                layers.append(ops.make_mlp_layer(w2, common.PACKED(w2), bias=b2, act="relu", residual=1))
+            ops.mlp_forward(x, layers, ops.make_epilogue(**head))
+            return prob, logit
         for i, (w1, b1, w2, b2) in enumerate(units):
             last = i == len(units) - 1
             h = torch.empty(B, I, device=dev, dtype=torch.float32)

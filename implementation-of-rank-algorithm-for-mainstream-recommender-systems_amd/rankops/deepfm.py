@@ -20,12 +20,12 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import Layer, check_eval, load_vocabulary, run_tail, table_rows
+from .common import EngineModule, Layer, check_eval, load_vocabulary, run_tail, table_rows
 
 WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
 
 
-class DeepFM(nn.Module):
+class DeepFM(EngineModule):
     def __init__(self, vocab_dir, embedding_dim=8, hidden_units=None, dropout_rate=0.1, batch_norm=True, *,
                  vocab_sizes=None):
         super().__init__()

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .common import InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
+from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
     table_rows
 
 FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
@@ -59,7 +59,7 @@ def din_attention(query, keys_table, seq, keys_length, is_softmax=False, weights
     return out
 
 
-class DIN(nn.Module):
+class DIN(EngineModule):
     def __init__(self, vocab_dir, hidden_units=None, activation='dice', dropout_rate=0.1, batch_norm=True,
                  use_softmax=False, l2_lambda=0.2, mini_batch_aware_regularization=True, *, vocab_sizes=None,
                  embedding_dim=16, interaction_weights="per_call"):

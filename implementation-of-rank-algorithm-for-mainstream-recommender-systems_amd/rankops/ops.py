@@ -115,9 +115,13 @@ def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, u
                                torch.cuda.current_stream(device).cuda_stream), "rk_din_attention")
 
 
+L2_WORKSPACE = 512  # RK_L2_WORKSPACE
+
+
 def row_l2norm_mean(x: torch.Tensor, col0: int, ncols: int, scale: float, out: torch.Tensor):
     lib = _lib.load()
-    check(lib.rk_row_l2norm_mean(ptr(x), x.stride(0), x.shape[0], col0, ncols, scale, ptr(out),
+    ws = torch.empty(L2_WORKSPACE, device=x.device, dtype=torch.float32)
+    check(lib.rk_row_l2norm_mean(ptr(x), x.stride(0), x.shape[0], col0, ncols, scale, ptr(ws), ptr(out),
                                  _lib.stream_of(x)), "rk_row_l2norm_mean")
     return out
 
@@ -159,6 +163,51 @@ def make_epilogue(**kw) -> Epilogue:
             v = v.data_ptr()
         setattr(ep, k, v)
     return ep
+
+
+_MLP_PTR_FIELDS = {f for f, t in _lib.MlpLayer._fields_ if t is ctypes.c_void_p}
+
+
+def pack_mlp_weight(weight: torch.Tensor) -> torch.Tensor:
+    """[n, k] nn.Linear weight -> the zero-padded [pad64(n), pad64(k)] layout rk_mlp_forward reads."""
+    lib = _lib.load()
+    n, k = weight.shape
+    rows, cols = ctypes.c_int64(), ctypes.c_int64()
+    check(lib.rk_mlp_packed_size(n, k, ctypes.byref(rows), ctypes.byref(cols)), "rk_mlp_packed_size")
+    out = torch.empty(rows.value, cols.value, device=weight.device, dtype=torch.float32)
+    w = weight.detach()
+    if w.stride(1) != 1:
+        w = w.contiguous()
+    check(lib.rk_mlp_pack_weight(w.data_ptr(), w.stride(0), n, k, out.data_ptr(), _lib.stream_of(out)),
+          "rk_mlp_pack_weight")
+    return out
+
+
+def make_mlp_layer(weight: torch.Tensor, packed: torch.Tensor, **kw) -> "_lib.MlpLayer":
+    """One fused-MLP layer: `weight` the [n, k] parameter (n is taken from it), `packed` its
+    pack_mlp_weight() image."""
+    L = _lib.MlpLayer()
+    L.w, L.ldw, L.n = packed.data_ptr(), packed.stride(0), weight.shape[0]
+    for k, v in kw.items():
+        if v is None:
+            continue
+        if k == "act" and isinstance(v, str):
+            v = ACT[v]
+        if k in _MLP_PTR_FIELDS and isinstance(v, torch.Tensor):
+            v = v.data_ptr()
+        setattr(L, k, v)
+    return L
+
+
+def mlp_forward(x: torch.Tensor, layers, head: Epilogue = None, out: torch.Tensor = None, *, K0: int = None):
+    """Whole MLP tail (all hidden layers + optional Linear(N,1)+sigmoid head) in one launch."""
+    lib = _lib.load()
+    arr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
+    K0 = x.shape[1] if K0 is None else K0
+    check(lib.rk_mlp_forward(x.data_ptr(), x.stride(0), x.shape[0], K0, arr, len(layers),
+                             ctypes.byref(head) if head is not None else None, ptr(out),
+                             out.stride(0) if out is not None else 0, _lib.stream_of(x)), "rk_mlp_forward")
+    return out
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M: int = None, K: int = None,

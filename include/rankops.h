@@ -119,6 +119,28 @@ typedef struct rk_epilogue {
   float* head_aux;
 } rk_epilogue;
 
+/* One hidden layer of a fused MLP tail (rk_mlp_forward): y = act(x.W^T + bias) with the same
+ * element-wise epilogue order as rk_epilogue; `residual` adds the input of the previous layer
+ * (DeepCrossing's ReLU(x + L2(ReLU(L1 x))), deepcrossing.py:37-41).                        */
+#define RK_MLP_MAX_LAYERS 8
+typedef struct rk_mlp_layer {
+  const float* w; /* [n, K] row-major */
+  int64_t ldw;
+  int32_t n;
+  int32_t act;
+  float slope;
+  int32_t residual;
+  const float* bias;
+  const float* pre_scale;
+  const float* pre_shift;
+  const float* act_scale;
+  const float* act_shift;
+  const float* act_alpha;
+  int32_t act_alpha_len;
+  const float* post_scale;
+  const float* post_shift;
+} rk_mlp_layer;
+
 /* ---- runtime ---- */
 int32_t rk_abi_version(void);
 const char* rk_last_error(void);
@@ -149,8 +171,11 @@ int rk_din_attention(const float* query, int64_t ld_query, const float* key_tabl
                      const float* w3, const float* b3, int32_t use_softmax, float* out,
                      int64_t ld_out, void* stream);
 
+/* out_scalar = scale * mean_r ||x[r, col0:col0+ncols]||_2, deterministic two-stage sum;
+ * workspace: RK_L2_WORKSPACE floats of device scratch.                                   */
+#define RK_L2_WORKSPACE 512
 int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols,
-                       float scale, float* out_scalar, void* stream);
+                       float scale, float* workspace, float* out_scalar, void* stream);
 
 int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                    const float* dense, int64_t ld_dense, int32_t num_dense,
@@ -167,6 +192,18 @@ int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T,
 int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_period,
               const float* w, int64_t ldw, int64_t M, int32_t N, int32_t K,
               const rk_epilogue* ep, float* y, int64_t ldy, void* stream);
+
+/* Packed layout of a fused-MLP weight: [pad64(n), pad64(k)], zero filled (rows and K padded to
+ * 64 so the kernel's loads are unconditional aligned float4s).  Pack once at load time.    */
+int rk_mlp_packed_size(int32_t n, int32_t k, int64_t* rows, int64_t* cols);
+int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k, float* out, void* stream);
+
+/* Whole MLP tail in one launch: layers[0..nlayers) on x [M, K0] (K0 <= 1024, widths <= 512;
+ * every layers[l].w packed by rk_mlp_pack_weight, ldw = pad64(K)), then the head of `head`
+ * (head_w/head_b/head_partial/fm combine/head_logit/head_prob/head_aux) when head->head_w is
+ * set, else the last activation is written to y.                                          */
+int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_mlp_layer* layers,
+                   int32_t nlayers, const rk_epilogue* head, float* y, int64_t ldy, void* stream);
 
 int rk_bn_fold(const float* mean, const float* var, const float* weight, const float* bias,
                float eps, int32_t n, float* scale, float* shift, void* stream);

@@ -227,3 +227,14 @@ def test_standalone_reference_functions():
         torch.manual_seed(13)
         got = rankops.din_attention(q.cuda(), table.cuda(), seq.cuda(), lens.cuda(), sm)
         torch.testing.assert_close(got.cpu(), expect, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [("dcn", {}), ("deepfm", {"dim": 32, "fields": FIELDS30}), ("din", {"T": 20}),
+                                  ("bst", {"T": 20}), ("deepcrossing", {"units": 2})], ids=_ids)
+def test_unfused_tail_path(case, monkeypatch):
+    """The per-layer rk_linear path (used when a tail does not fit rk_mlp_forward) stays exact."""
+    monkeypatch.setattr(rankops.common, "FUSED_MLP", False)
+    name, cfg = case
+    out, ref = run_pair(name, cfg, B=200)
+    _compare(out, ref, "unfused-" + _ids(case))
