@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-extras", action="store_true", help="skip the per-model extras")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--models", default="dcn,deepfm,bst,din_per_call")
     return ap.parse_args()
@@ -212,6 +213,52 @@ def cpu_baseline(name, model, cfg, batch, budget_s):
                       f"fp32, torch {torch.__version__} CPU)"}
 
 
+# ------------------------------------------------------------------ configs[4]: table-sharded DeepFM
+
+SHARDED_FIELDS = 30
+SHARDED_ROWS_PER_FIELD = 3_333_334  # 30 x 3,333,334 = 1.0e8 rows (second- and first-order tables)
+SHARDED_GLOBAL_BATCH = 65536
+
+
+def bench_sharded(world, rank, steps, warmup):
+    """Strong scaling: global batch 65536 split over the ranks, 1e8 embedding rows split by field.
+    Local compute runs as three captured hipGraph segments; the two RCCL all-to-alls run eagerly
+    between them (at world 1 they are plain device copies)."""
+    import helpers as H
+    from rankops.sharded import ShardedDeepFM, row_stride
+    dev = torch.device("cuda", torch.cuda.current_device())
+    fields = {f"field_{i:02d}": SHARDED_ROWS_PER_FIELD for i in range(SHARDED_FIELDS)}
+    torch.manual_seed(42)
+    with torch.device(dev):
+        model = ShardedDeepFM(fields, 32, [512, 256, 128], rank=rank, world_size=world)
+    H.randomize_eval_stats(model, 43)
+    model.eval()
+    B_l = SHARDED_GLOBAL_BATCH // world
+    rng = np.random.default_rng(5000 + rank)
+    cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l, dtype=np.int64)).to(dev) for f in fields}
+    out_i, in_i = model.index_splits(B_l)
+    out_r, in_r = model.row_splits(B_l)
+    recv_idx = torch.empty(sum(out_i), dtype=torch.int64, device=dev)
+    recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
+    g1, send = graph_of(lambda: model.pack_indices(cat))
+    g2, rows = graph_of(lambda: model.gather_local(recv_idx, world * B_l))
+    g3, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_l))
+
+    def step():
+        g1.replay()
+        model._exchange(recv_idx, send, out_i, in_i)
+        g2.replay()
+        model._exchange(recv_rows, rows.reshape(-1), out_r, in_r)
+        g3.replay()
+
+    t = max_over_ranks(world, time_replays(step, steps, warmup, world))
+    wire = B_l * SHARDED_FIELDS * (8 + 4 * row_stride(32)) * (world - 1) / world
+    return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
+            "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
+            "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
+            "scaling": "strong", "mode": "3 hipGraph segments + eager RCCL all_to_all_single"}
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank):
@@ -277,6 +324,13 @@ def main():
             del m2, inp2
             torch.cuda.empty_cache()
         result["models"] = extras
+    if not args.no_sharded:
+        torch.cuda.empty_cache()
+        try:
+            sh = bench_sharded(world, rank, args.steps, args.warmup)
+        except Exception as exc:  # reported, never fatal for the headline line
+            sh = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+        result["sharded_deepfm"] = sh
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(model_name, model.cpu(), cfg, args.batch, args.cpu_seconds)
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)

@@ -1,0 +1,204 @@
+"""Table-sharded DeepFM across the GPUs of one node (BASELINE configs[4]: 1e8 embedding rows,
+global batch 65536) — embedding lookup exchanged with two RCCL all-to-alls over xGMI.
+
+Layout: table-wise sharding.  Field f (in DeepFM field order) lives on rank f % P with both its
+second-order [V_f, D] and first-order [V_f, 1] tables; the dense layers are replicated.  Each
+rank holds a data-parallel slice of B_l samples with the indices of all F fields.  One forward:
+
+  1. index exchange   all_to_all_single: rank r receives, from every source s, the indices of
+                      r's fields for s's samples, laid out [s][b][f_r] (int64)
+  2. local gather     rk_concat_gather on r's tables -> rows [s][b][f_r][RS] with the D
+                      second-order floats at 0..D-1 and the first-order weight at D
+                      (RS = D + 1 rounded up to 4 floats so every row stays 16-B aligned)
+  3. row exchange     all_to_all_single back: each source gets [r][b][f_r][RS] from every owner
+  4. FM + MLP         rk_fm_gather over the received rows (dense segments, field order restored
+                      through out_col = f * D), then the fused MLP tail exactly as DeepFM
+
+At P = 1 both exchanges are skipped and the path equals `DeepFM.forward` on the same weights.
+The exchange volume per rank and step is B_l * F * (8 + 4 * RS) bytes, (P-1)/P of it on the
+wire.  Reference: DeepFM.forward, deepfm.py:121-151 (the reference is single-device; the
+sharding is the MI355X build's own).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import ops
+from .common import EngineModule, Layer, check_eval, run_tail
+
+
+def row_stride(dim: int) -> int:
+    return (dim + 1 + 3) // 4 * 4
+
+
+def field_owner(num_fields: int, world: int):
+    """Field index -> owning rank (round robin: 30 fields on 8 ranks = 4/4/4/4/4/4/3/3)."""
+    return [f % world for f in range(num_fields)]
+
+
+class ShardedDeepFM(EngineModule):
+    def __init__(self, field_rows: dict, embedding_dim=32, hidden_units=None, dropout_rate=0.1, batch_norm=True,
+                 *, group=None, rank: int = None, world_size: int = None):
+        super().__init__()
+        if hidden_units is None:
+            hidden_units = [512, 256, 128]
+        self.group = group
+        if world_size is None:
+            world_size = dist.get_world_size(group) if dist.is_initialized() else 1
+        if rank is None:
+            rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.rank, self.world = rank, world_size
+        self.fields = list(field_rows)
+        self.field_rows = dict(field_rows)
+        self.embedding_dim = embedding_dim
+        self.owner = field_owner(len(self.fields), world_size)
+        self.fields_of = [[f for i, f in enumerate(self.fields) if self.owner[i] == r] for r in range(world_size)]
+        self.local_fields = self.fields_of[rank]
+        self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
+                                                     for f in self.local_fields})
+        self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
+                                                      for f in self.local_fields})
+        self.deep_layers = nn.ModuleList()
+        self._tail = []
+        width = len(self.fields) * embedding_dim
+        for unit in hidden_units:
+            lin = nn.Linear(width, unit)
+            self.deep_layers.append(lin)
+            bn = None
+            if batch_norm:
+                bn = nn.BatchNorm1d(unit)
+                self.deep_layers.append(bn)
+            self.deep_layers.append(nn.ReLU())
+            if dropout_rate > 0:
+                self.deep_layers.append(nn.Dropout(dropout_rate))
+            self._tail.append(Layer(lin, pre_bn=bn, act="relu"))
+            width = unit
+        self.deep_output_layer = nn.Linear(width, 1)
+        self.final_layer = nn.Linear(3, 1)
+
+    @classmethod
+    def from_deepfm(cls, model, *, group=None, rank=None, world_size=None):
+        """Shard a full DeepFM's parameters: this rank keeps its fields' tables and all dense layers."""
+        rows = {f: e.num_embeddings for f, e in model.second_order_embeddings.items()}
+        hidden = [l.out_features for l in model.deep_layers if isinstance(l, nn.Linear)]
+        bn = any(isinstance(l, nn.BatchNorm1d) for l in model.deep_layers)
+        drop = any(isinstance(l, nn.Dropout) for l in model.deep_layers)
+        with torch.device("meta"):
+            sh = cls(rows, model.embedding_dim, hidden, 0.1 if drop else 0.0, bn, group=group, rank=rank,
+                     world_size=world_size)
+        sd = model.state_dict()
+        mine = {k: v for k, v in sd.items()
+                if not k.startswith(("first_order_embeddings.", "second_order_embeddings."))
+                or k.split(".")[1] in sh.local_fields}
+        sh = sh.to_empty(device=next(model.parameters()).device)
+        sh.load_state_dict(mine, strict=True)
+        return sh.eval()
+
+    # ------------------------------------------------------------------ exchange steps
+
+    def _exchange(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+        if self.world == 1:
+            out.copy_(inp)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        return out
+
+    def index_splits(self, B_l: int):
+        """(output_split_sizes, input_split_sizes) of the index all-to-all, in int64 elements."""
+        F_me = len(self.local_fields)
+        return [B_l * F_me] * self.world, [B_l * len(self.fields_of[r]) for r in range(self.world)]
+
+    def row_splits(self, B_l: int):
+        """(output_split_sizes, input_split_sizes) of the row all-to-all, in floats."""
+        RS, F_me = row_stride(self.embedding_dim), len(self.local_fields)
+        return [B_l * len(self.fields_of[r]) * RS for r in range(self.world)], [B_l * F_me * RS] * self.world
+
+    def pack_indices(self, category: dict) -> torch.Tensor:
+        """Send buffer of step 1: [r][b][f_r] index blocks (a small int64 permute)."""
+        blocks = []
+        for r in range(self.world):
+            fr = self.fields_of[r]
+            if fr:
+                blocks.append(torch.stack([category[f] for f in fr], 1).reshape(-1))
+        return torch.cat(blocks) if blocks else torch.empty(0, dtype=torch.int64, device=self._device())
+
+    def exchange_indices(self, category: dict, B_l: int) -> torch.Tensor:
+        """Step 1: send [r][b][f_r] index blocks; receive [s][b][f_me]."""
+        send = self.pack_indices(category)
+        out_s, in_s = self.index_splits(B_l)
+        recv = torch.empty(sum(out_s), dtype=torch.int64, device=send.device)
+        return self._exchange(recv, send, out_s, in_s)
+
+    def gather_local(self, recv_idx: torch.Tensor, rows_total: int) -> torch.Tensor:
+        """Step 2: rows [s*B_l + b][f_me][RS] from this rank's tables (rk_concat_gather)."""
+        D, RS, F_me = self.embedding_dim, row_stride(self.embedding_dim), len(self.local_fields)
+        out = torch.empty(rows_total, F_me * RS, device=recv_idx.device, dtype=torch.float32)
+        if F_me == 0 or rows_total == 0:
+            return out
+        second, first = [], []
+        for j, f in enumerate(self.local_fields):
+            idx = recv_idx[j:]  # element (R, j) sits at R * F_me + j
+            second.append(ops.table_segment(self.second_order_embeddings[f].weight, idx, j * RS, idx_stride=F_me))
+            first.append(ops.table_segment(self.first_order_embeddings[f].weight, idx, j * RS + D, idx_stride=F_me))
+        ops.concat_gather(second, rows_total, out)  # 16-B rows: vectorised path
+        ops.concat_gather(first, rows_total, out)
+        return out
+
+    def exchange_rows(self, rows: torch.Tensor, B_l: int) -> torch.Tensor:
+        """Step 3: send [s][b][f_me][RS] back to every source; receive [r][b][f_r][RS]."""
+        out_s, in_s = self.row_splits(B_l)
+        recv = torch.empty(sum(out_s), device=rows.device, dtype=torch.float32)
+        return self._exchange(recv, rows.reshape(-1), out_s, in_s)
+
+    def fm_and_tail(self, recv_rows: torch.Tensor, B_l: int):
+        """Step 4: FM + deep tail on the received rows (field order restored by out_col)."""
+        D, RS = self.embedding_dim, row_stride(self.embedding_dim)
+        dev = recv_rows.device
+        second, first = [], []
+        off = 0
+        base = {}
+        for r in range(self.world):
+            for j, f in enumerate(self.fields_of[r]):
+                base[f] = (off + j * RS, len(self.fields_of[r]) * RS)
+            off += B_l * len(self.fields_of[r]) * RS
+        for i, f in enumerate(self.fields):
+            o, ld = base[f]
+            second.append(_lib_dense(recv_rows, o, ld, D, i * D))
+            first.append(_lib_dense(recv_rows, o + D, ld, 1, i))
+        deep_in = torch.empty(B_l, len(self.fields) * D, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        ops.fm_gather(second, first, D, B_l, deep_in, fm1, fm2)
+        deep = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        total = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        run_tail(deep_in, self._tail, self.deep_output_layer,
+                 dict(fm1=fm1, fm2=fm2, final_w=self.final_layer.weight, final_b=self.final_layer.bias,
+                      head_aux=deep), total, prob)
+        return prob, total, fm1, fm2, deep
+
+    def _device(self):
+        return self.deep_output_layer.weight.device
+
+    def forward(self, category: dict):
+        """category: {field: [B_l] int64} for every field, this rank's samples."""
+        check_eval(self)
+        missing = [f for f in self.fields if f not in category]
+        if missing:
+            raise KeyError(f"ShardedDeepFM.forward: category features missing: {missing}")
+        cat = {f: ops.as_index(category[f], f"category[{f!r}]") for f in self.fields}
+        return self.run_steps(cat)
+
+    def run_steps(self, cat: dict):
+        B_l = cat[self.fields[0]].shape[0]
+        recv_idx = self.exchange_indices(cat, B_l)
+        rows = self.gather_local(recv_idx, self.world * B_l)
+        recv_rows = self.exchange_rows(rows, B_l)
+        return self.fm_and_tail(recv_rows, B_l)
+
+
+def _lib_dense(buf: torch.Tensor, offset: int, ld: int, dim: int, out_col: int):
+    from ._lib import Segment
+    return Segment(buf.data_ptr() + offset * 4, None, 0, ld, 0, dim, out_col)
