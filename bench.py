@@ -40,6 +40,10 @@ METRIC = "forward samples/sec at batch 4096 (DCN, DIN, BST) on 1/2/4/8 MI355X"
 
 # Algorithmic work per sample
 DIN_ATT_FLOP = 2 * 50 * (128 * 64 + 64 * 32 + 32)  # 1,028,200: att-MLP of din_attention, T=50, H=32
+DIN_FWD_FLOP = DIN_ATT_FLOP + 6_400 + 444_672       # whole DIN forward, reference formulation
+# what din_forward_kernel<32> issues per sample: split layer 1 (K=H) + layer 2 + layer 3 over 64 padded
+# positions, the per-sample bias u, and the fcn at padded widths (128->512->256->128)
+DIN_FWD_EXEC_FLOP = 2 * 64 * (32 * 64 + 64 * 32 + 32) + 2 * 64 * 32 + 2 * (128 * 512 + 512 * 256 + 256 * 128)
 DEEPFM_GATHER_BYTES = 30 * (8 + 128 + 4) + 30 * 128 + 8  # 8,048 B: gather+FM kernel
 BST_BLOCK_FLOP = 14_680_064
 DCN_FLOP = 379_236
@@ -157,26 +161,7 @@ def kernel_avg_ms(launch, iters=50):
     return start.elapsed_time(end) / iters
 
 
-# ------------------------------------------------------------------ dominant-kernel launchers
-
-def din_attention_launcher(model, inp):
-    """Re-launch exactly the forward's rk_din_attention call (same buffers, same stream)."""
-    from rankops import ops
-    from rankops.din import SEQ_KEY
-    B = inp["target"]["feedid"].shape[0]
-    dev = inp["target"]["feedid"].device
-    H = model.embeddings["feedid"].embedding_dim
-    width = 16 + 34 + 2 * H
-    row = torch.randn(B, width, device=dev)
-    seq = inp["sequence"][SEQ_KEY].contiguous()
-    lens = inp["sequence"][f"{SEQ_KEY}_length"]
-    w = model.att_weights.get(dev)
-
-    def launch():
-        ops.din_attention(ops._lib.fptr(row, 50), width, model.embeddings[SEQ_KEY].weight, seq, lens, seq.shape[1], H,
-                          w, model.use_softmax, ops._lib.fptr(row, 50 + H), width, B, dev)
-    return launch
-
+# ------------------------------------------------------------------ PMC traffic (profiles/traffic.json)
 
 def load_traffic(kernel: str, workload_name: str):
     path = os.path.join(REPO, "profiles", "traffic.json")
@@ -304,15 +289,18 @@ def main():
                    "interaction_weights": "frozen", "parallelism": f"replicas x{world}"},
     }
     if rank == 0:
-        launch = din_attention_launcher(model, inp)
+        launch = model.fused_kernel_launcher(inp["dense"], inp["category"], inp["sequence"], inp["target"])
         ms = kernel_avg_ms(launch)
-        flop = DIN_ATT_FLOP * args.batch
+        flop = DIN_FWD_FLOP * args.batch
         achieved = flop / (ms * 1e-3)
-        result["roofline"] = {"kernel": "din_attention_kernel<32>", "bound": "mfma",
+        result["roofline"] = {"kernel": "din_forward_kernel<32>", "bound": "mfma",
                               "achieved": round(achieved / 1e12, 3), "peak": PEAK_FP32_MFMA / 1e12,
                               "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
                               "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
-                              "traffic": load_traffic("din_attention_kernel", "din")}
+                              "flop_basis": "reference formulation per sample: att-MLP 1,028,200 + cross/"
+                                            "weighted sum 6,400 + fcn 444,672 (SURVEY §8d)",
+                              "executed_flop_per_launch": DIN_FWD_EXEC_FLOP * args.batch,
+                              "traffic": load_traffic("din_forward_kernel", "din")}
     if rank == 0 and world == 1 and not args.no_extras:
         extras = {}
         for name in [m for m in args.models.split(",") if m]:

@@ -24,6 +24,8 @@ int check_launch(const char* what);
 uint32_t* device_flags();
 // Number of CUs on the current device (cached).
 int num_cus();
+// out[0] = scale * (sum of part[0..n)) / rows, one wave, fixed order (embedding.hip).
+int launch_l2_final(const float* part, int n, int64_t rows, float scale, float* out, hipStream_t st);
 
 // ---- device helpers ----
 __device__ __forceinline__ float wave_sum(float v) {

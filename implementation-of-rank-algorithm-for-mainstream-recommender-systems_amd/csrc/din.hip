@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void din_attention_kernel(
     for (int c = 0; c < NQ; ++c) o[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     for (int tt = 0; tt < ntiles; ++tt) {
+      asm volatile("" ::: "memory");  // keep the loop-invariant LDS weight reads inside the loop
       const int t = tt * 32 + l32;
       const bool in_seq = t < T;
       f32x4 k[NQ];

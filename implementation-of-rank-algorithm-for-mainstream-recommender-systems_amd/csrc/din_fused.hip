@@ -1,0 +1,337 @@
+// Whole DIN eval forward in one launch (reference: DIN.forward din.py:294-323 with
+// din_attention din.py:42-84, Dice din.py:26-36 and the fcn stack din.py:272-285).
+//
+// A workgroup of 16 waves owns 16 samples.
+//  Phase A (one wave per sample):
+//   * gather the sample's feature row [dense | category embeddings | target feed] into LDS
+//     (the rk_concat_gather column map, built once per workgroup);
+//   * local-activation attention with the first att-MLP layer split algebraically:
+//       cross.W1^T = q.(W1a+W1c)^T + k.(W1b-W1c + diag(q) W1d)^T
+//     u = q.(W1a+W1c)^T + b1 is a per-sample bias (64 values, one per lane), and the MFMA A
+//     operand Weff[j][h] = (W1b-W1c)[j][h] + W1d[j][h]*q[h] is formed on the fly from two LDS
+//     rows and the query — layer 1 contracts over H instead of 4H (4x fewer MFMAs than the
+//     reference formulation); layers 2/3, the mask, the online softmax and the weighted key sum
+//     are those of din_attention_kernel (din.hip);
+//   * the attention output goes into the LDS row; the row's l2 norm (din.py:318-322) is taken.
+//  Phase B: the fcn tail + output layer + sigmoid over the 16 LDS rows (mlp_core.h).
+// The l2 term is finished by a one-wave reduction over the per-workgroup partial sums.
+#include "mlp_core.h"
+
+namespace rk {
+
+constexpr int kDinSegs = 32;
+struct DinSegs {
+  rk_segment s[kDinSegs];
+};
+
+struct DinArgs {
+  DinSegs segs;
+  int nseg, width, q_col, att_col, l2_col0;
+  const float* key_table;
+  int64_t key_rows, ld_key;
+  const int64_t* seq;
+  int64_t ld_seq;
+  int T;
+  const int64_t* seq_len;
+  int64_t batch;
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+  int use_softmax;
+  float* l2_part;
+  uint32_t* flags;
+  rk_mlp_layer L[RK_MLP_MAX_LAYERS];
+  int nl;
+  rk_epilogue head;
+  int ld0, ld1;
+};
+
+// LDS carve (floats): [Wk | Wqk | Wq] 3 x 64 x (H+4), W2 32 x 68, b1 64, b2 32, w3 32,
+// u 16 x 64, norms 16, then buf0 16 x ld0, buf1 16 x ld1; column map after that (bytes).
+template <int H>
+struct DinLds {
+  static constexpr int LDH = H + 4;
+  static constexpr int WK = 0, WQK = WK + 64 * LDH, WQ = WQK + 64 * LDH, W2 = WQ + 64 * LDH;
+  static constexpr int B1 = W2 + 32 * 68, B2 = B1 + 64, W3 = B2 + 32, U = W3 + 32, NORM = U + 16 * 64;
+  static constexpr int BUF0 = NORM + 16;
+};
+
+template <int H>
+__global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
+  using Ly = DinLds<H>;
+  constexpr int NQ = H / 8;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* const buf0 = sm + Ly::BUF0;
+  float* const buf1 = buf0 + kMlpRows * a.ld0;
+  uint8_t* const col_seg = reinterpret_cast<uint8_t*>(buf1 + kMlpRows * a.ld1);
+  uint8_t* const col_off = col_seg + 256;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, half = lane >> 5, hk = 4 * half;
+
+  // ---- stage the split attention weights and the column map
+  for (int i = tid; i < 64 * H; i += kMlpThreads) {
+    const int j = i / H, h = i % H;
+    const float* r = a.w1 + (int64_t)j * 4 * H;
+    sm[Ly::WQ + j * Ly::LDH + h] = r[h] + r[2 * H + h];
+    sm[Ly::WK + j * Ly::LDH + h] = r[H + h] - r[2 * H + h];
+    sm[Ly::WQK + j * Ly::LDH + h] = r[3 * H + h];
+  }
+  for (int i = tid; i < 32 * 64; i += kMlpThreads) sm[Ly::W2 + (i / 64) * 68 + (i % 64)] = a.w2[i];
+  if (tid < 64) sm[Ly::B1 + tid] = a.b1[tid];
+  if (tid < 32) {
+    sm[Ly::B2 + tid] = a.b2[tid];
+    sm[Ly::W3 + tid] = a.w3[tid];
+  }
+  for (int c = tid; c < a.width; c += kMlpThreads) {
+    uint8_t hit = 255, off = 0;
+    for (int s = 0; s < a.nseg; ++s)
+      if (c >= a.segs.s[s].out_col && c < a.segs.s[s].out_col + a.segs.s[s].dim) {
+        hit = (uint8_t)s;
+        off = (uint8_t)(c - a.segs.s[s].out_col);
+      }
+    col_seg[c] = hit;
+    col_off[c] = off;
+  }
+  __syncthreads();
+
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
+  const int64_t b = m0 + wave;
+  const bool live = wave < rows;
+  float* row = buf0 + wave * a.ld0;
+  uint32_t* flags = a.flags;
+
+  // ---- Phase A.1: the feature row (zero padded to pad64(width))
+  const int wp = pad64(a.width);
+  for (int c = lane; c < wp; c += 64) {
+    float v = 0.f;
+    if (live && c < a.width) {
+      const int s = col_seg[c];
+      if (s != 255) {
+        const float* src = segment_row(a.segs.s[s], b, flags);
+        if (src) v = src[col_off[c]];
+      }
+    }
+    row[c] = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+
+  float norm_part = 0.f;
+  if (live) {
+    // ---- Phase A.2: per-sample bias u[j] = b1[j] + q . Wq[j]   (lane j)
+    {
+      float u = sm[Ly::B1 + lane];
+      const float* wq = sm + Ly::WQ + lane * Ly::LDH;
+      const float* q = row + a.q_col;
+#pragma unroll
+      for (int h = 0; h < H; ++h) u = fmaf(q[h], wq[h], u);
+      sm[Ly::U + wave * 64 + lane] = u;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+
+    const int64_t len = a.seq_len[b];
+    const float sqrt_h = (float)__builtin_sqrt((double)H);
+    const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
+    float m_run = -INFINITY, l_run = 0.f;
+    f32x4_t o[NQ];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) o[c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int ntiles = (a.T + 31) / 32;
+
+    for (int tt = 0; tt < ntiles; ++tt) {
+      // the weight/bias LDS reads below are loop-invariant; hoisting them out of the tile loop
+      // costs ~96 VGPRs and spills at the 128-register budget of a 16-wave workgroup
+      asm volatile("" ::: "memory");
+      const int t = tt * 32 + l32;
+      const bool in_seq = t < a.T;
+      const float* krow = nullptr;
+      if (in_seq) {
+        const int64_t r = a.seq[b * a.ld_seq + t];
+        if (r >= 0 && r < a.key_rows)
+          krow = a.key_table + r * a.ld_key;
+        else
+          flag_oob(flags);
+      }
+      f32x4_t k[NQ];
+#pragma unroll
+      for (int c = 0; c < NQ; ++c)
+        k[c] = krow ? *reinterpret_cast<const f32x4_t*>(krow + 8 * c + hk) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+      // layer 1 (transposed) one 32-row block jt at a time, each folded straight into layer 2
+      // (acc2 = W2 . h1^T with the layer-1 accumulator as the B operand): one layer-1
+      // accumulator is live at a time.
+      f32x16 acc2;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        f32x16 acc1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
+        const int j = jt * 32 + l32;
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+          const f32x4_t wk = *reinterpret_cast<const f32x4_t*>(sm + Ly::WK + j * Ly::LDH + 8 * c + hk);
+          const f32x4_t wqk = *reinterpret_cast<const f32x4_t*>(sm + Ly::WQK + j * Ly::LDH + 8 * c + hk);
+          f32x4_t qc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) qc[e] = row[a.q_col + 8 * c + hk + e];
+          const f32x4_t weff = wk + wqk * qc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc1 = mfma32(weff[e], k[c][e], acc1);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float z = acc1[r] + sm[Ly::U + wave * 64 + jt * 32 + acc_row(r, lane)];
+          acc1[r] = z < 0.f ? 0.f : z;
+        }
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) {
+          const f32x4_t av = *reinterpret_cast<const f32x4_t*>(sm + Ly::W2 + l32 * 68 + jt * 32 + 8 * uu + hk);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc2 = mfma32(av[v], acc1[4 * uu + v], acc2);
+        }
+      }
+      // layer 3: score[t]
+      float sc = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j2 = acc_row(r, lane);
+        float z = acc2[r] + sm[Ly::B2 + j2];
+        z = z < 0.f ? 0.f : z;
+        sc = fmaf(z, sm[Ly::W3 + j2], sc);
+      }
+      sc += __shfl_xor(sc, 32, kWave);
+      sc = sc + a.b3[0];
+
+      const bool valid = in_seq && (int64_t)t < len;
+      if (a.use_softmax) {
+        const float s = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
+        const float m_new = fmaxf(m_run, wave_max(s));
+        const float scale_old = expf(m_run - m_new);
+        const float p = in_seq ? expf(s - m_new) : 0.f;
+        l_run = l_run * scale_old + wave_sum(half == 0 ? p : 0.f);
+        m_run = m_new;
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) o[c] = o[c] * scale_old + p * k[c];
+      } else {
+        const float w = valid ? sc : 0.f;
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) o[c] = o[c] + w * k[c];
+      }
+    }
+    const float inv_l = a.use_softmax ? 1.0f / l_run : 1.0f;
+#pragma unroll
+    for (int c = 0; c < NQ; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = half_sum(o[c][e]);
+        if (l32 == 4 * c + e) row[a.att_col + 8 * c + hk + e] = a.use_softmax ? v * inv_l : v;
+      }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (a.l2_part) {
+      float ss = 0.f;
+      for (int c = a.l2_col0 + lane; c < a.width; c += 64) ss = fmaf(row[c], row[c], ss);
+      norm_part = sqrtf(wave_sum(ss));
+    }
+  }
+  if (lane == 0) sm[Ly::NORM + wave] = norm_part;
+  __syncthreads();
+  if (a.l2_part && tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kMlpRows; ++w) t += sm[Ly::NORM + w];
+    a.l2_part[blockIdx.x] = t;
+  }
+
+  // ---- Phase B: fcn tail + head over the 16 rows
+  mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid);
+}
+
+}  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
+                          const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
+                          int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
+                          const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                          const float* b3, int32_t use_softmax, const rk_mlp_layer* layers, int32_t nlayers,
+                          const rk_epilogue* head, int32_t l2_col0, float l2_scale, float* l2_workspace,
+                          float* l2_out, void* stream) {
+  if (!row_segs || nseg <= 0 || nseg > kDinSegs)
+    return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %d row segments (max %d)", nseg, kDinSegs);
+  if (!key_table || !seq || !seq_len || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !head || !head->head_w)
+    return fail(RK_ERR_INVALID, "rk_din_forward: null pointer");
+  if (H != 8 && H != 16 && H != 32)
+    return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: embedding dim %d not in {8,16,32}", H);
+  if (width <= 0 || width > 255 || q_col < 0 || q_col + H > width || att_col < 0 || att_col + H > width ||
+      T <= 0 || ld_seq < T || key_rows <= 0 || ld_key < H || ld_key % 4 || ((uintptr_t)key_table & 15u))
+    return fail(RK_ERR_INVALID, "rk_din_forward: bad row/sequence layout (width=%d T=%d H=%d)", width, T, H);
+  if (l2_out && (!l2_workspace || l2_col0 < 0 || l2_col0 >= width))
+    return fail(RK_ERR_INVALID, "rk_din_forward: l2 term needs a workspace of ceil(batch/16) floats");
+  DinArgs a = {};
+  for (int s = 0; s < nseg; ++s) {
+    const rk_segment& g = row_segs[s];
+    if (!g.src || g.dim <= 0 || g.out_col < 0 || g.out_col + g.dim > width || g.dim > 255 || (g.idx && g.rows <= 0))
+      return fail(RK_ERR_INVALID, "rk_din_forward: row segment %d invalid", s);
+    a.segs.s[s] = g;
+  }
+  a.head = *head;
+  int need0 = 0, need1 = 0;
+  if (int e = mlp_validate(layers, nlayers, width, a.head, &need0, &need1, "rk_din_forward")) return e;
+  for (int l = 0; l < nlayers; ++l) a.L[l] = layers[l];
+  a.nl = nlayers;
+  a.nseg = nseg;
+  a.width = width;
+  a.q_col = q_col;
+  a.att_col = att_col;
+  a.l2_col0 = l2_col0;
+  a.key_table = key_table;
+  a.key_rows = key_rows;
+  a.ld_key = ld_key;
+  a.seq = seq;
+  a.ld_seq = ld_seq;
+  a.T = T;
+  a.seq_len = seq_len;
+  a.batch = batch;
+  a.w1 = w1;
+  a.b1 = b1;
+  a.w2 = w2;
+  a.b2 = b2;
+  a.w3 = w3;
+  a.b3 = b3;
+  a.use_softmax = use_softmax;
+  a.l2_part = l2_out ? l2_workspace : nullptr;
+  a.flags = device_flags();
+  a.ld0 = need0 + 4;
+  a.ld1 = need1 + 4;
+  if (batch < 0) return fail(RK_ERR_INVALID, "rk_din_forward: negative batch");
+  if (batch == 0) return RK_OK;
+  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  size_t base = 0;
+  switch (H) {
+    case 8: base = DinLds<8>::BUF0; break;
+    case 16: base = DinLds<16>::BUF0; break;
+    default: base = DinLds<32>::BUF0; break;
+  }
+  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + 512;
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
+  hipStream_t st = (hipStream_t)stream;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)din_forward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)din_forward_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)din_forward_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  switch (H) {
+    case 8: din_forward_kernel<8><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
+    case 16: din_forward_kernel<16><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
+    default: din_forward_kernel<32><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
+  }
+  if (int e = check_launch("rk_din_forward")) return e;
+  if (l2_out) return launch_l2_final(l2_workspace, (int)blocks, batch, l2_scale, l2_out, st);
+  return RK_OK;
+}

@@ -277,6 +277,11 @@ __global__ void bn_fold_kernel(const float* __restrict__ mean, const float* __re
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+int launch_l2_final(const float* part, int n, int64_t rows, float scale, float* out, hipStream_t st) {
+  row_l2norm_final_kernel<<<1, 64, 0, st>>>(part, n, rows, scale, out);
+  return check_launch("l2 final");
+}
+
 static int check_segments(const rk_segment* segs, int nseg, const char* what) {
   if (!segs || nseg <= 0 || nseg > RK_MAX_SEGMENTS) return fail(RK_ERR_INVALID, "%s: bad segment count %d", what, nseg);
   for (int i = 0; i < nseg; ++i) {

@@ -135,6 +135,11 @@ SIGNATURES = {
         [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, _EPI_P, c_void_p,
          c_int64, c_void_p],
     ),
+    "rk_din_forward": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
+         c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
+         c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
     "rk_mlp_packed_size": (ctypes.c_int, [c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_mlp_forward": (

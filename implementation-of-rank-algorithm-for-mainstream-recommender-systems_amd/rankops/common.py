@@ -215,6 +215,7 @@ class Layer:
 
 
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
+FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
 
 
 def _pad64(v: int) -> int:

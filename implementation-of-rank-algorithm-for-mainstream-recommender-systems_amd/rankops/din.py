@@ -20,7 +20,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import common, ops
+from .common import PACKED, fused_mlp_fits
 from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
     table_rows
 
@@ -115,8 +116,8 @@ class DIN(EngineModule):
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
 
-    def forward(self, dense, category, sequence, target):
-        check_eval(self)
+    def _plan(self, dense, category, sequence, target):
+        """Row layout [dense | category | target | attention] and the gather segments (din.py:296-310)."""
         dense_cols = [ops.as_f32(v, f"dense[{k!r}]") for k, v in dense.items()]
         B = dense_cols[0].shape[0]
         dev = dense_cols[0].device
@@ -128,7 +129,6 @@ class DIN(EngineModule):
                 idx = ops.as_index(category[name], f"category[{name!r}]")
                 segs.append(ops.table_segment(emb.weight, idx, col))
                 col += emb.embedding_dim
-        cat_dim = col - cat_col0
         tgt_emb = self.embeddings["feedid"]
         H = tgt_emb.embedding_dim
         tgt_idx = ops.as_index(target["feedid"], "target['feedid']")
@@ -136,22 +136,61 @@ class DIN(EngineModule):
         q_col = col
         att_col = q_col + H
         width = att_col + self.embeddings[SEQ_KEY].embedding_dim
-        row = torch.empty(B, width, device=dev, dtype=torch.float32)
-        ops.concat_gather(segs, B, row)
-
         seq = ops.as_index(sequence[SEQ_KEY], f"sequence[{SEQ_KEY!r}]").contiguous()
         seq_len = ops.as_index(sequence[f"{SEQ_KEY}_length"], "sequence length")
+        fused = (common.FUSED_DIN and H in (8, 16, 32) and width <= 255 and len(segs) <= 32
+                 and self.embeddings[SEQ_KEY].embedding_dim == H
+                 and fused_mlp_fits(width, [l.linear.out_features for l in self._tail]))
+        return dict(B=B, dev=dev, segs=segs, cat_col0=cat_col0, q_col=q_col, att_col=att_col, width=width, H=H,
+                    seq=seq, seq_len=seq_len, fused=fused, keep=(dense_cols, category, target))
+
+    def _launch_fused(self, pl, w, logit, prob, l2_reg):
+        layers = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs())
+                  for l in self._tail]
+        head = ops.make_epilogue(head_w=self.output_layer.weight, head_b=self.output_layer.bias,
+                                 head_logit=logit, head_prob=prob)
+        ops.din_forward(pl["segs"], pl["width"], pl["q_col"], pl["att_col"], self.embeddings[SEQ_KEY].weight,
+                        pl["seq"], pl["seq_len"], pl["H"], w, self.use_softmax, layers, head, pl["B"], pl["dev"],
+                        l2_col0=pl["cat_col0"], l2_scale=float(self.l2_lambda),
+                        l2_out=l2_reg if isinstance(l2_reg, torch.Tensor) else None)
+
+    def fused_kernel_launcher(self, dense, category, sequence, target):
+        """Zero-argument re-launch of this forward's rk_din_forward kernel (no l2 finish), for
+        kernel-level timing (bench.py roofline)."""
+        pl = self._plan(dense, category, sequence, target)
+        if not pl["fused"]:
+            raise RuntimeError("DIN configuration outside rk_din_forward's envelope")
+        w = self.att_weights.get(pl["dev"])
+        logit = torch.empty(pl["B"], 1, device=pl["dev"])
+        prob = torch.empty_like(logit)
+        return lambda: self._launch_fused(pl, w, logit, prob, None)
+
+    def forward(self, dense, category, sequence, target):
+        check_eval(self)
+        pl = self._plan(dense, category, sequence, target)
+        B, dev, segs, H = pl["B"], pl["dev"], pl["segs"], pl["H"]
+        cat_col0, q_col, att_col, width = pl["cat_col0"], pl["q_col"], pl["att_col"], pl["width"]
+        seq, seq_len = pl["seq"], pl["seq_len"]
         T = seq.shape[1]
         w = self.att_weights.get(dev)
-        ops.din_attention(ops._lib.fptr(row, q_col), width, self.embeddings[SEQ_KEY].weight, seq, seq_len, T, H, w,
-                          self.use_softmax, ops._lib.fptr(row, att_col), width, B, dev)
-
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        want_l2 = self.mini_batch_aware_regularization and self.l2_lambda > 0
+
+        if pl["fused"]:
+            # the whole forward in one launch (rk_din_forward)
+            l2_reg = torch.empty((), device=dev, dtype=torch.float32) if want_l2 else 0.0
+            self._launch_fused(pl, w, logit, prob, l2_reg)
+            return prob, logit, l2_reg
+
+        row = torch.empty(B, width, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, row)
+        ops.din_attention(ops._lib.fptr(row, q_col), width, self.embeddings[SEQ_KEY].weight, seq, seq_len, T, H, w,
+                          self.use_softmax, ops._lib.fptr(row, att_col), width, B, dev)
         run_tail(row, self._tail, self.output_layer, {}, logit, prob)
 
         l2_reg = 0.0
-        if self.mini_batch_aware_regularization and self.l2_lambda > 0:
+        if want_l2:
             l2_reg = torch.empty((), device=dev, dtype=torch.float32)
             ops.row_l2norm_mean(row, cat_col0, width - cat_col0, float(self.l2_lambda), l2_reg)
         return prob, logit, l2_reg

@@ -210,6 +210,24 @@ def mlp_forward(x: torch.Tensor, layers, head: Epilogue = None, out: torch.Tenso
     return out
 
 
+def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
+                head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None):
+    """Whole DIN eval forward (row gather, attention, fcn tail, head, l2 partials) in one launch."""
+    lib = _lib.load()
+    _lib.ensure_device(device)
+    w1, b1, w2, b2, w3, b3 = att_weights
+    arr = _seg_array(segs)
+    larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
+    ws = None
+    if l2_out is not None:
+        ws = torch.empty((batch + 15) // 16, device=device, dtype=torch.float32)
+    check(lib.rk_din_forward(arr, len(segs), width, q_col, att_col, ptr(key_table), key_table.shape[0],
+                             key_table.stride(0), ptr(seq), seq.stride(0), seq.shape[1], ptr(seq_len), batch, H,
+                             ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3), ptr(b3), 1 if use_softmax else 0, larr,
+                             len(layers), ctypes.byref(head), l2_col0, float(l2_scale), ptr(ws), ptr(l2_out),
+                             torch.cuda.current_stream(device).cuda_stream), "rk_din_forward")
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M: int = None, K: int = None,
            x_ptr: int = None, ldx: int = None, x_periodic: torch.Tensor = None, x_period: int = 0,
            y_ptr: int = None, ldy: int = None, epilogue: Epilogue = None):

@@ -177,6 +177,21 @@ int rk_din_attention(const float* query, int64_t ld_query, const float* key_tabl
 int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols,
                        float scale, float* workspace, float* out_scalar, void* stream);
 
+/* Whole DIN eval forward (din.py:294-323) in one launch + a one-wave l2 finish:
+ *   row[b] = concat(row_segs)  (width <= 255; target query at q_col, attention written at att_col)
+ *   row[b, att_col:+H] = din_attention(row[b, q_col:+H], key_table[seq[b]], seq_len[b])
+ *   head outputs = fcn layers (rk_mlp_layer, packed) + head (head_w/head_b/head_logit/head_prob)
+ *   l2_out = l2_scale * mean_b ||row[b, l2_col0:width]||_2 when l2_out != NULL
+ *     (l2_workspace: ceil(batch/16) floats).  H in {8, 16, 32}.                            */
+int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col,
+                   int32_t att_col, const float* key_table, int64_t key_rows, int64_t ld_key,
+                   const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
+                   int64_t batch, int32_t H, const float* w1, const float* b1, const float* w2,
+                   const float* b2, const float* w3, const float* b3, int32_t use_softmax,
+                   const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head,
+                   int32_t l2_col0, float l2_scale, float* l2_workspace, float* l2_out,
+                   void* stream);
+
 int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                    const float* dense, int64_t ld_dense, int32_t num_dense,
                    const float* dense_w, const float* dense_b, const float* att_w,

@@ -238,3 +238,20 @@ def test_unfused_tail_path(case, monkeypatch):
     name, cfg = case
     out, ref = run_pair(name, cfg, B=200)
     _compare(out, ref, "unfused-" + _ids(case))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [("din", {"T": 50, "dim": 32}), ("din", {"T": 50, "dim": 32, "softmax": True}),
+                                  ("din", {"T": 9, "activation": "prelu"})], ids=_ids)
+def test_din_split_path_vs_reference_formulation(case, monkeypatch):
+    """rk_din_forward (algebraically split att-MLP layer 1) and the reference-formulation
+    rk_din_attention + rk_mlp_forward path agree with the oracle and with each other."""
+    name, cfg = case
+    fused, ref = run_pair(name, cfg, B=257)
+    _compare(fused, ref, "fused-" + _ids(case))
+    monkeypatch.setattr(rankops.common, "FUSED_DIN", False)
+    plain, ref2 = run_pair(name, cfg, B=257)
+    _compare(plain, ref2, "plain-" + _ids(case))
+    for a, b in zip(H.as_tuple(fused), H.as_tuple(plain)):
+        if isinstance(a, torch.Tensor):
+            torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL)
