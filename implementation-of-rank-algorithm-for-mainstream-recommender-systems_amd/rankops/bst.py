@@ -25,7 +25,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import common, ops
 from .common import EngineModule, Layer, Packed, check_eval, run_tail, table_rows
 
 FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
@@ -160,6 +160,48 @@ class BSTModel(EngineModule):
         width = col + d
         row = torch.empty(B, width, device=dev, dtype=torch.float32)
         ops.concat_gather(segs, B, row)
+        nblk = len(self.transformer_blocks)
+        if nblk == 0:
+            raise NotImplementedError("BSTModel with zero transformer blocks")
+        for blk in self.transformer_blocks:
+            if T > blk.position_embedding.num_embeddings:
+                raise IndexError(f"BSTTransformer: sequence length {T} exceeds max_len "
+                                 f"{blk.position_embedding.num_embeddings}")
+        blocks = self._fused_blocks(T)
+        if blocks is not None:
+            # every block + pooling in one launch, activations in LDS (rk_bst_forward_blocks)
+            ops.bst_forward_blocks(self.embeddings['feedid'].weight, seq_feedid, seq_length, d,
+                                   self.transformer_blocks[0].nhead, blocks, ops._lib.fptr(row, col), width,
+                                   self.pooling_method != 'sum')
+        else:
+            self._run_blocks(row, col, width, seq_feedid, seq_length, B, T)
+        logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
+        return probs, logits
+
+    def _fused_blocks(self, T):
+        """Parameters for rk_bst_forward_blocks, or None outside its envelope (d_model 128,
+        4 heads, T <= 64, <= 4 blocks, contiguous 16-B aligned fp32 parameters)."""
+        blks = self.transformer_blocks
+        if not (common.FUSED_BST and self.d_model == 128 and 1 <= T <= 64 and len(blks) <= 4
+                and self.embeddings['feedid'].weight.stride(0) == 128
+                and all(b.nhead == 4 for b in blks)):
+            return None
+        out = []
+        for b in blks:
+            ts = (b.position_embedding.weight, b.w_q.weight, b.w_q.bias, b.w_k.weight, b.w_k.bias, b.w_v.weight,
+                  b.w_v.bias, b.w_o.weight, b.w_o.bias, b.ffn[0].weight, b.ffn[0].bias, b.ffn[3].weight,
+                  b.ffn[3].bias, b.norm1.weight, b.norm1.bias, b.norm2.weight, b.norm2.bias)
+            if any(t.dtype != torch.float32 or not t.is_contiguous() or t.data_ptr() % 16 for t in ts):
+                return None
+            out.append((ts, (b.norm1.eps, b.norm2.eps, b.ffn[1].negative_slope)))
+        return out
+
+    def _run_blocks(self, row, col, width, seq_feedid, seq_length, B, T):
+        """Per-layer path: gathered sequence in HBM, rk_linear x5 + rk_bst_attention per block."""
+        d = self.d_model
+        dev = row.device
         # behaviour sequence: x[b*T + t] = feedid_table[seq_feedid[b, t]]
         x = torch.empty(B * T, d, device=dev, dtype=torch.float32)
         flat = seq_feedid.view(-1)
@@ -171,9 +213,3 @@ class BSTModel(EngineModule):
                         pool_mean=self.pooling_method != 'sum')
             else:
                 x = blk.run(x, B, T, seq_length, out=torch.empty_like(x))
-        if nblk == 0:
-            raise NotImplementedError("BSTModel with zero transformer blocks")
-        logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
-        return probs, logits

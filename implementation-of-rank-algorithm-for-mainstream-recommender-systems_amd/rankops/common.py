@@ -216,6 +216,7 @@ class Layer:
 
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
 FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
+FUSED_BST = True  # BST: all transformer blocks + pooling in one rk_bst_forward_blocks launch
 
 
 def _pad64(v: int) -> int:

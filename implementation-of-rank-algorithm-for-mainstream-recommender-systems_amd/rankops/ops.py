@@ -143,6 +143,27 @@ def bst_attention(qkv, batch, T, d_model, heads, seq_len, ctx):
                                ctx.stride(0), _lib.stream_of(qkv)), "rk_bst_attention")
 
 
+BST_BLOCK_PARAMS = 17
+
+
+def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr, ld_pool, pool_mean):
+    """rk_bst_forward_blocks: `blocks` = list of (17 device tensors in the header's order,
+    (ln1_eps, ln2_eps, slope))."""
+    lib = _lib.load()
+    B, T = seq.shape
+    params = (ctypes.c_void_p * (BST_BLOCK_PARAMS * len(blocks)))()
+    scalars = (ctypes.c_float * (3 * len(blocks)))()
+    for i, (tensors, sc) in enumerate(blocks):
+        assert len(tensors) == BST_BLOCK_PARAMS
+        for k, t in enumerate(tensors):
+            params[BST_BLOCK_PARAMS * i + k] = ptr(t)
+        for k in range(3):
+            scalars[3 * i + k] = float(sc[k])
+    check(lib.rk_bst_forward_blocks(ptr(table), table.shape[0], table.stride(0), ptr(seq), seq.stride(0), T,
+                                    ptr(seq_len), B, d_model, heads, len(blocks), params, scalars, pool_out_ptr,
+                                    ld_pool, 1 if pool_mean else 0, _lib.stream_of(table)), "rk_bst_forward_blocks")
+
+
 def bn_fold(mean, var, weight, bias, eps, scale, shift):
     lib = _lib.load()
     check(lib.rk_bn_fold(ptr(mean), ptr(var), ptr(weight), ptr(bias), float(eps), mean.numel(), ptr(scale),

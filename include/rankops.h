@@ -26,6 +26,7 @@
  *   rk_row_l2norm_mean DIN mini-batch-aware l2 term          din.py:318-322
  *   rk_afm_forward     AFM.forward()                         afm.py:92-119
  *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84
+ *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -202,6 +203,22 @@ int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, in
 int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T,
                      int32_t d_model, int32_t heads, const int64_t* seq_len, float* ctx,
                      int64_t ld_ctx, void* stream);
+
+/* Every transformer block of BSTModel.forward plus the pooling (bst.py:66-91, 224-241) in one
+ * launch, one workgroup per sample, activations kept in LDS:
+ *   x = table[seq[b, :T]];  for each block i: x = block_i(x)  (mask keys >= seq_len[b])
+ *   pool_out[b, 0:128] = sum_t x[t]  (/ seq_len[b] when pool_mean)
+ * block_params: host array of 17 device pointers per block, in this order:
+ *   pos[max_len,128], wq, bq, wk, bk, wv, bv, wo, bo, w1 (ffn.0), b1, w2 (ffn.3), b2,
+ *   ln1_gamma, ln1_beta, ln2_gamma, ln2_beta   (nn.Linear [out,in] row-major, 16-B aligned)
+ * block_scalars: host array of 3 floats per block: ln1_eps, ln2_eps, leaky slope.
+ * Envelope: d_model 128, heads 4, 1 <= T <= 64, nblocks <= 4 (else RK_ERR_UNSUPPORTED).
+ * Replaces the rk_linear x5 + rk_bst_attention sequence of one block.                     */
+int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t ld_table,
+                          const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
+                          int64_t batch, int32_t d_model, int32_t heads, int32_t nblocks,
+                          const float* const* block_params, const float* block_scalars,
+                          float* pool_out, int64_t ld_pool, int32_t pool_mean, void* stream);
 
 /* ---- dense layers ---- */
 int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_period,

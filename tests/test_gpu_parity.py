@@ -36,6 +36,11 @@ CASES = [
     ("bst", {"T": 64, "dim": 128, "max_len": 64, "heads": 4}),
     ("bst", {"T": 20, "blocks": 2, "batch_norm": False}),
     ("bst", {"T": 1}),
+    # rk_bst_forward_blocks envelope (d_model 128, 4 heads, T <= 64)
+    ("bst", {"T": 50, "dim": 128, "pooling": "mean"}),
+    ("bst", {"T": 37, "dim": 128, "blocks": 2, "max_len": 40}),
+    ("bst", {"T": 64, "dim": 128, "blocks": 3, "max_len": 64}),
+    ("bst", {"T": 1, "dim": 128}),
 ]
 
 
@@ -255,3 +260,37 @@ def test_din_split_path_vs_reference_formulation(case, monkeypatch):
     for a, b in zip(H.as_tuple(fused), H.as_tuple(plain)):
         if isinstance(a, torch.Tensor):
             torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{"T": 64, "dim": 128, "max_len": 64}, {"T": 29, "dim": 128, "blocks": 2},
+                                 {"T": 50, "dim": 128, "pooling": "mean"}], ids=str)
+def test_bst_fused_blocks_vs_per_layer_path(cfg, monkeypatch):
+    """rk_bst_forward_blocks (whole block in LDS) and the per-layer rk_linear/rk_bst_attention
+    path agree with the oracle and with each other; length-0 rows stay NaN in both."""
+    inp = H.make_inputs("bst", cfg, 300)
+    inp["seq_length"][:3] = 0
+    inp["seq_length"][3:6] = cfg["T"]
+    inp["seq_length"][6:9] = 1
+    model = H.build("bst", cfg)
+    fused, ref = run_pair("bst", cfg, B=300, inputs=inp, model=model)
+    assert model._fused_blocks(cfg["T"]) is not None
+    _compare(fused, ref, "fused-bst")
+    assert torch.isnan(fused[1][:3].cpu()).all()
+    monkeypatch.setattr(rankops.common, "FUSED_BST", False)
+    plain, _ = run_pair("bst", cfg, B=300, inputs=inp, model=model)
+    for a, b in zip(fused, plain):
+        torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL, equal_nan=True)
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+def test_bst_fused_blocks_oob_sequence_index_is_flagged():
+    cfg = {"T": 16, "dim": 128}
+    model = H.build("bst", cfg).cuda()
+    inp = H.to_device(H.make_inputs("bst", cfg, 32), "cuda")
+    rankops.error_flags(reset=True)
+    inp["seq_feedid"][5, 2] = model.vocab_sizes["feedid"] + 3
+    with torch.no_grad():
+        H.call_model(model, "bst", inp)
+    assert rankops.error_flags(reset=True) & 1
