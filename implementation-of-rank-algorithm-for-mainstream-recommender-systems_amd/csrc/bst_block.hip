@@ -23,6 +23,7 @@ constexpr int kBT = 64;         // padded sequence rows
 constexpr int kBLD = kBD + 4;   // LDS row stride
 constexpr int kBWaves = 8;
 constexpr int kBMaxBlocks = 4;
+constexpr float kLog2eOverSqrtDh = 0.25503486f;  // log2(e) / sqrt(32): softmax scale, d_h = 32
 
 struct BstBlockW {
   const float* pos;  // [max_len, 128]
@@ -49,37 +50,162 @@ struct BstArgs {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// acc[j] += A[rt*32.., :] . W[ct_j*32.., :]^T over K = 128.  A rows from LDS (+ pos rows from
-// global for t < T when ADDPOS), W rows from global; 2-deep register prefetch of W.
-template <int NT, bool ADDPOS>
-__device__ __forceinline__ void gemm128(const float* __restrict__ A, const float* __restrict__ pos, int T,
-                                        const float* const (&W)[NT], f32x16 (&acc)[NT], int rt, int lane) {
-  const int l32 = lane & 31, hk = 4 * (lane >> 5);
-  const int row = rt * 32 + l32;
-  const float* arow = A + row * kBLD + hk;
-  const float* prow = (ADDPOS && row < T) ? pos + (int64_t)row * kBD + hk : nullptr;
+// Optional per-phase shader-clock counters (tools/bst_phases.hip builds with RK_BST_PHASES):
+// thread 0 adds the cycles since the previous barrier to g_bst_phase[i].
+#ifdef RK_BST_PHASES
+__device__ unsigned long long g_bst_phase[16];
+#define BST_PHASE(i)                                           \
+  do {                                                         \
+    if (tid == 0) {                                            \
+      const unsigned long long now_ = clock64();               \
+      atomicAdd(&g_bst_phase[i], now_ - t_phase);              \
+      t_phase = now_;                                          \
+    }                                                          \
+  } while (0)
+#else
+#define BST_PHASE(i) \
+  do {               \
+  } while (0)
+#endif
+
+// Weight-row stream of NT 32-row W tiles in MFMA B-operand order: lane (n = lane%32, half h)
+// holds W[n][32s + 8c + 4h + e] for super-chunk s (32 k = one 128-B line of each W row), chunk c,
+// e < 4.  A super-chunk's loads are issued back to back so every line is consumed while in L1;
+// super-chunk 0 can be issued before the phase barrier (WStream::start) so its latency overlaps
+// the previous phase's epilogue.
+template <int NT>
+struct WStream {
   const float* wrow[NT];
+  f4 bq[2][4][NT];
+  __device__ __forceinline__ void start(const float* const (&W)[NT], int lane) {
 #pragma unroll
-  for (int j = 0; j < NT; ++j) wrow[j] = W[j] + (int64_t)l32 * kBD + hk;
-  f4 bn[NT];
+    for (int j = 0; j < NT; ++j) wrow[j] = W[j] + (int64_t)(lane & 31) * kBD + 4 * (lane >> 5);
+    issue(0, 0);
+  }
+  __device__ __forceinline__ void issue(int s, int buf) {
 #pragma unroll
-  for (int j = 0; j < NT; ++j) bn[j] = *reinterpret_cast<const f4*>(wrow[j]);
-#pragma unroll 2
-  for (int c = 0; c < kBD / 8; ++c) {
-    f4 bc[NT];
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bc[j] = bn[j];
-    const int cn = c + 1 < kBD / 8 ? c + 1 : c;
+      for (int c = 0; c < 4; ++c) bq[buf][c][j] = *reinterpret_cast<const f4*>(wrow[j] + 32 * s + 8 * c);
+  }
+};
+
+// acc[j] += A[rt*32.., :] . W_j[0..32, :]^T over K = 128 (A in LDS, W streamed by `ws`, whose
+// super-chunk 0 is already in flight).  Fully unrolled; the next super-chunk is loaded while
+// this one feeds the MFMAs, the next A float4 one chunk ahead; sched_barrier keeps the compiler
+// from sinking the loads next to their use.
+template <int NT>
+__device__ __forceinline__ void gemm128(const float* __restrict__ A, WStream<NT>& ws, f32x16 (&acc)[NT], int rt,
+                                        int lane) {
+  constexpr int NS = kBD / 32;
+  const float* arow = A + (rt * 32 + (lane & 31)) * kBLD + 4 * (lane >> 5);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bn[j] = *reinterpret_cast<const f4*>(wrow[j] + 8 * cn);
-    f4 av = *reinterpret_cast<const f4*>(arow + 8 * c);
-    if (ADDPOS) {
-      if (prow) av = av + *reinterpret_cast<const f4*>(prow + 8 * c);
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  f4 a_cur = *reinterpret_cast<const f4*>(arow);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < NS) ws.issue(s + 1, (s + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int cc = 4 * s + c;
+      f4 a_next = a_cur;
+      if (cc + 1 < 4 * NS) a_next = *reinterpret_cast<const f4*>(arow + 8 * (cc + 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = mfma32(a_cur[e], ws.bq[s & 1][c][j][e], acc[j]);
+      a_cur = a_next;
     }
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its global
+// loads, so weight prefetches stay in flight across it (__syncthreads would drain vmcnt).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Sum over the 8 lanes of an aligned lane octet (xor butterfly inside the octet).
+__device__ __forceinline__ float octet_sum(float v) {
+  v += __shfl_xor(v, 1, kWave);
+  v += __shfl_xor(v, 2, kWave);
+  v += __shfl_xor(v, 4, kWave);
+  return v;
+}
+
+// LayerNorm of all 64 rows of S (two-pass mean / biased variance like nn.LayerNorm): thread tid
+// owns row tid/8 and columns 4*(tid%8) + 32*q + e (q, e < 4), i.e. each 32-column slice of a row is
+// one contiguous 128 B read by the row's 8 lanes.
+struct LnCols {
+  f4 g[4], b[4];
+};
+__device__ __forceinline__ LnCols ln_load(const float* g, const float* be, int tid) {
+  LnCols p;
+  const int c0 = 4 * (tid & 7);
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+  for (int q = 0; q < 4; ++q) {
+    p.g[q] = *reinterpret_cast<const f4*>(g + c0 + 32 * q);
+    p.b[q] = *reinterpret_cast<const f4*>(be + c0 + 32 * q);
+  }
+  return p;
+}
+// y = LN(S row).  Output modes: pool != NULL -> pool[wave][col] = sum of y over the wave's 8 rows
+// that are < T (the last block feeding the pooling); else S = y, and with `xp` set also
+// xp = y + pos[row] (rows < T, zero otherwise): the next block's raw and position-added inputs.
+__device__ __forceinline__ void layernorm_rows(float* S, const LnCols& p, float eps, int tid, float* pool, int T,
+                                               float* xp, const float* pos) {
+  const int r = tid >> 3, c0 = 4 * (tid & 7);
+  float* row = S + r * kBLD + c0;
+  const bool real = r < T;
+  f4 pv[4];
+  if (xp) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[j] = mfma32(av[e], bc[j][e], acc[j]);
+    for (int q = 0; q < 4; ++q) {
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      pv[q] = real ? *reinterpret_cast<const f4*>(pos + (int64_t)r * kBD + c0 + 32 * q) : z;
+    }
+  }
+  f4 x[4];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    x[q] = *reinterpret_cast<const f4*>(row + 32 * q);
+    s += (x[q][0] + x[q][1]) + (x[q][2] + x[q][3]);
+  }
+  const float mean = octet_sum(s) * (1.0f / kBD);
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[q][e] -= mean;
+      v += x[q][e] * x[q][e];
+    }
+  const float rstd = 1.0f / sqrtf(octet_sum(v) * (1.0f / kBD) + eps);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = x[q][e] * rstd * p.g[q][e] + p.b[q][e];
+    if (!pool) {
+      *reinterpret_cast<f4*>(row + 32 * q) = y;
+      if (xp) {
+        const f4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(xp + r * kBLD + c0 + 32 * q) = real ? y + pv[q] : z;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = real ? y[e] : 0.f;
+        t += __shfl_xor(t, 8, kWave);
+        t += __shfl_xor(t, 16, kWave);
+        t += __shfl_xor(t, 32, kWave);
+        y[e] = t;
+      }
+      if ((tid & 63) < 8) *reinterpret_cast<f4*>(pool + (tid >> 6) * kBD + c0 + 32 * q) = y;
+    }
   }
 }
 
@@ -88,22 +214,23 @@ __device__ __forceinline__ void zero(f32x16& a) {
   for (int r = 0; r < 16; ++r) a[r] = 0.f;
 }
 
-// Row LayerNorm of rows [w*8, w*8+8) of S (in place), lane owns columns lane and lane+64.
-__device__ __forceinline__ void layernorm_rows(float* S, const float* g, const float* be, float eps, int wave,
-                                               int lane) {
-  const float g0 = g[lane], g1 = g[lane + 64], b0 = be[lane], b1 = be[lane + 64];
-  for (int r = wave * 8; r < wave * 8 + 8; ++r) {
-    float* row = S + r * kBLD;
-    const float x0 = row[lane], x1 = row[lane + 64];
-    const float mean = wave_sum(x0 + x1) * (1.0f / kBD);
-    const float d0 = x0 - mean, d1 = x1 - mean;
-    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / kBD);
-    const float rstd = 1.0f / sqrtf(var + eps);
-    row[lane] = d0 * rstd * g0 + b0;
-    row[lane + 64] = d1 * rstd * g1 + b1;
+// acc (32x32 tile rt/ct) + bias -> dst rows, optional LeakyReLU / residual.
+__device__ __forceinline__ void store_tile(float* dst, const f32x16& acc, const float* bias, int rt, int ct, int lane,
+                                           const float* residual = nullptr, float slope = 1.f, bool leaky = false) {
+  const int col = ct * 32 + (lane & 31);
+  const float bb = bias[col];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int t = rt * 32 + acc_row(r, lane);
+    float z = acc[r] + bb;
+    if (leaky) z = z > 0.f ? z : z * slope;
+    if (residual) z = residual[t * kBLD + col] + z;
+    dst[t * kBLD + col] = z;
   }
 }
 
+// LDS per sample:  Xs = x + pos (Q/K input and the LN1 residual), Qs = x (V input), then Q / ctx /
+// pre-LN2 sum;  Ks = K, then out1;  Vs = V, then the FFN hidden activation.
 __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Xs = sm;
@@ -114,87 +241,105 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5, hk = 4 * half;
+  const int rt = wave >> 2, q4 = wave & 3;  // GEMM phases: row tile and column tile of this wave
   const int64_t b = blockIdx.x;
   const int T = a.T;
   const int64_t len = a.seq_len[b];
   const int nvalid = (int)(len < 0 ? 0 : (len > T ? T : len));
+#ifdef RK_BST_PHASES
+  unsigned long long t_phase = clock64();
+#endif
 
-  // ---- gather the behaviour sequence: Xs[t] = table[seq[b, t]] (rows >= T are zero)
+  WStream<1> ws1;
+  {
+    const float* W[1] = {a.blk[0].wv + q4 * 32 * kBD};
+    ws1.start(W, lane);
+  }
+  // ---- gather: Qs[t] = x = table[seq[b, t]], Xs[t] = x + pos[t]  (rows >= T zero)
   for (int i = tid; i < kBT * (kBD / 4); i += 512) {
     const int t = i / (kBD / 4), c = (i % (kBD / 4)) * 4;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
+    f4 v = {0.f, 0.f, 0.f, 0.f}, vp = v;
     if (t < T) {
       const int64_t r = a.seq[b * a.ld_seq + t];
+      const f4 pv = *reinterpret_cast<const f4*>(a.blk[0].pos + (int64_t)t * kBD + c);
       if (r >= 0 && r < a.rows)
         v = *reinterpret_cast<const f4*>(a.table + r * a.ld + c);
       else if (c == 0)
         flag_oob(a.flags);
+      vp = v + pv;
     }
-    *reinterpret_cast<f4*>(Xs + t * kBLD + c) = v;
+    *reinterpret_cast<f4*>(Qs + t * kBLD + c) = v;
+    *reinterpret_cast<f4*>(Xs + t * kBLD + c) = vp;
   }
-  __syncthreads();
+  lds_barrier(); BST_PHASE(0);
 
-  const float sqrt_dh = 5.65685424949238f;  // math.sqrt(32) -> fp32; scores are divided like bst.py:79
 
   for (int blk = 0; blk < a.nblocks; ++blk) {
     const BstBlockW& P = a.blk[blk];
-    // ---- 1. Q|K (x + pos) and V (x) projections: wave w -> row tile w/4, q/k col tiles
-    //         2(w%4), 2(w%4)+1 of the 8 Q|K tiles, and V col tile w%4
+    // ---- 1a. V = x . Wv^T + bv -> Vs   (wave: row tile rt, column tile q4)
+    WStream<2> ws2;
     {
-      const int rt = wave >> 2, q4 = wave & 3;
+      f32x16 acc[1];
+      gemm128<1>(Qs, ws1, acc, rt, lane);
+      const int ct0 = 2 * q4, ct1 = 2 * q4 + 1;  // of the 8 Q|K column tiles: 0..3 Q, 4..7 K
+      const float* W[2] = {(ct0 < 4 ? P.wq + ct0 * 32 * kBD : P.wk + (ct0 - 4) * 32 * kBD),
+                           (ct1 < 4 ? P.wq + ct1 * 32 * kBD : P.wk + (ct1 - 4) * 32 * kBD)};
+      ws2.start(W, lane);
+      store_tile(Vs, acc[0], P.bv, rt, q4, lane);
+    }
+    lds_barrier(); BST_PHASE(1);
+    // ---- 1b. [Q|K] = (x + pos) . W^T + b -> Qs, Ks   (wave: row tile rt, Q|K tiles 2q4, 2q4+1)
+    {
       f32x16 acc[2];
-      zero(acc[0]);
-      zero(acc[1]);
-      const int ct0 = 2 * q4, ct1 = 2 * q4 + 1;  // 0..3 -> Q tiles, 4..7 -> K tiles
-      const float* W2[2] = {(ct0 < 4 ? P.wq + ct0 * 32 * kBD : P.wk + (ct0 - 4) * 32 * kBD),
-                            (ct1 < 4 ? P.wq + ct1 * 32 * kBD : P.wk + (ct1 - 4) * 32 * kBD)};
-      gemm128<2, true>(Xs, P.pos, T, W2, acc, rt, lane);
-      f32x16 vacc[1];
-      zero(vacc[0]);
-      const float* W1[1] = {P.wv + q4 * 32 * kBD};
-      gemm128<1, false>(Xs, nullptr, T, W1, vacc, rt, lane);
+      gemm128<2>(Xs, ws2, acc, rt, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int ct = 2 * q4 + j;
-        float* dst = ct < 4 ? Qs : Ks;
-        const float* bias = ct < 4 ? P.bq : P.bk;
-        const int col = (ct & 3) * 32 + l32;
-        const float bb = bias[col];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[(rt * 32 + acc_row(r, lane)) * kBLD + col] = acc[j][r] + bb;
+        store_tile(ct < 4 ? Qs : Ks, acc[j], ct < 4 ? P.bq : P.bk, rt, ct & 3, lane);
       }
-      const int vcol = q4 * 32 + l32;
-      const float vb = P.bv[vcol];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) Vs[(rt * 32 + acc_row(r, lane)) * kBLD + vcol] = vacc[0][r] + vb;
     }
-    __syncthreads();
+    lds_barrier(); BST_PHASE(2);
 
     // ---- 2. attention: wave w -> head w/2, query tile w%2; ctx written over Q_h of that tile
     {
       const int h = wave >> 1, qt = wave & 1, hc = h * 32;
-      f32x16 S[2];
+      // all operands up front: Q_h (this query tile), K_h and the V_h column this lane feeds
+      f4 qv[4], kv[2][4];
+      float vv[2][16];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        zero(S[kt]);
+      for (int c = 0; c < 4; ++c) {
+        qv[c] = *reinterpret_cast<const f4*>(Qs + (qt * 32 + l32) * kBLD + hc + 8 * c + hk);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const f4 kv = *reinterpret_cast<const f4*>(Ks + (kt * 32 + l32) * kBLD + hc + 8 * c + hk);
-          const f4 qv = *reinterpret_cast<const f4*>(Qs + (qt * 32 + l32) * kBLD + hc + 8 * c + hk);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) S[kt] = mfma32(kv[e], qv[e], S[kt]);
-        }
+        for (int kt = 0; kt < 2; ++kt)
+          kv[kt][c] = *reinterpret_cast<const f4*>(Ks + (kt * 32 + l32) * kBLD + hc + 8 * c + hk);
       }
-      // scores / sqrt(d_h), keys >= len (and padding rows >= T) -> -inf, softmax over keys
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          vv[kt][s] = Vs[(kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * half) * kBLD + hc + l32];
+      f32x16 S[2];
+      zero(S[0]);
+      zero(S[1]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) S[kt] = mfma32(kv[kt][c][e], qv[c][e], S[kt]);
+      // softmax over keys of scores / sqrt(d_h), keys >= len (and padding rows >= T) -> -inf
+      // (bst.py:79-82): the max is taken on the raw scores (the positive scale commutes with it)
+      // and exp((s - m) / sqrt(d_h)) = exp2((s - m) * log2(e) / sqrt(d_h)) on v_exp_f32.  An
+      // all-masked row gives m = -inf, (-inf) - (-inf) = NaN, hence NaN like torch.
       float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kt * 32 + acc_row(r, lane);
-          const float s = key < nvalid ? S[kt][r] / sqrt_dh : -INFINITY;
-          S[kt][r] = s;
-          m = fmaxf(m, s);
+          const float sc = key < nvalid ? S[kt][r] : -INFINITY;
+          S[kt][r] = sc;
+          m = fmaxf(m, sc);
         }
       m = fmaxf(m, __shfl_xor(m, 32, kWave));
       float l = 0.f;
@@ -202,7 +347,7 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = expf(S[kt][r] - m);
+          const float p = __builtin_amdgcn_exp2f((S[kt][r] - m) * kLog2eOverSqrtDh);
           S[kt][r] = p;
           l += p;
         }
@@ -213,88 +358,57 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * half;
-          C = mfma32(Vs[key * kBLD + hc + l32], S[kt][s], C);
-        }
+        for (int s = 0; s < 16; ++s) C = mfma32(vv[kt][s], S[kt][s], C);
+      const float* W[1] = {P.wo + q4 * 32 * kBD};
+      ws1.start(W, lane);
       const float inv_l = 1.0f / l;
 #pragma unroll
       for (int r = 0; r < 16; ++r) Qs[(qt * 32 + l32) * kBLD + hc + acc_row(r, lane)] = C[r] * inv_l;
     }
-    __syncthreads();
+    lds_barrier(); BST_PHASE(3);
 
-    // ---- 3. out1 = LN1((x + pos) + (ctx . Wo^T + bo)) -> Ks
+    // ---- 3. pre-LN1 = (x + pos) + (ctx . Wo^T + bo) -> Ks;  LN1 in place
     {
-      const int rt = wave >> 2, ct = wave & 3;
       f32x16 acc[1];
-      zero(acc[0]);
-      const float* W[1] = {P.wo + ct * 32 * kBD};
-      gemm128<1, false>(Qs, nullptr, T, W, acc, rt, lane);
-      const int col = ct * 32 + l32;
-      const float bb = P.bo[col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = rt * 32 + acc_row(r, lane);
-        float res = Xs[t * kBLD + col];
-        if (t < T) res = res + P.pos[(int64_t)t * kBD + col];
-        Ks[t * kBLD + col] = res + (acc[0][r] + bb);
-      }
+      gemm128<1>(Qs, ws1, acc, rt, lane);
+      const float* W[1] = {P.w1 + q4 * 32 * kBD};
+      ws1.start(W, lane);
+      store_tile(Ks, acc[0], P.bo, rt, q4, lane, Xs);
     }
-    __syncthreads();
-    layernorm_rows(Ks, P.g1, P.be1, P.eps1, wave, lane);
-    __syncthreads();
+    const LnCols ln1 = ln_load(P.g1, P.be1, tid);
+    lds_barrier(); BST_PHASE(4);
+    layernorm_rows(Ks, ln1, P.eps1, tid, nullptr, T, nullptr, nullptr);
+    lds_barrier(); BST_PHASE(5);
 
     // ---- 4. f = LeakyReLU(out1 . W1^T + b1) -> Vs
     {
-      const int rt = wave >> 2, ct = wave & 3;
       f32x16 acc[1];
-      zero(acc[0]);
-      const float* W[1] = {P.w1 + ct * 32 * kBD};
-      gemm128<1, false>(Ks, nullptr, T, W, acc, rt, lane);
-      const int col = ct * 32 + l32;
-      const float bb = P.b1[col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float z = acc[0][r] + bb;
-        Vs[(rt * 32 + acc_row(r, lane)) * kBLD + col] = z > 0.f ? z : z * P.slope;
-      }
+      gemm128<1>(Ks, ws1, acc, rt, lane);
+      const float* W[1] = {P.w2 + q4 * 32 * kBD};
+      ws1.start(W, lane);
+      store_tile(Vs, acc[0], P.b1, rt, q4, lane, nullptr, P.slope, true);
     }
-    __syncthreads();
+    lds_barrier(); BST_PHASE(6);
 
-    // ---- 5. out = LN2(out1 + (f . W2^T + b2)) -> Qs (last block) or Xs (next block's input)
-    float* dst = (blk + 1 < a.nblocks) ? Xs : Qs;
+    // ---- 5. pre-LN2 = out1 + (f . W2^T + b2) -> Qs;  LN2 -> next block's Qs / Xs, or the pooling
+    const bool last = blk + 1 == a.nblocks;
     {
-      const int rt = wave >> 2, ct = wave & 3;
       f32x16 acc[1];
-      zero(acc[0]);
-      const float* W[1] = {P.w2 + ct * 32 * kBD};
-      gemm128<1, false>(Vs, nullptr, T, W, acc, rt, lane);
-      const int col = ct * 32 + l32;
-      const float bb = P.b2[col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = rt * 32 + acc_row(r, lane);
-        dst[t * kBLD + col] = Ks[t * kBLD + col] + (acc[0][r] + bb);
+      gemm128<1>(Vs, ws1, acc, rt, lane);
+      if (!last) {
+        const float* W[1] = {a.blk[blk + 1].wv + q4 * 32 * kBD};
+        ws1.start(W, lane);
       }
+      store_tile(Qs, acc[0], P.b2, rt, q4, lane, Ks);
     }
-    __syncthreads();
-    layernorm_rows(dst, P.g2, P.be2, P.eps2, wave, lane);
-    __syncthreads();
+    const LnCols ln2 = ln_load(P.g2, P.be2, tid);
+    lds_barrier(); BST_PHASE(7);
+    // last block: per-wave column sums of the LN2 rows < T (every real position of the batch,
+    // padded ones included, bst.py:238-241)
+    layernorm_rows(Qs, ln2, P.eps2, tid, last ? red : nullptr, T, last ? nullptr : Xs,
+                   last ? nullptr : a.blk[blk + 1].pos);
+    lds_barrier(); BST_PHASE(8);
   }
-
-  // ---- pooling over the T real positions (padded positions of the batch included, bst.py:238-241)
-  const float* out = Qs;  // the last block's LN2 output
-  {
-    float s0 = 0.f, s1 = 0.f;
-    for (int t = wave * 8; t < wave * 8 + 8; ++t)
-      if (t < T) {
-        s0 += out[t * kBLD + lane];
-        s1 += out[t * kBLD + lane + 64];
-      }
-    red[wave * kBD + lane] = s0;
-    red[wave * kBD + lane + 64] = s1;
-  }
-  __syncthreads();
   if (tid < kBD) {
     float s = 0.f;
 #pragma unroll
