@@ -61,8 +61,12 @@ int main(int argc, char** argv) {
   };
   run();
   CK(hipDeviceSynchronize());
+#ifdef RK_BST_PHASES
   unsigned long long zero[16] = {0};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(rk::g_bst_phase), zero, sizeof(zero)));
+  unsigned long long zw[80] = {0};
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(rk::g_bst_wave), zw, sizeof(zw)));
+#endif
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -72,14 +76,27 @@ int main(int argc, char** argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("batch %lld  %.1f us/launch\n", (long long)B, 1e3 * ms / iters);
+#ifdef RK_BST_PHASES
   unsigned long long ph[16];
   CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(rk::g_bst_phase), sizeof(ph)));
   const char* names[9] = {"gather", "v_proj", "qk_proj", "attention", "o_proj", "ln1", "ffn1", "ffn2", "ln2+pool"};
   unsigned long long tot = 0;
   for (int i = 0; i < 9; ++i) tot += ph[i];
-  printf("batch %lld  %.1f us/launch (phases with counters)\n", (long long)B, 1e3 * ms / iters);
   for (int i = 0; i < 9; ++i)
     printf("  %-10s %8.0f cycles/WG  %5.1f%%\n", names[i], (double)ph[i] / (iters * B), 100.0 * ph[i] / tot);
   printf("  total      %8.0f cycles/WG\n", (double)tot / (iters * B));
+  unsigned long long wv[10][8];
+  CK(hipMemcpyFromSymbol(wv, HIP_SYMBOL(rk::g_bst_wave), sizeof(wv)));
+  const char* marks[5] = {"v_proj", "qk_proj", "o_proj", "ffn1", "ffn2"};
+  const int mp[5] = {1, 2, 4, 6, 7};
+  for (int i = 0; i < 5; ++i) {
+    printf("  %-10s phase %6.0f, MFMA loop done per wave:", marks[i], (double)ph[mp[i]] / (iters * B));
+    for (int w = 0; w < 8; ++w) printf(" %6.0f", (double)wv[i][w] / (iters * B));
+    printf("\n  %-10s        %6s  epilogue done (before barrier):", "", "");
+    for (int w = 0; w < 8; ++w) printf(" %6.0f", (double)wv[5 + i][w] / (iters * B));
+    printf("\n");
+  }
+#endif
   return 0;
 }
