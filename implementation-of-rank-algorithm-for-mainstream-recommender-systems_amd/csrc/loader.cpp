@@ -1,0 +1,302 @@
+// Host input path: vocabulary bucketing (hazard H1) for raw ID string columns.  Contract and
+// reference lines: include/rankops_io.h.  Plain C++17 host code (no GPU), built into
+// librankops.so next to the kernels.
+//
+// A vocabulary is an open-addressing hash table (linear probing, power-of-two capacity >= 2x
+// keys) over an arena of key bytes; lookups compare the 64-bit hash, then the length, then the
+// bytes.  Columns arrive in the Apache Arrow layout so a pyarrow / parquet column is bucketed
+// in place, split over up to 16 threads.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/rankops.h"
+#include "../../include/rankops_io.h"
+
+#define RK_API extern "C" __attribute__((visibility("default")))
+
+namespace rk {
+int fail(int code, const char* fmt, ...);  // runtime.hip: records rk_last_error()
+}
+
+namespace {
+
+inline uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xFF51AFD7ED558CCDull);
+  while (n >= 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    p += 8;
+    n -= 8;
+  }
+  uint64_t w = 0;
+  std::memcpy(&w, p, n);
+  h = (h ^ w ^ ((uint64_t)n << 56)) * 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 31;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 29;
+  return h;
+}
+
+// Length of the str.isspace() character that starts at p (0 if none), UTF-8.
+inline size_t space_at(const unsigned char* p, const unsigned char* end) {
+  const unsigned c = p[0];
+  if ((c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20)) return 1;
+  if (c == 0xC2 && end - p >= 2 && (p[1] == 0x85 || p[1] == 0xA0)) return 2;  // U+0085, U+00A0
+  if (end - p >= 3) {
+    if (c == 0xE1 && p[1] == 0x9A && p[2] == 0x80) return 3;  // U+1680
+    if (c == 0xE2 && p[1] == 0x80 && (p[2] <= 0x8A || p[2] == 0xA8 || p[2] == 0xA9 || p[2] == 0xAF) && p[2] >= 0x80)
+      return 3;                                                // U+2000-200A, U+2028, U+2029, U+202F
+    if (c == 0xE2 && p[1] == 0x81 && p[2] == 0x9F) return 3;  // U+205F
+    if (c == 0xE3 && p[1] == 0x80 && p[2] == 0x80) return 3;  // U+3000
+  }
+  return 0;
+}
+
+// Length of the str.isspace() character that ends at end (0 if none), UTF-8.
+inline size_t space_before(const unsigned char* begin, const unsigned char* end) {
+  if (end - begin >= 1 && space_at(end - 1, end) == 1) return 1;
+  if (end - begin >= 2 && space_at(end - 2, end) == 2) return 2;
+  if (end - begin >= 3 && space_at(end - 3, end) == 3) return 3;
+  return 0;
+}
+
+struct Slot {
+  uint64_t h;
+  int64_t idx;  // -1: empty
+  uint32_t off, len;
+};
+
+inline bool bit_valid(const uint8_t* bits, int64_t off, int64_t i) {
+  if (!bits) return true;
+  const int64_t b = off + i;
+  return (bits[b >> 3] >> (b & 7)) & 1;
+}
+
+inline void value_span(const void* offsets, int bits, int64_t i, int64_t& a, int64_t& b) {
+  if (bits == 32) {
+    const int32_t* o = static_cast<const int32_t*>(offsets);
+    a = o[i];
+    b = o[i + 1];
+  } else {
+    const int64_t* o = static_cast<const int64_t*>(offsets);
+    a = o[i];
+    b = o[i + 1];
+  }
+}
+
+int thread_count(int requested, int64_t n) {
+  int t = requested > 0 ? requested : (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+  const int64_t per = 8192;  // below this many values per thread, spawning costs more than it saves
+  t = (int)std::max<int64_t>(1, std::min<int64_t>(t, (n + per - 1) / per));
+  return t;
+}
+
+template <class F>
+void parallel_for(int64_t n, int threads, F&& body) {
+  if (threads <= 1) {
+    body(0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    const int64_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    pool.emplace_back([&body, a, b] { body(a, b); });
+  }
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+struct rk_vocab {
+  std::vector<char> arena;
+  std::vector<Slot> slots;
+  uint64_t mask = 0;
+  int64_t size = 0;
+
+  void reserve(size_t keys) {
+    size_t cap = 16;
+    while (cap < 2 * keys + 2) cap <<= 1;
+    slots.assign(cap, Slot{0, -1, 0, 0});
+    mask = cap - 1;
+  }
+  void put(const char* k, size_t n, int64_t idx) {
+    const uint64_t h = hash_bytes(k, n);
+    for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+      Slot& e = slots[s];
+      if (e.idx < 0) {
+        e.h = h;
+        e.idx = idx;
+        e.off = (uint32_t)arena.size();
+        e.len = (uint32_t)n;
+        arena.insert(arena.end(), k, k + n);
+        return;
+      }
+      if (e.h == h && e.len == n && std::memcmp(arena.data() + e.off, k, n) == 0) {
+        e.idx = idx;  // a later duplicate line overwrites, like the dict comprehension
+        return;
+      }
+    }
+  }
+  int64_t get(const char* k, size_t n) const {
+    const uint64_t h = hash_bytes(k, n);
+    for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+      const Slot& e = slots[s];
+      if (e.idx < 0) return 0;  // not in the vocabulary -> row 0 (H1)
+      if (e.h == h && e.len == n && std::memcmp(arena.data() + e.off, k, n) == 0) return e.idx;
+    }
+  }
+};
+
+using namespace rk;
+
+RK_API rk_vocab* rk_vocab_parse(const char* text, int64_t nbytes, int32_t skip_empty_lines) {
+  if (nbytes < 0 || (!text && nbytes > 0)) {
+    fail(RK_ERR_INVALID, "rk_vocab_parse: bad buffer");
+    return nullptr;
+  }
+  if (nbytes >= (int64_t)UINT32_MAX) {
+    fail(RK_ERR_UNSUPPORTED, "rk_vocab_parse: %lld bytes (max 4 GiB)", (long long)nbytes);
+    return nullptr;
+  }
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(text);
+  const unsigned char* end = p + nbytes;
+  // lines as Python's universal-newline file iteration yields them
+  std::vector<std::pair<const unsigned char*, const unsigned char*>> lines;
+  for (const unsigned char* s = p; s < end;) {
+    const unsigned char* e = s;
+    while (e < end && *e != '\n' && *e != '\r') ++e;
+    lines.emplace_back(s, e);
+    if (e < end && *e == '\r' && e + 1 < end && e[1] == '\n') ++e;
+    s = e + 1;
+  }
+  rk_vocab* v = new rk_vocab();
+  v->reserve(lines.size());
+  v->arena.reserve((size_t)nbytes);
+  int64_t idx = 0;
+  for (auto [a, b] : lines) {  // str.strip()
+    for (size_t k; a < b && (k = space_at(a, b)) != 0;) a += k;
+    for (size_t k; b > a && (k = space_before(a, b)) != 0;) b -= k;
+    if (skip_empty_lines && a == b) continue;
+    v->put(reinterpret_cast<const char*>(a), (size_t)(b - a), idx++);
+  }
+  v->size = idx;
+  return v;
+}
+
+RK_API rk_vocab* rk_vocab_load(const char* path, int32_t skip_empty_lines) {
+  if (!path) {
+    fail(RK_ERR_INVALID, "rk_vocab_load: null path");
+    return nullptr;
+  }
+  FILE* f = std::fopen(path, "rb");
+  if (!f) {
+    fail(RK_ERR_INVALID, "rk_vocab_load: cannot open %s", path);
+    return nullptr;
+  }
+  std::vector<char> buf;
+  char tmp[1 << 16];
+  size_t got;
+  while ((got = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+  const bool err = std::ferror(f);
+  std::fclose(f);
+  if (err) {
+    fail(RK_ERR_RUNTIME, "rk_vocab_load: read error on %s", path);
+    return nullptr;
+  }
+  return rk_vocab_parse(buf.data(), (int64_t)buf.size(), skip_empty_lines);
+}
+
+RK_API int64_t rk_vocab_size(const rk_vocab* v) { return v ? v->size : -1; }
+
+RK_API void rk_vocab_free(rk_vocab* v) { delete v; }
+
+static int check_column(const char* who, const rk_vocab* v, bool need_vocab, const char* data, const void* offsets,
+                        int32_t offset_bits, int64_t n) {
+  if (n < 0) return fail(RK_ERR_INVALID, "%s: n = %lld", who, (long long)n);
+  if (need_vocab && !v) return fail(RK_ERR_INVALID, "%s: null vocabulary", who);
+  if (offset_bits != 32 && offset_bits != 64) return fail(RK_ERR_INVALID, "%s: offset_bits %d", who, offset_bits);
+  if (n > 0 && (!offsets || !data)) return fail(RK_ERR_INVALID, "%s: null column buffers", who);
+  return RK_OK;
+}
+
+RK_API int rk_bucketize(const rk_vocab* v, const char* data, const void* offsets, int32_t offset_bits,
+                        const uint8_t* valid_bits, int64_t valid_offset, int64_t n, int64_t* out, int64_t out_stride,
+                        int32_t threads) {
+  if (int rc = check_column("rk_bucketize", v, true, data, offsets, offset_bits, n)) return rc;
+  if (n > 0 && (!out || out_stride < 1)) return fail(RK_ERR_INVALID, "rk_bucketize: bad output");
+  parallel_for(n, thread_count(threads, n), [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      int64_t r = 0;
+      if (bit_valid(valid_bits, valid_offset, i)) {
+        int64_t s, e;
+        value_span(offsets, offset_bits, i, s, e);
+        r = v->get(data + s, (size_t)(e - s));
+      }
+      out[i * out_stride] = r;
+    }
+  });
+  return RK_OK;
+}
+
+RK_API int rk_sequence_lengths(const char* data, const void* offsets, int32_t offset_bits, const uint8_t* valid_bits,
+                               int64_t valid_offset, int64_t n, char sep, int64_t* lengths, int64_t* max_len,
+                               int32_t threads) {
+  if (int rc = check_column("rk_sequence_lengths", nullptr, false, data, offsets, offset_bits, n)) return rc;
+  if (n > 0 && !lengths) return fail(RK_ERR_INVALID, "rk_sequence_lengths: null lengths");
+  const int nt = thread_count(threads, n);
+  std::vector<int64_t> part(nt, 0);
+  const int64_t chunk = (n + nt - 1) / std::max(nt, 1);
+  parallel_for(n, nt, [&](int64_t a, int64_t b) {
+    int64_t m = 0;
+    for (int64_t i = a; i < b; ++i) {
+      int64_t len = 0;
+      if (bit_valid(valid_bits, valid_offset, i)) {
+        int64_t s, e;
+        value_span(offsets, offset_bits, i, s, e);
+        len = 1 + std::count(data + s, data + e, sep);  // "".split(',') == ['']
+      }
+      lengths[i] = len;
+      m = std::max(m, len);
+    }
+    part[chunk ? a / chunk : 0] = m;
+  });
+  if (max_len) *max_len = n ? *std::max_element(part.begin(), part.end()) : 0;
+  return RK_OK;
+}
+
+RK_API int rk_bucketize_sequences(const rk_vocab* v, const char* data, const void* offsets, int32_t offset_bits,
+                                  const uint8_t* valid_bits, int64_t valid_offset, int64_t n, char sep, int64_t T,
+                                  int64_t* out, int64_t ld_out, int64_t* lengths, int32_t threads) {
+  if (int rc = check_column("rk_bucketize_sequences", v, true, data, offsets, offset_bits, n)) return rc;
+  if (T < 0 || ld_out < T || (n > 0 && T > 0 && !out)) return fail(RK_ERR_INVALID, "rk_bucketize_sequences: bad output");
+  parallel_for(n, thread_count(threads, n), [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      int64_t* row = out + i * ld_out;
+      int64_t j = 0;
+      if (bit_valid(valid_bits, valid_offset, i)) {
+        int64_t s, e;
+        value_span(offsets, offset_bits, i, s, e);
+        const char* p = data + s;
+        const char* end = data + e;
+        while (j < T) {
+          const char* q = static_cast<const char*>(std::memchr(p, sep, (size_t)(end - p)));
+          const char* item_end = q ? q : end;
+          row[j++] = v->get(p, (size_t)(item_end - p));
+          if (!q) break;
+          p = q + 1;
+        }
+      }
+      if (lengths) lengths[i] = j;
+      for (; j < T; ++j) row[j] = 0;
+    }
+  });
+  return RK_OK;
+}

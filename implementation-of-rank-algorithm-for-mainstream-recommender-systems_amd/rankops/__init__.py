@@ -11,7 +11,9 @@ hand-written HIP kernels (gfx950) through the C ABI in include/rankops.h:
     BSTModel, BSTTransformer               algorithm/BST/bst.py
 
 `rankops.sharded.ShardedDeepFM` adds the table-sharded multi-GPU DeepFM lookup (RCCL
-all-to-all).  Import order matters: torch first, so librankops binds to torch's HIP runtime.
+all-to-all); `rankops.loader` (Vocabulary, BatchAssembler, wechat_vocabularies) replaces the
+reference's Dataset bucketing + collate with C++ column bucketing and one H2D copy per batch.
+Import order matters: torch first, so librankops binds to torch's HIP runtime.
 """
 import torch  # noqa: F401
 
@@ -22,9 +24,10 @@ from .dcn import DCNModel, cross_layer  # noqa: F401
 from .deepcrossing import DeepCrossingModel, residual_unit  # noqa: F401
 from .deepfm import DeepFM  # noqa: F401
 from .din import DIN, Dice, din_attention  # noqa: F401
+from .loader import BatchAssembler, Vocabulary, wechat_vocabularies  # noqa: F401
 
 __all__ = [
-    "AFM", "BSTModel", "BSTTransformer", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM", "Dice",
-    "RankOpsError", "create_feature_columns", "cross_layer", "din_attention", "error_flags",
-    "load_library", "residual_unit",
+    "AFM", "BSTModel", "BSTTransformer", "BatchAssembler", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM",
+    "Dice", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
+    "error_flags", "load_library", "residual_unit", "wechat_vocabularies",
 ]

@@ -1,4 +1,4 @@
-"""ctypes binding of the rankops C ABI (include/rankops.h).
+"""ctypes binding of the rankops C ABI (include/rankops.h, include/rankops_io.h).
 
 This is the reference-side FFI a maintainer adds next to the reference's `nn.Module`
 bodies: plain device pointers, sizes and the current HIP stream go in, nothing torch-typed
@@ -100,7 +100,7 @@ _SEG_P = POINTER(Segment)
 _EPI_P = POINTER(Epilogue)
 _MLP_P = POINTER(MlpLayer)
 
-# name -> (restype, argtypes); the exact set declared in include/rankops.h
+# name -> (restype, argtypes); the exact set declared in include/*.h
 SIGNATURES = {
     "rk_abi_version": (c_int32, []),
     "rk_last_error": (c_char_p, []),
@@ -150,6 +150,20 @@ SIGNATURES = {
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
     "rk_bn_fold": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),
+    # include/rankops_io.h (host input path)
+    "rk_vocab_load": (c_void_p, [c_char_p, c_int32]),
+    "rk_vocab_parse": (c_void_p, [c_char_p, c_int64, c_int32]),
+    "rk_vocab_size": (c_int64, [c_void_p]),
+    "rk_vocab_free": (None, [c_void_p]),
+    "rk_bucketize": (
+        ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32]),
+    "rk_sequence_lengths": (
+        ctypes.c_int,
+        [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, ctypes.c_char, c_void_p, POINTER(c_int64), c_int32]),
+    "rk_bucketize_sequences": (
+        ctypes.c_int,
+        [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, ctypes.c_char, c_int64, c_void_p, c_int64,
+         c_void_p, c_int32]),
 }
 
 _lib = None

@@ -1,0 +1,358 @@
+"""Host input path: raw wechat rows -> the model's forward arguments on the GPU.
+
+Replaces the reference's per-row `WechatDataset.__getitem__` (pandas `iloc` + Python dict
+lookups, dcn.py:94-111; din.py:131-173; bst.py:130-159; deepfm.py:56-70; afm.py:46-62;
+deepcrossing.py:86-104) and its collate (`din_collate_fn`, din.py:175-222; the default collate
+elsewhere) with column-wise C++ bucketing (`include/rankops_io.h`) over Apache Arrow string
+columns, written straight into one pinned host buffer that reaches the device in ONE
+host-to-device copy.  Semantics are the reference's bit for bit (hazard H1): the position of
+the stripped line in the vocabulary file (last duplicate wins), 0 for unknown or null values,
+DIN histories split on ',' ('' is one item) and zero-padded to the batch maximum, BST's
+one-item sequence padded to max_seq_length.  tests/test_loader.py checks every case against
+the pure-Python restatement in oracle/bucketing.py.
+
+    vocabs = wechat_vocabularies(vocab_dir)                 # once
+    asm = BatchAssembler("din", vocabs, device="cuda")
+    dense, category, sequence, target = asm(arrow_table)    # per batch (pyarrow.Table or dict)
+    prob, logit, l2 = din_model(dense, category, sequence, target)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+
+DENSE_FEATURES = (
+    "videoplayseconds", "u_read_comment_7d_sum", "u_like_7d_sum", "u_click_avatar_7d_sum",
+    "u_forward_7d_sum", "u_comment_7d_sum", "u_follow_7d_sum", "u_favorite_7d_sum",
+    "i_read_comment_7d_sum", "i_like_7d_sum", "i_click_avatar_7d_sum", "i_forward_7d_sum",
+    "i_comment_7d_sum", "i_follow_7d_sum", "i_favorite_7d_sum", "c_user_author_read_comment_7d_sum")
+VOCAB_FILES = {"userid": "userid.txt", "feedid": "feedid.txt", "device": "device.txt",
+               "authorid": "authorid.txt", "bgm_song_id": "bgm_song_id.txt",
+               "bgm_singer_id": "bgm_singer_id.txt", "manual_tag_list": "manual_tag_id.txt"}
+DIN_SEQ = "his_read_comment_7d_seq"
+CATEGORY = {
+    "dcn": ("userid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"),
+    "deepcrossing": ("userid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"),
+    "din": ("userid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"),
+    "bst": ("userid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"),
+    "deepfm": ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id"),
+    "afm": ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"),
+}
+
+
+class Vocabulary:
+    """One vocabulary file, bucketing in C++ (rk_vocab_*).  `len(v)` is len(vocab); embedding
+    tables have len(v) + 1 rows.  skip_empty_lines=True is AFM's variant (afm.py:33-35)."""
+
+    def __init__(self, path=None, *, text: bytes = None, skip_empty_lines=False):
+        lib = _lib.load()
+        if (path is None) == (text is None):
+            raise ValueError("Vocabulary: give exactly one of path / text")
+        if path is not None:
+            h = lib.rk_vocab_load(os.fsencode(path), 1 if skip_empty_lines else 0)
+        else:
+            h = lib.rk_vocab_parse(bytes(text), len(text), 1 if skip_empty_lines else 0)
+        if not h:
+            raise _lib.RankOpsError(f"Vocabulary: {_lib.last_error()}")
+        self._h = h
+        self.path = path
+        self.skip_empty_lines = skip_empty_lines
+
+    def __len__(self):
+        return int(_lib.load().rk_vocab_size(self._h))
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib._lib is not None:
+            _lib._lib.rk_vocab_free(h)
+
+    def lookup(self, column, out: np.ndarray = None, threads: int = 0) -> np.ndarray:
+        """int64 row of every value of `column` (0 for unknown / null / non-string values)."""
+        chunks = _arrow_chunks(column)
+        n = sum(len(c) for c in chunks)
+        if out is None:
+            out = np.empty(n, dtype=np.int64)
+        _bucketize_into(self, chunks, out.ctypes.data, 1, threads)
+        return out
+
+    def lookup_sequences(self, column, T: int = None, sep=",", threads: int = 0):
+        """(idx [n, T] int64 zero padded, lengths [n]) of sep-separated histories; T defaults to
+        the longest row (din_collate_fn)."""
+        chunks = _arrow_chunks(column)
+        n = sum(len(c) for c in chunks)
+        if T is None:
+            T = _max_items(chunks, sep, threads)
+        out = np.empty((n, T), dtype=np.int64)
+        lens = np.empty(n, dtype=np.int64)
+        _sequences_into(self, chunks, sep, T, out.ctypes.data, T, lens.ctypes.data, threads)
+        return out, lens
+
+
+def wechat_vocabularies(vocab_dir, fields=tuple(VOCAB_FILES), skip_empty_lines=False):
+    """{field: Vocabulary} with the reference's field -> file mapping (manual_tag_list reads
+    manual_tag_id.txt, dcn.py:66).  A missing file gives an empty vocabulary (dcn.py:86-87)."""
+    out = {}
+    for f in fields:
+        path = os.path.join(vocab_dir, VOCAB_FILES[f])
+        out[f] = Vocabulary(path, skip_empty_lines=skip_empty_lines) if os.path.exists(path) else \
+            Vocabulary(text=b"", skip_empty_lines=skip_empty_lines)
+    return out
+
+
+# ---------------------------------------------------------------- Arrow plumbing
+
+def _pa():
+    import pyarrow as pa
+    return pa
+
+
+def _arrow_chunks(column):
+    """Column -> list of pyarrow string / large_string Arrays (None for non-string columns, which
+    the reference never matches against its str-keyed dicts)."""
+    pa = _pa()
+    if isinstance(column, pa.ChunkedArray):
+        chunks = list(column.chunks)
+    elif isinstance(column, pa.Array):
+        chunks = [column]
+    else:
+        if hasattr(column, "to_numpy") and not isinstance(column, np.ndarray):  # pandas Series
+            column = column.to_numpy(dtype=object)
+        vals = list(column)
+        if all(v is None or isinstance(v, str) for v in vals):
+            chunks = [pa.array(vals, type=pa.string())]
+        else:  # mixed / non-str values: only str values can match (dict keys are str)
+            chunks = [pa.array([v if isinstance(v, str) else None for v in vals], type=pa.string())]
+    out = []
+    for c in chunks:
+        if pa.types.is_dictionary(c.type):
+            c = c.dictionary_decode()
+        if pa.types.is_string(c.type) or pa.types.is_large_string(c.type):
+            out.append(c)
+        else:
+            out.append(_NonString(len(c)))
+    return out
+
+
+class _NonString:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+def _buffers(arr):
+    """(data ptr, offsets ptr at the slice start, offset bits, validity ptr, validity bit offset)."""
+    pa = _pa()
+    bits = 64 if pa.types.is_large_string(arr.type) else 32
+    validity, offsets, data = arr.buffers()
+    off_ptr = offsets.address + arr.offset * (bits // 8)
+    data_ptr = data.address if data is not None and data.size > 0 else off_ptr  # any non-null pointer
+    valid_ptr = validity.address if (validity is not None and arr.null_count > 0) else None
+    return data_ptr, off_ptr, bits, valid_ptr, arr.offset
+
+
+def _bucketize_into(vocab, chunks, out_ptr, stride, threads):
+    lib = _lib.load()
+    pos = 0
+    for c in chunks:
+        n = len(c)
+        dst = out_ptr + pos * stride * 8
+        if isinstance(c, _NonString):
+            ctypes.memset(dst, 0, n * 8) if stride == 1 else [ctypes.memset(dst + i * stride * 8, 0, 8)
+                                                             for i in range(n)]
+        elif n:
+            d, o, bits, v, vo = _buffers(c)
+            _lib.check(lib.rk_bucketize(vocab._h, d, o, bits, v, vo, n, dst, stride, threads), "rk_bucketize")
+        pos += n
+
+
+def _max_items(chunks, sep, threads):
+    lib = _lib.load()
+    m = 0
+    for c in chunks:
+        if isinstance(c, _NonString) or not len(c):
+            continue
+        lens = np.empty(len(c), dtype=np.int64)
+        mx = ctypes.c_int64(0)
+        d, o, bits, v, vo = _buffers(c)
+        _lib.check(lib.rk_sequence_lengths(d, o, bits, v, vo, len(c), sep.encode(), lens.ctypes.data,
+                                           ctypes.byref(mx), threads), "rk_sequence_lengths")
+        m = max(m, int(mx.value))
+    return m
+
+
+def _sequences_into(vocab, chunks, sep, T, out_ptr, ld, len_ptr, threads):
+    lib = _lib.load()
+    pos = 0
+    for c in chunks:
+        n = len(c)
+        if isinstance(c, _NonString):  # not a str: the reference iterates it; only str items are rejected
+            raise TypeError("rankops.loader: a sequence column must hold strings")
+        if n:
+            d, o, bits, v, vo = _buffers(c)
+            _lib.check(lib.rk_bucketize_sequences(vocab._h, d, o, bits, v, vo, n, sep.encode(), T,
+                                                  out_ptr + pos * ld * 8, ld, len_ptr + pos * 8, threads),
+                       "rk_bucketize_sequences")
+        pos += n
+
+
+def _column(table, name):
+    pa = _pa()
+    if isinstance(table, pa.Table):
+        return table.column(name) if name in table.column_names else None
+    return table.get(name)
+
+
+def _num_rows(table):
+    pa = _pa()
+    if isinstance(table, pa.Table):
+        return table.num_rows
+    for v in table.values():
+        return len(v)
+    return 0
+
+
+def _dense_into(table, name, out: np.ndarray):
+    """row.get(f, 0.0) -> float32 (dcn.py:97): float64 values rounded to float32, nulls NaN."""
+    col = _column(table, name)
+    if col is None:
+        out[...] = 0.0
+        return
+    pa = _pa()
+    if isinstance(col, (pa.Array, pa.ChunkedArray)):
+        col = col.to_numpy(zero_copy_only=False)
+    out[...] = np.asarray(col, dtype=np.float64).astype(np.float32)
+
+
+# ---------------------------------------------------------------- batch assembly
+
+class BatchAssembler:
+    """Builds one model's forward arguments for a batch of raw rows.
+
+    All int64 index arrays and the float32 dense block are written into ONE pinned host buffer
+    (double-buffered: the next batch is assembled while the previous copy may still be in
+    flight), which reaches `device` in one asynchronous host-to-device copy on the current
+    stream; the returned tensors are views of that device buffer.  With device="cpu" the views
+    of the host buffer are returned (no copy)."""
+
+    def __init__(self, model: str, vocabs: dict, device="cuda", max_seq_length=50, threads: int = 0):
+        if model not in CATEGORY:
+            raise ValueError(f"BatchAssembler: unknown model {model!r}")
+        self.model = model
+        self.vocabs = vocabs
+        self.device = torch.device(device)
+        self.max_seq_length = max_seq_length
+        self.threads = threads
+        self._pinned = [None, None]
+        self._events = [None, None]
+        self._turn = 0
+
+    def _host_buffer(self, nbytes):
+        i = self._turn
+        self._turn ^= 1
+        if self._events[i] is not None:
+            self._events[i].synchronize()  # its previous copy must have left the buffer
+        buf = self._pinned[i]
+        if buf is None or buf.numel() < nbytes:
+            pin = self.device.type == "cuda"
+            buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, pin_memory=pin)
+            self._pinned[i] = buf
+        return i, buf
+
+    def __call__(self, table):
+        m = self.model
+        B = _num_rows(table)
+        cats = CATEGORY[m]
+        seq_T = 0
+        hist = None
+        if m == "din":
+            hist = _arrow_chunks(_column(table, DIN_SEQ)) if _column(table, DIN_SEQ) is not None else None
+            seq_T = _max_items(hist, ",", self.threads) if hist is not None else 0
+        elif m == "bst":
+            seq_T = self.max_seq_length
+        # int64 region: categories [F][B] | target [B] | seq [B][T] | lengths [B];  float32 dense [16][B] or [B][16]
+        n_i64 = len(cats) * B + (B if m == "din" else 0) + B * seq_T + (B if m in ("din", "bst") else 0)
+        n_f32 = 0 if m == "deepfm" else 16 * B
+        nbytes = n_i64 * 8 + n_f32 * 4
+        slot, buf = self._host_buffer(nbytes)
+        base = buf.data_ptr()
+        host_i64 = buf[:n_i64 * 8].view(torch.int64).numpy()
+        host_f32 = buf[n_i64 * 8:nbytes].view(torch.float32).numpy()
+
+        p = 0
+        cat_off = {}
+        for c in cats:
+            cat_off[c] = p
+            col = _column(table, c)
+            vocab = self.vocabs.get(c) if not (m == "afm" and c == "manual_tag_list") else None
+            if col is None or vocab is None:
+                host_i64[p:p + B] = 0  # no column / AFM's missing manual_tag_list.txt (afm.py:31-36)
+            else:
+                _bucketize_into(vocab, _arrow_chunks(col), base + p * 8, 1, self.threads)
+            p += B
+        tgt_off = seq_off = len_off = None
+        if m == "din":
+            tgt_off = p
+            col = _column(table, "feedid")
+            if col is None:
+                host_i64[p:p + B] = 0
+            else:
+                _bucketize_into(self.vocabs["feedid"], _arrow_chunks(col), base + p * 8, 1, self.threads)
+            p += B
+            seq_off, len_off = p, p + B * seq_T
+            if hist is None:  # row.get(col, []) on a missing column
+                host_i64[len_off:len_off + B] = 0
+            else:
+                _sequences_into(self.vocabs["feedid"], hist, ",", seq_T, base + seq_off * 8, seq_T,
+                                base + len_off * 8, self.threads)
+            p = len_off + B
+        elif m == "bst":
+            seq_off, len_off = p, p + B * seq_T
+            seq = host_i64[seq_off:len_off].reshape(B, seq_T)
+            seq[...] = 0
+            col = _column(table, "feedid")
+            if seq_T > 0:
+                if col is None:  # row.get("feedid", []) -> []: length 0
+                    host_i64[len_off:len_off + B] = 0
+                else:  # [row['feedid']]: one item (bst.py:142-150)
+                    _bucketize_into(self.vocabs["feedid"], _arrow_chunks(col), base + seq_off * 8, seq_T,
+                                    self.threads)
+                    host_i64[len_off:len_off + B] = 1
+            else:
+                host_i64[len_off:len_off + B] = 0
+            p = len_off + B
+        if n_f32:
+            dense = host_f32.reshape(16, B) if m == "din" else host_f32.reshape(B, 16)
+            for j, f in enumerate(DENSE_FEATURES):
+                _dense_into(table, f, dense[j] if m == "din" else dense[:, j])
+
+        if self.device.type == "cuda":
+            dev = buf[:nbytes].to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._events[slot] = ev
+        else:
+            dev = buf[:nbytes].clone()
+        i64 = dev[:n_i64 * 8].view(torch.int64)
+        f32 = dev[n_i64 * 8:nbytes].view(torch.float32)
+        category = {c: i64[cat_off[c]:cat_off[c] + B] for c in cats}
+        if m in ("dcn", "deepcrossing"):
+            return f32.view(B, 16), category
+        if m == "deepfm":
+            return (category,)
+        if m == "afm":
+            return f32.view(B, 16), category
+        if m == "bst":
+            return (f32.view(B, 16), category, i64[seq_off:len_off].view(B, seq_T),
+                    i64[len_off:len_off + B])
+        # din
+        dense = {f: f32[j * B:(j + 1) * B] for j, f in enumerate(DENSE_FEATURES)}
+        sequence = {DIN_SEQ: i64[seq_off:len_off].view(B, seq_T), DIN_SEQ + "_length": i64[len_off:len_off + B]}
+        target = {"feedid": i64[tgt_off:tgt_off + B]}
+        return dense, category, sequence, target

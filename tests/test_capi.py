@@ -1,7 +1,8 @@
 """CPU tests of the C ABI boundary: librankops.so loads, exports every function declared in
-include/rankops.h, the ctypes struct layouts match what a C compiler makes of the header,
+include/*.h, the ctypes struct layouts match what a C compiler makes of the header,
 and argument validation fails loudly (no device work is started on invalid input)."""
 import ctypes
+import glob
 import os
 import re
 import subprocess
@@ -13,12 +14,15 @@ import helpers as H
 from rankops import _lib
 
 HEADER = os.path.join(H.REPO, "include", "rankops.h")
+HEADERS = sorted(glob.glob(os.path.join(H.REPO, "include", "*.h")))
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rk_[a-z_0-9]+)\s*\(", text, flags=re.M)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rk_[a-z_0-9]+)\s*\(", text, flags=re.M))
+    return sorted(names)
 
 
 def test_library_loads_and_exports_header():
