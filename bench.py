@@ -14,7 +14,9 @@ no exchange step): every rank runs its own batch, `value` = all ranks' samples /
 Extra keys: `models` (N=1, rank 0) times DCN@4096, DeepFM configs[1] and BST configs[3] the
 same way; `roofline` prices the dominant kernel with HIP events around its own launches on the
 stream it runs on; `cpu_baseline` times the oracle (CPU restatement, per-call draws included)
-on a bounded sample of the same workload on this host.
+on a bounded sample of the same workload on this host; `loader` times the host input path
+(raw ID strings -> bucketed batch on the GPU -> forward, rankops.loader) against the reference's
+per-row Python Dataset logic.
 """
 from __future__ import annotations
 
@@ -60,6 +62,7 @@ def parse():
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--models", default="dcn,deepfm,bst,din_per_call")
+    ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     return ap.parse_args()
 
 
@@ -244,6 +247,75 @@ def bench_sharded(world, rank, steps, warmup):
             "scaling": "strong", "mode": "3 hipGraph segments + eager RCCL all_to_all_single"}
 
 
+# ------------------------------------------------------------------ host input path
+
+def bench_loader(model, batch, batches=8):
+    """Raw wechat rows -> DIN forward: C++ bucketing of Arrow string columns into one pinned
+    buffer + one H2D copy (rankops.BatchAssembler), then the forward; against the reference's
+    per-row Python Dataset + collate logic (oracle/bucketing.py, no pandas iloc) on this host.
+    Synthetic vocabularies at the wechat row counts, ids in the `<field>_<id>` format, histories
+    of U[1, 50] items."""
+    import tempfile
+    import pyarrow as pa
+    import helpers as H
+    import rankops
+    from oracle import bucketing as ob
+    rng = np.random.default_rng(77)
+    tmp = tempfile.mkdtemp(prefix="rk_vocab_")
+    words = {}
+    for f, n in H.WECHAT_VOCAB.items():
+        words[f] = [f"{f}_{i}" for i in rng.permutation(2 * n)[:n]]
+        with open(os.path.join(tmp, ob.VOCAB_FILES[f]), "w") as fh:
+            fh.write("".join(w + "\n" for w in words[f]))
+    tables = []
+    for b in range(batches):
+        cols = {}
+        for f, w in words.items():
+            cols[f] = pa.array([w[i] for i in rng.integers(0, len(w), batch)], type=pa.string())
+        feed = words["feedid"]
+        cols[ob.DIN_SEQ] = pa.array([",".join(feed[j] for j in rng.integers(0, len(feed), int(n)))
+                                     for n in rng.integers(1, 51, batch)], type=pa.string())
+        for f in ob.DENSE_FEATURES:
+            cols[f] = pa.array(np.log1p(rng.poisson(2.0, batch)).astype(np.float64))
+        tables.append(pa.table(cols))
+    vocabs = rankops.wechat_vocabularies(tmp)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    res = {}
+    for mode in ("device", "host"):
+        asm = rankops.BatchAssembler("din", vocabs, device="cuda", bucketing=mode)
+        for t in tables[:2]:
+            asm(t)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in tables:
+            asm(t)
+        torch.cuda.synchronize()
+        t_asm = time.perf_counter() - t0
+        with torch.no_grad():
+            for t in tables[:2]:
+                model(*asm(t))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for t in tables:
+                model(*asm(t))
+            torch.cuda.synchronize()
+        t_e2e = time.perf_counter() - t0
+        res[mode] = {"assemble_rows_per_s": round(batches * batch / t_asm, 1),
+                     "end_to_end_samples_per_s": round(batches * batch / t_e2e, 1)}
+    # the reference's Dataset + din_collate_fn logic, per row in Python, on one batch
+    ovocabs = {f: ob.vocab_indices(ob.load_vocabulary(os.path.join(tmp, ob.VOCAB_FILES[f]))) for f in ob.VOCAB_FILES}
+    rows = tables[0].to_pylist()
+    t0 = time.perf_counter()
+    ob.batch("din", rows, ovocabs)
+    t_py = time.perf_counter() - t0
+    return {"device_bucketing": res["device"], "host_bucketing": res["host"],
+            "python_dataset_rows_per_s": round(batch / t_py, 1), "batch": batch, "host_threads": threads,
+            "avg_history_items": 25.5,
+            "path": "Arrow string columns -> (device: raw bytes in one pinned buffer -> one H2D copy -> "
+                    "rk_bucketize*_device | host: rk_bucketize* into the pinned buffer -> one H2D copy) -> "
+                    "DIN forward (eager, frozen H2)"}
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank):
@@ -312,6 +384,11 @@ def main():
             del m2, inp2
             torch.cuda.empty_cache()
         result["models"] = extras
+    if rank == 0 and world == 1 and not args.no_loader:
+        try:
+            result["loader"] = bench_loader(model, args.batch)
+        except Exception as exc:  # reported, never fatal for the headline line
+            result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if not args.no_sharded:
         torch.cuda.empty_cache()
         try:

@@ -15,6 +15,7 @@
 
 #include "../../include/rankops.h"
 #include "../../include/rankops_io.h"
+#include "vocab_hash.h"
 
 #define RK_API extern "C" __attribute__((visibility("default")))
 
@@ -23,25 +24,6 @@ int fail(int code, const char* fmt, ...);  // runtime.hip: records rk_last_error
 }
 
 namespace {
-
-inline uint64_t hash_bytes(const char* p, size_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xFF51AFD7ED558CCDull);
-  while (n >= 8) {
-    uint64_t w;
-    std::memcpy(&w, p, 8);
-    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
-    h ^= h >> 29;
-    p += 8;
-    n -= 8;
-  }
-  uint64_t w = 0;
-  std::memcpy(&w, p, n);
-  h = (h ^ w ^ ((uint64_t)n << 56)) * 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 31;
-  h *= 0x94D049BB133111EBull;
-  h ^= h >> 29;
-  return h;
-}
 
 // Length of the str.isspace() character that starts at p (0 if none), UTF-8.
 inline size_t space_at(const unsigned char* p, const unsigned char* end) {
@@ -65,12 +47,6 @@ inline size_t space_before(const unsigned char* begin, const unsigned char* end)
   if (end - begin >= 3 && space_at(end - 3, end) == 3) return 3;
   return 0;
 }
-
-struct Slot {
-  uint64_t h;
-  int64_t idx;  // -1: empty
-  uint32_t off, len;
-};
 
 inline bool bit_valid(const uint8_t* bits, int64_t off, int64_t i) {
   if (!bits) return true;
@@ -115,22 +91,24 @@ void parallel_for(int64_t n, int threads, F&& body) {
 
 }  // namespace
 
+using rk::VocabSlot;
+
 struct rk_vocab {
   std::vector<char> arena;
-  std::vector<Slot> slots;
+  std::vector<VocabSlot> slots;
   uint64_t mask = 0;
   int64_t size = 0;
 
   void reserve(size_t keys) {
     size_t cap = 16;
     while (cap < 2 * keys + 2) cap <<= 1;
-    slots.assign(cap, Slot{0, -1, 0, 0});
+    slots.assign(cap, VocabSlot{0, -1, 0, 0});
     mask = cap - 1;
   }
   void put(const char* k, size_t n, int64_t idx) {
-    const uint64_t h = hash_bytes(k, n);
+    const uint64_t h = rk::vocab_hash(k, (uint32_t)n);
     for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-      Slot& e = slots[s];
+      VocabSlot& e = slots[s];
       if (e.idx < 0) {
         e.h = h;
         e.idx = idx;
@@ -146,9 +124,9 @@ struct rk_vocab {
     }
   }
   int64_t get(const char* k, size_t n) const {
-    const uint64_t h = hash_bytes(k, n);
+    const uint64_t h = rk::vocab_hash(k, (uint32_t)n);
     for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-      const Slot& e = slots[s];
+      const VocabSlot& e = slots[s];
       if (e.idx < 0) return 0;  // not in the vocabulary -> row 0 (H1)
       if (e.h == h && e.len == n && std::memcmp(arena.data() + e.off, k, n) == 0) return e.idx;
     }
@@ -218,6 +196,21 @@ RK_API int64_t rk_vocab_size(const rk_vocab* v) { return v ? v->size : -1; }
 
 RK_API void rk_vocab_free(rk_vocab* v) { delete v; }
 
+RK_API int rk_vocab_export_size(const rk_vocab* v, int64_t* slot_bytes, int64_t* arena_bytes, uint64_t* mask) {
+  if (!v || !slot_bytes || !arena_bytes || !mask) return fail(RK_ERR_INVALID, "rk_vocab_export_size: null argument");
+  *slot_bytes = (int64_t)(v->slots.size() * sizeof(VocabSlot));
+  *arena_bytes = (int64_t)std::max<size_t>(v->arena.size(), 1);
+  *mask = v->mask;
+  return RK_OK;
+}
+
+RK_API int rk_vocab_export(const rk_vocab* v, void* slots_out, void* arena_out) {
+  if (!v || !slots_out || !arena_out) return fail(RK_ERR_INVALID, "rk_vocab_export: null argument");
+  std::memcpy(slots_out, v->slots.data(), v->slots.size() * sizeof(VocabSlot));
+  if (!v->arena.empty()) std::memcpy(arena_out, v->arena.data(), v->arena.size());
+  return RK_OK;
+}
+
 static int check_column(const char* who, const rk_vocab* v, bool need_vocab, const char* data, const void* offsets,
                         int32_t offset_bits, int64_t n) {
   if (n < 0) return fail(RK_ERR_INVALID, "%s: n = %lld", who, (long long)n);
@@ -277,7 +270,8 @@ RK_API int rk_bucketize_sequences(const rk_vocab* v, const char* data, const voi
                                   int64_t* out, int64_t ld_out, int64_t* lengths, int32_t threads) {
   if (int rc = check_column("rk_bucketize_sequences", v, true, data, offsets, offset_bits, n)) return rc;
   if (T < 0 || ld_out < T || (n > 0 && T > 0 && !out)) return fail(RK_ERR_INVALID, "rk_bucketize_sequences: bad output");
-  parallel_for(n, thread_count(threads, n), [&](int64_t a, int64_t b) {
+  // a history row is ~tens of lookups: split by rows, sized by the lookups they carry
+  parallel_for(n, thread_count(threads, n * std::max<int64_t>(1, std::min<int64_t>(T, 32))), [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
       int64_t* row = out + i * ld_out;
       int64_t j = 0;

@@ -164,6 +164,16 @@ SIGNATURES = {
         ctypes.c_int,
         [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, ctypes.c_char, c_int64, c_void_p, c_int64,
          c_void_p, c_int32]),
+    "rk_vocab_export_size": (ctypes.c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(ctypes.c_uint64)]),
+    "rk_vocab_export": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "rk_bucketize_device": (
+        ctypes.c_int,
+        [c_void_p, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_void_p,
+         c_int64, c_void_p]),
+    "rk_bucketize_sequences_device": (
+        ctypes.c_int,
+        [c_void_p, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, ctypes.c_char,
+         c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
 }
 
 _lib = None

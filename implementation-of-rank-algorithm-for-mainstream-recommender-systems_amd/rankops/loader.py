@@ -3,9 +3,10 @@
 Replaces the reference's per-row `WechatDataset.__getitem__` (pandas `iloc` + Python dict
 lookups, dcn.py:94-111; din.py:131-173; bst.py:130-159; deepfm.py:56-70; afm.py:46-62;
 deepcrossing.py:86-104) and its collate (`din_collate_fn`, din.py:175-222; the default collate
-elsewhere) with column-wise C++ bucketing (`include/rankops_io.h`) over Apache Arrow string
-columns, written straight into one pinned host buffer that reaches the device in ONE
-host-to-device copy.  Semantics are the reference's bit for bit (hazard H1): the position of
+elsewhere) with column-wise bucketing (`include/rankops_io.h`) of Apache Arrow string columns:
+on the GPU (default: the raw string bytes travel in the batch's ONE pinned host-to-device copy
+and `rk_bucketize*_device` hash them against device copies of the vocabularies) or by C++ host
+threads writing the int64 rows into that pinned buffer.  Semantics are the reference's bit for bit (hazard H1): the position of
 the stripped line in the vocabulary file (last duplicate wins), 0 for unknown or null values,
 DIN histories split on ',' ('' is one item) and zero-padded to the batch maximum, BST's
 one-item sequence padded to max_seq_length.  tests/test_loader.py checks every case against
@@ -79,6 +80,35 @@ class Vocabulary:
             out = np.empty(n, dtype=np.int64)
         _bucketize_into(self, chunks, out.ctypes.data, 1, threads)
         return out
+
+    def to_device(self, device="cuda"):
+        """(slots, arena, mask): the hash table copied to `device` once (rk_vocab_export) for
+        the *_device lookups; cached per device."""
+        dev = torch.device(device)
+        key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+        cache = self.__dict__.setdefault("_device_tables", {})
+        if key not in cache:
+            lib = _lib.load()
+            sb, ab, mask = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_uint64()
+            _lib.check(lib.rk_vocab_export_size(self._h, ctypes.byref(sb), ctypes.byref(ab), ctypes.byref(mask)),
+                       "rk_vocab_export_size")
+            slots = torch.empty(sb.value, dtype=torch.uint8)
+            arena = torch.empty(ab.value, dtype=torch.uint8)
+            _lib.check(lib.rk_vocab_export(self._h, slots.data_ptr(), arena.data_ptr()), "rk_vocab_export")
+            cache[key] = (slots.to(dev), arena.to(dev), int(mask.value))
+        return cache[key]
+
+    def lookup_device(self, column, device="cuda") -> torch.Tensor:
+        """lookup() on the GPU (rk_bucketize_device): the column's raw strings are copied to
+        `device` and looked up there.  Returns an int64 device tensor."""
+        return _device_lookup(self, _arrow_chunks(column), torch.device(device), None, ",")
+
+    def lookup_sequences_device(self, column, T: int = None, sep=",", device="cuda"):
+        """lookup_sequences() on the GPU (rk_bucketize_sequences_device)."""
+        chunks = _arrow_chunks(column)
+        if T is None:
+            T = _max_items(chunks, sep, 0)
+        return _device_lookup(self, chunks, torch.device(device), T, sep)
 
     def lookup_sequences(self, column, T: int = None, sep=",", threads: int = 0):
         """(idx [n, T] int64 zero padded, lengths [n]) of sep-separated histories; T defaults to
@@ -202,6 +232,63 @@ def _sequences_into(vocab, chunks, sep, T, out_ptr, ld, len_ptr, threads):
         pos += n
 
 
+def _stage_chunk(c):
+    """Host copies (offsets rebased to 0, data, validity bytes, bit offset) of one Arrow chunk."""
+    pa = _pa()
+    n = len(c)
+    bits = 64 if pa.types.is_large_string(c.type) else 32
+    validity, offsets, data = c.buffers()
+    odt = np.int64 if bits == 64 else np.int32
+    offs = np.frombuffer(offsets, dtype=odt, count=c.offset + n + 1)[c.offset:]
+    lo, hi = int(offs[0]), int(offs[-1])
+    raw = np.frombuffer(data, dtype=np.uint8, count=hi)[lo:] if hi > lo else np.zeros(1, np.uint8)
+    vb = None
+    if c.null_count > 0:
+        b0 = c.offset >> 3
+        nb = (c.offset + n + 7) // 8 - b0
+        vb = np.frombuffer(validity, dtype=np.uint8, count=b0 + nb)[b0:]
+    return bits, (offs - offs.dtype.type(lo)), raw, vb, c.offset & 7
+
+
+def _device_lookup(vocab, chunks, dev, T, sep):
+    lib = _lib.load()
+    n = sum(len(c) for c in chunks)
+    if T is None:
+        out = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)[:n]
+        lens = None
+    else:
+        out = torch.zeros(n, T, dtype=torch.int64, device=dev)
+        lens = torch.zeros(n, dtype=torch.int64, device=dev)
+    slots, arena, mask = vocab.to_device(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    keep = []
+    r0 = 0
+    for c in chunks:
+        if isinstance(c, _NonString):
+            if T is not None:
+                raise TypeError("rankops.loader: a sequence column must hold strings")
+            r0 += len(c)
+            continue
+        if len(c) == 0:
+            continue
+        bits, offs, raw, vb, bit0 = _stage_chunk(c)
+        d_offs = torch.from_numpy(np.ascontiguousarray(offs)).to(dev)
+        d_raw = torch.from_numpy(np.ascontiguousarray(raw)).to(dev)
+        d_vb = torch.from_numpy(np.ascontiguousarray(vb)).to(dev) if vb is not None else None
+        keep += [d_offs, d_raw, d_vb]
+        args = (slots.data_ptr(), mask, arena.data_ptr(), d_raw.data_ptr(), d_offs.data_ptr(), bits,
+                d_vb.data_ptr() if d_vb is not None else None, bit0 if d_vb is not None else 0, len(c))
+        if T is None:
+            _lib.check(lib.rk_bucketize_device(*args, out.data_ptr() + r0 * 8, 1, stream), "rk_bucketize_device")
+        else:
+            _lib.check(lib.rk_bucketize_sequences_device(*args, sep.encode(), T, out.data_ptr() + r0 * T * 8, T,
+                                                         lens.data_ptr() + r0 * 8, stream),
+                       "rk_bucketize_sequences_device")
+        r0 += len(c)
+    torch.cuda.current_stream(dev).synchronize()  # the staged inputs are freed on return
+    return out if T is None else (out, lens)
+
+
 def _column(table, name):
     pa = _pa()
     if isinstance(table, pa.Table):
@@ -235,15 +322,25 @@ def _dense_into(table, name, out: np.ndarray):
 class BatchAssembler:
     """Builds one model's forward arguments for a batch of raw rows.
 
-    All int64 index arrays and the float32 dense block are written into ONE pinned host buffer
-    (double-buffered: the next batch is assembled while the previous copy may still be in
-    flight), which reaches `device` in one asynchronous host-to-device copy on the current
-    stream; the returned tensors are views of that device buffer.  With device="cpu" the views
-    of the host buffer are returned (no copy)."""
+    bucketing="device" (default on a GPU): the batch's raw Arrow string buffers (rebased per
+    column) and its float32 dense block are packed into ONE pinned host buffer, sent in one
+    asynchronous host-to-device copy, and rk_bucketize_device / rk_bucketize_sequences_device
+    turn the strings into int64 rows in HBM against the vocabularies' device tables.
+    bucketing="host": the int64 rows are produced by the C++ host lookups straight into the
+    pinned buffer, then copied the same way.  The pinned buffers are double-buffered (the next
+    batch is packed while the previous copy may still be in flight); the returned tensors are
+    views of device buffers.  With device="cpu" the host path returns host tensors."""
 
-    def __init__(self, model: str, vocabs: dict, device="cuda", max_seq_length=50, threads: int = 0):
+    def __init__(self, model: str, vocabs: dict, device="cuda", max_seq_length=50, threads: int = 0,
+                 bucketing: str = None):
         if model not in CATEGORY:
             raise ValueError(f"BatchAssembler: unknown model {model!r}")
+        bucketing = bucketing or ("device" if torch.device(device).type == "cuda" else "host")
+        if bucketing not in ("host", "device"):
+            raise ValueError(f"BatchAssembler: bucketing must be 'host' or 'device', got {bucketing!r}")
+        if bucketing == "device" and torch.device(device).type != "cuda":
+            raise ValueError("BatchAssembler: device bucketing needs a GPU device")
+        self.bucketing = bucketing
         self.model = model
         self.vocabs = vocabs
         self.device = torch.device(device)
@@ -266,6 +363,8 @@ class BatchAssembler:
         return i, buf
 
     def __call__(self, table):
+        if self.bucketing == "device":
+            return self._call_device(table)
         m = self.model
         B = _num_rows(table)
         cats = CATEGORY[m]
@@ -355,4 +454,149 @@ class BatchAssembler:
         dense = {f: f32[j * B:(j + 1) * B] for j, f in enumerate(DENSE_FEATURES)}
         sequence = {DIN_SEQ: i64[seq_off:len_off].view(B, seq_T), DIN_SEQ + "_length": i64[len_off:len_off + B]}
         target = {"feedid": i64[tgt_off:tgt_off + B]}
+        return dense, category, sequence, target
+
+    # ---------------------------------------------------------------- device bucketing
+    def _string_jobs(self, table, B):
+        """[(kind, vocab, chunks, ...)] of the string columns this model buckets."""
+        m = self.model
+        jobs = []
+        for c in CATEGORY[m]:
+            col = _column(table, c)
+            vocab = self.vocabs.get(c) if not (m == "afm" and c == "manual_tag_list") else None
+            jobs.append(("cat", c, vocab, None if (col is None or vocab is None) else _arrow_chunks(col)))
+        if m == "din":
+            col = _column(table, "feedid")
+            jobs.append(("target", "feedid", self.vocabs["feedid"], None if col is None else _arrow_chunks(col)))
+            hist = _column(table, DIN_SEQ)
+            jobs.append(("hist", DIN_SEQ, self.vocabs["feedid"], None if hist is None else _arrow_chunks(hist)))
+        elif m == "bst":
+            col = _column(table, "feedid")
+            jobs.append(("bstseq", "feedid", self.vocabs["feedid"], None if col is None else _arrow_chunks(col)))
+        return jobs
+
+    def _call_device(self, table):
+        m = self.model
+        B = _num_rows(table)
+        dev = self.device
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        jobs = self._string_jobs(table, B)
+        seq_T = 0
+        for kind, _, _, chunks in jobs:
+            if kind == "hist" and chunks is not None:
+                if any(isinstance(c, _NonString) for c in chunks):
+                    raise TypeError("rankops.loader: a sequence column must hold strings")
+                seq_T = _max_items(chunks, ",", self.threads)
+        if m == "bst":
+            seq_T = self.max_seq_length
+        # staging plan: per string chunk [offsets | validity | data], then the dense block
+        plan = []
+        nbytes = 0
+
+        def reserve(n):
+            nonlocal nbytes
+            off = nbytes
+            nbytes += (n + 15) // 16 * 16
+            return off
+
+        for j, (kind, name, vocab, chunks) in enumerate(jobs):
+            if chunks is None:
+                continue
+            for ci, c in enumerate(chunks):
+                if isinstance(c, _NonString) or len(c) == 0:
+                    continue
+                n = len(c)
+                bits = 64 if _pa().types.is_large_string(c.type) else 32
+                validity, offsets, data = c.buffers()
+                odt = np.int64 if bits == 64 else np.int32
+                offs = np.frombuffer(offsets, dtype=odt, count=c.offset + n + 1, offset=0)[c.offset:]
+                lo, hi = int(offs[0]), int(offs[-1])
+                has_nulls = c.null_count > 0
+                plan.append(dict(job=j, chunk=ci, n=n, bits=bits, offs=offs, lo=lo, hi=hi, data=data,
+                                 validity=validity if has_nulls else None, bit0=c.offset,
+                                 o_off=reserve(offs.nbytes), v_off=reserve((n + 7 + 7) // 8) if has_nulls else None,
+                                 d_off=reserve(max(hi - lo, 1))))
+        n_f32 = 0 if m == "deepfm" else 16 * B
+        f_off = reserve(n_f32 * 4)
+        slot, buf = self._host_buffer(nbytes)
+        hb = buf.numpy()
+        for p in plan:
+            o = p["offs"]
+            dst = hb[p["o_off"]:p["o_off"] + o.nbytes].view(o.dtype)
+            np.subtract(o, o.dtype.type(p["lo"]), out=dst)
+            if p["hi"] > p["lo"]:
+                hb[p["d_off"]:p["d_off"] + p["hi"] - p["lo"]] = np.frombuffer(p["data"], dtype=np.uint8,
+                                                                               count=p["hi"], offset=0)[p["lo"]:]
+            if p["validity"] is not None:
+                b0 = p["bit0"] >> 3
+                nb = (p["bit0"] + p["n"] + 7) // 8 - b0
+                hb[p["v_off"]:p["v_off"] + nb] = np.frombuffer(p["validity"], dtype=np.uint8,
+                                                               count=b0 + nb, offset=0)[b0:]
+        if n_f32:
+            dense_h = hb[f_off:f_off + n_f32 * 4].view(np.float32)
+            dense_h = dense_h.reshape(16, B) if m == "din" else dense_h.reshape(B, 16)
+            for jj, f in enumerate(DENSE_FEATURES):
+                _dense_into(table, f, dense_h[jj] if m == "din" else dense_h[:, jj])
+        staged = buf[:max(nbytes, 1)].to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._events[slot] = ev
+        sbase = staged.data_ptr()
+
+        # int64 outputs on the device: categories [F][B] | target [B] | seq [B][T] | lengths [B]
+        cats = CATEGORY[m]
+        n_i64 = len(cats) * B + (B if m == "din" else 0) + B * seq_T + (B if m in ("din", "bst") else 0)
+        i64 = torch.zeros(max(n_i64, 1), dtype=torch.int64, device=dev)
+        obase = i64.data_ptr()
+        out_off = {}
+        p_ = 0
+        for kind, name, _, _ in jobs:
+            if kind in ("cat", "target"):
+                out_off[(kind, name)] = p_
+                p_ += B
+        seq_off = len_off = None
+        if m in ("din", "bst"):
+            seq_off, len_off = p_, p_ + B * seq_T
+        row_of_chunk = {}
+        for j, (kind, name, vocab, chunks) in enumerate(jobs):
+            if chunks is None:
+                continue
+            r = 0
+            for ci, c in enumerate(chunks):
+                row_of_chunk[(j, ci)] = r
+                r += len(c)
+        for p in plan:
+            kind, name, vocab, _ = jobs[p["job"]]
+            slots, arena, mask = vocab.to_device(dev)
+            r0 = row_of_chunk[(p["job"], p["chunk"])]
+            valid = sbase + p["v_off"] if p["v_off"] is not None else None
+            bit0 = (p["bit0"] & 7) if p["v_off"] is not None else 0
+            args = (slots.data_ptr(), mask, arena.data_ptr(), sbase + p["d_off"], sbase + p["o_off"], p["bits"],
+                    valid, bit0, p["n"])
+            if kind in ("cat", "target"):
+                _lib.check(lib.rk_bucketize_device(*args, obase + (out_off[(kind, name)] + r0) * 8, 1, stream),
+                           "rk_bucketize_device")
+            elif kind == "bstseq":
+                if seq_T > 0:
+                    _lib.check(lib.rk_bucketize_device(*args, obase + (seq_off + r0 * seq_T) * 8, seq_T, stream),
+                               "rk_bucketize_device")
+            else:  # DIN history
+                _lib.check(lib.rk_bucketize_sequences_device(*args, b",", seq_T, obase + (seq_off + r0 * seq_T) * 8,
+                                                             seq_T, obase + (len_off + r0) * 8, stream),
+                           "rk_bucketize_sequences_device")
+        if m == "bst":  # [row['feedid']]: one item per row (bst.py:142-150); no column: length 0
+            has_col = any(k == "bstseq" and ch is not None for k, _, _, ch in jobs)
+            i64[len_off:len_off + B].fill_(1 if (has_col and seq_T > 0) else 0)
+        f32 = staged[f_off:f_off + n_f32 * 4].view(torch.float32)
+        category = {c: i64[out_off[("cat", c)]:out_off[("cat", c)] + B] for c in cats}
+        if m in ("dcn", "deepcrossing", "afm"):
+            return f32.view(B, 16), category
+        if m == "deepfm":
+            return (category,)
+        if m == "bst":
+            return (f32.view(B, 16), category, i64[seq_off:len_off].view(B, seq_T), i64[len_off:len_off + B])
+        dense = {f: f32[jj * B:(jj + 1) * B] for jj, f in enumerate(DENSE_FEATURES)}
+        sequence = {DIN_SEQ: i64[seq_off:len_off].view(B, seq_T), DIN_SEQ + "_length": i64[len_off:len_off + B]}
+        target = {"feedid": i64[out_off[("target", "feedid")]:out_off[("target", "feedid")] + B]}
         return dense, category, sequence, target

@@ -1,8 +1,10 @@
 /*
  * rankops_io.h — host-side C ABI of the rankops input path: raw ID strings
  * -> int64 embedding rows with the reference's bucketing semantics (hazard H1), batch-assembled
- * for one host-to-device copy.  Host code only (no GPU calls); thread-safe for concurrent calls
- * on the same vocabulary.
+ * for one host-to-device copy.  The rk_vocab_* / rk_bucketize* / rk_sequence_lengths calls are
+ * host code (thread-safe for concurrent calls on one vocabulary); the *_device variants enqueue
+ * the same lookup on a HIP stream against a vocabulary table exported to device memory
+ * (rk_vocab_export), with all column buffers in device memory.
  *
  * Reference interfaces replaced (file:line in the reference snapshot):
  *   rk_vocab_load / rk_vocab_parse   _load_vocabulary + the vocab_indices dict comprehension:
@@ -30,7 +32,7 @@
  *     values are looked up exactly as given (no strip);
  *   - sequences: value.split(sep) (an empty string is one empty item), every item looked up;
  *     length = number of items; a null value is an empty sequence (row.get(col, []));
- *     rows are zero-padded (or truncated, lengths capped: bst.py:144) to T columns.
+ *     rows are zero-padded (or truncated, lengths capped: bst.py:146) to T columns.
  *
  * String columns use the Apache Arrow layout: value i is data[offsets[i] .. offsets[i+1]),
  * offsets int32 (offset_bits = 32, Arrow "string") or int64 (64, "large_string"); validity is
@@ -71,6 +73,23 @@ int rk_bucketize_sequences(const rk_vocab* v, const char* data, const void* offs
                            int32_t offset_bits, const uint8_t* valid_bits, int64_t valid_offset,
                            int64_t n, char sep, int64_t T, int64_t* out, int64_t ld_out,
                            int64_t* lengths, int32_t threads);
+
+/* Device copy of a vocabulary: the hash table image (slot_bytes, 24-B slots) and key arena
+ * (arena_bytes) to copy into device memory as they are; `mask` is passed to the *_device calls. */
+int rk_vocab_export_size(const rk_vocab* v, int64_t* slot_bytes, int64_t* arena_bytes, uint64_t* mask);
+int rk_vocab_export(const rk_vocab* v, void* slots_out, void* arena_out);
+
+/* rk_bucketize / rk_bucketize_sequences on the GPU: slots/arena = device copies of the export,
+ * data/offsets/valid_bits/out/lengths device pointers; enqueued on `stream`, no sync.        */
+int rk_bucketize_device(const void* slots, uint64_t mask, const char* arena, const char* data,
+                        const void* offsets, int32_t offset_bits, const uint8_t* valid_bits,
+                        int64_t valid_offset, int64_t n, int64_t* out, int64_t out_stride,
+                        void* stream);
+int rk_bucketize_sequences_device(const void* slots, uint64_t mask, const char* arena,
+                                  const char* data, const void* offsets, int32_t offset_bits,
+                                  const uint8_t* valid_bits, int64_t valid_offset, int64_t n,
+                                  char sep, int64_t T, int64_t* out, int64_t ld_out,
+                                  int64_t* lengths, void* stream);
 
 #ifdef __cplusplus
 }
