@@ -96,7 +96,11 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
   const int rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
   const int64_t b = m0 + wave;
+#ifdef RK_DIN_SKIP_A  // timing experiment only (tools/din_phase_time.py): phase B on zero rows
+  const bool live = false;
+#else
   const bool live = wave < rows;
+#endif
   float* row = buf0 + wave * a.ld0;
   uint32_t* flags = a.flags;
 
@@ -246,6 +250,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
 
   // ---- Phase B: fcn tail + head over the 16 rows
+#ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
+  return;
+#endif
   mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid);
 }
 

@@ -4,6 +4,8 @@
 //
 // Reference tails covered: dcn.py:144-152,175-180; deepfm.py:100-112,143-151;
 // din.py:272-285,312-316; bst.py:203-214,245-247; deepcrossing.py:25-42,157-162.
+#include <cstdlib>
+
 #include "mlp_core.h"
 
 namespace rk {
@@ -23,32 +25,63 @@ struct MlpArgs {
   int off1;      // float offset of buffer 1
 };
 
+// RT row tiles of 16 rows per workgroup: every weight element streamed from L2 serves 16*RT rows
+template <int RT>
 __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int ROWS = kMlpRows * RT;
   const int tid = threadIdx.x;
-  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.M - m0);
+#ifdef RK_MLP_PHASES
+  const unsigned long long k_t0 = clock64();
+  const unsigned long long w0 = wall_clock64();
+  if (tid == 0) {
+    atomicMin(&g_mlp_span[0], w0);
+    atomicMax(&g_mlp_span[2], w0);  // last workgroup start
+  }
+#endif
+  const int64_t m0 = (int64_t)blockIdx.x * ROWS;
+  const int rows = (int)min<int64_t>(ROWS, a.M - m0);
   float* const buf0 = sm;
   float* const buf1 = sm + a.off1;
 
-  // stage the input tile, zero-padded to a multiple of 64 columns
+  // stage the input tile, zero-padded to a multiple of 64 columns (inside mlp_rows: after layer
+  // 0's weight prefetch has been issued)
   const int K0p = pad64(a.K0);
-  if (a.x_vec) {
-    const int q = K0p / 4;
-    for (int i = tid; i < kMlpRows * q; i += kMlpThreads) {
-      const int r = i / q, c = (i % q) * 4;
-      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-      if (r < rows && c < a.K0) v = *reinterpret_cast<const f32x4_t*>(a.x + (m0 + r) * a.ldx + c);
-      *reinterpret_cast<f32x4_t*>(buf0 + r * a.ld0 + c) = v;
+  auto stage = [&]() {
+    if (a.x_vec) {
+      const int q = K0p / 4;
+      for (int i = tid; i < ROWS * q; i += kMlpThreads) {
+        const int r = i / q, c = (i % q) * 4;
+        f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+        if (r < rows && c < a.K0) v = *reinterpret_cast<const f32x4_t*>(a.x + (m0 + r) * a.ldx + c);
+        *reinterpret_cast<f32x4_t*>(buf0 + r * a.ld0 + c) = v;
+      }
+    } else {
+      for (int i = tid; i < ROWS * K0p; i += kMlpThreads) {
+        const int r = i / K0p, c = i % K0p;
+        buf0[r * a.ld0 + c] = (r < rows && c < a.K0) ? a.x[(m0 + r) * a.ldx + c] : 0.f;
+      }
     }
-  } else {
-    for (int i = tid; i < kMlpRows * K0p; i += kMlpThreads) {
-      const int r = i / K0p, c = i % K0p;
-      buf0[r * a.ld0 + c] = (r < rows && c < a.K0) ? a.x[(m0 + r) * a.ldx + c] : 0.f;
+  };
+  mlp_rows<RT>(a.L, a.nl, a.K0, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, a.y, a.ldy, tid, stage);
+  MLP_MARK(3 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. head)
+#ifdef RK_MLP_PHASES
+  if (tid == 0) {
+    const unsigned long long w1 = wall_clock64();
+    atomicMax(&g_mlp_span[1], w1);
+    atomicMax(&g_mlp_span[3], w1 - w0);  // longest workgroup
+    atomicAdd(&g_mlp_span[4], w1 - w0);  // sum of workgroup durations
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (blockIdx.x < 8192) {
+      g_mlp_wg[blockIdx.x][0] = hw;
+      g_mlp_wg[blockIdx.x][1] = xcc;
+      g_mlp_wg[blockIdx.x][2] = (unsigned)(w1 - w0);
+      g_mlp_wg[blockIdx.x][3] = (unsigned)(w0 - g_mlp_span[0]);
     }
   }
-  __syncthreads();
-  mlp_rows(a.L, a.nl, a.K0, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, a.y, a.ldy, tid);
+#endif
 }
 
 __global__ void mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int n, int k, int np, int kp,
@@ -129,8 +162,15 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   // row stride = width + 4 (width is a multiple of 64): conflict-free float4 row reads
   a.ld0 = need0 + 4;
   a.ld1 = need1 + 4;
-  a.off1 = kMlpRows * a.ld0;
-  const size_t shm = (size_t)kMlpRows * (a.ld0 + a.ld1) * sizeof(float);
+  // rows per workgroup: 16.  32 (two row tiles per wave: half the L2 weight traffic per row)
+  // measured slower at batch 4096 — DCN 46.6 vs 52.6 us: half the workgroups, same per-workgroup
+  // latency — and is kept as an option (RANKOPS_MLP_ROWS=32) where the buffers fit in LDS.
+  const size_t row_bytes = (size_t)(a.ld0 + a.ld1) * sizeof(float);
+  int rt = 1;
+  if (const char* e = getenv("RANKOPS_MLP_ROWS")) rt = (atoi(e) == 32 && 32 * row_bytes <= 160 * 1024) ? 2 : 1;
+  const int rows_per_wg = kMlpRows * rt;
+  a.off1 = rows_per_wg * a.ld0;
+  const size_t shm = rows_per_wg * row_bytes;
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward: widths need %zu B of LDS", shm);
   a.x = x;
   a.ldx = ldx;
@@ -140,13 +180,17 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   a.y = y;
   a.ldy = ldy;
   if (M == 0) return RK_OK;
-  const int64_t blocks = (M + kMlpRows - 1) / kMlpRows;
+  const int64_t blocks = (M + rows_per_wg - 1) / rows_per_wg;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward: M too large");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)mlp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mlp_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mlp_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  mlp_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  if (rt == 2)
+    mlp_kernel<2><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  else
+    mlp_kernel<1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   return check_launch("rk_mlp_forward");
 }

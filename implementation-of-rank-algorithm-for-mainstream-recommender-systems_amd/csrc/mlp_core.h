@@ -1,13 +1,17 @@
 // Fused-MLP machinery shared by rk_mlp_forward (mlp.hip) and the fused DIN forward (din_fused.hip).
 //
-// 16 rows per workgroup of 16 waves (4 per SIMD).  Activations live in two LDS buffers; each
-// layer reads one and writes the other.  Layer math is FP32 MFMA v_mfma_f32_16x16x4_f32 (exact
-// f32): wave w owns output tiles w and w+16 (16 columns each).  Per 16-deep K chunk a lane reads
-// one float4 of its A row from LDS (k = 16c + 4*(lane>>4) + e) and one float4 of its weight row
-// per tile from global memory, then issues 4 MFMAs per tile.  Weights are pre-packed
-// (rk_mlp_pack_weight: rows padded to 64 columns, K padded to 64, zero fill), so every weight
-// load is an unconditional aligned float4 and the chunk count is a multiple of the 4-deep
-// register prefetch ring; weights stay L2-resident across the workgroups.
+// 16 rows (x RT row tiles) per workgroup of 16 waves (4 per SIMD).  Activations live in two LDS
+// buffers; each layer reads one and writes the other.  Layer math is FP32 MFMA
+// v_mfma_f32_16x16x4_f32 (exact f32): wave w owns output tiles w and w+16 (16 columns each).  Per
+// 16-deep K chunk a lane reads one float4 of its A row from LDS (k = 16c + 4*(lane>>4) + e, one
+// chunk ahead) and one float4 of its weight row per tile from global memory (a 4-deep register
+// ring), then issues 4 MFMAs per tile.  Weights are pre-packed (rk_mlp_pack_weight: rows padded
+// to 64 columns, K padded to 64, zero fill), so every weight load is an unconditional aligned
+// float4.  Each layer's weight ring and per-column epilogue parameters are issued before the
+// barrier that closes the previous layer (LayerPipe::prepare + an LDS-only barrier), and the
+// epilogue parameters sit in registers: read after the LDS stores they were re-fetched per
+// element behind the whole weight-load queue (tools/mlp_phases.hip: DeepFM layer-0 epilogue
+// 38k -> 8k cycles; DIN 48.8 -> 51.4 M samples/s).
 #pragma once
 
 #include "common.h"
@@ -18,6 +22,7 @@ constexpr int kMlpRows = 16;
 constexpr int kMlpWaves = 16;
 constexpr int kMlpThreads = 64 * kMlpWaves;
 constexpr int kMlpPD = 4;    // prefetch depth (chunks)
+
 constexpr int kMlpPad = 64;  // K and N padding of packed weights
 constexpr int kMlpMaxN = 512;
 
@@ -29,116 +34,231 @@ __device__ __forceinline__ f32x4_t mfma16(float a, float b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float layer_act(const rk_mlp_layer& L, float z, int n) {
-  switch (L.act) {
-    case RK_ACT_RELU:
-      return z < 0.f ? 0.f : z;
-    case RK_ACT_LEAKY:
-      return z > 0.f ? z : z * L.slope;
-    case RK_ACT_DICE: {
-      const float xn = z * L.act_scale[n] + L.act_shift[n];
-      const float p = 1.0f / (1.0f + expf(-xn));
-      return L.act_alpha[n] * (1.0f - p) * z + p * z;
-    }
-    case RK_ACT_PRELU: {
-      const float a = L.act_alpha[L.act_alpha_len == 1 ? 0 : n];
-      return z > 0.f ? z : a * z;
-    }
-    default:
-      return z;
-  }
+// Per-column epilogue parameters of one output column, loaded into registers before the MFMA
+// loop: read in the epilogue they would be re-fetched after every LDS store (the compiler cannot
+// prove the generic output pointer does not alias them), each fetch waiting on the whole vmcnt
+// queue of weight loads.
+struct ColEpi {
+  float bias, pre_s, pre_b, act_s, act_b, alpha, post_s, post_b;
+};
+
+__device__ __forceinline__ ColEpi col_epi(const rk_mlp_layer& L, int n) {
+  ColEpi e;
+  e.bias = L.bias ? L.bias[n] : 0.f;
+  e.pre_s = L.pre_scale ? L.pre_scale[n] : 1.f;
+  e.pre_b = L.pre_scale ? L.pre_shift[n] : 0.f;
+  e.post_s = L.post_scale ? L.post_scale[n] : 1.f;
+  e.post_b = L.post_scale ? L.post_shift[n] : 0.f;
+  e.act_s = L.act == RK_ACT_DICE ? L.act_scale[n] : 0.f;
+  e.act_b = L.act == RK_ACT_DICE ? L.act_shift[n] : 0.f;
+  e.alpha = L.act == RK_ACT_DICE ? L.act_alpha[n]
+          : L.act == RK_ACT_PRELU ? L.act_alpha[L.act_alpha_len == 1 ? 0 : n] : 0.f;
+  return e;
 }
 
-// One layer for a wave owning TPW tiles (t = wave + 16*j).
-template <int TPW>
-__device__ __forceinline__ void mlp_layer(const rk_mlp_layer& L, const float* __restrict__ in, int ldin,
-                                          float* __restrict__ out, int ldout, int Kp, int wave, int lane) {
-  const int li = lane & 15, kq = 4 * (lane >> 4);
-  const int kchunks = Kp / 16;  // multiple of kMlpPD
-  const int64_t ldw = L.ldw;
-  const float* wrow[TPW];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) wrow[j] = L.w + (int64_t)(16 * (wave + kMlpWaves * j) + li) * ldw + kq;
+// The element-wise epilogue in the reference's order (bias, residual, pre-BN, activation,
+// post-BN); `act` is wave-uniform.
+__device__ __forceinline__ float col_apply(const ColEpi& e, int act, float slope, float z, bool has_res, float res,
+                                           bool has_pre, bool has_post) {
+  z += e.bias;
+  if (has_res) z = res + z;
+  if (has_pre) z = z * e.pre_s + e.pre_b;
+  switch (act) {
+    case RK_ACT_RELU:
+      z = z < 0.f ? 0.f : z;
+      break;
+    case RK_ACT_LEAKY:
+      z = z > 0.f ? z : z * slope;
+      break;
+    case RK_ACT_DICE: {
+      const float p = 1.0f / (1.0f + expf(-(z * e.act_s + e.act_b)));
+      z = e.alpha * (1.0f - p) * z + p * z;
+      break;
+    }
+    case RK_ACT_PRELU:
+      z = z > 0.f ? z : e.alpha * z;
+      break;
+    default:
+      break;
+  }
+  if (has_post) z = z * e.post_s + e.post_b;
+  return z;
+}
 
-  f32x4_t acc[TPW];
-  f32x4_t ring[kMlpPD][TPW];
+// Optional per-layer shader-clock counters (tools/mlp_phases.hip builds with RK_MLP_PHASES):
+// g_mlp_phase[3*l + {0,1,2}] += cycles from the layer's start to (MFMA loop done, epilogue
+// stored, barrier passed), wave 0 of each workgroup.
+#ifdef RK_MLP_PHASES
+__device__ unsigned long long g_mlp_phase[3 * RK_MLP_MAX_LAYERS + 2];
+__device__ unsigned long long g_mlp_span[5];  // wall_clock64 (100 MHz): first start, last end, last start, max, sum
+__device__ unsigned g_mlp_wg[8192][4];  // per workgroup: HW_ID, XCC_ID, wall duration, start offset (10 ns)
+#define MLP_MARK(i, t0) \
+  do {                  \
+    if (tid == 0) atomicAdd(&g_mlp_phase[i], clock64() - (t0)); \
+  } while (0)
+#else
+#define MLP_MARK(i, t0) \
+  do {                  \
+  } while (0)
+#endif
+
+// Weight ring and per-column epilogue parameters of one layer for a wave owning TPW column tiles
+// (t = wave + 16*j).  prepare() issues the first PD weight chunks and the parameter loads; it runs
+// before the barrier that closes the previous layer, so that latency overlaps the previous
+// layer's tail instead of opening this one.
+template <int TPW, int PD = kMlpPD>
+struct LayerPipe {
+  const float* wrow[TPW];
+  f32x4_t ring[PD][TPW];
+  ColEpi ep[TPW];
+  __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int wave, int lane) {
+    const int li = lane & 15, kq = 4 * (lane >> 4);
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TPW; ++j) {
+      const int n = 16 * (wave + kMlpWaves * j) + li;
+      wrow[j] = L.w + (int64_t)n * L.ldw + kq;
+      ep[j] = col_epi(L, n < L.n ? n : 0);
+    }
 #pragma unroll
-  for (int s = 0; s < kMlpPD; ++s)
+    for (int s = 0; s < PD; ++s)
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + 16 * s);
+      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + 16 * s);
+  }
+};
+
+// One layer (weights already in flight in P) over RT row tiles of 16 rows: each weight float4
+// feeds RT x 4 MFMAs.
+template <int TPW, int RT = 1, int PD = kMlpPD>
+__device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_layer& L, const float* __restrict__ in,
+                                          int ldin, float* __restrict__ out, int ldout, int Kp, int wave, int lane,
+                                          int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  const int kchunks = Kp / 16;  // multiple of PD
+  f32x4_t acc[TPW][RT];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[j][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const float* arow = in + li * ldin + kq;
-  for (int c0 = 0; c0 < kchunks; c0 += kMlpPD) {
+  // A float4s run one chunk ahead of their MFMAs (the sched_barrier below keeps the compiler
+  // from hoisting the next chunk's reads itself)
+  f32x4_t an[RT];
 #pragma unroll
-    for (int s = 0; s < kMlpPD; ++s) {
+  for (int t = 0; t < RT; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin);
+  for (int c0 = 0; c0 < kchunks; c0 += PD) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) {
       const int c = c0 + s;
-      const f32x4_t av = *reinterpret_cast<const f32x4_t*>(arow + 16 * c);
+      f32x4_t av[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) av[t] = an[t];
+      const int cA = min(c + 1, kchunks - 1);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin + 16 * cA);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int j = 0; j < TPW; ++j) acc[j] = mfma16(av[e], ring[s][j][e], acc[j]);
-      // refill this slot with chunk c + PD (clamped: the tail re-reads the last chunk, unused)
-      const int cn = min(c + kMlpPD, kchunks - 1);
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + 16 * cn);
+          for (int t = 0; t < RT; ++t) acc[j][t] = mfma16(av[t][e], P.ring[s][j][e], acc[j][t]);
+      // refill this slot with chunk c + PD (clamped: the tail re-reads the last chunk, unused)
+      const int cn = min(c + PD, kchunks - 1);
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) P.ring[s][j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + 16 * cn);
       // keep the refill here: sinking it to the end of the unrolled body would leave each
       // slot's latency uncovered by the other slots' MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 
+#ifdef RK_MLP_PHASES
+  if (wave == 0 && lane == 0) atomicAdd(&g_mlp_phase[dbg_mark], clock64() - dbg_t0);
+#endif
+  const int act = L.act;
+  const float slope = L.slope;
+  const bool has_res = L.residual != 0, has_pre = L.pre_scale != nullptr, has_post = L.post_scale != nullptr;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int n = 16 * (wave + kMlpWaves * j) + li;
     const bool real = n < L.n;
+    // x + f(x): the previous layer's input still sits in `out` (read all, then write: same lane)
+    float res[RT][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = (lane >> 4) * 4 + r;
-      float z = 0.f;
-      if (real) {
-        z = acc[j][r];
-        if (L.bias) z += L.bias[n];
-        // x + f(x): the previous layer's input still sits in `out` (read-then-write, same lane)
-        if (L.residual) z = out[row * ldout + n] + z;
-        if (L.pre_scale) z = z * L.pre_scale[n] + L.pre_shift[n];
-        z = layer_act(L, z, n);
-        if (L.post_scale) z = z * L.post_scale[n] + L.post_shift[n];
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) res[t][r] = has_res ? out[(16 * t + (lane >> 4) * 4 + r) * ldout + n] : 0.f;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * t + (lane >> 4) * 4 + r;
+        const float z =
+            real ? col_apply(P.ep[j], act, slope, acc[j][t][r], has_res, res[t][r], has_pre, has_post) : 0.f;
+        out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
       }
-      out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
-    }
   }
 }
 
-// Runs layers[0..nl) on the 16 rows staged (zero-padded to pad64(K0) columns) in buf0, then the
-// head (one wave per row) or a plain copy of the last activation to y.  Must be called by all
-// kMlpThreads threads of the workgroup.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its global
+// loads, so the next layer's weight prefetch stays in flight across it.
+__device__ __forceinline__ void mlp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Runs layers[0..nl) on the 16*RT rows staged (zero-padded to pad64(K0) columns) in buf0, then
+// the head (one wave per row) or a plain copy of the last activation to y.  Must be called by
+// all kMlpThreads threads of the workgroup.
+// `stage()` (default: nothing) fills buf0 after layer 0's weights are already in flight, so the
+// two memory round trips that open the workgroup overlap; a barrier follows it.
+struct NoStage {
+  __device__ void operator()() const {}
+};
+
+template <int RT = 1, class Stage = NoStage>
 __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers, int nl, int K0, float* buf0,
                                          int ld0, float* buf1, int ld1, int64_t m0, int rows,
-                                         const rk_epilogue& h, float* y, int64_t ldy, int tid) {
+                                         const rk_epilogue& h, float* y, int64_t ldy, int tid,
+                                         Stage stage = Stage()) {
   const int lane = tid & 63, wave = tid >> 6;
+  LayerPipe<2> p2;
+  LayerPipe<1> p1;
+  auto prepare = [&](int l) {
+    const int nt = pad64(layers[l].n) / 16;  // multiple of 4
+    if (wave + kMlpWaves < nt)
+      p2.prepare(layers[l], wave, lane);
+    else if (wave < nt)
+      p1.prepare(layers[l], wave, lane);
+  };
+  if (nl > 0) prepare(0);
+  stage();
+  mlp_lds_barrier();
   int Kp = pad64(K0);
   for (int l = 0; l < nl; ++l) {
+    const unsigned long long t0 =
+#ifdef RK_MLP_PHASES
+        clock64();
+#else
+        0;
+#endif
     const rk_mlp_layer& L = layers[l];
-    const int ntiles = pad64(L.n) / 16;  // multiple of 4
+    const int ntiles = pad64(L.n) / 16;
     const float* in = (l & 1) ? buf1 : buf0;
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
-    if (wave + kMlpWaves < ntiles) {
-      mlp_layer<2>(L, in, ldin, out, ldout, Kp, wave, lane);
-    } else if (wave < ntiles) {
-      mlp_layer<1>(L, in, ldin, out, ldout, Kp, wave, lane);
-    }
-    __syncthreads();
+    if (wave + kMlpWaves < ntiles)
+      mlp_layer<2, RT>(p2, L, in, ldin, out, ldout, Kp, wave, lane, 3 * l, t0);
+    else if (wave < ntiles)
+      mlp_layer<1, RT>(p1, L, in, ldin, out, ldout, Kp, wave, lane, 3 * l, t0);
+    if (l + 1 < nl) prepare(l + 1);
+    MLP_MARK(3 * l + 1, t0);
+    mlp_lds_barrier();
+    MLP_MARK(3 * l + 2, t0);
     Kp = pad64(L.n);
   }
   const float* fin = (nl & 1) ? buf1 : buf0;
   const int ldf = (nl & 1) ? ld1 : ld0;
   const int K = nl ? layers[nl - 1].n : K0;
   if (h.head_w) {
-    if (wave < rows) {
-      const int r = wave;
+    for (int r = wave; r < rows; r += kMlpWaves) {
       float p = 0.f;
       for (int n = lane; n < K; n += 64) p = fmaf(fin[r * ldf + n], h.head_w[n], p);
       p = wave_sum(p);

@@ -5,6 +5,8 @@
 //   2  A from LDS, B float4 streamed from a 64 KB global weight (L2-resident), 1-chunk prefetch
 //   3  A from LDS, B streamed in 4-chunk super-chunks, double buffered (bst_block WStream)
 //   4  A from LDS, B float4 from LDS
+//   5+ MLP-shaped (mlp_core.h): 1024-thread workgroups (4 waves / SIMD), v_mfma_f32_16x16x4_f32,
+//      one 16-row A tile from LDS, TPW weight tiles streamed with a PD-chunk register ring
 // Prints achieved TFLOP/s and cycles per MFMA per SIMD.
 #include <hip/hip_runtime.h>
 
@@ -104,6 +106,79 @@ void run(const float* W, float* out, int cus) {
          MODE, NCH, ms, tf, 100 * tf / 157.3, per_wg / mfma_per_simd, per_wg / (ms * 1e6));
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// MLP-shaped stream: K = 512 (32 chunks of 16), W tile rows read from a 256 KB weight (L2),
+// TPW tiles per wave, ring depth PD, A one chunk ahead (APF) or in the same chunk.
+template <int TPW, int PD, bool APF, bool SPLIT>
+__global__ __launch_bounds__(1024) void calib_mlp(const float* __restrict__ W, float* out, int iters) {
+  __shared__ float A[16 * 516];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 16 * 516; i += 1024) A[i] = 0.001f * (i & 7);
+  __syncthreads();
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  constexpr int KC = 32;
+  const float* wrow[TPW];
+  for (int j = 0; j < TPW; ++j) wrow[j] = W + (size_t)(16 * ((wave + 16 * j) & 15) + li) * 512 + kq;
+  f32x4 acc[TPW][2];
+  for (int j = 0; j < TPW; ++j) acc[j][0] = acc[j][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const float* arow = A + li * 516 + kq;
+  for (int it = 0; it < iters; ++it) {
+    f32x4 ring[PD][TPW];
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4*>(wrow[j] + 16 * s);
+    f32x4 an = *reinterpret_cast<const f32x4*>(arow);
+    for (int c0 = 0; c0 < KC; c0 += PD) {
+#pragma unroll
+      for (int s = 0; s < PD; ++s) {
+        const int c = c0 + s;
+        f32x4 av;
+        if (APF) {
+          av = an;
+          an = *reinterpret_cast<const f32x4*>(arow + 16 * min(c + 1, KC - 1));
+        } else {
+          av = *reinterpret_cast<const f32x4*>(arow + 16 * c);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < TPW; ++j) {
+            f32x4& a = acc[j][SPLIT ? (e & 1) : 0];
+            a = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], ring[s][j][e], a, 0, 0, 0);
+          }
+        const int cn = min(c + PD, KC - 1);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4*>(wrow[j] + 16 * cn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  float sacc = 0.f;
+  for (int j = 0; j < TPW; ++j)
+    for (int r = 0; r < 4; ++r) sacc += acc[j][0][r] + acc[j][1][r];
+  out[blockIdx.x * 1024 + threadIdx.x] = sacc;
+}
+
+template <int TPW, int PD, bool APF, bool SPLIT>
+void run_mlp(const float* W, float* out, int cus) {
+  const int iters = 100;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  calib_mlp<TPW, PD, APF, SPLIT><<<cus, 1024>>>(W, out, iters);
+  hipEventRecord(e0);
+  calib_mlp<TPW, PD, APF, SPLIT><<<cus, 1024>>>(W, out, iters);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double flop = (double)cus * 16 * iters * 32 * 4 * TPW * 16 * 16 * 4 * 2;
+  printf("mlp TPW %d PD %d Aprefetch %d split-acc %d: %.3f ms  %.1f TFLOP/s (%.1f%%)\n", TPW, PD, (int)APF,
+         (int)SPLIT, ms, flop / (ms * 1e-3) / 1e12, 100 * flop / (ms * 1e-3) / 157.3e12);
+}
+
 int main() {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -123,5 +198,15 @@ int main() {
   run<2, 3>(W, out, cus);
   run<1, 4>(W, out, cus);
   run<2, 4>(W, out, cus);
+  float* W2;
+  hipMalloc(&W2, 512 * 512 * 4);
+  hipMemset(W2, 0, 512 * 512 * 4);
+  run_mlp<1, 4, false, false>(W2, out, cus);
+  run_mlp<1, 4, true, false>(W2, out, cus);
+  run_mlp<1, 4, true, true>(W2, out, cus);
+  run_mlp<1, 8, true, true>(W2, out, cus);
+  run_mlp<2, 4, false, false>(W2, out, cus);
+  run_mlp<2, 4, true, false>(W2, out, cus);
+  run_mlp<2, 8, true, false>(W2, out, cus);
   return 0;
 }
