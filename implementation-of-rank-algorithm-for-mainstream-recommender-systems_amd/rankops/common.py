@@ -217,10 +217,24 @@ class Layer:
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
 FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
 FUSED_BST = True  # BST: all transformer blocks + pooling in one rk_bst_forward_blocks launch
+# A first layer this wide runs as its own 2D-tiled GEMM (rk_linear_tiled) before the fused tail:
+# in the 16-row fused kernel every CU would stream the whole weight (DeepFM 960 -> 512: 2 MB)
+TILED_FIRST_MIN_K = 512
+TILED_FIRST_MIN_ROWS = 2048
 
 
 def _pad64(v: int) -> int:
     return (v + 63) // 64 * 64
+
+
+_CUS = {}
+
+
+def _num_cus(device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _CUS:
+        _CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _CUS[idx]
 
 
 def fused_mlp_fits(k0: int, widths) -> bool:
@@ -266,7 +280,18 @@ def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit:
     if FUSED_MLP and fused_mlp_fits(x.shape[1], [l.linear.out_features for l in layers]):
         mls = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs()) for l in layers]
         ep = ops.make_epilogue(head_w=head_w, head_b=head.bias, head_logit=logit, head_prob=prob, **head_kwargs)
-        ops.mlp_forward(x, mls, ep)
+        # leading layers at least TILED_FIRST_MIN_K wide run as 2D-tiled GEMMs (64 x 128 tiles)
+        # while that grid still fills the GPU (DeepFM: 960 -> 512 yes, 512 -> 256 no: 128 tiles
+        # measured slower than the fused kernel), the rest fused
+        i = 0
+        cus = _num_cus(dev)
+        while (TILED_FIRST_MIN_K and i < len(mls) - 1 and h.shape[1] >= TILED_FIRST_MIN_K
+               and B >= TILED_FIRST_MIN_ROWS and mls[i].residual == 0
+               and ((B + 63) // 64) * ((_pad64(mls[i].n) + 127) // 128) >= cus):
+            y = torch.empty(B, layers[i].linear.out_features, device=dev, dtype=torch.float32)
+            ops.linear_tiled(h, mls[i], y)
+            h, i = y, i + 1
+        ops.mlp_forward(h, mls[i:], ep)
         return
     for i, layer in enumerate(layers):
         last = i == len(layers) - 1

@@ -231,6 +231,15 @@ def mlp_forward(x: torch.Tensor, layers, head: Epilogue = None, out: torch.Tenso
     return out
 
 
+def linear_tiled(x: torch.Tensor, layer: "_lib.MlpLayer", out: torch.Tensor, K: int = None):
+    """One packed MLP layer as a 2D-tiled GEMM (rk_linear_tiled) into `out` [M, n]."""
+    lib = _lib.load()
+    K = x.shape[1] if K is None else K
+    check(lib.rk_linear_tiled(x.data_ptr(), x.stride(0), x.shape[0], K, ctypes.byref(layer), out.data_ptr(),
+                              out.stride(0), _lib.stream_of(x)), "rk_linear_tiled")
+    return out
+
+
 def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
                 head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None):
     """Whole DIN eval forward (row gather, attention, fcn tail, head, l2 partials) in one launch."""

@@ -27,6 +27,7 @@
  *   rk_afm_forward     AFM.forward()                         afm.py:92-119
  *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
+ *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -236,6 +237,13 @@ int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k, float*
  * set, else the last activation is written to y.                                          */
 int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_mlp_layer* layers,
                    int32_t nlayers, const rk_epilogue* head, float* y, int64_t ldy, void* stream);
+
+/* One MLP layer as a 2D-tiled GEMM (64-row x 128-column tiles): y[M, n] = epilogue(x . W^T) with
+ * W packed by rk_mlp_pack_weight (ldw = pad64(K)) and the element-wise part of the rk_mlp_layer
+ * epilogue (bias, BatchNorm affines, activation; no residual).  For a wide first layer
+ * (deepfm.py:100-112, 960 -> 512) it reads every weight 64 times per 4096 rows instead of 256. */
+int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_mlp_layer* layer,
+                    float* y, int64_t ldy, void* stream);
 
 int rk_bn_fold(const float* mean, const float* var, const float* weight, const float* bias,
                float eps, int32_t n, float* scale, float* shift, void* stream);

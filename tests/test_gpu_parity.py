@@ -294,3 +294,34 @@ def test_bst_fused_blocks_oob_sequence_index_is_flagged():
     with torch.no_grad():
         H.call_model(model, "bst", inp)
     assert rankops.error_flags(reset=True) & 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [True, False])
+def test_deepfm_wide_first_layer_tiled(tiled, monkeypatch):
+    """DeepFM configs[1] shape (30 fields x 32: a 960-wide first layer) at batch >= 2048 runs its
+    first layer through rk_linear_tiled; both paths match the oracle and each other."""
+    monkeypatch.setattr(rankops.common, "TILED_FIRST_MIN_K", 512 if tiled else 0)
+    cfg = {"dim": 32, "fields": FIELDS30}
+    out, ref = run_pair("deepfm", cfg, B=2100)
+    _compare(out, ref, f"deepfm-wide-tiled{tiled}")
+
+
+@pytest.mark.gpu
+def test_linear_tiled_direct():
+    """rk_linear_tiled against torch fp32 on ragged shapes (M not a multiple of 64, n not a
+    multiple of 128, K not a multiple of 256), with BatchNorm affine + LeakyReLU."""
+    g = torch.Generator().manual_seed(4)
+    for M, K, n in ((333, 960, 512), (64, 70, 50), (1000, 300, 200)):
+        x = torch.randn(M, K, generator=g).cuda()
+        w = (0.05 * torch.randn(n, K, generator=g)).cuda()
+        b = torch.randn(n, generator=g).cuda()
+        sc = (1 + 0.1 * torch.randn(n, generator=g)).cuda()
+        sh = (0.1 * torch.randn(n, generator=g)).cuda()
+        packed = rankops.ops.pack_mlp_weight(w)
+        layer = rankops.ops.make_mlp_layer(w, packed, bias=b, pre_scale=sc, pre_shift=sh, act="leaky", slope=0.01)
+        y = torch.empty(M, n, device="cuda")
+        rankops.ops.linear_tiled(x, layer, y)
+        z = (x.double() @ w.double().T + b.double()) * sc.double() + sh.double()
+        ref = torch.where(z > 0, z, 0.01 * z).float()
+        torch.testing.assert_close(y, ref, atol=1e-4, rtol=1e-4)
