@@ -16,7 +16,8 @@ same way; `roofline` prices the dominant kernel with HIP events around its own l
 stream it runs on; `cpu_baseline` times the oracle (CPU restatement, per-call draws included)
 on a bounded sample of the same workload on this host; `loader` times the host input path
 (raw ID strings -> bucketed batch on the GPU -> forward, rankops.loader) against the reference's
-per-row Python Dataset logic.
+per-row Python Dataset logic; `eval_metrics` times evaluate()'s loss / accuracy / AUC over 256
+eval batches on the device (rankops.EvalAccumulator) against the reference's host-copy + sklearn path.
 """
 from __future__ import annotations
 
@@ -316,6 +317,54 @@ def bench_loader(model, batch, batches=8):
                     "DIN forward (eager, frozen H2)"}
 
 
+def bench_metrics(batch, batches=256):
+    """evaluate()'s metric bookkeeping over `batches` eval batches already on the GPU: rankops
+    EvalAccumulator (rk_eval_batch per batch, rk_auc once) against the reference's path
+    (dcn.py:227-237: loss.item() + .cpu().numpy() per batch, then sklearn accuracy / roc_auc)."""
+    import rankops
+    from sklearn.metrics import accuracy_score, roc_auc_score
+    g = torch.Generator(device="cuda").manual_seed(5)
+    logits = [torch.randn(batch, device="cuda", generator=g) * 2 for _ in range(batches)]
+    probs = [torch.sigmoid(x) for x in logits]
+    labels = [(torch.rand(batch, device="cuda", generator=g) < 0.3).float() for _ in range(batches)]
+    n = batch * batches
+
+    def device_eval():
+        acc = rankops.EvalAccumulator.for_model("dcn", "cuda")
+        for p, y, x in zip(probs, labels, logits):
+            acc.add(p, y, logits=x)
+        return acc.result()
+
+    device_eval()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = device_eval()
+    t_dev = time.perf_counter() - t0
+    # the AUC kernel chain alone, on the concatenated scores
+    cat_p, cat_y = torch.cat(probs), torch.cat(labels)
+    rankops.roc_auc(cat_p, cat_y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        rankops.roc_auc(cat_p, cat_y)
+    torch.cuda.synchronize()
+    t_auc = (time.perf_counter() - t0) / 10
+
+    crit = torch.nn.BCEWithLogitsLoss()
+    t0 = time.perf_counter()
+    total, all_l, all_p = 0.0, [], []
+    for p, y, x in zip(probs, labels, logits):
+        total += crit(x, y).item()
+        all_l.extend(y.cpu().numpy())
+        all_p.extend(p.cpu().numpy())
+    ref = (total / batches, accuracy_score(all_l, np.round(all_p)), roc_auc_score(all_l, all_p))
+    t_ref = time.perf_counter() - t0
+    return {"rows": n, "batches": batches, "device_eval_ms": round(1e3 * t_dev, 2),
+            "device_rows_per_s": round(n / t_dev, 1), "rk_auc_ms": round(1e3 * t_auc, 3),
+            "reference_path_ms": round(1e3 * t_ref, 1), "reference_rows_per_s": round(n / t_ref, 1),
+            "auc_abs_diff": abs(r[2] - ref[2]), "acc_equal": r[1] == ref[1], "loss_abs_diff": abs(r[0] - ref[0])}
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank):
@@ -389,6 +438,11 @@ def main():
             result["loader"] = bench_loader(model, args.batch)
         except Exception as exc:  # reported, never fatal for the headline line
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    if rank == 0 and world == 1 and not args.no_loader:
+        try:
+            result["eval_metrics"] = bench_metrics(args.batch)
+        except Exception as exc:  # reported, never fatal for the headline line
+            result["eval_metrics"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if not args.no_sharded:
         torch.cuda.empty_cache()
         try:

@@ -12,7 +12,8 @@ hand-written HIP kernels (gfx950) through the C ABI in include/rankops.h:
 
 `rankops.sharded.ShardedDeepFM` adds the table-sharded multi-GPU DeepFM lookup (RCCL
 all-to-all); `rankops.loader` (Vocabulary, BatchAssembler, wechat_vocabularies) replaces the
-reference's Dataset bucketing + collate with C++ column bucketing and one H2D copy per batch.
+reference's Dataset bucketing + collate with C++ column bucketing and one H2D copy per batch;
+`rankops.metrics` (EvalAccumulator, roc_auc) computes evaluate()'s loss / accuracy / AUC on the GPU.
 Import order matters: torch first, so librankops binds to torch's HIP runtime.
 """
 import torch  # noqa: F401
@@ -25,9 +26,10 @@ from .deepcrossing import DeepCrossingModel, residual_unit  # noqa: F401
 from .deepfm import DeepFM  # noqa: F401
 from .din import DIN, Dice, din_attention  # noqa: F401
 from .loader import BatchAssembler, Vocabulary, wechat_vocabularies  # noqa: F401
+from .metrics import EvalAccumulator, roc_auc  # noqa: F401
 
 __all__ = [
     "AFM", "BSTModel", "BSTTransformer", "BatchAssembler", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM",
     "Dice", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
-    "error_flags", "load_library", "residual_unit", "wechat_vocabularies",
+    "error_flags", "load_library", "residual_unit", "wechat_vocabularies", "EvalAccumulator", "roc_auc",
 ]

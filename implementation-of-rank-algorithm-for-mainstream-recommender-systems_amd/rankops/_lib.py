@@ -148,6 +148,9 @@ SIGNATURES = {
     "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_mlp_forward": (
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
+    "rk_eval_batch": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p, c_void_p]),
+    "rk_auc_workspace_size": (ctypes.c_int, [c_int64, POINTER(c_int64)]),
+    "rk_auc": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rk_linear_tiled": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_void_p, c_int64, c_void_p]),
     "rk_bn_fold": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),

@@ -28,6 +28,7 @@
  *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
+ *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -244,6 +245,22 @@ int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_
  * (deepfm.py:100-112, 960 -> 512) it reads every weight 64 times per 4096 rows instead of 256. */
 int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_mlp_layer* layer,
                     float* y, int64_t ldy, void* stream);
+
+/* ---- evaluation metrics (the reference's evaluate(): dcn.py:214-239, same in every model) ---- */
+/* One batch into accum (3 x 8 bytes, zero it first): [0] double sum over batches of the batch's
+ * mean loss — loss_kind 0: BCEWithLogitsLoss(logits, labels) (dcn.py:229, bst.py:300,
+ * deepcrossing.py:212); 1: BCELoss(probs, labels), logs clamped at -100 (din.py:379, deepfm.py:198,
+ * afm.py:203, fwfm.py:176; logits may be NULL) — plus *extra if non-NULL (DIN's l2_reg, din.py:380);
+ * [1] uint64 count of rint(probs) == labels (accuracy_score(labels, np.round(probs)));
+ * [2] uint64 number of batches.                                                            */
+int rk_eval_batch(const float* logits, const float* probs, const float* labels, int64_t n,
+                  int32_t loss_kind, const float* extra, void* accum, void* stream);
+/* Exact roc_auc_score(labels, scores) (dcn.py:237) for n <= 2^32-1: Mann-Whitney U with ties
+ * credited 1/2, from a radix sort and int64 counts; *out (device double) = NaN for a NaN score or a
+ * single class.  workspace: rk_auc_workspace_size(n) bytes of device memory.                      */
+int rk_auc_workspace_size(int64_t n, int64_t* bytes);
+int rk_auc(const float* scores, const float* labels, int64_t n, void* workspace, int64_t ws_bytes,
+           double* out, void* stream);
 
 int rk_bn_fold(const float* mean, const float* var, const float* weight, const float* bias,
                float eps, int32_t n, float* scale, float* shift, void* stream);
