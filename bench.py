@@ -49,6 +49,7 @@ DIN_FWD_FLOP = DIN_ATT_FLOP + 6_400 + 444_672       # whole DIN forward, referen
 DIN_FWD_EXEC_FLOP = 2 * 64 * (32 * 64 + 64 * 32 + 32) + 2 * 64 * 32 + 2 * (128 * 512 + 512 * 256 + 256 * 128)
 DEEPFM_GATHER_BYTES = 30 * (8 + 128 + 4) + 30 * 128 + 8  # 8,048 B: gather+FM kernel
 BST_BLOCK_FLOP = 14_680_064
+FWFM_BYTES_PER_SAMPLE = 6 * (8 + 32 + 4) + 4
 DCN_FLOP = 379_236
 
 
@@ -62,7 +63,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--models", default="dcn,deepfm,bst,din_per_call")
+    ap.add_argument("--models", default="dcn,deepfm,bst,fwfm,din_per_call")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     return ap.parse_args()
 
@@ -114,6 +115,9 @@ def workload(name: str, batch: int, seed: int):
     elif name == "bst":
         cfg = {"vocab": H.WECHAT_VOCAB, "T": 64, "dim": 128, "heads": 4, "max_len": 64}
         model_name = "bst"
+    elif name == "fwfm":
+        cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8}
+        model_name = "fwfm"
     else:
         raise ValueError(name)
     with torch.device(dev):
@@ -429,6 +433,13 @@ def main():
             r, m2, inp2, cfg2, mn2 = bench_one(name, batch, args.steps, args.warmup, 1, 0)
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
+            if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob
+                r["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * r["samples_per_s"] / 1e9, 1)
+                r["bytes_per_sample"] = FWFM_BYTES_PER_SAMPLE
+                big, mb, _, _, _ = bench_one("fwfm", 1 << 20, max(5, args.steps // 5), 3, 1, 0)
+                big["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * big["samples_per_s"] / 1e9, 1)
+                r["batch_1m"] = big
+                del mb
             extras[name] = r
             del m2, inp2
             torch.cuda.empty_cache()

@@ -10,7 +10,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rankops.h"
@@ -123,13 +125,18 @@ struct rk_vocab {
       }
     }
   }
-  int64_t get(const char* k, size_t n) const {
+  // index of key k, or -1 when it is not in the vocabulary
+  int64_t find(const char* k, size_t n) const {
     const uint64_t h = rk::vocab_hash(k, (uint32_t)n);
     for (uint64_t s = h & mask;; s = (s + 1) & mask) {
       const VocabSlot& e = slots[s];
-      if (e.idx < 0) return 0;  // not in the vocabulary -> row 0 (H1)
+      if (e.idx < 0) return -1;
       if (e.h == h && e.len == n && std::memcmp(arena.data() + e.off, k, n) == 0) return e.idx;
     }
+  }
+  int64_t get(const char* k, size_t n) const {
+    const int64_t r = find(k, n);
+    return r < 0 ? 0 : r;  // not in the vocabulary -> row 0 (H1)
   }
 };
 
@@ -292,5 +299,135 @@ RK_API int rk_bucketize_sequences(const rk_vocab* v, const char* data, const voi
       for (; j < T; ++j) row[j] = 0;
     }
   });
+  return RK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// FwFM LabelEncoder bucketing (fwfm.py:48-67), over one whole dataset column.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int64_t kNaN = -2, kOOV = -1;
+
+// int(s) for the ASCII forms Python accepts: whitespace, sign, digits with single '_' between
+bool parse_py_int(const unsigned char* a, const unsigned char* b, int64_t& out) {
+  for (size_t k; a < b && (k = space_at(a, b)) != 0;) a += k;
+  for (size_t k; b > a && (k = space_before(a, b)) != 0;) b -= k;
+  bool neg = false;
+  if (a < b && (*a == '+' || *a == '-')) neg = *a++ == '-';
+  if (a == b || *a == '_' || b[-1] == '_') return false;
+  unsigned __int128 v = 0;
+  for (const unsigned char* p = a; p < b; ++p) {
+    if (*p == '_') {
+      if (p[1] == '_') return false;
+      continue;
+    }
+    if (*p < '0' || *p > '9') return false;
+    v = v * 10 + (*p - '0');
+    if (v > (unsigned __int128)INT64_MAX + 1) return false;
+  }
+  if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+  out = neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)v;
+  return true;
+}
+
+}  // namespace
+
+RK_API int rk_label_encode(const rk_vocab* v, const char* data, const void* offsets, int32_t offset_bits,
+                           const uint8_t* valid_bits, int64_t valid_offset, int64_t n, int64_t* out,
+                           int64_t* mode_index, int32_t threads) {
+  if (int rc = check_column("rk_label_encode", nullptr, false, data, offsets, offset_bits, n)) return rc;
+  if (n > 0 && !out) return fail(RK_ERR_INVALID, "rk_label_encode: null output");
+  if (mode_index) *mode_index = -1;
+  const int nt = thread_count(threads, n);
+  auto value = [&](int64_t i, int64_t& s, int64_t& e) -> bool {  // false: NaN (null or the string "None")
+    if (!bit_valid(valid_bits, valid_offset, i)) return false;
+    value_span(offsets, offset_bits, i, s, e);
+    return !(e - s == 4 && std::memcmp(data + s, "None", 4) == 0);
+  };
+  if (!v || v->size == 0) {
+    // no vocabulary: data[feature].fillna(0).astype(int) (fwfm.py:66-67)
+    std::vector<int64_t> bad(nt, -1);
+    const int64_t chunk = (n + nt - 1) / std::max(nt, 1);
+    parallel_for(n, nt, [&](int64_t a, int64_t b) {
+      for (int64_t i = a; i < b; ++i) {
+        int64_t s, e, r = 0;
+        if (value(i, s, e) && !parse_py_int(reinterpret_cast<const unsigned char*>(data + s),
+                                            reinterpret_cast<const unsigned char*>(data + e), r)) {
+          bad[chunk ? a / chunk : 0] = i;
+          return;
+        }
+        out[i] = r;
+      }
+    });
+    for (int64_t i : bad)
+      if (i >= 0) {
+        int64_t s, e;
+        value_span(offsets, offset_bits, i, s, e);
+        return fail(RK_ERR_INVALID, "rk_label_encode: invalid literal for int() with base 10: '%.*s'",
+                    (int)std::min<int64_t>(e - s, 200), data + s);
+      }
+    return RK_OK;
+  }
+  // pass 1: vocabulary index, kOOV or kNaN per row; per-index counts; OOV rows per thread
+  std::vector<uint64_t> counts((size_t)v->size, 0);
+  std::vector<std::vector<int64_t>> oov_rows(nt);
+  const int64_t chunk = (n + nt - 1) / std::max(nt, 1);
+  parallel_for(n, nt, [&](int64_t a, int64_t b) {
+    auto& mine = oov_rows[chunk ? a / chunk : 0];
+    for (int64_t i = a; i < b; ++i) {
+      int64_t s, e, r = kNaN;
+      if (value(i, s, e)) {
+        r = v->find(data + s, (size_t)(e - s));
+        if (r >= 0)
+          __atomic_fetch_add(&counts[(size_t)r], 1, __ATOMIC_RELAXED);
+        else
+          mine.push_back(i);
+      }
+      out[i] = r;
+    }
+  });
+  // series.mode(dropna=True).values[0]: the most frequent value, ties -> the smallest string
+  // (code-point order == UTF-8 byte order)
+  std::vector<std::string_view> key_of((size_t)v->size);
+  for (const VocabSlot& e : v->slots)
+    if (e.idx >= 0) key_of[(size_t)e.idx] = std::string_view(v->arena.data() + e.off, e.len);
+  uint64_t best = 0;
+  std::string_view best_key;
+  bool best_in_vocab = false;
+  int64_t best_idx = -1;
+  auto offer = [&](uint64_t c, std::string_view k, bool in_vocab, int64_t idx) {
+    if (c == 0) return;
+    if (c > best || (c == best && k < best_key)) {
+      best = c;
+      best_key = k;
+      best_in_vocab = in_vocab;
+      best_idx = idx;
+    }
+  };
+  for (size_t r = 0; r < counts.size(); ++r) offer(counts[r], key_of[r], true, (int64_t)r);
+  std::unordered_map<std::string_view, uint64_t> oov;
+  for (auto& rows : oov_rows)
+    for (int64_t i : rows) {
+      int64_t s, e;
+      value_span(offsets, offset_bits, i, s, e);
+      ++oov[std::string_view(data + s, (size_t)(e - s))];
+    }
+  for (auto& [k, c] : oov) offer(c, k, false, -1);
+  if (n == 0) return RK_OK;
+  if (best == 0) {  // every value NaN: the mode is 'unknown'
+    best_key = "unknown";
+    best_idx = v->find("unknown", 7);
+    best_in_vocab = best_idx >= 0;
+  }
+  if (!best_in_vocab)  // the reference's LabelEncoder.transform raises here
+    return fail(RK_ERR_INVALID, "rk_label_encode: y contains previously unseen labels: '%.*s' (the column's mode)",
+                (int)std::min<size_t>(best_key.size(), 200), best_key.data());
+  // pass 2: NaN and out-of-vocabulary rows take the mode's index
+  parallel_for(n, nt, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i)
+      if (out[i] < 0) out[i] = best_idx;
+  });
+  if (mode_index) *mode_index = best_idx;
   return RK_OK;
 }

@@ -9,6 +9,7 @@ hand-written HIP kernels (gfx950) through the C ABI in include/rankops.h:
     AFM, create_feature_columns            algorithm/AFM/afm.py
     DeepCrossingModel, residual_unit       algorithm/DeepCrossing/deepcrossing.py
     BSTModel, BSTTransformer               algorithm/BST/bst.py
+    FwFM                                   algorithm/FwFM/fwfm.py
 
 `rankops.sharded.ShardedDeepFM` adds the table-sharded multi-GPU DeepFM lookup (RCCL
 all-to-all); `rankops.loader` (Vocabulary, BatchAssembler, wechat_vocabularies) replaces the
@@ -25,11 +26,13 @@ from .dcn import DCNModel, cross_layer  # noqa: F401
 from .deepcrossing import DeepCrossingModel, residual_unit  # noqa: F401
 from .deepfm import DeepFM  # noqa: F401
 from .din import DIN, Dice, din_attention  # noqa: F401
-from .loader import BatchAssembler, Vocabulary, wechat_vocabularies  # noqa: F401
+from .fwfm import FwFM  # noqa: F401
+from .loader import BatchAssembler, Vocabulary, label_encode, wechat_vocabularies  # noqa: F401
 from .metrics import EvalAccumulator, roc_auc  # noqa: F401
 
 __all__ = [
     "AFM", "BSTModel", "BSTTransformer", "BatchAssembler", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM",
-    "Dice", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
+    "Dice", "FwFM", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
     "error_flags", "load_library", "residual_unit", "wechat_vocabularies", "EvalAccumulator", "roc_auc",
+    "label_encode",
 ]

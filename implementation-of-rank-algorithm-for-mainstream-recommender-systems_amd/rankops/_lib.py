@@ -148,6 +148,8 @@ SIGNATURES = {
     "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_mlp_forward": (
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
+    "rk_fwfm_forward": (ctypes.c_int, [POINTER(Segment), POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_eval_batch": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p, c_void_p]),
     "rk_auc_workspace_size": (ctypes.c_int, [c_int64, POINTER(c_int64)]),
     "rk_auc": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -161,6 +163,9 @@ SIGNATURES = {
     "rk_vocab_free": (None, [c_void_p]),
     "rk_bucketize": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32]),
+    "rk_label_encode": (
+        ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_void_p, POINTER(c_int64),
+                       c_int32]),
     "rk_sequence_lengths": (
         ctypes.c_int,
         [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_int64, ctypes.c_char, c_void_p, POINTER(c_int64), c_int32]),

@@ -1,0 +1,59 @@
+"""FwFM (field-weighted factorization machine) on the rankops engine — drop-in for
+algorithm/FwFM/fwfm.py.
+
+`FwFM(field_dims, embed_dim)` keeps the reference constructor, parameter creation order (so a
+seeded construction draws the same weights) and state_dict keys (`linear.<f>.weight`,
+`embedding.<f>.weight`, `field_weight`, `bias`; fwfm.py:87-112), and
+`forward(x) -> sigmoid(y).squeeze(1)` over `x = {'userid', 'feedid', 'device', 'authorid',
+'bgm_song_id', 'bgm_singer_id'}` int64 index tensors (fwfm.py:114-139).  Tables have
+`len(vocab)` rows (no +1, fwfm.py:235-242); the indices come from the dataset-level
+LabelEncoder bucketing in `rankops.loader.label_encode` (fwfm.py:48-67).
+
+The whole forward — 12 gathers, the 15 weighted pair dots, the linear term, bias and sigmoid — is
+one rk_fwfm_forward launch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common import EngineModule, check_eval
+
+FWFM_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
+
+
+class FwFM(EngineModule):
+    def __init__(self, field_dims, embed_dim, *, field_names=FWFM_FIELDS):
+        super().__init__()
+        self.field_dims = field_dims
+        self.num_fields = len(field_dims)
+        self.embed_dim = embed_dim
+        if len(field_names) != self.num_fields:
+            raise ValueError(f"FwFM: {self.num_fields} field_dims but {len(field_names)} field names")
+        self.field_names = tuple(field_names)
+        self.linear = nn.ModuleList([nn.Embedding(n, 1) for n in field_dims])
+        self.embedding = nn.ModuleList([nn.Embedding(n, embed_dim) for n in field_dims])
+        for emb in self.embedding:
+            nn.init.xavier_uniform_(emb.weight)
+        self.num_pairs = self.num_fields * (self.num_fields - 1) // 2
+        self.field_weight = nn.Parameter(torch.randn(self.num_pairs), requires_grad=True)
+        self.bias = nn.Parameter(torch.zeros(1))
+
+    def forward(self, x, *, return_logit=False):
+        """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit)."""
+        check_eval(self)
+        idx0 = ops.as_index(x[self.field_names[0]], f"x[{self.field_names[0]!r}]")
+        B = idx0.shape[0]
+        emb, lin = [], []
+        for f, name in enumerate(self.field_names):
+            idx = ops.as_index(x[name], f"x[{name!r}]")
+            if idx.shape != (B,):
+                raise ValueError(f"FwFM.forward: x[{name!r}] has shape {tuple(idx.shape)}, expected ({B},)")
+            emb.append(ops.table_segment(self.embedding[f].weight, idx, 0))
+            lin.append(ops.table_segment(self.linear[f].weight, idx, 0))
+        prob = torch.empty(B, device=idx0.device, dtype=torch.float32)
+        logit = torch.empty(B, device=idx0.device, dtype=torch.float32) if return_logit else None
+        ops.fwfm_forward(emb, lin, self.embed_dim, B, ops.as_f32(self.field_weight, "field_weight"),
+                         ops.as_f32(self.bias, "bias"), logit, prob)
+        return (prob, logit) if return_logit else prob

@@ -123,6 +123,46 @@ class Vocabulary:
         return out, lens
 
 
+def label_encode(column, vocab: "Vocabulary | None", threads: int = 0) -> np.ndarray:
+    """FwFM's dataset-level LabelEncoder bucketing of one whole column (fwfm.py:29-31,48-67):
+    null and "None" are NaN; NaN and out-of-vocabulary values take the index of the column's
+    mode (most frequent non-NaN value, ties -> smallest string; 'unknown' when every value is
+    NaN); index = position of the last occurrence of the stripped line in the vocabulary file
+    (LabelEncoder with classes_ = the file's lines, no empty-line skipping, no +1).  Raises
+    ValueError where the reference's LabelEncoder.transform raises (the mode itself is not in
+    the vocabulary).  An empty / missing vocabulary parses the values as Python int()
+    (`.fillna(0).astype(int)`, ASCII digits only).  rk_label_encode, C++ threads."""
+    pa = _pa()
+    lib = _lib.load()
+    if isinstance(column, pa.ChunkedArray):
+        arr = pa.concat_arrays(column.chunks) if column.num_chunks != 1 else column.chunk(0)
+    elif isinstance(column, pa.Array):
+        arr = column
+    else:
+        if hasattr(column, "to_numpy") and not isinstance(column, np.ndarray):  # pandas Series
+            column = column.to_numpy(dtype=object)
+        arr = pa.array(list(column))
+    if pa.types.is_dictionary(arr.type):
+        arr = arr.dictionary_decode()
+    if pa.types.is_integer(arr.type) and arr.null_count == 0:
+        arr = arr.cast(pa.string())  # .astype(str) of an int column: str(int)
+    if not (pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type) or pa.types.is_null(arr.type)):
+        raise TypeError(f"label_encode: column type {arr.type} is not supported (string, or integer without nulls)")
+    if pa.types.is_null(arr.type):
+        arr = arr.cast(pa.string())
+    n = len(arr)
+    out = np.empty(n, dtype=np.int64)
+    if n == 0:
+        return out
+    d, o, bits, v, vo = _buffers(arr)
+    mode = ctypes.c_int64()
+    rc = lib.rk_label_encode(vocab._h if vocab is not None and len(vocab) else None, d, o, bits, v, vo, n,
+                             out.ctypes.data, ctypes.byref(mode), threads)
+    if rc != 0:
+        raise ValueError(_lib.last_error())
+    return out
+
+
 def wechat_vocabularies(vocab_dir, fields=tuple(VOCAB_FILES), skip_empty_lines=False):
     """{field: Vocabulary} with the reference's field -> file mapping (manual_tag_list reads
     manual_tag_id.txt, dcn.py:66).  A missing file gives an empty vocabulary (dcn.py:86-87)."""

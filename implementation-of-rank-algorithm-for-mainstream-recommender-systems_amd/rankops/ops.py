@@ -137,6 +137,13 @@ def afm_forward(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h
           "rk_afm_forward")
 
 
+def fwfm_forward(emb, lin, dim, batch, field_weight, bias, logit, prob):
+    lib = _lib.load()
+    _lib.ensure_device(prob.device)
+    check(lib.rk_fwfm_forward(_seg_array(emb), _seg_array(lin), len(emb), dim, batch, ptr(field_weight), ptr(bias),
+                              ptr(logit), ptr(prob), _lib.stream_of(prob)), "rk_fwfm_forward")
+
+
 def bst_attention(qkv, batch, T, d_model, heads, seq_len, ctx):
     lib = _lib.load()
     check(lib.rk_bst_attention(ptr(qkv), qkv.stride(0), batch, T, d_model, heads, ptr(seq_len), ptr(ctx),

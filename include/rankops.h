@@ -29,6 +29,7 @@
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
+ *   rk_fwfm_forward    FwFM.forward()                        fwfm.py:114-139
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -245,6 +246,16 @@ int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_
  * (deepfm.py:100-112, 960 -> 512) it reads every weight 64 times per 4096 rows instead of 256. */
 int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_mlp_layer* layer,
                     float* y, int64_t ldy, void* stream);
+
+/* FwFM.forward (fwfm.py:114-139): per sample, logit = sum_f linear[f] row + sum_{i<j} field_weight[p]
+ * <embeddings[i] row, embeddings[j] row> + bias[0] (p runs i-major over i < j, fwfm.py:129-136),
+ * prob = sigmoid(logit).  embeddings[f]: table segments of width dim (out_col ignored);
+ * linear[f]: the first-order tables (dim 1).  2 <= num_fields <= 16, 1 <= dim <= 256 (dim > 64
+ * needs 16-byte aligned rows).  logit may be NULL.  Out-of-range indices read zero rows and raise
+ * RK_FLAG_INDEX_OOB.                                                                             */
+int rk_fwfm_forward(const rk_segment* embeddings, const rk_segment* linear, int32_t num_fields,
+                    int32_t dim, int64_t batch, const float* field_weight, const float* bias,
+                    float* logit, float* prob, void* stream);
 
 /* ---- evaluation metrics (the reference's evaluate(): dcn.py:214-239, same in every model) ---- */
 /* One batch into accum (3 x 8 bytes, zero it first): [0] double sum over batches of the batch's

@@ -15,6 +15,9 @@
  *   rk_bucketize                     the per-row category / target lookups of __getitem__:
  *                                    dcn.py:94-104; din.py:131-143,158-163; bst.py:130-140;
  *                                    deepfm.py:56-66; afm.py:46-54; deepcrossing.py:86-100
+ *   rk_label_encode                  FwFM's dataset-level LabelEncoder bucketing: fwfm.py:29-31
+ *                                    ('None' -> NaN), fwfm.py:48-67 (mode fill, OOV -> mode,
+ *                                    LabelEncoder.transform with classes_ = the vocabulary lines)
  *   rk_sequence_lengths,             DIN history: str.split(',') + per-item feedid lookup
  *   rk_bucketize_sequences           (din.py:145-157) and din_collate_fn's zero padding to the
  *                                    batch maximum (din.py:175-213); BST's one-item sequence
@@ -76,6 +79,17 @@ int rk_bucketize_sequences(const rk_vocab* v, const char* data, const void* offs
 
 /* Device copy of a vocabulary: the hash table image (slot_bytes, 24-B slots) and key arena
  * (arena_bytes) to copy into device memory as they are; `mask` is passed to the *_device calls. */
+/* FwFM LabelEncoder bucketing of one whole column (fwfm.py:48-67): a null or the string "None" is
+ * NaN; out[i] = vocabulary index (last occurrence, no +1) of value i, with NaN and out-of-vocabulary
+ * values replaced by the column's mode — the most frequent non-NaN value (ties: smallest string in
+ * code-point order), "unknown" when every value is NaN — reported in *mode_index (may be NULL).
+ * Fails with RK_ERR_INVALID ("y contains previously unseen labels") when the mode is not in the
+ * vocabulary, where sklearn's LabelEncoder.transform raises.  v == NULL or an empty vocabulary:
+ * the values are parsed as Python int() (ASCII digits, optional sign / '_' / whitespace), NaN -> 0
+ * (fwfm.py:66-67).  Load the vocabulary with skip_empty_lines = 0 (fwfm.py:43-44).             */
+int rk_label_encode(const rk_vocab* v, const char* data, const void* offsets, int32_t offset_bits,
+                    const uint8_t* valid_bits, int64_t valid_offset, int64_t n, int64_t* out,
+                    int64_t* mode_index, int32_t threads);
 int rk_vocab_export_size(const rk_vocab* v, int64_t* slot_bytes, int64_t* arena_bytes, uint64_t* mask);
 int rk_vocab_export(const rk_vocab* v, void* slots_out, void* arena_out);
 

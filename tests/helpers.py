@@ -146,6 +146,8 @@ def build(name: str, cfg: dict, seed: int = 42):
                              nhead=cfg.get("heads", 4), num_transformer_blocks=cfg.get("blocks", 1),
                              max_seq_length=cfg.get("max_len", 50), pooling_method=cfg.get("pooling", "sum"),
                              vocab_sizes=vocab)
+    elif name == "fwfm":
+        m = rankops.FwFM([vocab[f] for f in rankops.fwfm.FWFM_FIELDS], cfg.get("dim", 8))
     else:
         raise ValueError(name)
     randomize_eval_stats(m, seed + 1)
@@ -164,6 +166,9 @@ def make_inputs(name: str, cfg: dict, B: int, seed: int = 1000):
         return afm_inputs(B, afm_feature_columns(vocab), seed)
     if name == "bst":
         return bst_inputs(B, cfg.get("T", 50), vocab, seed, cfg.get("min_len", 1))
+    if name == "fwfm":  # tables have len(vocab) rows (no +1): indices in [0, len)
+        g = torch.Generator().manual_seed(seed)
+        return {"x": {f: torch.randint(0, vocab[f], (B,), generator=g) for f in rankops.fwfm.FWFM_FIELDS}}
     raise ValueError(name)
 
 
@@ -178,6 +183,8 @@ def call_model(model, name, inp):
         return model(inp["dense_input"], inp["category_input"])
     if name == "bst":
         return model(inp["dense"], inp["category"], inp["seq_feedid"], inp["seq_length"])
+    if name == "fwfm":
+        return model(inp["x"])
     raise ValueError(name)
 
 
