@@ -14,7 +14,9 @@ hand-written HIP kernels (gfx950) through the C ABI in include/rankops.h:
 `rankops.sharded.ShardedDeepFM` adds the table-sharded multi-GPU DeepFM lookup (RCCL
 all-to-all); `rankops.loader` (Vocabulary, BatchAssembler, wechat_vocabularies) replaces the
 reference's Dataset bucketing + collate with C++ column bucketing and one H2D copy per batch;
-`rankops.metrics` (EvalAccumulator, roc_auc) computes evaluate()'s loss / accuracy / AUC on the GPU.
+`rankops.metrics` (EvalAccumulator, roc_auc) computes evaluate()'s loss / accuracy / AUC on the GPU;
+`rankops.train` holds the HIP backward (train-mode forwards return autograd-connected outputs)
+and `rankops.Adam`, a one-launch torch.optim.Adam.
 Import order matters: torch first, so librankops binds to torch's HIP runtime.
 """
 import torch  # noqa: F401
@@ -29,10 +31,11 @@ from .din import DIN, Dice, din_attention  # noqa: F401
 from .fwfm import FwFM  # noqa: F401
 from .loader import BatchAssembler, Vocabulary, label_encode, wechat_vocabularies  # noqa: F401
 from .metrics import EvalAccumulator, roc_auc  # noqa: F401
+from .train import Adam  # noqa: F401
 
 __all__ = [
     "AFM", "BSTModel", "BSTTransformer", "BatchAssembler", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM",
     "Dice", "FwFM", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
     "error_flags", "load_library", "residual_unit", "wechat_vocabularies", "EvalAccumulator", "roc_auc",
-    "label_encode",
+    "label_encode", "Adam",
 ]

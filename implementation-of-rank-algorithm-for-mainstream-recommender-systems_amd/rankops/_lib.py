@@ -95,6 +95,11 @@ class MlpLayer(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", c_int64)]
+
+
 RK_MLP_MAX_LAYERS = 8
 _SEG_P = POINTER(Segment)
 _EPI_P = POINTER(Epilogue)
@@ -150,6 +155,16 @@ SIGNATURES = {
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
     "rk_fwfm_forward": (ctypes.c_int, [POINTER(Segment), POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_gemm": (ctypes.c_int, [c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                               c_int64, c_void_p, c_int64, c_void_p, c_int32, c_int32, c_void_p]),
+    "rk_logit_head_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32,
+                                              c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int64, c_void_p,
+                                              c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
+                                             c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),
+    "rk_embedding_backward": (ctypes.c_int, [_SEG_P, c_int32, c_int64, c_void_p, c_int64, c_void_p]),
+    "rk_adam_step": (ctypes.c_int, [POINTER(AdamTensor), c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_double, c_int64, c_void_p]),
     "rk_eval_batch": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p, c_void_p]),
     "rk_auc_workspace_size": (ctypes.c_int, [c_int64, POINTER(c_int64)]),
     "rk_auc": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),

@@ -3,7 +3,9 @@
 `DCNModel(vocab_dir, hidden_units=[512, 256, 128], num_cross_layer=1)` keeps the reference
 constructor, parameter creation order (so a seeded construction gives the same weights),
 `state_dict` keys (dcn.py:130-152: no cross-layer keys) and `forward(dense, category) ->
-(probability, logit)` (dcn.py:161-180).  The forward is three kinds of HIP launch:
+(probability, logit)` (dcn.py:161-180).  In train mode with autograd recording, the same
+forward runs under `rankops.train._DCNTrain`, whose backward is HIP too (loss.backward() fills
+every .grad).  The forward is three kinds of HIP launch:
 
   rk_dcn_cross   gather the 6 fields + dense into x0 [B, 50], run the cross layers, and
                  produce the cross half of output_layer (dcn.py:163-173, 177-178)
@@ -19,9 +21,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
-from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_cross_layers, load_vocabulary, run_tail, \
-    table_rows
+from . import ops, train
+from .common import EngineModule, InteractionWeights, Layer, draw_cross_layers, load_vocabulary, run_tail, table_rows
 
 
 def cross_layer(x0: torch.Tensor, xl: torch.Tensor, index: int) -> torch.Tensor:
@@ -71,7 +72,8 @@ class DCNModel(EngineModule):
         return load_vocabulary(vocab_dir, filename)
 
     def forward(self, dense, category):
-        check_eval(self)
+        # no BatchNorm / Dropout: the train-mode forward computes what the eval forward does; with
+        # autograd recording it also keeps the activations for the HIP backward (rankops.train)
         dense = ops.as_f32(dense, "dense")
         B = dense.shape[0]
         dev = dense.device
@@ -86,6 +88,8 @@ class DCNModel(EngineModule):
             segs.append(ops.table_segment(emb.weight, idx, col))
             col += emb.embedding_dim
         cw, cb = self.cross_weights.get(dev)
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            return train.dcn_train_forward(self, dense, idx_keep, cw, cb)
         x0 = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
         partial = torch.empty(B, device=dev, dtype=torch.float32)
         head_w = self.output_layer.weight

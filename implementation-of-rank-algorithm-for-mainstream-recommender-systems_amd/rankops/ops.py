@@ -283,3 +283,65 @@ def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M
     check(lib.rk_linear(xp, lx, ptr(x_periodic), x_period, weight.data_ptr(), weight.stride(0), M, N, K,
                         ctypes.byref(ep), y_ptr, ldy or 0, _lib.stream_of(x)), "rk_linear")
     return out
+
+
+# ---------------------------------------------------------------- training (§8(f) #2)
+
+def gemm(trans_a: bool, trans_b: bool, M: int, N: int, R: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
+         C: torch.Tensor, ldc: int = None, *, A_mask: torch.Tensor = None, row_sums: torch.Tensor = None,
+         accumulate: bool = False, split: int = 0):
+    """C[m, n] (+)= sum_r opA(m, r) opB(n, r) (rk_gemm; layouts in include/rankops.h)."""
+    lib = _lib.load()
+    check(lib.rk_gemm(int(trans_a), int(trans_b), M, N, R, ptr(A), lda, ptr(A_mask), ptr(B), ldb, ptr(C),
+                      C.stride(0) if ldc is None else ldc, ptr(row_sums), int(accumulate), split,
+                      _lib.stream_of(C)), "rk_gemm")
+    return C
+
+
+def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, *, relu_out: torch.Tensor = None,
+                    need_dx: bool = True, dx: torch.Tensor = None):
+    """nn.Linear (+ ReLU when relu_out = the layer's post-ReLU output) backward:
+    dz = dy * [relu_out > 0]; dW = dz^T x; db = sum_b dz; dx = dz W.  -> (dx, dW, db)."""
+    Bsz, N = dy.shape
+    K = weight.shape[1]
+    if relu_out is not None and (relu_out.shape != dy.shape or relu_out.stride() != dy.stride()):
+        raise ValueError("rankops.linear_backward: relu_out must have dy's shape and strides")
+    dW = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+    db = torch.empty(N, device=dy.device, dtype=torch.float32)
+    gemm(True, True, N, K, Bsz, dy, dy.stride(0), x, x.stride(0), dW, A_mask=relu_out, row_sums=db)
+    if need_dx:
+        if dx is None:
+            dx = torch.empty(Bsz, K, device=dy.device, dtype=torch.float32)
+        gemm(False, True, Bsz, K, N, dy, dy.stride(0), weight, weight.stride(0), dx, A_mask=relu_out)
+    return dx, dW, db
+
+
+def logit_head_backward(dlogit, dprob, prob, xa, xb, w, dxa, dxb, dw, db, g_out=None):
+    lib = _lib.load()
+    check(lib.rk_logit_head_backward(ptr(dlogit), ptr(dprob), ptr(prob), xa.shape[0], ptr(xa), xa.stride(0),
+                                     xa.shape[1], ptr(xb), xb.stride(0) if xb is not None else 0,
+                                     xb.shape[1] if xb is not None else 0, ptr(w), ptr(dxa),
+                                     dxa.stride(0) if dxa is not None else 0, ptr(dxb),
+                                     dxb.stride(0) if dxb is not None else 0, ptr(dw), ptr(db), ptr(g_out),
+                                     _lib.stream_of(xa)), "rk_logit_head_backward")
+
+
+def dcn_cross_backward(x0, cross_w, cross_b, num_layers, dxl, dx0, accumulate=True):
+    lib = _lib.load()
+    check(lib.rk_dcn_cross_backward(ptr(x0), x0.stride(0), x0.shape[0], x0.shape[1], ptr(cross_w), ptr(cross_b),
+                                    num_layers, ptr(dxl), dxl.stride(0), ptr(dx0), dx0.stride(0), int(accumulate),
+                                    _lib.stream_of(x0)), "rk_dcn_cross_backward")
+
+
+def embedding_backward(grad_segs, batch, dx):
+    lib = _lib.load()
+    check(lib.rk_embedding_backward(_seg_array(grad_segs), len(grad_segs), batch, ptr(dx), dx.stride(0),
+                                    _lib.stream_of(dx)), "rk_embedding_backward")
+
+
+def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, stream):
+    """entries: list of (param, grad, exp_avg, exp_avg_sq) contiguous float32 tensors."""
+    lib = _lib.load()
+    arr = (_lib.AdamTensor * len(entries))(*[_lib.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(),
+                                                             v.data_ptr(), p.numel()) for p, g, m, v in entries])
+    check(lib.rk_adam_step(arr, len(entries), lr, beta1, beta2, eps, weight_decay, step, stream), "rk_adam_step")

@@ -1,0 +1,192 @@
+"""Training on the rankops engine.
+
+The reference scripts train with autograd and torch.optim.Adam:
+
+    model.train(); optimizer = optim.Adam(model.parameters(), lr=...)          # dcn.py:275
+    optimizer.zero_grad(); prob, logit = model(dense, category)                # dcn.py:195-196
+    loss = criterion(logit.squeeze(), label); loss.backward(); optimizer.step()  # dcn.py:198-201
+
+A rankops model in train mode returns outputs attached to a `torch.autograd.Function` whose
+forward runs the HIP forward kernels with the activations the backward needs kept in HBM, and
+whose backward runs the HIP backward kernels (include/rankops.h, "training") and hands the
+parameter gradients back to autograd — so `loss.backward()` fills every `.grad` as the
+reference does and the unchanged loop works with `torch.optim.Adam` or with `rankops.Adam`
+(the same update as one fused launch over all tensors, `rk_adam_step`).
+
+Models with training support: DCNModel (`dcn.py:114-180`: embeddings, cross stack, ReLU MLP,
+output_layer + sigmoid; no BatchNorm / Dropout, so train and eval forwards coincide).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .common import const
+
+
+# ---------------------------------------------------------------- shared pieces
+
+def mlp_relu_forward(x, linears, head_w, head_b, partial, logit, prob):
+    """Linear+ReLU stack with the Linear(N,1)+sigmoid head; returns the activations [x, h1, ...].
+    The head reads head_partial (the other input block's share of the logit) when given."""
+    B, dev = x.shape[0], x.device
+    hs = [x]
+    h = x
+    for i, lin in enumerate(linears):
+        last = i == len(linears) - 1
+        y = torch.empty(B, lin.out_features, device=dev, dtype=torch.float32)
+        if last and lin.out_features <= 256:
+            ep = ops.make_epilogue(bias=lin.bias, act="relu", head_w=head_w, head_b=head_b, head_logit=logit,
+                                   head_prob=prob, head_partial=partial)
+        else:
+            ep = ops.make_epilogue(bias=lin.bias, act="relu")
+        ops.linear(h, lin.weight, y, epilogue=ep)
+        hs.append(y)
+        h = y
+    if linears[-1].out_features > 256:  # head as its own N = 1 GEMM
+        ep = ops.make_epilogue(bias=head_b, head_w=const(dev, 1.0), head_b=const(dev, 0.0), head_logit=logit,
+                               head_prob=prob, head_partial=partial)
+        ops.linear(h, head_w, None, epilogue=ep)
+    return hs
+
+
+def mlp_relu_backward(dh, hs, linears):
+    """Backward of mlp_relu_forward's hidden stack from dL/d(last activation); returns
+    (dL/dx, [(dW, db) per layer])."""
+    grads = [None] * len(linears)
+    for i in range(len(linears) - 1, -1, -1):
+        dx, dW, db = ops.linear_backward(dh, hs[i], linears[i].weight, relu_out=hs[i + 1])
+        grads[i] = (dW, db)
+        dh = dx
+    return dh, grads
+
+
+def _grad_out(g, like):
+    if g is None:
+        return None
+    return g.to(torch.float32).reshape(like.shape).contiguous()
+
+
+# ---------------------------------------------------------------- DCN
+
+class _DCNTrain(torch.autograd.Function):
+    """DCNModel forward + backward; inputs after the fixed arguments are the module parameters in
+    `_dcn_params` order."""
+
+    @staticmethod
+    def forward(ctx, model, dense, idx, cw, cb, *params):
+        B, dev = dense.shape[0], dense.device
+        d = model.input_dim
+        segs = [ops.dense_segment(dense, model.num_dense_features, 0)]
+        col = model.num_dense_features
+        for (name, emb), i in zip(model.embeddings.items(), idx):
+            segs.append(ops.table_segment(emb.weight, i, col))
+            col += emb.embedding_dim
+        x0 = torch.empty(B, d, device=dev, dtype=torch.float32)
+        xl = torch.empty(B, d, device=dev, dtype=torch.float32)
+        partial = torch.empty(B, device=dev, dtype=torch.float32)
+        w_out = model.output_layer.weight
+        ops.dcn_cross(segs, B, d, cw, cb, model.num_cross_layer, w_out.data_ptr(), x0, partial, dev, xl_out=xl)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        linears = [m for m in model.dnn if isinstance(m, torch.nn.Linear)]
+        hs = mlp_relu_forward(x0, linears, w_out[:, d:], model.output_layer.bias, partial, logit, prob)
+        ctx.model = model
+        ctx.idx = idx
+        ctx.save_for_backward(x0, xl, prob, cw, cb, *hs[1:])
+        return prob, logit
+
+    @staticmethod
+    def backward(ctx, dprob, dlogit):
+        model = ctx.model
+        x0, xl, prob, cw, cb, *hidden = ctx.saved_tensors
+        hs = [x0] + hidden
+        B, d = x0.shape
+        dev = x0.device
+        w_out = model.output_layer.weight
+        dprob, dlogit = _grad_out(dprob, prob), _grad_out(dlogit, prob)
+        dxl = torch.empty(B, d, device=dev, dtype=torch.float32)
+        dh = torch.empty_like(hs[-1])
+        dw_out = torch.empty_like(w_out)
+        db_out = torch.empty(1, device=dev, dtype=torch.float32)
+        ops.logit_head_backward(dlogit, dprob, prob, xl, hs[-1], w_out, dxl, dh, dw_out, db_out)
+        linears = [m for m in model.dnn if isinstance(m, torch.nn.Linear)]
+        dx0, lin_grads = mlp_relu_backward(dh, hs, linears)
+        ops.dcn_cross_backward(x0, cw, cb, model.num_cross_layer, dxl, dx0, accumulate=True)
+        emb_grads, gsegs = [], []
+        col = model.num_dense_features
+        for (name, emb), i in zip(model.embeddings.items(), ctx.idx):
+            g = torch.zeros_like(emb.weight)
+            emb_grads.append(g)
+            gsegs.append(ops.table_segment(g, i, col))
+            col += emb.embedding_dim
+        ops.embedding_backward(gsegs, B, dx0)
+        flat = [t for pair in lin_grads for t in pair]
+        return (None, None, None, None, None, *emb_grads, *flat, dw_out, db_out)
+
+
+def _dcn_params(model):
+    linears = [m for m in model.dnn if isinstance(m, torch.nn.Linear)]
+    return ([e.weight for e in model.embeddings.values()] + [t for l in linears for t in (l.weight, l.bias)]
+            + [model.output_layer.weight, model.output_layer.bias])
+
+
+def dcn_train_forward(model, dense, idx, cw, cb):
+    if model.output_layer.bias is None or any(m.bias is None for m in model.dnn if isinstance(m, torch.nn.Linear)):
+        raise NotImplementedError("rankops DCN training expects the reference's biased Linear layers")
+    return _DCNTrain.apply(model, dense, idx, cw, cb, *_dcn_params(model))
+
+
+# ---------------------------------------------------------------- optimizer
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam with the update as one rk_adam_step launch over all tensors of a group.
+    Same constructor, param_groups and state layout (`step`, `exp_avg`, `exp_avg_sq`), so state
+    dicts move between this class and torch.optim.Adam.  amsgrad / maximize / differentiable /
+    sparse gradients are not implemented and raise."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, *,
+                 maximize=False, foreach=None, capturable=False, differentiable=False, fused=None):
+        if amsgrad or maximize or differentiable:
+            raise NotImplementedError("rankops.Adam: amsgrad / maximize / differentiable are not implemented")
+        if not 0.0 <= float(lr):
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, maximize=maximize,
+                        foreach=foreach, capturable=capturable, differentiable=differentiable, fused=fused)
+        super().__init__(params, defaults)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            by_step = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise NotImplementedError("rankops.Adam: sparse gradients")
+                if p.device.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise RuntimeError("rankops.Adam: parameters must be contiguous float32 ROCm tensors")
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["step"] += 1
+                g = p.grad if p.grad.is_contiguous() and p.grad.dtype == torch.float32 else \
+                    p.grad.to(torch.float32).contiguous()
+                step = int(state["step"].item())
+                by_step.setdefault(step, []).append((p, g, state["exp_avg"], state["exp_avg_sq"]))
+            for step, entries in by_step.items():
+                dev = entries[0][0].device
+                ops.adam_step(entries, float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"], step,
+                              torch.cuda.current_stream(dev).cuda_stream)
+        return loss

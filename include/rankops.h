@@ -30,6 +30,12 @@
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
  *   rk_fwfm_forward    FwFM.forward()                        fwfm.py:114-139
+ *   training (loss.backward() + optimizer.step() of the train() loops, dcn.py:196-201):
+ *   rk_gemm            the Linear backward GEMMs (dX = dZ W, dW = dZ^T X, db)   dcn.py:147-150
+ *   rk_logit_head_backward  output_layer + sigmoid backward      dcn.py:177-179
+ *   rk_dcn_cross_backward   cross_layer backward w.r.t. x0        dcn.py:46-49
+ *   rk_embedding_backward   nn.Embedding dense weight gradient    dcn.py:131-138,163-166
+ *   rk_adam_step       torch.optim.Adam step (all tensors, one launch)  dcn.py:275
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -256,6 +262,56 @@ int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_
 int rk_fwfm_forward(const rk_segment* embeddings, const rk_segment* linear, int32_t num_fields,
                     int32_t dim, int64_t batch, const float* field_weight, const float* bias,
                     float* logit, float* prob, void* stream);
+
+/* ---- training (§8(f) #2) ---------------------------------------------------------------- */
+/* C[m, n] (+)= sum_r opA(m, r) * opB(n, r) on FP32 MFMA, with
+ *   opA(m, r) = trans_a ? A[r*lda + m] : A[m*lda + r], times [A_mask(m, r) > 0] when A_mask
+ *               (same layout and lda as A: the ReLU backward dz = dh * [h > 0]) is non-NULL;
+ *   opB(n, r) = trans_b ? B[r*ldb + n] : B[n*ldb + r];
+ *   row_sums[m] (+)= sum_r opA(m, r) when non-NULL (bias gradients).
+ * nn.Linear backward: dX = dZ W  -> rk_gemm(0, 1, B, K, N, dZ, ldz, mask, W, K, dX, ...);
+ *                     dW = dZ^T X -> rk_gemm(1, 1, N, K, B, dZ, ldz, mask, X, ldx, dW, K, db, ...).
+ * split <= 0 picks a reduction split (float atomics) that fills the GPU; accumulate = 0
+ * overwrites C / row_sums.                                                                  */
+int rk_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t R, const float* A,
+            int64_t lda, const float* A_mask, const float* B, int64_t ldb, float* C, int64_t ldc,
+            float* row_sums, int32_t accumulate, int32_t split, void* stream);
+
+/* Linear(ka + kb, 1) + sigmoid head over rows [xa | xb] (kb may be 0):
+ * g = dlogit + dprob * (1 - prob) * prob (either grad may be NULL); dxa/dxb = g w (NULL: not
+ * written); dw[ka + kb] = sum_b g x; db[0] = sum_b g (both overwritten); g_out[b] = g.       */
+int rk_logit_head_backward(const float* dlogit, const float* dprob, const float* prob, int64_t batch,
+                           const float* xa, int64_t ld_xa, int32_t ka, const float* xb, int64_t ld_xb,
+                           int32_t kb, const float* w, float* dxa, int64_t ld_dxa, float* dxb,
+                           int64_t ld_dxb, float* dw, float* db, float* g_out, void* stream);
+
+/* Gradient of num_layers cross layers (rk_dcn_cross's stack, weights [L, width]) w.r.t. x0 given
+ * dL/dx_L; written to dx0 (added when accumulate).  width <= 256, num_layers <= 8.           */
+int rk_dcn_cross_backward(const float* x0, int64_t ld_x0, int64_t batch, int32_t width,
+                          const float* cross_w, const float* cross_b, int32_t num_layers,
+                          const float* dxl, int64_t ld_dxl, float* dx0, int64_t ld_dx0,
+                          int32_t accumulate, void* stream);
+
+/* Dense nn.Embedding weight gradients: for every table segment (src = the [rows, dim] gradient
+ * buffer, written with float atomics — zero it first), grad[idx[b]] += dx[b, out_col:+dim].
+ * Dense segments (idx == NULL) are skipped; out-of-range indices raise RK_FLAG_INDEX_OOB.   */
+int rk_embedding_backward(const rk_segment* grads, int32_t nseg, int64_t batch, const float* dx,
+                          int64_t ld_dx, void* stream);
+
+typedef struct rk_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} rk_adam_tensor;
+
+/* One torch.optim.Adam step (amsgrad = maximize = False; L2 weight_decay added to the gradient)
+ * for every tensor in the list; `step` is the 1-based step count after increment.  Scalars are
+ * doubles (Python floats): derived values (1 - beta, lr / bias_correction1, ...) are formed in
+ * double and rounded to float once, as torch does.                                            */
+int rk_adam_step(const rk_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, int64_t step, void* stream);
 
 /* ---- evaluation metrics (the reference's evaluate(): dcn.py:214-239, same in every model) ---- */
 /* One batch into accum (3 x 8 bytes, zero it first): [0] double sum over batches of the batch's

@@ -1,0 +1,253 @@
+"""GPU parity of the training path: each backward kernel against torch
+autograd in fp32/fp64 on the CPU, rankops.Adam against torch.optim.Adam, and whole DCN train
+steps (forward, loss.backward(), optimizer.step()) against the oracle restatement of
+DCNModel.forward (oracle/reference_forward.py, dcn.py:161-180) differentiated by autograd —
+the reference's own training mechanism.  Tolerances are written per test."""
+import numpy as np
+import pytest
+import torch
+
+import helpers as H
+import rankops
+from oracle import reference_forward as ref
+from rankops import ops
+
+
+def _gemm_case(TA, TB, M, N, R, masked, seed):
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randn((R, M) if TA else (M, R), generator=g)
+    B = torch.randn((R, N) if TB else (N, R), generator=g)
+    mask = (torch.rand(A.shape, generator=g) > 0.4).float() * torch.rand(A.shape, generator=g) if masked else None
+    opA = (A.t() if TA else A).double()
+    if masked:
+        opA = opA * ((mask.t() if TA else mask) > 0).double()
+    opB = (B.t() if TB else B).double()
+    return A, B, mask, opA @ opB.t(), opA.sum(1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("TA", [0, 1])
+@pytest.mark.parametrize("TB", [0, 1])
+@pytest.mark.parametrize("shape", [(1, 1, 1), (64, 64, 32), (100, 70, 33), (4096, 50, 512), (512, 48, 4096),
+                                   (3, 300, 1000)])
+@pytest.mark.parametrize("split", [0, 1, 3])
+def test_gemm_matches_fp64(TA, TB, shape, split):
+    M, N, R = shape
+    A, B, mask, want, rs = _gemm_case(TA, TB, M, N, R, masked=(M + N) % 2 == 0, seed=M * 7 + N + R)
+    C = torch.full((M, N), 7.0, device="cuda")
+    sums = torch.full((M,), 7.0, device="cuda")
+    Ad, Bd = A.cuda(), B.cuda()
+    ops.gemm(TA, TB, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=mask.cuda() if mask is not None else None,
+             row_sums=sums, split=split)
+    tol = 1e-4 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
+    torch.testing.assert_close(sums.cpu().double(), rs, rtol=0, atol=tol)
+    # accumulate adds on top
+    ops.gemm(TA, TB, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=mask.cuda() if mask is not None else None,
+             accumulate=True, split=split)
+    torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
+
+
+@pytest.mark.gpu
+def test_gemm_strided_output():
+    A, B, _, want, _ = _gemm_case(0, 1, 37, 20, 45, False, 1)
+    C = torch.zeros(37, 64, device="cuda")
+    ops.gemm(False, True, 37, 20, 45, A.cuda(), 45, B.cuda(), 20, C, 64)
+    torch.testing.assert_close(C[:, :20].cpu().double(), want, rtol=0, atol=1e-4)
+    assert float(C[:, 20:].abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,K", [(4096, 512, 50), (1000, 256, 512), (7, 128, 256)])
+def test_linear_relu_backward(B, N, K):
+    g = torch.Generator().manual_seed(B + N)
+    x = torch.randn(B, K, generator=g)
+    lin = torch.nn.Linear(K, N)
+    xr = x.clone().requires_grad_(True)
+    y = torch.relu(lin(xr))
+    dy = torch.randn(B, N, generator=g)
+    y.backward(dy)
+    h = y.detach().cuda()
+    dx, dW, db = ops.linear_backward(dy.cuda(), x.cuda(), lin.weight.detach().cuda(), relu_out=h)
+    torch.testing.assert_close(dx.cpu(), xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dW.cpu(), lin.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db.cpu(), lin.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ka,kb", [(50, 128), (50, 300), (7, 0)])
+def test_logit_head_backward(ka, kb):
+    B = 1000
+    g = torch.Generator().manual_seed(ka + kb)
+    xa, xb = torch.randn(B, ka, generator=g), torch.randn(B, kb, generator=g)
+    lin = torch.nn.Linear(ka + kb, 1)
+    xa_r, xb_r = xa.clone().requires_grad_(True), xb.clone().requires_grad_(True)
+    logit = lin(torch.cat([xa_r, xb_r], 1))
+    prob = torch.sigmoid(logit)
+    dlogit, dprob = torch.randn(B, 1, generator=g), torch.randn(B, 1, generator=g)
+    torch.autograd.backward([logit, prob], [dlogit, dprob])
+    dev = "cuda"
+    dxa, dxb = torch.empty(B, ka, device=dev), torch.empty(B, kb, device=dev)
+    dw, db = torch.empty(1, ka + kb, device=dev), torch.empty(1, device=dev)
+    ops.logit_head_backward(dlogit.cuda(), dprob.cuda(), prob.detach().cuda(), xa.cuda(),
+                            xb.cuda() if kb else None, lin.weight.detach().cuda(), dxa, dxb if kb else None, dw, db)
+    torch.testing.assert_close(dxa.cpu(), xa_r.grad, rtol=1e-5, atol=1e-5)
+    if kb:
+        torch.testing.assert_close(dxb.cpu(), xb_r.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dw.cpu(), lin.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db.cpu(), lin.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,d", [(1, 50), (3, 50), (0, 50), (8, 200)])
+def test_dcn_cross_backward(L, d):
+    B = 513
+    g = torch.Generator().manual_seed(L * 100 + d)
+    x0 = torch.randn(B, d, generator=g)
+    cw, cb = torch.randn(L, d, generator=g) * 0.2, torch.randn(L, d, generator=g) * 0.1
+    x0r = x0.double().requires_grad_(True)  # fp64 reference: deep stacks amplify fp32 rounding
+    xl = x0r
+    for l in range(L):
+        xl = ref.dcn_cross_layer(x0r, xl, cw[l].double().reshape(d, 1), cb[l].double().reshape(d, 1))
+    dxl = torch.randn(B, d, generator=g)
+    xl.backward(dxl.double())
+    base = torch.randn(B, d, generator=g)
+    dx0 = base.clone().cuda()
+    ops.dcn_cross_backward(x0.cuda(), cw.cuda(), cb.cuda(), L, dxl.cuda(), dx0, accumulate=True)
+    want = base.double() + x0r.grad
+    torch.testing.assert_close(dx0.cpu().double(), want, rtol=1e-4, atol=1e-5 * float(want.abs().max()))
+
+
+@pytest.mark.gpu
+def test_embedding_backward_dense_grad():
+    B, W = 4096, 30
+    g = torch.Generator().manual_seed(3)
+    dx = torch.randn(B, W, generator=g)
+    rows = [5, 1000, 2]
+    idx = [torch.randint(0, r, (B,), generator=g) for r in rows]
+    idx[0][:100] = 3  # a hot row
+    grads = [torch.zeros(r, d, device="cuda") for r, d in zip(rows, (4, 16, 2))]
+    dxd = dx.cuda()
+    idx_d = [i.cuda() for i in idx]  # segments hold raw pointers: keep the tensors alive
+    segs = [ops.dense_segment(dxd, 8, 0)]
+    col = 8
+    for gr, i in zip(grads, idx_d):
+        segs.append(ops.table_segment(gr, i, col))
+        col += gr.shape[1]
+    ops.embedding_backward(segs, B, dxd)
+    col = 8
+    for gr, i in zip(grads, idx):
+        want = torch.zeros(gr.shape).index_add_(0, i, dx[:, col:col + gr.shape[1]])
+        torch.testing.assert_close(gr.cpu(), want, rtol=1e-5, atol=1e-4)
+        col += gr.shape[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_adam_matches_torch(wd):
+    g = torch.Generator().manual_seed(11)
+    shapes = [(1000, 16), (3,), (512, 50), (1,), (70000,)]
+    ps = [torch.randn(s, generator=g).cuda() for s in shapes]
+    qs = [p.clone() for p in ps]
+    pa = [torch.nn.Parameter(p) for p in ps]
+    qa = [torch.nn.Parameter(q) for q in qs]
+    ours = rankops.Adam(pa, lr=3e-3, weight_decay=wd)
+    theirs = torch.optim.Adam(qa, lr=3e-3, weight_decay=wd)
+    for step in range(6):
+        for a, b in zip(pa, qa):
+            gr = torch.randn(a.shape, generator=g).cuda() * (step + 1)
+            a.grad, b.grad = gr.clone(), gr.clone()
+        if step == 3:
+            pa[1].grad = None  # a parameter that skips a step keeps its own step count
+            qa[1].grad = None
+        ours.step()
+        theirs.step()
+    for a, b in zip(pa, qa):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-6)
+    for a, b in zip(pa, qa):
+        sa, sb = ours.state[a], theirs.state[b]
+        assert float(sa["step"]) == float(sb["step"])
+        # a few elements differ by an ulp (fma contraction of the lerp / addcmul)
+        torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-6)
+    # state dicts are interchangeable with torch.optim.Adam
+    ours2 = rankops.Adam(pa, lr=3e-3, weight_decay=wd)
+    ours2.load_state_dict(theirs.state_dict())
+    assert float(ours2.state[pa[0]]["step"]) == 6.0
+
+
+def _dcn_oracle_params(model):
+    return {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+
+
+def _dcn_step_check(model, cfg, B, seed, steps, opt_kind):
+    inp = H.make_inputs("dcn", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    p = _dcn_oracle_params(model)
+    names = [n for n, _ in model.named_parameters()]
+    opt = rankops.Adam(model.parameters(), lr=1e-3) if opt_kind == "rankops" else \
+        torch.optim.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in names], lr=1e-3)
+    crit = torch.nn.BCEWithLogitsLoss()
+    dinp = H.to_device(inp, "cuda")
+    hidden = len(cfg.get("hidden", [512, 256, 128]))
+    L = cfg.get("cross", 1)
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        torch.manual_seed(1234 + step)  # per-call cross draws: same generator state on both sides
+        prob, logit = H.call_model(model, "dcn", dinp)
+        loss = crit(logit.squeeze(), label.cuda())
+        loss.backward()
+        torch.manual_seed(1234 + step)
+        rprob, rlogit = ref.dcn_forward(p, inp["dense"], inp["category"], L, hidden)
+        rloss = crit(rlogit.squeeze(), label)
+        rloss.backward()
+        torch.testing.assert_close(logit.detach().cpu(), rlogit.detach(), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(prob.detach().cpu(), rprob.detach(), rtol=1e-4, atol=1e-4)
+        assert abs(float(loss.detach()) - float(rloss.detach())) < 1e-5
+        for n, prm in model.named_parameters():
+            want = p[n].grad
+            scale = max(1e-3, float(want.abs().max()))
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=2e-4 * scale, msg=f"grad {n} step {step}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in model.named_parameters():
+            torch.testing.assert_close(prm.detach().cpu(), p[n].detach(), rtol=1e-4, atol=1e-5,
+                                       msg=f"param {n} after step {step}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{}, {"cross": 3}, {"cross": 0}, {"hidden": [64, 300]}, {"vocab": H.WECHAT_VOCAB}],
+                         ids=["default", "cross3", "cross0", "wide_last", "wechat"])
+def test_dcn_train_steps_match_autograd(cfg):
+    model = H.build("dcn", cfg).cuda().train()
+    _dcn_step_check(model, cfg, 1024, seed=2000, steps=3, opt_kind="rankops")
+
+
+@pytest.mark.gpu
+def test_dcn_train_with_torch_adam_and_eval_after():
+    """The reference loop unchanged (torch.optim.Adam), then eval forward on the updated weights."""
+    model = H.build("dcn", {}).cuda().train()
+    _dcn_step_check(model, {}, 512, seed=2100, steps=2, opt_kind="torch")
+    model.eval()
+    inp = H.to_device(H.make_inputs("dcn", {}, 64, seed=5), "cuda")
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    torch.manual_seed(9)
+    with torch.no_grad():
+        prob, logit = H.call_model(model, "dcn", inp)
+    torch.manual_seed(9)
+    rprob, rlogit = ref.dcn_forward(p, H.to_device(inp, "cpu")["dense"], H.to_device(inp, "cpu")["category"], 1, 3)
+    torch.testing.assert_close(logit.cpu(), rlogit, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_dcn_train_no_grad_is_forward_only():
+    model = H.build("dcn", {"interaction_weights": "frozen"}).cuda().train()
+    inp = H.to_device(H.make_inputs("dcn", {}, 32), "cuda")
+    with torch.no_grad():
+        prob, logit = H.call_model(model, "dcn", inp)
+    assert not prob.requires_grad
+    prob2, logit2 = H.call_model(model, "dcn", inp)
+    assert prob2.requires_grad
+    torch.testing.assert_close(prob2.detach(), prob)
