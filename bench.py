@@ -369,6 +369,61 @@ def bench_metrics(batch, batches=256):
             "auc_abs_diff": abs(r[2] - ref[2]), "acc_equal": r[1] == ref[1], "loss_abs_diff": abs(r[0] - ref[0])}
 
 
+def bench_train(batch, steps, warmup):
+    """DCN training step (§8(f) #2) at `batch`, wechat tables: zero_grad, forward, BCEWithLogits
+    loss, loss.backward() (HIP backward kernels), Adam step — the reference's train() loop body
+    (dcn.py:195-201) with the per-call cross draws frozen; inputs in HBM.  Timed eagerly
+    (rankops.Adam) and as one captured hipGraph per step (rankops.Adam(capturable=True))."""
+    import helpers as H
+    import rankops
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    inp = None
+    res = {"model": "DCN", "batch": batch}
+    crit = torch.nn.BCEWithLogitsLoss()
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = H.build("dcn", cfg).cuda().train()
+        if inp is None:
+            inp = H.to_device(H.make_inputs("dcn", cfg, batch, seed=77), "cuda")
+            label = (torch.rand(batch, device="cuda") < 0.3).float()
+        opt = rankops.Adam(model.parameters(), lr=1e-3, capturable=(mode == "graph"))
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            prob, logit = model(inp["dense"], inp["category"])
+            loss = crit(logit.squeeze(), label)
+            loss.backward()
+            opt.step()
+
+        run = step
+        if mode == "graph":
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(g):
+                step()
+            run = g.replay
+        for _ in range(warmup):
+            run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / steps
+        res[mode] = {"samples_per_s": round(batch / t, 1), "ms_per_step": round(1e3 * t, 4)}
+        res["params"] = sum(p.numel() for p in model.parameters())
+        del model, opt
+    res["mode"] = ("forward + loss.backward() + Adam over all params (dense embedding gradients, as "
+                   "nn.Embedding(sparse=False) + torch.optim.Adam do)")
+    return res
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank):
@@ -449,6 +504,11 @@ def main():
             result["loader"] = bench_loader(model, args.batch)
         except Exception as exc:  # reported, never fatal for the headline line
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    if rank == 0 and world == 1 and not args.no_extras:
+        try:
+            result["train"] = bench_train(args.batch, max(10, args.steps // 2), 3)
+        except Exception as exc:  # reported, never fatal for the headline line
+            result["train"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_loader:
         try:
             result["eval_metrics"] = bench_metrics(args.batch)

@@ -114,6 +114,7 @@ int mlp_validate(const rk_mlp_layer* layers, int nlayers, int K0, const rk_epilo
       return fail(RK_ERR_INVALID, "%s: Dice layer %d incomplete", what, l);
     if (L.act == RK_ACT_PRELU && !L.act_alpha) return fail(RK_ERR_INVALID, "%s: PReLU needs alpha", what);
     if (L.act < 0 || L.act > RK_ACT_PRELU) return fail(RK_ERR_INVALID, "%s: unknown activation %d", what, L.act);
+    if (L.store && L.ld_store < L.n) return fail(RK_ERR_INVALID, "%s: layer %d store ld < n", what, l);
     if ((L.pre_scale != nullptr) != (L.pre_shift != nullptr) || (L.post_scale != nullptr) != (L.post_shift != nullptr))
       return fail(RK_ERR_INVALID, "%s: affine scale/shift must come in pairs", what);
     if (L.residual && (l == 0 || L.n != (l >= 2 ? layers[l - 2].n : K0)))

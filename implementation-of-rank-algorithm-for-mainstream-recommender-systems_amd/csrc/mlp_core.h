@@ -131,7 +131,7 @@ struct LayerPipe {
 template <int TPW, int RT = 1, int PD = kMlpPD>
 __device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_layer& L, const float* __restrict__ in,
                                           int ldin, float* __restrict__ out, int ldout, int Kp, int wave, int lane,
-                                          int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
+                                          int64_t m0, int rows, int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const int kchunks = Kp / 16;  // multiple of PD
   f32x4_t acc[TPW][RT];
@@ -178,6 +178,8 @@ __device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_la
   const int act = L.act;
   const float slope = L.slope;
   const bool has_res = L.residual != 0, has_pre = L.pre_scale != nullptr, has_post = L.post_scale != nullptr;
+  float* const store = L.store;
+  const int64_t ld_store = L.ld_store;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int n = 16 * (wave + kMlpWaves * j) + li;
@@ -196,6 +198,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_la
         const float z =
             real ? col_apply(P.ep[j], act, slope, acc[j][t][r], has_res, res[t][r], has_pre, has_post) : 0.f;
         out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
+        if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
       }
   }
 }
@@ -245,9 +248,9 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
     if (wave + kMlpWaves < ntiles)
-      mlp_layer<2, RT>(p2, L, in, ldin, out, ldout, Kp, wave, lane, 3 * l, t0);
+      mlp_layer<2, RT>(p2, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
     else if (wave < ntiles)
-      mlp_layer<1, RT>(p1, L, in, ldin, out, ldout, Kp, wave, lane, 3 * l, t0);
+      mlp_layer<1, RT>(p1, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
     if (l + 1 < nl) prepare(l + 1);
     MLP_MARK(3 * l + 1, t0);
     mlp_lds_barrier();

@@ -29,46 +29,58 @@ namespace rk {
 // current tile's MFMAs.
 // ------------------------------------------------------------------------------------------
 constexpr int kGT = 64;       // output tile edge
-constexpr int kGR = 32;       // reduction step
+constexpr int kGR = 64;       // reduction step (2048 MFMA cycles per wave: covers a global round trip)
 constexpr int kGLD = kGT + 1;  // LDS row stride
+constexpr int kGV = kGT * kGR / 256;  // staged values per thread and operand
 
 template <bool T>
 __device__ __forceinline__ void stage_load(const float* __restrict__ P, int64_t ld, const float* __restrict__ mask,
                                            int64_t rows, int64_t R, int64_t row0, int64_t r0, int tid,
-                                           float (&v)[8]) {
-  // 64 rows x 32 reduction values = 2048 = 8 per thread, coalesced along the contiguous dim
+                                           float (&v)[kGV]) {
+  // 64 rows x 64 reduction values, kGV per thread, coalesced along the contiguous dim.  Loads
+  // are unconditional (out-of-range lanes read element 0 and are zeroed afterwards) so all of
+  // them, and the mask's, are in flight together instead of one branch + wait per element.
+  int64_t off[kGV];
+  bool ok[kGV];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < kGV; ++i) {
     int rr, mm;
     if (T) {  // contiguous along rows
       mm = tid & 63;
       rr = (tid >> 6) + 4 * i;
     } else {  // contiguous along the reduction
-      rr = tid & 31;
-      mm = (tid >> 5) + 8 * i;
+      rr = tid & 63;
+      mm = (tid >> 6) + 4 * i;
     }
     const int64_t m = row0 + mm, r = r0 + rr;
-    float x = 0.f;
-    if (m < rows && r < R) {
-      const int64_t off = T ? r * ld + m : m * ld + r;
-      x = P[off];
-      if (mask && !(mask[off] > 0.f)) x = 0.f;
-    }
-    v[i] = x;
+    ok[i] = m < rows && r < R;
+    off[i] = ok[i] ? (T ? r * ld + m : m * ld + r) : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < kGV; ++i) v[i] = P[off[i]];
+  if (mask) {
+    float mk[kGV];
+#pragma unroll
+    for (int i = 0; i < kGV; ++i) mk[i] = mask[off[i]];
+#pragma unroll
+    for (int i = 0; i < kGV; ++i) v[i] = (ok[i] && mk[i] > 0.f) ? v[i] : 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < kGV; ++i) v[i] = ok[i] ? v[i] : 0.f;
   }
 }
 
 template <bool T>
-__device__ __forceinline__ void stage_store(float* __restrict__ S, int tid, const float (&v)[8]) {
+__device__ __forceinline__ void stage_store(float* __restrict__ S, int tid, const float (&v)[kGV]) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < kGV; ++i) {
     int rr, mm;
     if (T) {
       mm = tid & 63;
       rr = (tid >> 6) + 4 * i;
     } else {
-      rr = tid & 31;
-      mm = (tid >> 5) + 8 * i;
+      rr = tid & 63;
+      mm = (tid >> 6) + 4 * i;
     }
     S[rr * kGLD + mm] = v[i];
   }
@@ -92,7 +104,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float rsum = 0.f;
-  float va[8], vb[8];
+  float va[kGV], vb[kGV];
   if (rb < re) {
     stage_load<TA>(A, lda, A_mask, M, re, m0, rb, tid, va);
     stage_load<TB>(B, ldb, nullptr, N, re, n0, rb, tid, vb);
@@ -106,14 +118,23 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
       stage_load<TB>(B, ldb, nullptr, N, re, n0, r0 + kGR, tid, vb);
     }
     if (sums && tid < kGT) {
-#pragma unroll 8
+#pragma unroll 16
       for (int r = 0; r < kGR; ++r) rsum += As[r * kGLD + tid];
     }
     const float* a_col = As + wm * 32 + (lane & 31);
     const float* b_col = Bs + wn * 32 + (lane & 31);
     const int k1 = lane >> 5;
+    // all operand reads of the step first: one wait, then 32 back-to-back MFMAs (reading them one
+    // MFMA at a time put an LDS round trip in front of every MFMA)
+    float av[kGR / 2], bv[kGR / 2];
 #pragma unroll
-    for (int k = 0; k < kGR; k += 2) acc = mfma32(a_col[(k + k1) * kGLD], b_col[(k + k1) * kGLD], acc);
+    for (int k = 0; k < kGR / 2; ++k) {
+      av[k] = a_col[(2 * k + k1) * kGLD];
+      bv[k] = b_col[(2 * k + k1) * kGLD];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < kGR / 2; ++k) acc = mfma32(av[k], bv[k], acc);
     __syncthreads();
   }
   const int64_t n = n0 + wn * 32 + (lane & 31);
@@ -288,14 +309,24 @@ struct GradSegs {
   rk_segment s[RK_MAX_SEGMENTS];
 };
 
+// Small tables (rows * dim <= kEmbLdsFloats: device, tags, ...) take every sample, so global
+// atomics on them serialise: those are accumulated per workgroup in LDS first and flushed once.
+constexpr int kEmbLdsFloats = 8192;
+
 __global__ __launch_bounds__(256) void embedding_backward_kernel(GradSegs segs, int64_t batch,
                                                                  const float* __restrict__ dx, int64_t ld_dx,
                                                                  uint32_t* flags) {
+  __shared__ float acc[kEmbLdsFloats];
   const rk_segment& s = segs.s[blockIdx.y];
   if (!s.idx) return;
   const int dim = s.dim;
   const int64_t n = batch * dim;
   float* grad = const_cast<float*>(s.src);
+  const bool priv = s.rows * dim <= kEmbLdsFloats;
+  if (priv) {
+    for (int i = threadIdx.x; i < s.rows * dim; i += blockDim.x) acc[i] = 0.f;
+    __syncthreads();
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = i / dim;
     const int j = (int)(i - b * dim);
@@ -304,7 +335,18 @@ __global__ __launch_bounds__(256) void embedding_backward_kernel(GradSegs segs, 
       if (j == 0) flag_oob(flags);
       continue;
     }
-    atomicAdd(grad + r * s.src_ld + j, dx[b * ld_dx + s.out_col + j]);
+    const float v = dx[b * ld_dx + s.out_col + j];
+    if (priv)
+      atomicAdd(acc + r * dim + j, v);
+    else
+      atomicAdd(grad + r * s.src_ld + j, v);
+  }
+  if (priv) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < s.rows * dim; i += blockDim.x) {
+      const float v = acc[i];
+      if (v != 0.f) atomicAdd(grad + (i / dim) * s.src_ld + i % dim, v);
+    }
   }
 }
 
@@ -322,13 +364,24 @@ struct AdamList {
   int64_t chunk_start[kAdamMaxTensors + 1];
 };
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamList list, int n, float one_minus_b1, float beta2,
-                                                   float one_minus_b2, float eps, float weight_decay,
+// CAPTURABLE: the step count lives in device memory (torch's capturable=True layout, one float
+// per tensor, incremented by adam_step_inc_kernel first) and the bias corrections are formed on
+// the device in float in torch's capturable order:
+//   step_size = 1 / ((beta1^t - 1) / lr);  bc2_sqrt = sqrt(-(beta2^t - 1));
+//   p += m / ((sqrt(v) / bc2_sqrt + eps) / step_size)
+template <bool CAPTURABLE>
+__global__ __launch_bounds__(256) void adam_kernel(AdamList list, int n, float one_minus_b1, float beta1, float beta2,
+                                                   float one_minus_b2, float eps, float weight_decay, float lr,
                                                    float step_size, float bc2_sqrt) {
   const int64_t chunk = blockIdx.x;
   int t = 0;
   while (t + 1 < n && list.chunk_start[t + 1] <= chunk) ++t;
   const rk_adam_tensor& T = list.t[t];
+  if (CAPTURABLE) {
+    const float st = *T.step;
+    step_size = 1.f / ((powf(beta1, st) - 1.f) / lr);  // negative
+    bc2_sqrt = sqrtf(-(powf(beta2, st) - 1.f));
+  }
   const int64_t base = (chunk - list.chunk_start[t]) * kAdamChunk;
   const int64_t end = min<int64_t>(T.numel, base + kAdamChunk);
   for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
@@ -339,12 +392,22 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamList list, int n, float o
     m = m + one_minus_b1 * (g - m);  // lerp, weight < 0.5 branch
     float v = T.exp_avg_sq[i] * beta2;
     v = v + one_minus_b2 * g * g;  // addcmul_: self + value * t1 * t2
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p + (-step_size) * (m / denom);
+    if (CAPTURABLE) {
+      const float denom = (sqrtf(v) / bc2_sqrt + eps) / step_size;
+      p = p + m / denom;
+    } else {
+      const float denom = sqrtf(v) / bc2_sqrt + eps;
+      p = p + (-step_size) * (m / denom);
+    }
     T.exp_avg[i] = m;
     T.exp_avg_sq[i] = v;
     T.param[i] = p;
   }
+}
+
+__global__ void adam_step_inc_kernel(AdamList list, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) *list.t[t].step += 1.f;
 }
 
 }  // namespace rk
@@ -448,7 +511,8 @@ RK_API int rk_embedding_backward(const rk_segment* grads, int32_t nseg, int64_t 
 
 RK_API int rk_adam_step(const rk_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
                         double weight_decay, int64_t step, void* stream) {
-  if (!tensors || n < 0 || step < 1 || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f))
+  if (!tensors || n < 0 || (step < 1 && !(n > 0 && tensors[0].step)) || !(beta1 >= 0.0 && beta1 < 1.0) ||
+      !(beta2 >= 0.0 && beta2 < 1.0))
     return fail(RK_ERR_INVALID, "rk_adam_step: bad arguments");
   // every scalar derived in double like torch's Python-side arithmetic, then rounded to float
   // (the kernels' opmath): 1 - beta2 from a float beta2 would be off by 1e-5 relative
@@ -458,6 +522,7 @@ RK_API int rk_adam_step(const rk_adam_tensor* tensors, int32_t n, double lr, dou
   const float bc2_sqrt = (float)std::sqrt(bc2);
   const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   hipStream_t st = (hipStream_t)stream;
+  const bool capturable = n > 0 && tensors[0].step != nullptr;
   for (int base = 0; base < n; base += kAdamMaxTensors) {
     AdamList list;
     const int cnt = std::min(kAdamMaxTensors, n - base);
@@ -466,14 +531,22 @@ RK_API int rk_adam_step(const rk_adam_tensor* tensors, int32_t n, double lr, dou
       const rk_adam_tensor& t = tensors[base + i];
       if (t.numel < 0 || (t.numel > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)))
         return fail(RK_ERR_INVALID, "rk_adam_step: tensor %d invalid", base + i);
+      if ((t.step != nullptr) != capturable)
+        return fail(RK_ERR_INVALID, "rk_adam_step: device step counters must be given for all tensors or none");
       list.t[i] = t;
       list.chunk_start[i] = chunks;
       chunks += (t.numel + kAdamChunk - 1) / kAdamChunk;
     }
     list.chunk_start[cnt] = chunks;
+    if (capturable) adam_step_inc_kernel<<<1, kAdamMaxTensors, 0, st>>>(list, cnt);
     if (chunks == 0) continue;
-    adam_kernel<<<(unsigned)chunks, 256, 0, st>>>(list, cnt, omb1, (float)beta2, omb2, (float)eps,
-                                                  (float)weight_decay, step_size, bc2_sqrt);
+    if (capturable)
+      adam_kernel<true><<<(unsigned)chunks, 256, 0, st>>>(list, cnt, omb1, (float)beta1, (float)beta2, omb2,
+                                                          (float)eps, (float)weight_decay, (float)lr, 0.f, 0.f);
+    else
+      adam_kernel<false><<<(unsigned)chunks, 256, 0, st>>>(list, cnt, omb1, (float)beta1, (float)beta2, omb2,
+                                                           (float)eps, (float)weight_decay, (float)lr, step_size,
+                                                           bc2_sqrt);
   }
   return check_launch("rk_adam_step");
 }

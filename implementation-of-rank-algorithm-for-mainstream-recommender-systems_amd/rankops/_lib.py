@@ -92,12 +92,14 @@ class MlpLayer(ctypes.Structure):
         ("act_alpha_len", c_int32),
         ("post_scale", c_void_p),
         ("post_shift", c_void_p),
+        ("store", c_void_p),
+        ("ld_store", c_int64),
     ]
 
 
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
-                ("numel", c_int64)]
+                ("numel", c_int64), ("step", c_void_p)]
 
 
 RK_MLP_MAX_LAYERS = 8

@@ -105,6 +105,10 @@ class InteractionWeights:
     def get(self, device):
         if self.mode == "frozen" and self._cached is not None and self._cached[0] == device:
             return self._cached[1]
+        if torch.device(device).type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("per-call interaction weights are drawn on the host each forward and cannot be "
+                               "captured in a hipGraph; use interaction_weights='frozen' (or run the forward once "
+                               "before capturing)")
         host = self._draw()
         dev = _to_device(host, device)
         if self.mode == "frozen":

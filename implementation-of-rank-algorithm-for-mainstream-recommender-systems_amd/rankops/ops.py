@@ -340,8 +340,9 @@ def embedding_backward(grad_segs, batch, dx):
 
 
 def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, stream):
-    """entries: list of (param, grad, exp_avg, exp_avg_sq) contiguous float32 tensors."""
+    """entries: list of (param, grad, exp_avg, exp_avg_sq[, device step tensor]) float32 tensors."""
     lib = _lib.load()
-    arr = (_lib.AdamTensor * len(entries))(*[_lib.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(),
-                                                             v.data_ptr(), p.numel()) for p, g, m, v in entries])
+    arr = (_lib.AdamTensor * len(entries))(*[
+        _lib.AdamTensor(e[0].data_ptr(), e[1].data_ptr(), e[2].data_ptr(), e[3].data_ptr(), e[0].numel(),
+                        e[4].data_ptr() if len(e) > 4 else None) for e in entries])
     check(lib.rk_adam_step(arr, len(entries), lr, beta1, beta2, eps, weight_decay, step, stream), "rk_adam_step")

@@ -20,8 +20,8 @@ from __future__ import annotations
 
 import torch
 
-from . import ops
-from .common import const
+from . import common, ops
+from .common import PACKED, const, fused_mlp_fits
 
 
 # ---------------------------------------------------------------- shared pieces
@@ -30,18 +30,32 @@ def mlp_relu_forward(x, linears, head_w, head_b, partial, logit, prob):
     """Linear+ReLU stack with the Linear(N,1)+sigmoid head; returns the activations [x, h1, ...].
     The head reads head_partial (the other input block's share of the logit) when given."""
     B, dev = x.shape[0], x.device
-    hs = [x]
+    hs = [x] + [torch.empty(B, lin.out_features, device=dev, dtype=torch.float32) for lin in linears]
+    if common.FUSED_MLP and fused_mlp_fits(x.shape[1], [lin.out_features for lin in linears]):
+        # one rk_mlp_forward launch, each layer's activations also stored for the backward
+        # under graph capture the packing is captured too (replays repack the updated weights);
+        # a cached image would be frozen into the graph
+        pack = ops.pack_mlp_weight if torch.cuda.is_current_stream_capturing() else PACKED
+        # the packed images must stay referenced until the launch: the layer descriptors hold raw
+        # pointers, and a freed image's block would be handed to the next allocation
+        packed = [pack(lin.weight) for lin in linears]
+        mls = [ops.make_mlp_layer(lin.weight, pw, bias=lin.bias, act="relu", store=y, ld_store=y.stride(0))
+               for lin, pw, y in zip(linears, packed, hs[1:])]
+        ep = ops.make_epilogue(head_w=head_w, head_b=head_b, head_logit=logit, head_prob=prob,
+                               head_partial=partial)
+        ops.mlp_forward(x, mls, ep)
+        del packed
+        return hs
     h = x
     for i, lin in enumerate(linears):
         last = i == len(linears) - 1
-        y = torch.empty(B, lin.out_features, device=dev, dtype=torch.float32)
+        y = hs[i + 1]
         if last and lin.out_features <= 256:
             ep = ops.make_epilogue(bias=lin.bias, act="relu", head_w=head_w, head_b=head_b, head_logit=logit,
                                    head_prob=prob, head_partial=partial)
         else:
             ep = ops.make_epilogue(bias=lin.bias, act="relu")
         ops.linear(h, lin.weight, y, epilogue=ep)
-        hs.append(y)
         h = y
     if linears[-1].out_features > 256:  # head as its own N = 1 GEMM
         ep = ops.make_epilogue(bias=head_b, head_w=const(dev, 1.0), head_b=const(dev, 0.0), head_logit=logit,
@@ -59,6 +73,23 @@ def mlp_relu_backward(dh, hs, linears):
         grads[i] = (dW, db)
         dh = dx
     return dh, grads
+
+
+def embedding_grads(weights, idx, col0, dx):
+    """Dense nn.Embedding gradients of the tables whose rows sit side by side in dx from column
+    col0 on: one zero-filled flat buffer for all tables (one fill), then rk_embedding_backward."""
+    total = sum(w.numel() for w in weights)
+    flat = torch.zeros(total, device=dx.device, dtype=torch.float32)
+    grads, segs = [], []
+    off, col = 0, col0
+    for w, i in zip(weights, idx):
+        g = flat[off:off + w.numel()].view(w.shape)
+        grads.append(g)
+        segs.append(ops.table_segment(g, i, col))
+        off += w.numel()
+        col += w.shape[1]
+    ops.embedding_backward(segs, dx.shape[0], dx)
+    return grads
 
 
 def _grad_out(g, like):
@@ -113,14 +144,8 @@ class _DCNTrain(torch.autograd.Function):
         linears = [m for m in model.dnn if isinstance(m, torch.nn.Linear)]
         dx0, lin_grads = mlp_relu_backward(dh, hs, linears)
         ops.dcn_cross_backward(x0, cw, cb, model.num_cross_layer, dxl, dx0, accumulate=True)
-        emb_grads, gsegs = [], []
-        col = model.num_dense_features
-        for (name, emb), i in zip(model.embeddings.items(), ctx.idx):
-            g = torch.zeros_like(emb.weight)
-            emb_grads.append(g)
-            gsegs.append(ops.table_segment(g, i, col))
-            col += emb.embedding_dim
-        ops.embedding_backward(gsegs, B, dx0)
+        emb_grads = embedding_grads([e.weight for e in model.embeddings.values()], ctx.idx,
+                                    model.num_dense_features, dx0)
         flat = [t for pair in lin_grads for t in pair]
         return (None, None, None, None, None, *emb_grads, *flat, dw_out, db_out)
 
@@ -167,6 +192,7 @@ class Adam(torch.optim.Optimizer):
                 loss = closure()
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
+            capturable = group["capturable"]
             by_step = {}
             for p in group["params"]:
                 if p.grad is None:
@@ -177,16 +203,28 @@ class Adam(torch.optim.Optimizer):
                     raise RuntimeError("rankops.Adam: parameters must be contiguous float32 ROCm tensors")
                 state = self.state[p]
                 if len(state) == 0:
-                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    # torch's layout: a float32 step tensor, on the device when capturable
+                    state["step"] = torch.zeros((), dtype=torch.float32, device=p.device) if capturable \
+                        else torch.tensor(0.0, dtype=torch.float32)
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state["step"] += 1
                 g = p.grad if p.grad.is_contiguous() and p.grad.dtype == torch.float32 else \
                     p.grad.to(torch.float32).contiguous()
-                step = int(state["step"].item())
-                by_step.setdefault(step, []).append((p, g, state["exp_avg"], state["exp_avg_sq"]))
+                if capturable:  # incremented on the device by rk_adam_step: graph-capturable
+                    if state["step"].device != p.device:
+                        state["step"] = state["step"].to(p.device)
+                    by_step.setdefault(0, []).append((p, g, state["exp_avg"], state["exp_avg_sq"], state["step"]))
+                else:
+                    if state["step"].device.type != "cpu":
+                        state["step"] = state["step"].cpu()
+                    state["step"] += 1
+                    by_step.setdefault(int(state["step"].item()), []).append(
+                        (p, g, state["exp_avg"], state["exp_avg_sq"]))
             for step, entries in by_step.items():
                 dev = entries[0][0].device
                 ops.adam_step(entries, float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"], step,
                               torch.cuda.current_stream(dev).cuda_stream)
+                # the kernel wrote through raw pointers: bump the version counters as torch's
+                # in-place ops would, so weight-derived caches (packed MLP images) are rebuilt
+                torch.autograd.graph.increment_version([t for e in entries for t in (e[0], e[2], e[3])])
         return loss

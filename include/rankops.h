@@ -149,6 +149,9 @@ typedef struct rk_mlp_layer {
   int32_t act_alpha_len;
   const float* post_scale;
   const float* post_shift;
+  float* store; /* optional: this layer's activations also written to store[m * ld_store + n]
+                   (the training forward keeps them for the backward) */
+  int64_t ld_store;
 } rk_mlp_layer;
 
 /* ---- runtime ---- */
@@ -304,10 +307,13 @@ typedef struct rk_adam_tensor {
   float* exp_avg;
   float* exp_avg_sq;
   int64_t numel;
+  float* step; /* optional device step counter (torch capturable=True): incremented on the device,
+                  bias corrections formed there; give it for all tensors of a call or for none */
 } rk_adam_tensor;
 
 /* One torch.optim.Adam step (amsgrad = maximize = False; L2 weight_decay added to the gradient)
- * for every tensor in the list; `step` is the 1-based step count after increment.  Scalars are
+ * for every tensor in the list; `step` is the 1-based step count after increment (ignored when
+ * the tensors carry device step counters: then the call is graph-capturable).  Scalars are
  * doubles (Python floats): derived values (1 - beta, lr / bias_correction1, ...) are formed in
  * double and rounded to float once, as torch does.                                            */
 int rk_adam_step(const rk_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,

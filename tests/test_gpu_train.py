@@ -251,3 +251,70 @@ def test_dcn_train_no_grad_is_forward_only():
     prob2, logit2 = H.call_model(model, "dcn", inp)
     assert prob2.requires_grad
     torch.testing.assert_close(prob2.detach(), prob)
+
+
+@pytest.mark.gpu
+def test_adam_capturable_matches_torch_capturable():
+    g = torch.Generator().manual_seed(12)
+    shapes = [(1000, 16), (3,), (70000,)]
+    pa = [torch.nn.Parameter(torch.randn(s, generator=g).cuda()) for s in shapes]
+    qa = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+    ours = rankops.Adam(pa, lr=2e-3, capturable=True)
+    theirs = torch.optim.Adam(qa, lr=2e-3, capturable=True)
+    for step in range(5):
+        for a, b in zip(pa, qa):
+            gr = torch.randn(a.shape, generator=g).cuda()
+            a.grad, b.grad = gr.clone(), gr.clone()
+        ours.step()
+        theirs.step()
+    for a, b in zip(pa, qa):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-6)
+        assert ours.state[a]["step"].device.type == "cuda" and float(ours.state[a]["step"]) == 5.0
+
+
+@pytest.mark.gpu
+def test_dcn_train_step_graph_capture_matches_eager():
+    """Whole train step (zero_grad, forward, loss.backward(), capturable rankops.Adam) captured in
+    one hipGraph and replayed, against the same steps run eagerly on a twin model."""
+    cfg = {"interaction_weights": "frozen"}
+    B = 512
+    a = H.build("dcn", cfg).cuda().train()
+    b = H.build("dcn", cfg).cuda().train()
+    b.load_state_dict(a.state_dict())
+    inp = H.to_device(H.make_inputs("dcn", cfg, B, seed=3), "cuda")
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(4)) < 0.3).float().cuda()
+    crit = torch.nn.BCEWithLogitsLoss()
+    oa = rankops.Adam(a.parameters(), lr=1e-3, capturable=True)
+    ob = rankops.Adam(b.parameters(), lr=1e-3, capturable=True)
+    torch.manual_seed(0)
+    H.call_model(a, "dcn", inp)  # frozen cross draw
+    torch.manual_seed(0)
+    H.call_model(b, "dcn", inp)
+
+    def step(model, opt):
+        opt.zero_grad(set_to_none=True)
+        prob, logit = H.call_model(model, "dcn", inp)
+        loss = crit(logit.squeeze(), label)
+        loss.backward()
+        opt.step()
+        return loss
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step(a, oa)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    oa.zero_grad(set_to_none=True)
+    with torch.cuda.graph(graph):
+        static_loss = step(a, oa)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    for _ in range(2 + 3):  # warmups + replays (capturing records the step, it does not run it)
+        eager_loss = step(b, ob)
+    torch.cuda.synchronize()
+    assert abs(float(static_loss.detach()) - float(eager_loss.detach())) < 1e-5
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.detach(), pb.detach(), rtol=1e-5, atol=1e-6, msg=n)
