@@ -163,6 +163,14 @@ __global__ void zero2d_kernel(float* __restrict__ p, int64_t rows, int64_t cols,
     p[(i / cols) * ld + i % cols] = 0.f;
 }
 
+__global__ void relu_backward_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                     float* __restrict__ out, int64_t n, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = y[i] > 0.f ? dy[i] : 0.f;
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
 static void zero2d(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t st) {
   const int64_t n = rows * cols;
   if (n <= 0) return;
@@ -454,6 +462,14 @@ RK_API int rk_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64
   RK_GEMM_CASE(true, true)
 #undef RK_GEMM_CASE
   return check_launch("rk_gemm");
+}
+
+RK_API int rk_relu_backward(const float* dy, const float* y, float* out, int64_t n, int32_t accumulate, void* stream) {
+  if (n < 0 || (n > 0 && (!dy || !y || !out))) return fail(RK_ERR_INVALID, "rk_relu_backward: bad arguments");
+  if (n == 0) return RK_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 8 * num_cus());
+  relu_backward_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(dy, y, out, n, accumulate);
+  return check_launch("rk_relu_backward");
 }
 
 RK_API int rk_logit_head_backward(const float* dlogit, const float* dprob, const float* prob, int64_t batch,

@@ -162,6 +162,7 @@ SIGNATURES = {
     "rk_logit_head_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32,
                                               c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int64, c_void_p,
                                               c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_embedding_backward": (ctypes.c_int, [_SEG_P, c_int32, c_int64, c_void_p, c_int64, c_void_p]),

@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, train
 from . import common
 from .common import InteractionWeights, check_eval, const, draw_residual_units, fused_mlp_fits, load_vocabulary, \
     table_rows
@@ -62,7 +62,8 @@ class DeepCrossingModel(common.EngineModule):
         return load_vocabulary(vocab_dir, filename)
 
     def forward(self, dense, category):
-        check_eval(self)
+        # no BatchNorm / Dropout: train mode computes the eval forward; with autograd recording it
+        # runs under rankops.train._DeepCrossingTrain (HIP backward)
         dense = ops.as_f32(dense, "dense")
         B = dense.shape[0]
         dev = dense.device
@@ -74,6 +75,9 @@ class DeepCrossingModel(common.EngineModule):
             idx = ops.as_index(category[name], f"category[{name!r}]")
             segs.append(ops.table_segment(emb.weight, idx, col))
             col += emb.embedding_dim
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            idx = [ops.as_index(category[name], f"category[{name!r}]") for name in self.embeddings]
+            return train.deepcrossing_train_forward(self, dense, idx, self.residual_weights.get(dev))
         x = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
         ops.concat_gather(segs, B, x)
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)

@@ -326,6 +326,15 @@ def logit_head_backward(dlogit, dprob, prob, xa, xb, w, dxa, dxb, dw, db, g_out=
                                      _lib.stream_of(xa)), "rk_logit_head_backward")
 
 
+def relu_backward(dy, y, out, accumulate=False):
+    lib = _lib.load()
+    if not (dy.is_contiguous() and y.is_contiguous() and out.is_contiguous()) or dy.shape != y.shape != out.shape:
+        raise ValueError("rankops.relu_backward: contiguous tensors of one shape expected")
+    check(lib.rk_relu_backward(ptr(dy), ptr(y), ptr(out), dy.numel(), int(accumulate), _lib.stream_of(dy)),
+          "rk_relu_backward")
+    return out
+
+
 def dcn_cross_backward(x0, cross_w, cross_b, num_layers, dxl, dx0, accumulate=True):
     lib = _lib.load()
     check(lib.rk_dcn_cross_backward(ptr(x0), x0.stride(0), x0.shape[0], x0.shape[1], ptr(cross_w), ptr(cross_b),

@@ -13,8 +13,10 @@ parameter gradients back to autograd — so `loss.backward()` fills every `.grad
 reference does and the unchanged loop works with `torch.optim.Adam` or with `rankops.Adam`
 (the same update as one fused launch over all tensors, `rk_adam_step`).
 
-Models with training support: DCNModel (`dcn.py:114-180`: embeddings, cross stack, ReLU MLP,
-output_layer + sigmoid; no BatchNorm / Dropout, so train and eval forwards coincide).
+Models with training support (no BatchNorm / Dropout in them, so their train and eval forwards
+coincide): DCNModel (`dcn.py:114-180`: embeddings, cross stack, ReLU MLP, output_layer +
+sigmoid) and DeepCrossingModel (`deepcrossing.py:106-163`: embeddings, residual units,
+output_layer + sigmoid).
 """
 from __future__ import annotations
 
@@ -160,6 +162,92 @@ def dcn_train_forward(model, dense, idx, cw, cb):
     if model.output_layer.bias is None or any(m.bias is None for m in model.dnn if isinstance(m, torch.nn.Linear)):
         raise NotImplementedError("rankops DCN training expects the reference's biased Linear layers")
     return _DCNTrain.apply(model, dense, idx, cw, cb, *_dcn_params(model))
+
+
+# ---------------------------------------------------------------- DeepCrossing
+
+class _DeepCrossingTrain(torch.autograd.Function):
+    """DeepCrossingModel forward + backward (deepcrossing.py:146-163): gather, residual units
+    (per-call Linear(d, I) / Linear(I, d) drawn like the reference — not module parameters, so
+    only the gradient w.r.t. their input is propagated), output_layer + sigmoid."""
+
+    @staticmethod
+    def forward(ctx, model, dense, idx, units, *params):
+        B, dev = dense.shape[0], dense.device
+        d, I = model.input_dim, model.residual_internal_dim
+        segs = [ops.dense_segment(dense, model.num_dense_features, 0)]
+        col = model.num_dense_features
+        for emb, i in zip(model.embeddings.values(), idx):
+            segs.append(ops.table_segment(emb.weight, i, col))
+            col += emb.embedding_dim
+        x0 = torch.empty(B, d, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, x0)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head = dict(head_w=model.output_layer.weight, head_b=model.output_layer.bias, head_logit=logit,
+                    head_prob=prob)
+        acts = []  # h_1, y_1, h_2, y_2, ...
+        for _ in units:
+            acts += [torch.empty(B, I, device=dev, dtype=torch.float32),
+                     torch.empty(B, d, device=dev, dtype=torch.float32)]
+        widths = [w for _ in units for w in (I, d)]
+        if units and common.FUSED_MLP and fused_mlp_fits(d, widths):
+            pack = ops.pack_mlp_weight if torch.cuda.is_current_stream_capturing() else PACKED
+            packed = [(pack(w1), pack(w2)) for w1, b1, w2, b2 in units]
+            layers = []
+            for (w1, b1, w2, b2), (p1, p2), j in zip(units, packed, range(0, len(acts), 2)):
+                layers.append(ops.make_mlp_layer(w1, p1, bias=b1, act="relu", store=acts[j], ld_store=I))
+                layers.append(ops.make_mlp_layer(w2, p2, bias=b2, act="relu", residual=1, store=acts[j + 1],
+                                                 ld_store=d))
+            ops.mlp_forward(x0, layers, ops.make_epilogue(**head))
+            del packed
+        else:
+            x = x0
+            for (w1, b1, w2, b2), j in zip(units, range(0, len(acts), 2)):
+                ops.linear(x, w1, acts[j], epilogue=ops.make_epilogue(bias=b1, act="relu"))
+                ops.linear(acts[j], w2, acts[j + 1], epilogue=ops.make_epilogue(
+                    bias=b2, residual=x, ld_residual=x.stride(0), act="relu"))
+                x = acts[j + 1]
+            ep = ops.make_epilogue(bias=model.output_layer.bias, head_w=const(dev, 1.0), head_b=const(dev, 0.0),
+                                   head_logit=logit, head_prob=prob)
+            ops.linear(x, model.output_layer.weight, None, epilogue=ep)
+        ctx.model, ctx.idx = model, idx
+        ctx.save_for_backward(x0, prob, *[t for u in units for t in (u[0], u[2])], *acts)
+        return prob, logit
+
+    @staticmethod
+    def backward(ctx, dprob, dlogit):
+        model = ctx.model
+        x0, prob, *rest = ctx.saved_tensors
+        n = (len(rest)) // 4
+        ws, acts = rest[:2 * n], rest[2 * n:]
+        B, d = x0.shape
+        dev = x0.device
+        last = acts[-1] if n else x0
+        dy = torch.empty(B, d, device=dev, dtype=torch.float32)
+        dw_out = torch.empty_like(model.output_layer.weight)
+        db_out = torch.empty(1, device=dev, dtype=torch.float32)
+        ops.logit_head_backward(_grad_out(dlogit, prob), _grad_out(dprob, prob), prob, last, None,
+                                model.output_layer.weight, dy, None, dw_out, db_out)
+        for u in range(n - 1, -1, -1):
+            w1, w2 = ws[2 * u], ws[2 * u + 1]
+            h, y = acts[2 * u], acts[2 * u + 1]
+            I = h.shape[1]
+            # y = relu(x + h W2^T + b2), h = relu(x W1^T + b1)
+            dh = torch.empty(B, I, device=dev, dtype=torch.float32)
+            ops.gemm(False, True, B, I, d, dy, d, w2, I, dh, A_mask=y)           # dz2 W2
+            dx = torch.empty(B, d, device=dev, dtype=torch.float32)
+            ops.relu_backward(dy, y, dx)                                        # residual path
+            ops.gemm(False, True, B, d, I, dh, I, w1, d, dx, A_mask=h, accumulate=True)  # + dz1 W1
+            dy = dx
+        emb_grads = embedding_grads([e.weight for e in model.embeddings.values()], ctx.idx,
+                                    model.num_dense_features, dy)
+        return (None, None, None, None, *emb_grads, dw_out, db_out)
+
+
+def deepcrossing_train_forward(model, dense, idx, units):
+    params = [e.weight for e in model.embeddings.values()] + [model.output_layer.weight, model.output_layer.bias]
+    return _DeepCrossingTrain.apply(model, dense, idx, units, *params)
 
 
 # ---------------------------------------------------------------- optimizer

@@ -34,6 +34,7 @@
  *   rk_gemm            the Linear backward GEMMs (dX = dZ W, dW = dZ^T X, db)   dcn.py:147-150
  *   rk_logit_head_backward  output_layer + sigmoid backward      dcn.py:177-179
  *   rk_dcn_cross_backward   cross_layer backward w.r.t. x0        dcn.py:46-49
+ *   rk_relu_backward   ReLU backward (residual_unit's outer ReLU) deepcrossing.py:41
  *   rk_embedding_backward   nn.Embedding dense weight gradient    dcn.py:131-138,163-166
  *   rk_adam_step       torch.optim.Adam step (all tensors, one launch)  dcn.py:275
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
@@ -279,6 +280,11 @@ int rk_fwfm_forward(const rk_segment* embeddings, const rk_segment* linear, int3
 int rk_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t R, const float* A,
             int64_t lda, const float* A_mask, const float* B, int64_t ldb, float* C, int64_t ldc,
             float* row_sums, int32_t accumulate, int32_t split, void* stream);
+
+/* out[i] (+)= dy[i] * [y[i] > 0] over n contiguous floats (ReLU backward from its output; the
+ * residual path of residual_unit, deepcrossing.py:41).                                        */
+int rk_relu_backward(const float* dy, const float* y, float* out, int64_t n, int32_t accumulate,
+                     void* stream);
 
 /* Linear(ka + kb, 1) + sigmoid head over rows [xa | xb] (kb may be 0):
  * g = dlogit + dprob * (1 - prob) * prob (either grad may be NULL); dxa/dxb = g w (NULL: not

@@ -318,3 +318,44 @@ def test_dcn_train_step_graph_capture_matches_eager():
     assert abs(float(static_loss.detach()) - float(eager_loss.detach())) < 1e-5
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.detach(), pb.detach(), rtol=1e-5, atol=1e-6, msg=n)
+
+
+def _dc_step_check(cfg, B, seed, steps):
+    model = H.build("deepcrossing", cfg).cuda().train()
+    inp = H.make_inputs("deepcrossing", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    names = [n for n, _ in model.named_parameters()]
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in names], lr=1e-3)
+    crit = torch.nn.BCEWithLogitsLoss()
+    dinp = H.to_device(inp, "cuda")
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        torch.manual_seed(4321 + step)  # per-call residual-unit draws on both sides
+        prob, logit = H.call_model(model, "deepcrossing", dinp)
+        loss = crit(logit.squeeze(), label.cuda())
+        loss.backward()
+        torch.manual_seed(4321 + step)
+        rprob, rlogit = ref.deepcrossing_forward(p, inp["dense"], inp["category"], cfg.get("internal", 128),
+                                                 cfg.get("units", 1))
+        rloss = crit(rlogit.squeeze(), label)
+        rloss.backward()
+        torch.testing.assert_close(logit.detach().cpu(), rlogit.detach(), rtol=1e-4, atol=1e-4)
+        for n, prm in model.named_parameters():
+            want = p[n].grad
+            scale = max(1e-3, float(want.abs().max()))
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=2e-4 * scale, msg=f"grad {n} step {step}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in model.named_parameters():
+            torch.testing.assert_close(prm.detach().cpu(), p[n].detach(), rtol=1e-4, atol=1e-5,
+                                       msg=f"param {n} after step {step}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{}, {"units": 3, "internal": 64}, {"units": 0}, {"units": 2, "internal": 600}],
+                         ids=["default", "units3", "units0", "wide_internal"])
+def test_deepcrossing_train_steps_match_autograd(cfg):
+    _dc_step_check(cfg, 1024, seed=2200, steps=3)
