@@ -162,6 +162,22 @@ SIGNATURES = {
     "rk_logit_head_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32,
                                               c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int64, c_void_p,
                                               c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_rng_next": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "rk_dropout_mask": (ctypes.c_int, [ctypes.c_uint64, c_void_p, c_int64, c_int32, ctypes.c_double, c_void_p,
+                                       c_void_p]),
+    "rk_bn_act_train_forward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32, c_void_p,
+                                               c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_int32, ctypes.c_double, ctypes.c_uint64, c_void_p,
+                                               c_void_p, c_int64, c_void_p]),
+    "rk_bn_act_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_double,
+                                          ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                          c_void_p]),
+    "rk_fm_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32,
+                                      c_void_p, c_int64, c_void_p]),
+    "rk_fm_combine_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, train
 from .common import EngineModule, Layer, check_eval, load_vocabulary, run_tail, table_rows
 
 WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
@@ -58,16 +58,21 @@ class DeepFM(EngineModule):
             width = unit
         self.deep_output_layer = nn.Linear(width, 1)
         self.final_layer = nn.Linear(3, 1)
+        self._dropout = train.DropoutStreams()
 
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
 
     def forward(self, category):
-        check_eval(self)
+        if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            check_eval(self)  # a train-mode forward without autograd is not implemented
         names = [c for c in self.second_order_embeddings if c in category]
         if len(names) != self.num_categories:
             missing = [c for c in self.second_order_embeddings if c not in category]
             raise KeyError(f"DeepFM.forward: category features missing: {missing}")
+        if self.training:  # BatchNorm batch statistics, Dropout, HIP backward (rankops.train)
+            idx = [ops.as_index(category[n], f"category[{n!r}]") for n in names]
+            return train.deepfm_train_forward(self, names, idx)
         D = self.embedding_dim
         first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
         B = first.shape[0]

@@ -355,3 +355,53 @@ def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, stream):
         _lib.AdamTensor(e[0].data_ptr(), e[1].data_ptr(), e[2].data_ptr(), e[3].data_ptr(), e[0].numel(),
                         e[4].data_ptr() if len(e) > 4 else None) for e in entries])
     check(lib.rk_adam_step(arr, len(entries), lr, beta1, beta2, eps, weight_decay, step, stream), "rk_adam_step")
+
+
+def rng_next(counter: torch.Tensor, slot: torch.Tensor):
+    lib = _lib.load()
+    check(lib.rk_rng_next(ptr(counter), ptr(slot), _lib.stream_of(counter)), "rk_rng_next")
+
+
+def dropout_mask(seed: int, slot: torch.Tensor, batch: int, n: int, p: float) -> torch.Tensor:
+    lib = _lib.load()
+    out = torch.empty(batch, n, device=slot.device, dtype=torch.float32)
+    check(lib.rk_dropout_mask(seed, ptr(slot), batch, n, p, ptr(out), _lib.stream_of(out)), "rk_dropout_mask")
+    return out
+
+
+def bn_act_train_forward(z, bias, bn, relu, p, seed, slot, y, save_mean, save_invstd, workspace):
+    """bn: an nn.BatchNorm1d (train mode) or None."""
+    lib = _lib.load()
+    track = bn is not None and bn.track_running_stats and bn.running_mean is not None
+    check(lib.rk_bn_act_train_forward(
+        ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), int(bn is not None),
+        ptr(bn.weight) if bn is not None else None, ptr(bn.bias) if bn is not None else None,
+        float(bn.eps) if bn is not None else 0.0, float(bn.momentum) if bn is not None else 0.0,
+        ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None, ptr(workspace),
+        ptr(save_mean), ptr(save_invstd), int(relu), float(p), seed, ptr(slot), ptr(y), y.stride(0),
+        _lib.stream_of(z)), "rk_bn_act_train_forward")
+
+
+def bn_act_backward(dy, z, bias, bn, relu, p, seed, slot, save_mean, save_invstd, workspace, dz, dgamma, dbeta):
+    lib = _lib.load()
+    check(lib.rk_bn_act_backward(
+        ptr(dy), dy.stride(0), ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), int(bn is not None),
+        ptr(bn.weight) if bn is not None else None, ptr(bn.bias) if bn is not None else None, ptr(save_mean),
+        ptr(save_invstd), int(relu), float(p), seed, ptr(slot), ptr(workspace), ptr(dz), dz.stride(0), ptr(dgamma),
+        ptr(dbeta), _lib.stream_of(dy)), "rk_bn_act_backward")
+
+
+def fm_backward(deep_in, d_deep, dfm2, num_fields, dim, out):
+    lib = _lib.load()
+    check(lib.rk_fm_backward(ptr(deep_in), deep_in.stride(0), ptr(d_deep), d_deep.stride(0) if d_deep is not None else 0,
+                             ptr(dfm2), deep_in.shape[0], num_fields, dim, ptr(out), out.stride(0),
+                             _lib.stream_of(deep_in)), "rk_fm_backward")
+
+
+def fm_combine_backward(dprob, dtotal, dfm1_in, dfm2_in, ddeep_in, prob, fm1, fm2, deep, final_w, dfm1, dfm2, ddeep,
+                        dfinal_w, dfinal_b):
+    lib = _lib.load()
+    check(lib.rk_fm_combine_backward(ptr(dprob), ptr(dtotal), ptr(dfm1_in), ptr(dfm2_in), ptr(ddeep_in), ptr(prob),
+                                     ptr(fm1), ptr(fm2), ptr(deep), ptr(final_w), prob.shape[0], ptr(dfm1), ptr(dfm2),
+                                     ptr(ddeep), ptr(dfinal_w), ptr(dfinal_b), _lib.stream_of(prob)),
+          "rk_fm_combine_backward")

@@ -77,17 +77,18 @@ def mlp_relu_backward(dh, hs, linears):
     return dh, grads
 
 
-def embedding_grads(weights, idx, col0, dx):
+def embedding_grads(weights, idx, col0, dx, cols=None):
     """Dense nn.Embedding gradients of the tables whose rows sit side by side in dx from column
-    col0 on: one zero-filled flat buffer for all tables (one fill), then rk_embedding_backward."""
+    col0 on (or at the given `cols`): one zero-filled flat buffer for all tables (one fill),
+    then rk_embedding_backward."""
     total = sum(w.numel() for w in weights)
     flat = torch.zeros(total, device=dx.device, dtype=torch.float32)
     grads, segs = [], []
     off, col = 0, col0
-    for w, i in zip(weights, idx):
+    for k, (w, i) in enumerate(zip(weights, idx)):
         g = flat[off:off + w.numel()].view(w.shape)
         grads.append(g)
-        segs.append(ops.table_segment(g, i, col))
+        segs.append(ops.table_segment(g, i, col if cols is None else cols[k]))
         off += w.numel()
         col += w.shape[1]
     ops.embedding_backward(segs, dx.shape[0], dx)
@@ -248,6 +249,178 @@ class _DeepCrossingTrain(torch.autograd.Function):
 def deepcrossing_train_forward(model, dense, idx, units):
     params = [e.weight for e in model.embeddings.values()] + [model.output_layer.weight, model.output_layer.bias]
     return _DeepCrossingTrain.apply(model, dense, idx, units, *params)
+
+
+# ---------------------------------------------------------------- DeepFM
+
+def deep_units(layers):
+    """(Linear, BatchNorm1d or None, ReLU?, dropout p) per unit of a Linear/[BN]/ReLU/[Dropout]
+    sequence (deepfm.py:100-109)."""
+    units = []
+    for m in layers:
+        if isinstance(m, torch.nn.Linear):
+            units.append([m, None, False, 0.0])
+        elif isinstance(m, torch.nn.BatchNorm1d):
+            units[-1][1] = m
+        elif isinstance(m, torch.nn.ReLU):
+            units[-1][2] = True
+        elif isinstance(m, torch.nn.Dropout):
+            units[-1][3] = float(m.p) if m.training else 0.0
+        else:
+            raise NotImplementedError(f"rankops training: unsupported layer {type(m).__name__}")
+    for lin, bn, relu, _ in units:
+        if bn is not None and (bn.momentum is None or not bn.training):
+            raise NotImplementedError("rankops training: BatchNorm1d needs a numeric momentum and train mode")
+    return units
+
+
+class DropoutStreams:
+    """Per-model dropout stream counter on the device (advanced by rk_rng_next once per train
+    forward, so hipGraph replays draw fresh masks) and the seed (torch.initial_seed() when first
+    used: seeded runs repeat their masks)."""
+
+    def __init__(self):
+        self.counter = None
+        self.seed = None
+
+    def next(self, device):
+        if self.counter is None or self.counter.device != device:
+            self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+            self.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF
+        slot = torch.empty(1, dtype=torch.int64, device=device)
+        ops.rng_next(self.counter, slot)
+        return self.seed, slot
+
+
+def deep_stack_forward(x, units, seed, slot):
+    """Train-mode Linear -> [BN] -> ReLU -> [Dropout] stack; returns per-unit saved tensors."""
+    B, dev = x.shape[0], x.device
+    saved = []
+    h = x
+    for u, (lin, bn, relu, p) in enumerate(units):
+        n = lin.out_features
+        z = torch.empty(B, n, device=dev, dtype=torch.float32)
+        ops.gemm(False, False, B, n, lin.in_features, h, h.stride(0), lin.weight, lin.weight.stride(0), z)
+        y = torch.empty(B, n, device=dev, dtype=torch.float32)
+        mean = torch.empty(n, device=dev, dtype=torch.float32)
+        invstd = torch.empty(n, device=dev, dtype=torch.float32)
+        ws = torch.empty(2 * n, device=dev, dtype=torch.float64)
+        ops.bn_act_train_forward(z, lin.bias, bn, relu, p, seed + u, slot, y, mean, invstd, ws)
+        if bn is not None and bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        saved.append((z, y, mean, invstd))
+        h = y
+    return saved
+
+
+def deep_stack_backward(dy, x, units, saved, seed, slot):
+    """Backward of deep_stack_forward from dL/d(last output); returns (dL/dx, per-unit grads
+    [dW, db, (dgamma, dbeta)])."""
+    B, dev = x.shape[0], x.device
+    grads = [None] * len(units)
+    for u in range(len(units) - 1, -1, -1):
+        lin, bn, relu, p = units[u]
+        z, y, mean, invstd = saved[u]
+        n, K = lin.out_features, lin.in_features
+        h_in = saved[u - 1][1] if u > 0 else x
+        dz = torch.empty(B, n, device=dev, dtype=torch.float32)
+        ws = torch.empty(2 * n, device=dev, dtype=torch.float64)
+        dg = torch.empty(n, device=dev, dtype=torch.float32) if bn is not None and bn.weight is not None else None
+        dbt = torch.empty(n, device=dev, dtype=torch.float32) if bn is not None and bn.bias is not None else None
+        ops.bn_act_backward(dy, z, lin.bias, bn, relu, p, seed + u, slot, mean, invstd, ws, dz, dg, dbt)
+        dW = torch.empty(n, K, device=dev, dtype=torch.float32)
+        db = torch.empty(n, device=dev, dtype=torch.float32)
+        ops.gemm(True, True, n, K, B, dz, dz.stride(0), h_in, h_in.stride(0), dW, row_sums=db)
+        dx = torch.empty(B, K, device=dev, dtype=torch.float32)
+        ops.gemm(False, True, B, K, n, dz, dz.stride(0), lin.weight, lin.weight.stride(0), dx)
+        g = [dW, db if lin.bias is not None else None]
+        if bn is not None:
+            g += [t for t in (dg, dbt) if t is not None]
+        grads[u] = g
+        dy = dx
+    return dy, grads
+
+
+def _unit_params(units):
+    out = []
+    for lin, bn, _, _ in units:
+        out += [lin.weight] + ([lin.bias] if lin.bias is not None else [])
+        if bn is not None:
+            out += [t for t in (bn.weight, bn.bias) if t is not None]
+    return out
+
+
+class _DeepFMTrain(torch.autograd.Function):
+    """DeepFM forward + backward in train mode (deepfm.py:121-151): FM gather, Linear -> BN(batch
+    statistics) -> ReLU -> Dropout units, deep_output_layer, final_layer + sigmoid."""
+
+    @staticmethod
+    def forward(ctx, model, names, idx, *params):
+        D = model.embedding_dim
+        F = len(names)
+        B, dev = idx[0].shape[0], idx[0].device
+        second, first = [], []
+        for f, (name, i) in enumerate(zip(names, idx)):
+            second.append(ops.table_segment(model.second_order_embeddings[name].weight, i, f * D))
+            first.append(ops.table_segment(model.first_order_embeddings[name].weight, i, f))
+        deep_in = torch.empty(B, F * D, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        ops.fm_gather(second, first, D, B, deep_in, fm1, fm2)
+        units = deep_units(model.deep_layers)
+        seed, slot = model._dropout.next(dev)
+        saved = deep_stack_forward(deep_in, units, seed, slot)
+        last = saved[-1][1] if saved else deep_in
+        deep = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        total = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        ep = ops.make_epilogue(head_w=model.deep_output_layer.weight, head_b=model.deep_output_layer.bias, fm1=fm1,
+                               fm2=fm2, final_w=model.final_layer.weight, final_b=model.final_layer.bias,
+                               head_aux=deep, head_logit=total, head_prob=prob)
+        ops.mlp_forward(last, [], ep)
+        ctx.model, ctx.names, ctx.idx, ctx.units, ctx.seed = model, names, idx, units, seed
+        ctx.save_for_backward(deep_in, fm1, fm2, deep, prob, slot, *[t for s in saved for t in s])
+        return prob, total, fm1, fm2, deep
+
+    @staticmethod
+    def backward(ctx, dprob, dtotal, dfm1_o, dfm2_o, ddeep_o):
+        model, units = ctx.model, ctx.units
+        deep_in, fm1, fm2, deep, prob, slot, *flat = ctx.saved_tensors
+        saved = [tuple(flat[4 * u:4 * u + 4]) for u in range(len(units))]
+        B, dev = deep_in.shape[0], deep_in.device
+        D, F = model.embedding_dim, len(ctx.names)
+        go = [_grad_out(g, prob) for g in (dprob, dtotal, dfm1_o, dfm2_o, ddeep_o)]
+        dfm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        dfm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        ddeep = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        dfinal_w = torch.empty_like(model.final_layer.weight)
+        dfinal_b = torch.empty(1, device=dev, dtype=torch.float32)
+        ops.fm_combine_backward(*go, prob, fm1, fm2, deep, model.final_layer.weight, dfm1, dfm2, ddeep, dfinal_w,
+                                dfinal_b)
+        last = saved[-1][1] if saved else deep_in
+        dy = torch.empty_like(last)
+        dw_do = torch.empty_like(model.deep_output_layer.weight)
+        db_do = torch.empty(1, device=dev, dtype=torch.float32)
+        ops.logit_head_backward(ddeep, None, None, last, None, model.deep_output_layer.weight, dy, None, dw_do, db_do)
+        d_deep_in, unit_grads = deep_stack_backward(dy, deep_in, units, saved, ctx.seed, slot)
+        d_second = torch.empty(B, F * D, device=dev, dtype=torch.float32)
+        ops.fm_backward(deep_in, d_deep_in, dfm2, F, D, d_second)
+        g2 = embedding_grads([model.second_order_embeddings[n].weight for n in ctx.names], ctx.idx, 0, d_second)
+        g1 = embedding_grads([model.first_order_embeddings[n].weight for n in ctx.names], ctx.idx, 0, dfm1,
+                             cols=[0] * F)
+        flat_g = [t for g in unit_grads for t in g if t is not None]
+        return (None, None, None, *g1, *g2, *flat_g, dw_do, db_do, dfinal_w, dfinal_b)
+
+
+def deepfm_train_forward(model, names, idx):
+    if model.deep_output_layer.bias is None or model.final_layer.bias is None:
+        raise NotImplementedError("rankops DeepFM training expects the reference's biased output layers")
+    units = deep_units(model.deep_layers)
+    params = ([model.first_order_embeddings[n].weight for n in names]
+              + [model.second_order_embeddings[n].weight for n in names] + _unit_params(units)
+              + [model.deep_output_layer.weight, model.deep_output_layer.bias, model.final_layer.weight,
+                 model.final_layer.bias])
+    return _DeepFMTrain.apply(model, names, idx, *params)
 
 
 # ---------------------------------------------------------------- optimizer

@@ -37,6 +37,10 @@
  *   rk_relu_backward   ReLU backward (residual_unit's outer ReLU) deepcrossing.py:41
  *   rk_embedding_backward   nn.Embedding dense weight gradient    dcn.py:131-138,163-166
  *   rk_adam_step       torch.optim.Adam step (all tensors, one launch)  dcn.py:275
+ *   rk_bn_act_train_forward / rk_bn_act_backward  Linear -> BatchNorm1d (train) -> ReLU -> Dropout
+ *                      and its backward                       deepfm.py:100-109
+ *   rk_fm_backward, rk_fm_combine_backward  FM and final_layer + sigmoid backward  deepfm.py:122-151
+ *   rk_rng_next, rk_dropout_mask  dropout stream counter / explicit mask
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -306,6 +310,51 @@ int rk_dcn_cross_backward(const float* x0, int64_t ld_x0, int64_t batch, int32_t
  * Dense segments (idx == NULL) are skipped; out-of-range indices raise RK_FLAG_INDEX_OOB.   */
 int rk_embedding_backward(const rk_segment* grads, int32_t nseg, int64_t batch, const float* dx,
                           int64_t ld_dx, void* stream);
+
+/* Dropout streams: *slot = *counter; *counter += 1 (one thread, stream-ordered, graph-safe). */
+int rk_rng_next(int64_t* counter, int64_t* slot, void* stream);
+
+/* The keep mask a dropout stream draws, as the multiplier it applies: out[b*n + j] = 1/(1-p) or 0.
+ * keep(i) = mix64(seed, *stream_slot, i) >= p * 2^32 (splitmix64 finaliser; not torch's Philox). */
+int rk_dropout_mask(uint64_t seed, const int64_t* stream_slot, int64_t batch, int32_t n,
+                    double dropout_p, float* out, void* stream);
+
+/* y = Dropout_p(ReLU(BatchNorm1d_train(z + bias))) over [batch, n] (deepfm.py:101-108):
+ * batch statistics (biased variance) in fp64, save_mean / save_invstd written, running_mean /
+ * running_var updated with momentum and the unbiased variance (both may be NULL); batch_norm =
+ * 0 skips the normalisation, relu = 0 the ReLU, dropout_p = 0 the dropout.  workspace: 2n
+ * doubles.  gamma / beta may be NULL (affine = False).                                        */
+int rk_bn_act_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
+                            int32_t batch_norm, const float* gamma, const float* beta, float eps,
+                            float momentum, float* running_mean, float* running_var,
+                            double* workspace, float* save_mean, float* save_invstd, int32_t relu,
+                            double dropout_p, uint64_t seed, const int64_t* stream_slot, float* y,
+                            int64_t ldy, void* stream);
+
+/* Backward of rk_bn_act_train_forward given dy: dz (gradient w.r.t. z, i.e. the Linear output
+ * before its bias), dgamma / dbeta (may be NULL).  Same seed / stream slot as the forward.    */
+int rk_bn_act_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch,
+                       int32_t n, const float* bias, int32_t batch_norm, const float* gamma,
+                       const float* beta, const float* save_mean, const float* save_invstd,
+                       int32_t relu, double dropout_p, uint64_t seed, const int64_t* stream_slot,
+                       double* workspace, float* dz, int64_t lddz, float* dgamma, float* dbeta,
+                       void* stream);
+
+/* DeepFM FM backward (deepfm.py:122-140): out[b, f*dim + d] = d_deep[b, f*dim + d] +
+ * dfm2[b] * (S_d - e_{f,d}), e = the saved deep input (concatenated second-order rows),
+ * S_d = sum_f e_{f,d}.  d_deep / dfm2 may be NULL (zero).                                      */
+int rk_fm_backward(const float* deep_in, int64_t ld_in, const float* d_deep, int64_t ld_d,
+                   const float* dfm2, int64_t batch, int32_t num_fields, int32_t dim, float* out,
+                   int64_t ld_out, void* stream);
+
+/* final_layer(cat[fm1, fm2, deep]) + sigmoid backward (deepfm.py:147-150) with incoming grads of
+ * all five outputs (each may be NULL): g = dtotal + dprob (1 - p) p; dfm1 = dfm1_in + g w0,
+ * dfm2 = dfm2_in + g w1, ddeep = ddeep_in + g w2; dfinal_w[3], dfinal_b[1] overwritten.        */
+int rk_fm_combine_backward(const float* dprob, const float* dtotal, const float* dfm1_in,
+                           const float* dfm2_in, const float* ddeep_in, const float* prob,
+                           const float* fm1, const float* fm2, const float* deep,
+                           const float* final_w, int64_t batch, float* dfm1, float* dfm2,
+                           float* ddeep, float* dfinal_w, float* dfinal_b, void* stream);
 
 typedef struct rk_adam_tensor {
   float* param;

@@ -130,6 +130,34 @@ def deepfm_forward(p, category, fields, num_hidden=3, batch_norm=True, dropout_r
     return torch.sigmoid(total), total, fm_first, fm_second, deep_logit
 
 
+def deepfm_forward_train(p, category, fields, num_hidden=3, batch_norm=True, dropout_rate=0.1, masks=None,
+                         momentum=0.1, eps=1e-5):
+    """DeepFM.forward in model.train() (deepfm.py:121-151): BatchNorm1d with batch statistics
+    (running_mean / running_var in `p` updated in place, num_batches_tracked += 1), Dropout as the
+    given per-unit multiplier masks (0 or 1/(1-p)); differentiable w.r.t. the tensors in `p`."""
+    first = [F.embedding(category[c], p[f"first_order_embeddings.{c}.weight"]) for c in fields if c in category]
+    fm_first = torch.sum(torch.cat(first, dim=1), dim=1, keepdim=True)
+    second = [F.embedding(category[c], p[f"second_order_embeddings.{c}.weight"]) for c in fields if c in category]
+    sum_embedding = torch.sum(torch.stack(second, dim=1), dim=1)
+    sum_embedding_square = torch.square(sum_embedding)
+    square_sum_embedding = torch.sum(torch.stack([torch.square(e) for e in second], dim=1), dim=1)
+    fm_second = 0.5 * torch.sum(sum_embedding_square - square_sum_embedding, dim=1, keepdim=True)
+    h = torch.cat(second, dim=1)
+    for u, (lin, bn) in enumerate(deepfm_layout(num_hidden, batch_norm, dropout_rate)):
+        h = _lin(h, p, f"deep_layers.{lin}.")
+        if bn is not None:
+            pre = f"deep_layers.{bn}."
+            h = F.batch_norm(h, p[pre + "running_mean"], p[pre + "running_var"], p[pre + "weight"], p[pre + "bias"],
+                             training=True, momentum=momentum, eps=eps)
+            p[pre + "num_batches_tracked"] += 1
+        h = torch.relu(h)
+        if masks is not None and masks[u] is not None:
+            h = h * masks[u]
+    deep_logit = _lin(h, p, "deep_output_layer.")
+    total = _lin(torch.cat([fm_first, fm_second, deep_logit], dim=1), p, "final_layer.")
+    return torch.sigmoid(total), total, fm_first, fm_second, deep_logit
+
+
 # ---------------------------------------------------------------------------- DIN
 
 def dice_eval(x, p, prefix):

@@ -105,8 +105,8 @@ def test_python_layer_refuses_cpu_tensors():
         H.call_model(m, "dcn", inp)
     with pytest.raises(RuntimeError, match="ROCm GPU"):  # DCN trains on the engine, still GPU-only
         H.call_model(m.train(), "dcn", inp)
-    fm = H.build("deepfm", {}).train()  # no training path yet: refused, never a silent eager fallback
+    afm = H.build("afm", {}).train()  # no training path yet: refused, never a silent eager fallback
     with pytest.raises(NotImplementedError):
-        H.call_model(fm, "deepfm", H.make_inputs("deepfm", {}, 4))
+        H.call_model(afm, "afm", H.make_inputs("afm", {}, 4))
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         rankops.cross_layer(torch.zeros(2, 50), torch.zeros(2, 50), 0)

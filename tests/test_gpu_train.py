@@ -359,3 +359,109 @@ def _dc_step_check(cfg, B, seed, steps):
                          ids=["default", "units3", "units0", "wide_internal"])
 def test_deepcrossing_train_steps_match_autograd(cfg):
     _dc_step_check(cfg, 1024, seed=2200, steps=3)
+
+
+def _deepfm_masks(model, B):
+    """The dropout multipliers the last train forward drew (rk_dropout_mask on its stream)."""
+    from rankops import train as rt
+    units = rt.deep_units(model.deep_layers)
+    slot = model._dropout.counter - 1
+    return [ops.dropout_mask(model._dropout.seed + u, slot, B, lin.out_features, p).cpu() if p > 0 else None
+            for u, (lin, bn, relu, p) in enumerate(units)]
+
+
+def _deepfm_step_check(cfg, B, seed, steps):
+    model = H.build("deepfm", cfg).cuda().train()
+    fields = list(cfg.get("fields", {f: 0 for f in rankops.deepfm.WECHAT_FIELDS}).keys())
+    hidden = len(cfg.get("hidden", [512, 256, 128]))
+    inp = H.make_inputs("deepfm", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    sd = model.state_dict()
+    params = dict(model.named_parameters())
+    p = {k: (v.detach().cpu().clone().requires_grad_(True) if k in params else v.detach().cpu().clone())
+         for k, v in sd.items()}
+    names = list(params)
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in names], lr=1e-3)
+    crit = torch.nn.BCELoss()
+    dinp = H.to_device(inp, "cuda")
+    layers = list(model.deep_layers)
+    bn_fed_biases = {f"deep_layers.{i}.bias" for i, m in enumerate(layers[:-1])
+                     if isinstance(m, torch.nn.Linear) and isinstance(layers[i + 1], torch.nn.BatchNorm1d)}
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        out = H.call_model(model, "deepfm", dinp)
+        loss = crit(out[0].squeeze(), label.cuda())
+        loss.backward()
+        masks = _deepfm_masks(model, B)
+        ref = ref_forward_train(p, inp["category"], fields, hidden, cfg.get("batch_norm", True),
+                                cfg.get("dropout", 0.1), masks)
+        rloss = crit(ref[0].squeeze(), label)
+        rloss.backward()
+        for i, (o, r) in enumerate(zip(out, ref)):
+            torch.testing.assert_close(o.detach().cpu(), r.detach(), rtol=1e-4, atol=1e-4, msg=f"output {i}")
+        for k, v in model.state_dict().items():
+            # running statistics and num_batches_tracked; after the first step the running_mean
+            # also carries the noise-driven pre-BN biases (skipped below), so compare it once
+            if k not in params and (step == 0 or not k.endswith("running_mean")):
+                torch.testing.assert_close(v.cpu(), p[k], rtol=1e-4, atol=1e-5, msg=f"buffer {k} step {step}")
+        for n, prm in model.named_parameters():
+            want = p[n].grad
+            scale = max(1e-3, float(want.abs().max()))
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=5e-4 * scale, msg=f"grad {n} step {step}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in model.named_parameters():
+            if n in bn_fed_biases:
+                # a Linear bias right before BatchNorm has a zero true gradient (BN removes any shift);
+                # both sides hold rounding noise there, which Adam normalises to +-lr steps
+                continue
+            _assert_adam_params_close(prm.detach().cpu(), p[n].detach(), lr=1e-3, steps=1,
+                                      what=f"param {n} after step {step}")
+        # re-synchronise the oracle to the engine so every step is checked from the same state
+        # (Adam's noise-level sign flips would otherwise compound across steps)
+        with torch.no_grad():
+            for k, v in model.state_dict().items():
+                p[k].copy_(v.cpu())
+            for n, prm in model.named_parameters():
+                for key in ("exp_avg", "exp_avg_sq"):
+                    ref_opt.state[p[n]][key].copy_(opt.state[prm][key].cpu())
+
+
+def _assert_adam_params_close(got, want, lr, steps, what):
+    """Adam moves every element by about lr per step whatever its gradient's size, so elements whose
+    gradient is at rounding-noise level (|g| << the tensor's scale; fp32 sums in another order) may
+    step the other way: allow up to 0.5% of elements within 2 lr per step, the rest within 1e-5."""
+    diff = (got - want).abs()
+    bad = diff > 1e-5 + 1e-4 * want.abs()
+    frac = float(bad.float().mean())
+    assert frac <= 0.005, f"{what}: {frac:.4%} of elements differ (max {float(diff.max()):.3g})"
+    assert float(diff.max()) <= 2 * lr * steps + 1e-5, f"{what}: max diff {float(diff.max()):.3g}"
+
+
+def ref_forward_train(p, category, fields, hidden, bn, dropout, masks):
+    return ref.deepfm_forward_train(p, category, fields, hidden, bn, dropout, masks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{}, {"batch_norm": False}, {"vocab": H.WECHAT_VOCAB},
+                                 {"dim": 32, "fields": {f"field_{i:02d}": 500 + 37 * i for i in range(30)}}],
+                         ids=["default", "no_bn", "wechat", "fields30"])
+def test_deepfm_train_steps_match_autograd(cfg):
+    _deepfm_step_check(cfg, 1024, seed=2300, steps=3)
+
+
+@pytest.mark.gpu
+def test_dropout_mask_rate_and_freshness():
+    counter = torch.zeros(1, dtype=torch.int64, device="cuda")
+    slot = torch.empty(1, dtype=torch.int64, device="cuda")
+    ops.rng_next(counter, slot)
+    m1 = ops.dropout_mask(7, slot, 4096, 512, 0.1)
+    ops.rng_next(counter, slot)
+    m2 = ops.dropout_mask(7, slot, 4096, 512, 0.1)
+    keep1 = (m1 > 0).float().mean().item()
+    assert abs(keep1 - 0.9) < 0.005
+    assert set(torch.unique(m1).tolist()) == {0.0, float(torch.tensor(1 / 0.9, dtype=torch.float32))}
+    assert (m1 != m2).float().mean().item() > 0.1  # a new stream draws a new mask
+    assert int(counter) == 2
