@@ -369,29 +369,30 @@ def bench_metrics(batch, batches=256):
             "auc_abs_diff": abs(r[2] - ref[2]), "acc_equal": r[1] == ref[1], "loss_abs_diff": abs(r[0] - ref[0])}
 
 
-def bench_train(batch, steps, warmup):
+def bench_train(batch, steps, warmup, name="dcn"):
     """DCN training step (§8(f) #2) at `batch`, wechat tables: zero_grad, forward, BCEWithLogits
     loss, loss.backward() (HIP backward kernels), Adam step — the reference's train() loop body
     (dcn.py:195-201) with the per-call cross draws frozen; inputs in HBM.  Timed eagerly
     (rankops.Adam) and as one captured hipGraph per step (rankops.Adam(capturable=True))."""
     import helpers as H
     import rankops
-    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"} if name == "dcn" else \
+        {"vocab": H.WECHAT_VOCAB}
     inp = None
-    res = {"model": "DCN", "batch": batch}
-    crit = torch.nn.BCEWithLogitsLoss()
+    res = {"model": {"dcn": "DCN", "deepfm": "DeepFM"}[name], "batch": batch}
+    crit = torch.nn.BCEWithLogitsLoss() if name == "dcn" else torch.nn.BCELoss()
     for mode in ("eager", "graph"):
         torch.manual_seed(0)
-        model = H.build("dcn", cfg).cuda().train()
+        model = H.build(name, cfg).cuda().train()
         if inp is None:
-            inp = H.to_device(H.make_inputs("dcn", cfg, batch, seed=77), "cuda")
+            inp = H.to_device(H.make_inputs(name, cfg, batch, seed=77), "cuda")
             label = (torch.rand(batch, device="cuda") < 0.3).float()
         opt = rankops.Adam(model.parameters(), lr=1e-3, capturable=(mode == "graph"))
 
         def step():
             opt.zero_grad(set_to_none=True)
-            prob, logit = model(inp["dense"], inp["category"])
-            loss = crit(logit.squeeze(), label)
+            out = H.call_model(model, name, inp)
+            loss = crit(out[1].squeeze(), label) if name == "dcn" else crit(out[0].squeeze(), label)
             loss.backward()
             opt.step()
 
@@ -506,7 +507,7 @@ def main():
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_extras:
         try:
-            result["train"] = bench_train(args.batch, max(10, args.steps // 2), 3)
+            result["train"] = {m: bench_train(args.batch, max(10, args.steps // 2), 3, m) for m in ("dcn", "deepfm")}
         except Exception as exc:  # reported, never fatal for the headline line
             result["train"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_loader:
