@@ -195,10 +195,12 @@ def test_cpu_inputs_raise():
 
 @pytest.mark.gpu
 def test_training_mode_raises():
-    model = H.build("deepfm", {}).cuda().train()
-    inp = H.to_device(H.make_inputs("deepfm", {}, 8), "cuda")
+    """Models whose backward is not built yet refuse a train-mode forward instead of silently
+    running eval semantics (DCN, DeepCrossing and DeepFM train: tests/test_gpu_train.py)."""
+    model = H.build("bst", {"T": 20}).cuda().train()
+    inp = H.to_device(H.make_inputs("bst", {"T": 20}, 8), "cuda")
     with pytest.raises(NotImplementedError):
-        H.call_model(model, "deepfm", inp)
+        H.call_model(model, "bst", inp)
 
 
 @pytest.mark.gpu
