@@ -169,6 +169,22 @@ def kernel_avg_ms(launch, iters=50):
     return start.elapsed_time(end) / iters
 
 
+def graph_kernel_avg_ms(launch, per_graph=20, iters=10):
+    """Average device time of one launch of a short kernel: `per_graph` back-to-back launches
+    captured in one hipGraph, replayed `iters` times, HIP events on the replay stream (host
+    launch cost excluded; the ~1.5 us dependent-kernel boundary per launch included)."""
+    g, _ = graph_of(lambda: [launch() for _ in range(per_graph)])
+    st = torch.cuda.current_stream()
+    g.replay()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(st)
+    for _ in range(iters):
+        g.replay()
+    end.record(st)
+    end.synchronize()
+    return start.elapsed_time(end) / (iters * per_graph)
+
+
 # ------------------------------------------------------------------ PMC traffic (profiles/traffic.json)
 
 def load_traffic(kernel: str, workload_name: str):
@@ -425,6 +441,32 @@ def bench_train(batch, steps, warmup, name="dcn"):
     return res
 
 
+# ------------------------------------------------------------------ embedding-gather roofline (DeepFM configs[1])
+
+def gather_roofline(model, inp, cfg, batch, big_batch=65536):
+    """rk_fm_gather alone (fm_gather_kernel: 30 second-order rows of 128 B + 30 first-order
+    weights + 30 indices read, the 3,840 B deep-input row + fm1/fm2 written per sample) over
+    configs[1]'s 30 x 1e6-row tables, timed with HIP events around hipGraph replays of back-to-back
+    launches (graph_kernel_avg_ms: host launch cost excluded), at the config's batch
+    and at a larger batch over the same tables (steady-state rate, launch ramp amortised)."""
+    import helpers as H
+    out = {"kernel": "fm_gather_kernel<8>", "bound": "hbm", "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+           "bytes_per_sample": DEEPFM_GATHER_BYTES,
+           "tables": "30 fields x 1,000,000 rows x 32 fp32 (3.84 GB) + 30 x 1e6 x 1 (beyond the 256 MiB MALL)"}
+    for b, cat in ((batch, inp["category"]),
+                   (big_batch, H.to_device(H.make_inputs("deepfm", cfg, big_batch, seed=1234),
+                                           torch.device("cuda", torch.cuda.current_device()))["category"])):
+        ms = graph_kernel_avg_ms(model.gather_launcher(cat))
+        achieved = DEEPFM_GATHER_BYTES * b / (ms * 1e-3)
+        tr = load_traffic("fm_gather_kernel", "deepfm" if b == batch else f"deepfm@{b}")
+        out[f"batch_{b}"] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
+                             "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
+        if tr:  # PMC-measured HBM bytes at the same launch time
+            out[f"batch_{b}"]["hbm_gb_per_s"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
+            out[f"batch_{b}"]["hbm_frac"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / PEAK_HBM, 4)
+    return out
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank):
@@ -489,6 +531,8 @@ def main():
             r, m2, inp2, cfg2, mn2 = bench_one(name, batch, args.steps, args.warmup, 1, 0)
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
+            if name == "deepfm":
+                r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob
                 r["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * r["samples_per_s"] / 1e9, 1)
                 r["bytes_per_sample"] = FWFM_BYTES_PER_SAMPLE

@@ -63,6 +63,34 @@ class DeepFM(EngineModule):
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
 
+    def _gather_plan(self, names, category):
+        D = self.embedding_dim
+        first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
+        B, dev = first.shape[0], first.device
+        second_segs, first_segs = [], []
+        for f, name in enumerate(names):
+            idx = ops.as_index(category[name], f"category[{name!r}]")
+            second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
+            first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
+        deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        return (second_segs, first_segs, D, B, deep_in, fm1, fm2)
+
+    def _gather_fm(self, names, category):
+        """rk_fm_gather: both embedding orders, fm1, fm2 and the deep input row in one pass
+        (deepfm.py:122-140,142)."""
+        plan = self._gather_plan(names, category)
+        ops.fm_gather(*plan)
+        return plan[4], plan[5], plan[6]
+
+    def gather_launcher(self, category):
+        """Zero-argument re-launch of this forward's rk_fm_gather kernel, for kernel-level timing
+        (bench.py gather roofline)."""
+        names = [c for c in self.second_order_embeddings if c in category]
+        plan = self._gather_plan(names, category)
+        return lambda: ops.fm_gather(*plan)
+
     def forward(self, category):
         if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
             check_eval(self)  # a train-mode forward without autograd is not implemented
@@ -73,19 +101,8 @@ class DeepFM(EngineModule):
         if self.training:  # BatchNorm batch statistics, Dropout, HIP backward (rankops.train)
             idx = [ops.as_index(category[n], f"category[{n!r}]") for n in names]
             return train.deepfm_train_forward(self, names, idx)
-        D = self.embedding_dim
-        first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
-        B = first.shape[0]
-        dev = first.device
-        second_segs, first_segs = [], []
-        for f, name in enumerate(names):
-            idx = ops.as_index(category[name], f"category[{name!r}]")
-            second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
-            first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
-        deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32)
-        fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        ops.fm_gather(second_segs, first_segs, D, B, deep_in, fm1, fm2)
+        deep_in, fm1, fm2 = self._gather_fm(names, category)
+        B, dev = deep_in.shape[0], deep_in.device
         deep = torch.empty(B, 1, device=dev, dtype=torch.float32)
         total = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)

@@ -178,6 +178,8 @@ int rk_dcn_cross(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t wi
                  int64_t ld_xl_in, float* xl_out, int64_t ld_xl_out, float* cross_partial,
                  void* stream);
 
+/* Segments are either all embedding tables (idx != NULL) or all dense (row b of src); dim/4 a
+ * power of two, dim <= 256, at most 32 fields. */
 int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_order,
                  int32_t num_fields, int32_t dim, int64_t batch, float* deep_in,
                  int64_t ld_deep, float* fm1, float* fm2, void* stream);
