@@ -386,16 +386,18 @@ def bench_metrics(batch, batches=256):
 
 
 def bench_train(batch, steps, warmup, name="dcn"):
-    """DCN training step (§8(f) #2) at `batch`, wechat tables: zero_grad, forward, BCEWithLogits
-    loss, loss.backward() (HIP backward kernels), Adam step — the reference's train() loop body
-    (dcn.py:195-201) with the per-call cross draws frozen; inputs in HBM.  Timed eagerly
+    """Training step (§8(f) #2) at `batch`, wechat tables: zero_grad, forward, the script's loss
+    (DCN BCEWithLogits on the logit, DeepFM BCE on the probability, DIN BCE + l2_reg), loss.backward()
+    (HIP backward kernels), Adam step — the reference's train() loop body (dcn.py:195-201,
+    deepfm.py:166-171, din.py:339-347) with the per-call H2 draws frozen; inputs in HBM.  Timed eagerly
     (rankops.Adam) and as one captured hipGraph per step (rankops.Adam(capturable=True))."""
     import helpers as H
     import rankops
-    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"} if name == "dcn" else \
-        {"vocab": H.WECHAT_VOCAB}
+    cfg = {"dcn": {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"},
+           "deepfm": {"vocab": H.WECHAT_VOCAB},
+           "din": {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32, "interaction_weights": "frozen"}}[name]
     inp = None
-    res = {"model": {"dcn": "DCN", "deepfm": "DeepFM"}[name], "batch": batch}
+    res = {"model": {"dcn": "DCN", "deepfm": "DeepFM", "din": "DIN"}[name], "batch": batch}
     crit = torch.nn.BCEWithLogitsLoss() if name == "dcn" else torch.nn.BCELoss()
     for mode in ("eager", "graph"):
         torch.manual_seed(0)
@@ -409,6 +411,8 @@ def bench_train(batch, steps, warmup, name="dcn"):
             opt.zero_grad(set_to_none=True)
             out = H.call_model(model, name, inp)
             loss = crit(out[1].squeeze(), label) if name == "dcn" else crit(out[0].squeeze(), label)
+            if name == "din":  # ce_loss + l2_reg (din.py:343-344)
+                loss = loss + out[2]
             loss.backward()
             opt.step()
 
@@ -551,7 +555,8 @@ def main():
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_extras:
         try:
-            result["train"] = {m: bench_train(args.batch, max(10, args.steps // 2), 3, m) for m in ("dcn", "deepfm")}
+            result["train"] = {m: bench_train(args.batch, max(10, args.steps // 2), 3, m)
+                               for m in ("dcn", "deepfm", "din")}
         except Exception as exc:  # reported, never fatal for the headline line
             result["train"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_loader:

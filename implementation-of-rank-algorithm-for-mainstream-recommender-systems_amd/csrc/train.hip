@@ -318,42 +318,62 @@ struct GradSegs {
 };
 
 // Small tables (rows * dim <= kEmbLdsFloats: device, tags, ...) take every sample, so global
-// atomics on them serialise: those are accumulated per workgroup in LDS first and flushed once.
+// atomics on them serialise: those are accumulated per workgroup in LDS first and flushed once
+// (PRIV).  Large tables add straight into the gradient with global atomics; each thread issues
+// kEmbUnroll index and dx loads before its first atomic, so the memory round trips overlap.
+// Zero contributions are skipped (see below).
 constexpr int kEmbLdsFloats = 8192;
+constexpr int kEmbUnroll = 8;
 
+template <bool PRIV>
 __global__ __launch_bounds__(256) void embedding_backward_kernel(GradSegs segs, int64_t batch,
                                                                  const float* __restrict__ dx, int64_t ld_dx,
                                                                  uint32_t* flags) {
-  __shared__ float acc[kEmbLdsFloats];
+  __shared__ float acc[PRIV ? kEmbLdsFloats : 1];
   const rk_segment& s = segs.s[blockIdx.y];
   if (!s.idx) return;
   const int dim = s.dim;
   const int64_t n = batch * dim;
   float* grad = const_cast<float*>(s.src);
-  const bool priv = s.rows * dim <= kEmbLdsFloats;
-  if (priv) {
+  if (PRIV != (s.rows * dim <= kEmbLdsFloats)) return;  // the other instantiation owns this segment
+  if (PRIV) {
     for (int i = threadIdx.x; i < s.rows * dim; i += blockDim.x) acc[i] = 0.f;
     __syncthreads();
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = i / dim;
-    const int j = (int)(i - b * dim);
-    const int64_t r = s.idx[b * s.idx_stride];
-    if (r < 0 || r >= s.rows) {
-      if (j == 0) flag_oob(flags);
-      continue;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n; i0 += stride * kEmbUnroll) {
+    int64_t r[kEmbUnroll];
+    float v[kEmbUnroll];
+    int j[kEmbUnroll];
+#pragma unroll
+    for (int u = 0; u < kEmbUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      const int64_t b = i < n ? i / dim : 0;
+      j[u] = (int)(i - b * dim);
+      r[u] = i < n ? s.idx[b * s.idx_stride] : -1;
+      v[u] = i < n ? dx[b * ld_dx + s.out_col + j[u]] : 0.f;
     }
-    const float v = dx[b * ld_dx + s.out_col + j];
-    if (priv)
-      atomicAdd(acc + r * dim + j, v);
-    else
-      atomicAdd(grad + r * s.src_ld + j, v);
+#pragma unroll
+    for (int u = 0; u < kEmbUnroll; ++u) {
+      if (i0 + u * stride >= n) continue;
+      if (r[u] < 0 || r[u] >= s.rows) {
+        if (j[u] == 0) flag_oob(flags);
+        continue;
+      }
+      // adding 0 changes nothing: padded history positions (index 0, zero gradient) would
+      // otherwise all hit row 0 and serialise on its atomics
+      if (v[u] == 0.f) continue;
+      if (PRIV)
+        atomicAdd(acc + r[u] * dim + j[u], v[u]);
+      else
+        atomicAdd(grad + r[u] * s.src_ld + j[u], v[u]);
+    }
   }
-  if (priv) {
+  if (PRIV) {
     __syncthreads();
     for (int i = threadIdx.x; i < s.rows * dim; i += blockDim.x) {
-      const float v = acc[i];
-      if (v != 0.f) atomicAdd(grad + (i / dim) * s.src_ld + i % dim, v);
+      const float x = acc[i];
+      if (x != 0.f) atomicAdd(grad + (i / dim) * s.src_ld + i % dim, x);
     }
   }
 }
@@ -519,9 +539,18 @@ RK_API int rk_embedding_backward(const rk_segment* grads, int32_t nseg, int64_t 
   }
   if (batch == 0 || widest == 0) return RK_OK;
   const int64_t per = batch * widest;
-  const unsigned bx = (unsigned)std::min<int64_t>((per + 255) / 256, 2 * num_cus());
-  embedding_backward_kernel<<<dim3(bx, (unsigned)nseg), 256, 0, (hipStream_t)stream>>>(t, batch, dx, ld_dx,
-                                                                                       device_flags());
+  bool any_priv = false, any_global = false;
+  for (int i = 0; i < nseg; ++i)
+    if (t.s[i].idx) (t.s[i].rows * t.s[i].dim <= kEmbLdsFloats ? any_priv : any_global) = true;
+  hipStream_t st = (hipStream_t)stream;
+  if (any_priv) {  // a few workgroups per small table: each flushes its whole LDS image once
+    const unsigned bx = (unsigned)std::min<int64_t>((per + 255) / 256, 2 * num_cus());
+    embedding_backward_kernel<true><<<dim3(bx, (unsigned)nseg), 256, 0, st>>>(t, batch, dx, ld_dx, device_flags());
+  }
+  if (any_global) {
+    const unsigned bx = (unsigned)std::min<int64_t>((per + 256 * kEmbUnroll - 1) / (256 * kEmbUnroll), 8 * num_cus());
+    embedding_backward_kernel<false><<<dim3(bx, (unsigned)nseg), 256, 0, st>>>(t, batch, dx, ld_dx, device_flags());
+  }
   return check_launch("rk_embedding_backward");
 }
 

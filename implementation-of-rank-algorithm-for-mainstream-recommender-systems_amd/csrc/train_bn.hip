@@ -270,6 +270,103 @@ static uint32_t dropout_threshold(double p) {
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
+
+// ---- DIN's Dice activation in train mode (din.py:26-36): x = z + bias, xhat = BatchNorm1d(affine
+// = False) of x with the batch statistics, p = sigmoid(xhat), y = alpha * (1 - p) * x + p * x.
+// The Dice BatchNorm's running statistics are updated like bn_apply_kernel's.
+__global__ __launch_bounds__(256) void dice_apply_kernel(const float* __restrict__ z, int64_t ldz, int64_t B, int N,
+                                                         const float* __restrict__ bias, const double* __restrict__ sum,
+                                                         const double* __restrict__ sq,
+                                                         const float* __restrict__ alpha, float eps, float momentum,
+                                                         float* __restrict__ running_mean,
+                                                         float* __restrict__ running_var, float* __restrict__ save_mean,
+                                                         float* __restrict__ save_invstd, float* __restrict__ y,
+                                                         int64_t ldy) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * kBnCols + lane;
+  if (n >= N) return;
+  const int64_t b0 = (int64_t)blockIdx.y * kBnRows;
+  const int64_t b1 = min<int64_t>(B, b0 + kBnRows);
+  const float bb = bias ? bias[n] : 0.f;
+  const BnCol c = bn_col(sum, sq, n, B, eps);
+  const float a = alpha[n];
+  if (blockIdx.y == 0 && w == 0) {
+    save_mean[n] = c.mean;
+    save_invstd[n] = c.invstd;
+    if (running_mean) {
+      const double var_b = sq[n] / (double)B - (sum[n] / (double)B) * (sum[n] / (double)B);
+      const float unbiased = (float)(B > 1 ? var_b * (double)B / (double)(B - 1) : var_b);
+      running_mean[n] = momentum * c.mean + (1.f - momentum) * running_mean[n];
+      running_var[n] = momentum * unbiased + (1.f - momentum) * running_var[n];
+    }
+  }
+  for (int64_t b = b0 + w; b < b1; b += 4) {
+    const float x = z[b * ldz + n] + bb;
+    const float p = 1.0f / (1.0f + expf(-((x - c.mean) * c.invstd)));
+    y[b * ldy + n] = a * (1.0f - p) * x + p * x;
+  }
+}
+
+// Dice backward.  With g = dy: dx = g * (alpha (1 - p) + p)  [direct]
+//   + invstd * (dxhat - mean_b dxhat - xhat * mean_b(dxhat * xhat))  [through the batch statistics],
+// dxhat = g * x * (1 - alpha) * p * (1 - p);  dalpha = sum_b g * x * (1 - p).
+// STATS pass: ws[0..N) += dxhat, ws[N..2N) += dxhat * xhat, ws[2N..3N) += g * x * (1 - p).
+template <bool STATS>
+__global__ __launch_bounds__(256) void dice_backward_kernel(const float* __restrict__ dy, int64_t lddy,
+                                                            const float* __restrict__ z, int64_t ldz, int64_t B, int N,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ alpha,
+                                                            const float* __restrict__ save_mean,
+                                                            const float* __restrict__ save_invstd,
+                                                            double* __restrict__ ws, float* __restrict__ dz,
+                                                            int64_t lddz) {
+  __shared__ double red[3][4][kBnCols];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * kBnCols + lane;
+  const int64_t b0 = (int64_t)blockIdx.y * kBnRows;
+  const int64_t b1 = min<int64_t>(B, b0 + kBnRows);
+  double s1 = 0.0, s2 = 0.0, sa = 0.0;
+  if (n < N) {
+    const float bb = bias ? bias[n] : 0.f;
+    const float mean = save_mean[n], invstd = save_invstd[n], a = alpha[n];
+    float k1 = 0.f, k2 = 0.f;
+    if (!STATS) {
+      k1 = (float)(ws[n] / (double)B);
+      k2 = (float)(ws[N + n] / (double)B);
+    }
+    for (int64_t b = b0 + w; b < b1; b += 4) {
+      const float x = z[b * ldz + n] + bb;
+      const float xhat = (x - mean) * invstd;
+      const float p = 1.0f / (1.0f + expf(-xhat));
+      const float g = dy[b * lddy + n];
+      const float dxhat = g * x * (1.0f - a) * p * (1.0f - p);
+      if (STATS) {
+        s1 += (double)dxhat;
+        s2 += (double)dxhat * (double)xhat;
+        sa += (double)(g * x * (1.0f - p));
+      } else {
+        dz[b * lddz + n] = g * (a * (1.0f - p) + p) + invstd * (dxhat - k1 - xhat * k2);
+      }
+    }
+  }
+  if (STATS) {
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    red[2][w][lane] = sa;
+    __syncthreads();
+    if (w == 0 && n < N) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        atomicAdd(ws + (int64_t)k * N + n, red[k][0][lane] + red[k][1][lane] + red[k][2][lane] + red[k][3][lane]);
+    }
+  }
+}
+
+__global__ void f64_to_f32_kernel(const double* __restrict__ src, int n, float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -367,4 +464,36 @@ RK_API int rk_fm_combine_backward(const float* dprob, const float* dtotal, const
         dprob, dtotal, dfm1_in, dfm2_in, ddeep_in, prob, fm1, fm2, deep, final_w, batch, dfm1, dfm2, ddeep, dfinal_w,
         dfinal_b);
   return check_launch("rk_fm_combine_backward");
+}
+
+RK_API int rk_dice_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
+                                 const float* alpha, float eps, float momentum, float* running_mean,
+                                 float* running_var, double* workspace, float* save_mean, float* save_invstd,
+                                 float* y, int64_t ldy, void* stream) {
+  if (!z || !y || !alpha || !workspace || !save_mean || !save_invstd || batch <= 0 || n <= 0 || ldz < n ||
+      ldy < n || (running_mean != nullptr) != (running_var != nullptr))
+    return fail(RK_ERR_INVALID, "rk_dice_train_forward: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((n + kBnCols - 1) / kBnCols), (unsigned)((batch + kBnRows - 1) / kBnRows));
+  zero_f64_kernel<<<(2 * n + 255) / 256, 256, 0, st>>>(workspace, 2 * n);
+  bn_stats_kernel<<<grid, 256, 0, st>>>(z, ldz, batch, n, bias, workspace, workspace + n);
+  dice_apply_kernel<<<grid, 256, 0, st>>>(z, ldz, batch, n, bias, workspace, workspace + n, alpha, eps, momentum,
+                                          running_mean, running_var, save_mean, save_invstd, y, ldy);
+  return check_launch("rk_dice_train_forward");
+}
+
+RK_API int rk_dice_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch, int32_t n,
+                            const float* bias, const float* alpha, const float* save_mean, const float* save_invstd,
+                            double* workspace, float* dz, int64_t lddz, float* dalpha, void* stream) {
+  if (!dy || !z || !dz || !alpha || !save_mean || !save_invstd || !workspace || batch <= 0 || n <= 0)
+    return fail(RK_ERR_INVALID, "rk_dice_backward: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((n + kBnCols - 1) / kBnCols), (unsigned)((batch + kBnRows - 1) / kBnRows));
+  zero_f64_kernel<<<(3 * n + 255) / 256, 256, 0, st>>>(workspace, 3 * n);
+  dice_backward_kernel<true><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, alpha, save_mean, save_invstd,
+                                                   workspace, nullptr, 0);
+  if (dalpha) f64_to_f32_kernel<<<(n + 255) / 256, 256, 0, st>>>(workspace + 2 * n, n, dalpha);
+  dice_backward_kernel<false><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, alpha, save_mean, save_invstd,
+                                                    workspace, dz, lddz);
+  return check_launch("rk_dice_backward");
 }

@@ -178,6 +178,23 @@ SIGNATURES = {
     "rk_fm_combine_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p, c_void_p]),
+    "rk_dice_train_forward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_float,
+                                             c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_int64, c_void_p]),
+    "rk_dice_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rk_din_att_cross": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64,
+                                        c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rk_din_att_pool_forward": (ctypes.c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                               c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int64, c_int32,
+                                               c_void_p]),
+    "rk_din_att_pool_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                                c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
+                                                c_void_p, c_void_p]),
+    "rk_din_cross_fold": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
+                                         c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_row_l2norm_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_void_p,
+                                              c_void_p, c_int64, c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

@@ -20,7 +20,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import common, ops
+from . import common, ops, train
 from .common import PACKED, fused_mlp_fits
 from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
     table_rows
@@ -112,6 +112,7 @@ class DIN(EngineModule):
         self.output_layer = nn.Linear(width, 1)
         self.att_weights = InteractionWeights(
             interaction_weights, lambda: draw_din_attention(self.embeddings[SEQ_KEY].embedding_dim))
+        self._dropout = train.DropoutStreams()
 
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
@@ -124,15 +125,18 @@ class DIN(EngineModule):
         segs = [ops.dense_segment(v, 1, i) for i, v in enumerate(dense_cols)]
         col = len(dense_cols)
         cat_col0 = col
+        lookups = []  # (table weight, index, column) for the training backward
         for name, emb in self.embeddings.items():
             if name in category:
                 idx = ops.as_index(category[name], f"category[{name!r}]")
                 segs.append(ops.table_segment(emb.weight, idx, col))
+                lookups.append((emb.weight, idx, col))
                 col += emb.embedding_dim
         tgt_emb = self.embeddings["feedid"]
         H = tgt_emb.embedding_dim
         tgt_idx = ops.as_index(target["feedid"], "target['feedid']")
         segs.append(ops.table_segment(tgt_emb.weight, tgt_idx, col))
+        lookups.append((tgt_emb.weight, tgt_idx, col))
         q_col = col
         att_col = q_col + H
         width = att_col + self.embeddings[SEQ_KEY].embedding_dim
@@ -142,7 +146,8 @@ class DIN(EngineModule):
                  and self.embeddings[SEQ_KEY].embedding_dim == H
                  and fused_mlp_fits(width, [l.linear.out_features for l in self._tail]))
         return dict(B=B, dev=dev, segs=segs, cat_col0=cat_col0, q_col=q_col, att_col=att_col, width=width, H=H,
-                    seq=seq, seq_len=seq_len, fused=fused, keep=(dense_cols, category, target))
+                    seq=seq, seq_len=seq_len, fused=fused, keep=(dense_cols, category, target), lookups=lookups,
+                    seq_key=SEQ_KEY, want_l2=self.mini_batch_aware_regularization and self.l2_lambda > 0)
 
     def _launch_fused(self, pl, w, logit, prob, l2_reg):
         layers = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs())
@@ -166,8 +171,14 @@ class DIN(EngineModule):
         return lambda: self._launch_fused(pl, w, logit, prob, None)
 
     def forward(self, dense, category, sequence, target):
-        check_eval(self)
+        if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            check_eval(self)  # a train-mode forward without autograd is not implemented
         pl = self._plan(dense, category, sequence, target)
+        if self.training:  # Dice/BatchNorm batch statistics, Dropout, HIP backward (rankops.train)
+            if self.embeddings[SEQ_KEY].embedding_dim != pl["H"]:
+                raise NotImplementedError("rankops DIN training: target and history embeddings must share a width")
+            prob, logit, l2 = train.din_train_forward(self, pl, self.att_weights.get(pl["dev"]))
+            return prob, logit, (l2 if pl["want_l2"] else 0.0)
         B, dev, segs, H = pl["B"], pl["dev"], pl["segs"], pl["H"]
         cat_col0, q_col, att_col, width = pl["cat_col0"], pl["q_col"], pl["att_col"], pl["width"]
         seq, seq_len = pl["seq"], pl["seq_len"]

@@ -391,6 +391,60 @@ def bn_act_backward(dy, z, bias, bn, relu, p, seed, slot, save_mean, save_invstd
         ptr(dbeta), _lib.stream_of(dy)), "rk_bn_act_backward")
 
 
+def dice_train_forward(z, bias, dice, y, save_mean, save_invstd, workspace):
+    """Dice (din.py:26-36) with batch statistics on z + bias; `dice` is the Dice module (its .bn
+    running statistics and num_batches_tracked are updated as torch's train-mode BatchNorm does)."""
+    lib = _lib.load()
+    bn = dice.bn
+    track = bn.track_running_stats and bn.running_mean is not None
+    check(lib.rk_dice_train_forward(ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), ptr(dice.alpha),
+                                    float(bn.eps), float(bn.momentum), ptr(bn.running_mean) if track else None,
+                                    ptr(bn.running_var) if track else None, ptr(workspace), ptr(save_mean),
+                                    ptr(save_invstd), ptr(y), y.stride(0), _lib.stream_of(z)), "rk_dice_train_forward")
+    if track and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+
+
+def dice_backward(dy, z, bias, dice, save_mean, save_invstd, workspace, dz, dalpha):
+    lib = _lib.load()
+    check(lib.rk_dice_backward(ptr(dy), dy.stride(0), ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias),
+                               ptr(dice.alpha), ptr(save_mean), ptr(save_invstd), ptr(workspace), ptr(dz),
+                               dz.stride(0), ptr(dalpha), _lib.stream_of(dy)), "rk_dice_backward")
+
+
+def din_att_cross(x, q_col, key_table, seq, T, H, keys, cross):
+    lib = _lib.load()
+    check(lib.rk_din_att_cross(ptr(x), x.stride(0), q_col, ptr(key_table), key_table.shape[0], key_table.stride(0),
+                               ptr(seq), seq.stride(0), x.shape[0], T, H, ptr(keys), ptr(cross),
+                               _lib.stream_of(x)), "rk_din_att_cross")
+
+
+def din_att_pool_forward(a2, w3, b3, keys, seq_len, T, H, softmax, weights, x, att_col):
+    lib = _lib.load()
+    check(lib.rk_din_att_pool_forward(ptr(a2), a2.shape[1], ptr(w3), ptr(b3), ptr(keys), ptr(seq_len), x.shape[0],
+                                      T, H, int(bool(softmax)), ptr(weights), ptr(x), x.stride(0), att_col,
+                                      _lib.stream_of(x)), "rk_din_att_pool_forward")
+
+
+def din_att_pool_backward(dx, att_col, weights, keys, a2, w3, seq_len, T, H, softmax, dkeys, da2):
+    lib = _lib.load()
+    check(lib.rk_din_att_pool_backward(ptr(dx), dx.stride(0), att_col, ptr(weights), ptr(keys), ptr(a2),
+                                       a2.shape[1], ptr(w3), ptr(seq_len), dx.shape[0], T, H, int(bool(softmax)),
+                                       ptr(dkeys), ptr(da2), _lib.stream_of(dx)), "rk_din_att_pool_backward")
+
+
+def din_cross_fold(dcross, x, q_col, keys, T, H, dkeys, dx):
+    lib = _lib.load()
+    check(lib.rk_din_cross_fold(ptr(dcross), ptr(x), x.stride(0), q_col, ptr(keys), x.shape[0], T, H, ptr(dkeys),
+                                ptr(dx), dx.stride(0), _lib.stream_of(dx)), "rk_din_cross_fold")
+
+
+def row_l2norm_backward(x, col0, ncols, scale, grad_out, dx):
+    lib = _lib.load()
+    check(lib.rk_row_l2norm_backward(ptr(x), x.stride(0), x.shape[0], col0, ncols, float(scale), ptr(grad_out),
+                                     ptr(dx), dx.stride(0), _lib.stream_of(dx)), "rk_row_l2norm_backward")
+
+
 def fm_backward(deep_in, d_deep, dfm2, num_fields, dim, out):
     lib = _lib.load()
     check(lib.rk_fm_backward(ptr(deep_in), deep_in.stride(0), ptr(d_deep), d_deep.stride(0) if d_deep is not None else 0,

@@ -423,6 +423,190 @@ def deepfm_train_forward(model, names, idx):
     return _DeepFMTrain.apply(model, names, idx, *params)
 
 
+# ---------------------------------------------------------------- DIN
+
+def din_units(model):
+    """(Linear, Dice module, BatchNorm1d or None, dropout p) per fcn unit (din.py:272-284)."""
+    units = []
+    for m in model.fcn:
+        if isinstance(m, torch.nn.Linear):
+            units.append([m, None, None, 0.0])
+        elif isinstance(m, torch.nn.BatchNorm1d):
+            units[-1][2] = m
+        elif isinstance(m, torch.nn.Dropout):
+            units[-1][3] = float(m.p) if m.training else 0.0
+        elif isinstance(m, torch.nn.PReLU):
+            raise NotImplementedError("rankops DIN training: activation='prelu' is not implemented (use 'dice')")
+        else:  # Dice
+            units[-1][1] = m
+    for lin, act, bn, _ in units:
+        if lin.bias is None or act is None:
+            raise NotImplementedError("rankops DIN training expects the reference's Linear + Dice units")
+        if act.bn.momentum is None or (bn is not None and bn.momentum is None):
+            raise NotImplementedError("rankops DIN training: BatchNorm1d needs a numeric momentum")
+    return units
+
+
+class _DINTrain(torch.autograd.Function):
+    """DIN forward + backward in train mode (din.py:294-323): gather, din_attention (att_net's
+    layers as GEMMs on rk_linear with the activations kept for the backward, the weights drawn per
+    call like the reference and not trained), fcn units Linear -> Dice -> BatchNorm1d -> Dropout
+    with batch statistics, output_layer + sigmoid, and the mini-batch-aware l2 term.
+    Inputs after the fixed arguments are the parameters in `_din_params` order."""
+
+    @staticmethod
+    def forward(ctx, model, pl, att, emb_plan, *params):
+        B, dev, H = pl["B"], pl["dev"], pl["H"]
+        q_col, att_col, width, cat_col0 = pl["q_col"], pl["att_col"], pl["width"], pl["cat_col0"]
+        seq, seq_len = pl["seq"], pl["seq_len"]
+        T = seq.shape[1]
+        f32 = dict(device=dev, dtype=torch.float32)
+        x = torch.empty(B, width, **f32)
+        ops.concat_gather(pl["segs"], B, x)  # [dense | category | target]; the attention columns below
+        w1, b1, w2, b2, w3, b3 = att
+        keys = torch.empty(B, T, H, **f32)
+        cross = torch.empty(B * T, 4 * H, **f32)
+        ops.din_att_cross(x, q_col, model.embeddings[pl["seq_key"]].weight, seq, T, H, keys, cross)
+        a1 = torch.empty(B * T, w1.shape[0], **f32)
+        ops.linear(cross, w1, a1, epilogue=ops.make_epilogue(bias=b1, act="relu"))
+        a2 = torch.empty(B * T, w2.shape[0], **f32)
+        ops.linear(a1, w2, a2, epilogue=ops.make_epilogue(bias=b2, act="relu"))
+        del cross
+        wts = torch.empty(B, T, **f32)
+        ops.din_att_pool_forward(a2, w3.reshape(-1), b3, keys, seq_len, T, H, model.use_softmax, wts, x, att_col)
+        units = din_units(model)
+        seed, slot = model._dropout.next(dev)
+        saved = []
+        h = x
+        for u, (lin, dice, bn, p) in enumerate(units):
+            n, K = lin.out_features, lin.in_features
+            z = torch.empty(B, n, **f32)
+            ops.gemm(False, False, B, n, K, h, h.stride(0), lin.weight, lin.weight.stride(0), z)
+            y1 = torch.empty(B, n, **f32)
+            m1, s1 = torch.empty(n, **f32), torch.empty(n, **f32)
+            ops.dice_train_forward(z, lin.bias, dice, y1, m1, s1, torch.empty(2 * n, device=dev, dtype=torch.float64))
+            y2, m2, s2 = y1, m1, s1
+            if bn is not None or p > 0:
+                y2 = torch.empty(B, n, **f32)
+                m2, s2 = torch.empty(n, **f32), torch.empty(n, **f32)
+                ops.bn_act_train_forward(y1, None, bn, False, p, seed + u, slot, y2, m2, s2,
+                                         torch.empty(2 * n, device=dev, dtype=torch.float64))
+                if bn is not None and bn.track_running_stats and bn.num_batches_tracked is not None:
+                    bn.num_batches_tracked.add_(1)
+            saved.append((z, y1, m1, s1, y2, m2, s2))
+            h = y2
+        logit = torch.empty(B, 1, **f32)
+        prob = torch.empty(B, 1, **f32)
+        ops.mlp_forward(h, [], ops.make_epilogue(head_w=model.output_layer.weight, head_b=model.output_layer.bias,
+                                                 head_logit=logit, head_prob=prob))
+        l2 = torch.zeros((), **f32)
+        if pl["want_l2"]:
+            ops.row_l2norm_mean(x, cat_col0, width - cat_col0, float(model.l2_lambda), l2)
+        ctx.model, ctx.pl, ctx.units, ctx.seed, ctx.emb_plan = model, pl, units, seed, emb_plan
+        ctx.save_for_backward(x, keys, a1, a2, wts, prob, slot, w1, w2, w3, *[t for s in saved for t in s])
+        return prob, logit, l2
+
+    @staticmethod
+    def backward(ctx, dprob, dlogit, dl2):
+        model, pl, units = ctx.model, ctx.pl, ctx.units
+        x, keys, a1, a2, wts, prob, slot, w1, w2, w3, *flat = ctx.saved_tensors
+        saved = [tuple(flat[7 * u:7 * u + 7]) for u in range(len(units))]
+        B, dev, H = pl["B"], pl["dev"], pl["H"]
+        T = keys.shape[1]
+        f32 = dict(device=dev, dtype=torch.float32)
+        last = saved[-1][4] if saved else x
+        dy = torch.empty_like(last)
+        w_out = model.output_layer.weight
+        dw_out = torch.empty_like(w_out)
+        db_out = torch.empty(1, **f32)
+        ops.logit_head_backward(_grad_out(dlogit, prob), _grad_out(dprob, prob), prob, last, None, w_out, dy, None,
+                                dw_out, db_out)
+        unit_grads = [None] * len(units)
+        for u in range(len(units) - 1, -1, -1):
+            lin, dice, bn, p = units[u]
+            z, y1, m1, s1, y2, m2, s2 = saved[u]
+            n, K = lin.out_features, lin.in_features
+            h_in = saved[u - 1][4] if u > 0 else x
+            dy1 = dy
+            dg = dbt = None
+            if bn is not None or p > 0:
+                dy1 = torch.empty(B, n, **f32)
+                if bn is not None:
+                    dg = torch.empty(n, **f32) if bn.weight is not None else None
+                    dbt = torch.empty(n, **f32) if bn.bias is not None else None
+                ops.bn_act_backward(dy, y1, None, bn, False, p, ctx.seed + u, slot, m2, s2,
+                                    torch.empty(2 * n, device=dev, dtype=torch.float64), dy1, dg, dbt)
+            dz = torch.empty(B, n, **f32)
+            dalpha = torch.empty(n, **f32)
+            ops.dice_backward(dy1, z, lin.bias, dice, m1, s1, torch.empty(3 * n, device=dev, dtype=torch.float64), dz,
+                              dalpha)
+            dW = torch.empty(n, K, **f32)
+            db = torch.empty(n, **f32)
+            ops.gemm(True, True, n, K, B, dz, dz.stride(0), h_in, h_in.stride(0), dW, row_sums=db)
+            dx = torch.empty(B, K, **f32)
+            ops.gemm(False, True, B, K, n, dz, dz.stride(0), lin.weight, lin.weight.stride(0), dx)
+            unit_grads[u] = [dW, db, dalpha] + ([t for t in (dg, dbt) if t is not None] if bn is not None else [])
+            dy = dx
+        dxr = dy  # dL/d[dense | category | target | attention]
+        if pl["want_l2"] and dl2 is not None:
+            ops.row_l2norm_backward(x, pl["cat_col0"], pl["width"] - pl["cat_col0"], float(model.l2_lambda) / B,
+                                    dl2.to(torch.float32).reshape(1).contiguous(), dxr)
+        # din_attention backward: weighted sum and scores, then att_net (its weights are not trained)
+        M = B * T
+        dkeys = torch.empty(B, T, H, **f32)
+        da2 = torch.empty(M, a2.shape[1], **f32)
+        ops.din_att_pool_backward(dxr, pl["att_col"], wts, keys, a2, w3.reshape(-1), pl["seq_len"], T, H,
+                                  model.use_softmax, dkeys, da2)
+        da1 = torch.empty(M, a1.shape[1], **f32)
+        ops.gemm(False, True, M, a1.shape[1], a2.shape[1], da2, da2.stride(0), w2, w2.stride(0), da1)
+        dcross = torch.empty(M, 4 * H, **f32)
+        ops.gemm(False, True, M, 4 * H, a1.shape[1], da1, da1.stride(0), w1, w1.stride(0), dcross, A_mask=a1)
+        ops.din_cross_fold(dcross, x, pl["q_col"], keys, T, H, dkeys, dxr)
+        del dcross
+        # nn.Embedding gradients: one zeroed buffer per distinct table, every lookup scattered into it
+        weights, looks = ctx.emb_plan
+        total = sum(w.numel() for w in weights)
+        flat_g = torch.zeros(total, **f32)
+        grads, off = [], 0
+        for w in weights:
+            grads.append(flat_g[off:off + w.numel()].view(w.shape))
+            off += w.numel()
+        segs = [ops.table_segment(grads[k], i, col) for k, i, col in looks]
+        ops.embedding_backward(segs, B, dxr)
+        ops.embedding_backward([ops.table_segment(grads[pl["seq_slot"]], pl["seq"].reshape(-1), 0)], M,
+                               dkeys.view(M, H))
+        flat = [t for g in unit_grads for t in g]
+        return (None, None, None, None, *grads, *flat, dw_out, db_out)
+
+
+def _din_params(model, units):
+    out = []
+    for lin, dice, bn, _ in units:
+        out += [lin.weight, lin.bias, dice.alpha]
+        if bn is not None:
+            out += [t for t in (bn.weight, bn.bias) if t is not None]
+    return out + [model.output_layer.weight, model.output_layer.bias]
+
+
+def din_train_forward(model, pl, att):
+    """DIN train-mode forward with autograd (rankops.DIN.forward in model.train())."""
+    units = din_units(model)
+    # distinct embedding tables in first-use order and the (table slot, index, column) lookups
+    weights, looks = [], []
+
+    def slot_of(w):
+        for k, t in enumerate(weights):
+            if t is w:
+                return k
+        weights.append(w)
+        return len(weights) - 1
+
+    for w, idx, col in pl["lookups"]:
+        looks.append((slot_of(w), idx, col))
+    pl = dict(pl, seq_slot=slot_of(model.embeddings[pl["seq_key"]].weight))
+    return _DINTrain.apply(model, pl, att, (weights, looks), *weights, *_din_params(model, units))
+
+
 # ---------------------------------------------------------------- optimizer
 
 class Adam(torch.optim.Optimizer):

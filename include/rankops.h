@@ -41,6 +41,10 @@
  *                      and its backward                       deepfm.py:100-109
  *   rk_fm_backward, rk_fm_combine_backward  FM and final_layer + sigmoid backward  deepfm.py:122-151
  *   rk_rng_next, rk_dropout_mask  dropout stream counter / explicit mask
+ *   rk_dice_train_forward / rk_dice_backward  Dice with batch statistics and its backward  din.py:26-36
+ *   rk_din_att_cross, rk_din_att_pool_forward, rk_din_att_pool_backward, rk_din_cross_fold
+ *                      din_attention() train forward pieces and backward   din.py:42-84
+ *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -357,6 +361,45 @@ int rk_fm_combine_backward(const float* dprob, const float* dtotal, const float*
                            const float* fm1, const float* fm2, const float* deep,
                            const float* final_w, int64_t batch, float* dfm1, float* dfm2,
                            float* ddeep, float* dfinal_w, float* dfinal_b, void* stream);
+
+/* Dice (din.py:26-36) in train mode: x = z + bias, xhat = BatchNorm1d(affine=False) with the batch
+ * statistics (running stats updated with momentum), y = alpha * (1 - sigmoid(xhat)) * x +
+ * sigmoid(xhat) * x.  workspace: 2n doubles (forward), 3n (backward).  Backward writes dz =
+ * dL/d(z + bias) and dalpha (when non-NULL).                                                  */
+int rk_dice_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
+                          const float* alpha, float eps, float momentum, float* running_mean,
+                          float* running_var, double* workspace, float* save_mean, float* save_invstd,
+                          float* y, int64_t ldy, void* stream);
+int rk_dice_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch,
+                     int32_t n, const float* bias, const float* alpha, const float* save_mean,
+                     const float* save_invstd, double* workspace, float* dz, int64_t lddz,
+                     float* dalpha, void* stream);
+
+/* din_attention train pieces (din.py:42-84).  keys [B, T, H] = key_table[seq] (gathered), cross
+ * [B*T, 4H] = [q, k, q-k, q*k] with q = x[b, q_col:+H]; the att_net layers run on rk_linear.
+ * pool_forward: s = a2 . w3 + b3, masked (softmax: padded with -2^32+1, / sqrt(H)) weights saved
+ * to weights [B, T], out = sum_t w_t k_t written to x[b, att_col:+H].  T <= 1024, H <= 64.
+ * pool_backward: from dout = dx[b, att_col:+H]: dkeys = w_t dout (overwritten) and
+ * da2 = ds_t w3 [a2 > 0].  cross_fold: d(cross) -> dq added to dx[b, q_col:+H], dkeys added.  */
+int rk_din_att_cross(const float* x, int64_t ldx, int32_t q_col, const float* key_table,
+                     int64_t key_rows, int64_t ld_key, const int64_t* seq, int64_t ld_seq,
+                     int64_t batch, int32_t T, int32_t H, float* keys, float* cross, void* stream);
+int rk_din_att_pool_forward(const float* a2, int32_t a2_width, const float* w3, const float* b3,
+                            const float* keys, const int64_t* seq_len, int64_t batch, int32_t T,
+                            int32_t H, int32_t use_softmax, float* weights, float* x, int64_t ldx,
+                            int32_t att_col, void* stream);
+int rk_din_att_pool_backward(const float* dx, int64_t lddx, int32_t att_col, const float* weights,
+                             const float* keys, const float* a2, int32_t a2_width, const float* w3,
+                             const int64_t* seq_len, int64_t batch, int32_t T, int32_t H,
+                             int32_t use_softmax, float* dkeys, float* da2, void* stream);
+int rk_din_cross_fold(const float* dcross, const float* x, int64_t ldx, int32_t q_col,
+                      const float* keys, int64_t batch, int32_t T, int32_t H, float* dkeys, float* dx,
+                      int64_t lddx, void* stream);
+
+/* Backward of out = scale * mean_r ||x[r, col0:+ncols]||_2 (rk_row_l2norm_mean): called with
+ * scale / rows, adds grad_out[0] * scale * x / ||x_r|| to dx[r, col0 + c] (0 for a zero row).   */
+int rk_row_l2norm_backward(const float* x, int64_t ldx, int64_t rows, int32_t col0, int32_t ncols,
+                           float scale, const float* grad_out, float* dx, int64_t lddx, void* stream);
 
 typedef struct rk_adam_tensor {
   float* param;

@@ -237,6 +237,49 @@ def din_forward(p, dense, category, sequence, target, num_hidden=3, activation="
     return probability, logit, l2_reg
 
 
+def dice_train(x, p, prefix, momentum=0.1, eps=1e-5):
+    """Dice.forward in model.train() (din.py:33-36): its BatchNorm1d(affine=False) normalises with the
+    batch statistics and updates the running statistics held in `p`."""
+    pre = prefix + "bn."
+    x_normed = F.batch_norm(x, p[pre + "running_mean"], p[pre + "running_var"], None, None, training=True,
+                            momentum=momentum, eps=eps)
+    p[pre + "num_batches_tracked"] += 1
+    x_p = torch.sigmoid(x_normed)
+    return p[prefix + "alpha"] * (1.0 - x_p) * x + x_p * x
+
+
+def din_forward_train(p, dense, category, sequence, target, num_hidden=3, batch_norm=True, dropout_rate=0.1,
+                      use_softmax=False, l2_lambda=0.2, mini_batch_aware_regularization=True, att=None, masks=None,
+                      momentum=0.1, eps=1e-5):
+    """DIN.forward in model.train() (din.py:294-323, activation='dice'): Dice and BatchNorm1d with batch
+    statistics (running statistics in `p` updated in place), Dropout as the given per-unit multiplier
+    masks (0 or 1/(1-p)); differentiable w.r.t. the tensors in `p`."""
+    dense_input = torch.cat([dense[c].unsqueeze(1) for c in dense], dim=1)
+    category_emb = [F.embedding(category[c], p[f"embeddings.{c}.weight"]) for c in DIN_EMB if c in category]
+    target_feed_emb = F.embedding(target["feedid"], p["embeddings.feedid.weight"])
+    seq_emb = F.embedding(sequence["his_read_comment_7d_seq"], p["embeddings.his_read_comment_7d_seq.weight"])
+    seq_length = sequence["his_read_comment_7d_seq_length"]
+    attention_output = din_attention(target_feed_emb, seq_emb, seq_length, use_softmax, att)
+    net = torch.cat([dense_input] + category_emb + [target_feed_emb, attention_output], dim=1)
+    for u, (lin, act, bn) in enumerate(din_layout(num_hidden, "dice", batch_norm, dropout_rate)):
+        net = _lin(net, p, f"fcn.{lin}.")
+        net = dice_train(net, p, f"fcn.{act}.", momentum, eps)
+        if bn is not None:
+            pre = f"fcn.{bn}."
+            net = F.batch_norm(net, p[pre + "running_mean"], p[pre + "running_var"], p[pre + "weight"],
+                               p[pre + "bias"], training=True, momentum=momentum, eps=eps)
+            p[pre + "num_batches_tracked"] += 1
+        if masks is not None and masks[u] is not None:
+            net = net * masks[u]
+    logit = _lin(net, p, "output_layer.")
+    probability = torch.sigmoid(logit)
+    l2_reg = 0.0
+    if mini_batch_aware_regularization and l2_lambda > 0:
+        embedding_vars = torch.cat([torch.cat(category_emb, dim=1), target_feed_emb, attention_output], dim=1)
+        l2_reg = l2_lambda * torch.norm(embedding_vars, p=2, dim=1).mean()
+    return probability, logit, l2_reg
+
+
 # ---------------------------------------------------------------------------- AFM
 
 def afm_forward(p, dense_input, category_input, category_features):

@@ -452,6 +452,123 @@ def test_deepfm_train_steps_match_autograd(cfg):
     _deepfm_step_check(cfg, 1024, seed=2300, steps=3)
 
 
+def _din_masks(model, B):
+    from rankops import train as rt
+    slot = model._dropout.counter - 1
+    return [ops.dropout_mask(model._dropout.seed + u, slot, B, lin.out_features, p).cpu() if p > 0 else None
+            for u, (lin, act, bn, p) in enumerate(rt.din_units(model))]
+
+
+def _din_step_check(cfg, B, seed, steps):
+    """DIN train steps (din.py:339-347: forward, BCELoss(prob) + l2_reg, backward, Adam) against the
+    oracle's train-mode DIN.forward differentiated by autograd, with the same frozen att_net
+    weights and the dropout masks the engine drew."""
+    cfg = dict(cfg, interaction_weights="frozen")
+    model = H.build("din", cfg).cuda().train()
+    att = [t.cpu() for t in model.att_weights.get(torch.device("cuda", 0))]
+    hidden = len(cfg.get("hidden", [512, 256, 128]))
+    inp = H.make_inputs("din", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    params = dict(model.named_parameters())
+    p = {k: (v.detach().cpu().clone().requires_grad_(True) if k in params else v.detach().cpu().clone())
+         for k, v in model.state_dict().items()}
+    names = list(params)
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in names], lr=1e-3)
+    crit = torch.nn.BCELoss()
+    dinp = H.to_device(inp, "cuda")
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        out = H.call_model(model, "din", dinp)
+        loss = crit(out[0].squeeze(), label.cuda()) + out[2]
+        loss.backward()
+        masks = _din_masks(model, B)
+        r = ref.din_forward_train(p, inp["dense"], inp["category"], inp["sequence"], inp["target"], hidden,
+                                  cfg.get("batch_norm", True), 0.1, cfg.get("softmax", False), cfg.get("l2", 0.2),
+                                  True, att, masks)
+        rloss = crit(r[0].squeeze(), label) + r[2]
+        rloss.backward()
+        for i, (o, w) in enumerate(zip(out, r)):
+            if isinstance(w, torch.Tensor):
+                torch.testing.assert_close(o.detach().cpu().reshape(w.shape), w.detach(), rtol=1e-4, atol=1e-4,
+                                           msg=lambda m: f"output {i} step {step}: {m}")
+            else:
+                assert o == w
+        for k, v in model.state_dict().items():
+            if k not in params and (step == 0 or not k.endswith("running_mean")):
+                torch.testing.assert_close(v.cpu(), p[k], rtol=1e-4, atol=1e-5, msg=lambda m: f"buffer {k} step {step}: {m}")
+        for n, prm in model.named_parameters():
+            want = p[n].grad
+            if want is None:
+                assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, n
+                continue
+            scale = max(1e-3, float(want.abs().max()))
+            # the query / history-key gradients sum T positions of att-MLP cross-feature terms that
+            # largely cancel (fp32 noise ~2e-3 of the table's largest gradient at T = 50, H = 32)
+            tol = (5e-3 if n.startswith("embeddings.") else 5e-4) * scale
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=tol, msg=lambda m: f"grad {n} step {step}: {m}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in model.named_parameters():
+            if p[n].grad is not None:
+                _assert_adam_params_close(prm.detach().cpu(), p[n].detach(), lr=1e-3, steps=1,
+                                          what=f"param {n} after step {step}")
+        with torch.no_grad():  # re-synchronise the oracle to the engine (see _deepfm_step_check)
+            for k, v in model.state_dict().items():
+                p[k].copy_(v.cpu())
+            for n, prm in model.named_parameters():
+                if prm in opt.state and p[n] in ref_opt.state:
+                    for key in ("exp_avg", "exp_avg_sq"):
+                        ref_opt.state[p[n]][key].copy_(opt.state[prm][key].cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{"T": 20}, {"T": 20, "softmax": True}, {"T": 12, "batch_norm": False, "l2": 0.0},
+                                 {"T": 50, "dim": 32, "vocab": H.WECHAT_VOCAB}, {"T": 70, "min_len": 0}],
+                         ids=["default", "softmax", "no_bn_no_l2", "bench_shape", "long_empty"])
+def test_din_train_steps_match_autograd(cfg):
+    _din_step_check(cfg, 512, seed=2400, steps=2)
+
+
+@pytest.mark.gpu
+def test_din_train_graph_capture_matches_eager():
+    """A whole DIN train step (frozen att_net, capturable Adam) captured in one hipGraph gives the
+    same parameters as the eager step."""
+    cfg = {"T": 20, "interaction_weights": "frozen"}
+    inp = H.to_device(H.make_inputs("din", cfg, 256, seed=31), "cuda")
+    label = (torch.rand(256, device="cuda") < 0.3).float()
+    crit = torch.nn.BCELoss()
+    results = []
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = H.build("din", cfg).cuda().train()
+        opt = rankops.Adam(model.parameters(), lr=1e-3, capturable=(mode == "graph"))
+
+        def step():
+            opt.zero_grad(set_to_none=False)
+            out = H.call_model(model, "din", inp)
+            (crit(out[0].squeeze(), label) + out[2]).backward()
+            opt.step()
+
+        if mode == "eager":
+            for _ in range(3):
+                step()
+        else:
+            step()  # draws the frozen weights, allocates the optimizer state
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            g.replay()
+            g.replay()
+        torch.cuda.synchronize()
+        results.append({n: t.detach().cpu().clone() for n, t in model.named_parameters()})
+    for n in results[0]:
+        torch.testing.assert_close(results[1][n], results[0][n], rtol=1e-5, atol=1e-6, msg=n)
+
+
 @pytest.mark.gpu
 def test_dropout_mask_rate_and_freshness():
     counter = torch.zeros(1, dtype=torch.int64, device="cuda")
