@@ -156,6 +156,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
           krow = a.key_table + r * a.ld_key;
         else
           flag_oob(flags);
+#ifdef RK_DIN_NO_GATHER  // timing experiment only: the keys come from 32 cache-resident rows
+        krow = a.key_table + (int64_t)l32 * a.ld_key;
+#endif
       }
       f32x4_t k[NQ];
 #pragma unroll

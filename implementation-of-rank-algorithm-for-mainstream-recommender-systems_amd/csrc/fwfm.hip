@@ -91,6 +91,87 @@ __global__ __launch_bounds__(64) void fwfm_forward_kernel(FwfmTables t, int F, i
   }
 }
 
+// FwFM backward (training) from dL/dprob (the script's BCELoss on the
+// probabilities, fwfm.py:150-156, 245):  dz = dprob * (1 - prob) * prob (torch's sigmoid backward),
+//   d_emb[b, i*dim + c] = dz * sum_{j != i} r_{p(i,j)} E_j[c]      (the embedding-row gradients)
+//   d_r[p] += dz * <E_i, E_j>,  d_bias += dz,  dz_out[b] = dz      (the linear-table gradient rows)
+// Same lane layout as the forward; 4 waves per workgroup, the d_r / d_bias partials are summed in
+// LDS and flushed with one float atomic per pair and workgroup.
+constexpr int kFwfmMaxPairs = kFwfmMaxFields * (kFwfmMaxFields - 1) / 2;
+
+template <int G, int VEC>
+__global__ __launch_bounds__(256) void fwfm_backward_kernel(FwfmTables t, int F, int dim, int64_t batch,
+                                                            const float* __restrict__ field_weight,
+                                                            const float* __restrict__ prob,
+                                                            const float* __restrict__ dprob, float* __restrict__ d_emb,
+                                                            int64_t ld_demb, float* __restrict__ dz_out,
+                                                            float* __restrict__ d_field_weight,
+                                                            float* __restrict__ d_bias, uint32_t* flags) {
+  using V = VecT<VEC>;
+  using T = typename V::T;
+  constexpr int SPW = 64 / G;
+  __shared__ float red[kFwfmMaxPairs + 1];
+  const int P = F * (F - 1) / 2;
+  for (int i = threadIdx.x; i <= P; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane % G;
+  const int64_t b = ((int64_t)blockIdx.x * 4 + wave) * SPW + lane / G;
+  const bool live = b < batch;
+  const int col = q * VEC;
+  const bool has_cols = col < dim;
+  const float* rp[kFwfmMaxFields];
+#pragma unroll
+  for (int f = 0; f < kFwfmMaxFields; ++f) {
+    rp[f] = nullptr;
+    if (f < F && live) {
+      const float* r = segment_row(t.emb[f], b, flags);
+      rp[f] = has_cols && r ? r + col : nullptr;
+    }
+  }
+  T v[kFwfmMaxFields];
+#pragma unroll
+  for (int f = 0; f < kFwfmMaxFields; ++f) v[f] = rp[f] ? *reinterpret_cast<const T*>(rp[f]) : V::zero();
+  const float y = live ? prob[b] : 0.f;
+  const float dz = live ? dprob[b] * (1.0f - y) * y : 0.f;
+  // embedding-row gradients
+#pragma unroll
+  for (int i = 0; i < kFwfmMaxFields; ++i) {
+    if (i >= F) break;
+    T acc = V::zero();
+#pragma unroll
+    for (int j = 0; j < kFwfmMaxFields; ++j) {
+      if (j >= F) break;
+      if (j == i) continue;
+      const int a = i < j ? i : j, c = i < j ? j : i;
+      const int p = a * F - a * (a + 1) / 2 + (c - a - 1);  // i-major pair index of (a, c)
+      acc = acc + field_weight[p] * v[j];
+    }
+    if (live && has_cols) *reinterpret_cast<T*>(d_emb + b * ld_demb + (int64_t)i * dim + col) = dz * acc;
+  }
+  // pair-weight and bias gradients
+  int p = 0;
+#pragma unroll
+  for (int i = 0; i < kFwfmMaxFields; ++i) {
+    if (i >= F) break;
+#pragma unroll
+    for (int j = i + 1; j < kFwfmMaxFields; ++j) {
+      if (j >= F) break;
+      float s = V::dot(v[i], v[j]);
+#pragma unroll
+      for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+      if (live && q == 0) atomicAdd(&red[p], dz * s);
+      ++p;
+    }
+  }
+  if (live && q == 0) {
+    atomicAdd(&red[P], dz);
+    dz_out[b] = dz;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i <= P; i += blockDim.x) atomicAdd(i < P ? d_field_weight + i : d_bias, red[i]);
+}
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace rk
@@ -146,4 +227,60 @@ RK_API int rk_fwfm_forward(const rk_segment* embeddings, const rk_segment* linea
   RK_FWFM_CASE(64, 1)
 #undef RK_FWFM_CASE
   return fail(RK_ERR_UNSUPPORTED, "rk_fwfm_forward: dim %d", dim);
+}
+
+RK_API int rk_fwfm_backward(const rk_segment* embeddings, int32_t num_fields, int32_t dim, int64_t batch,
+                            const float* field_weight, const float* prob, const float* dprob, float* d_emb,
+                            int64_t ld_demb, float* dz, float* d_field_weight, float* d_bias, void* stream) {
+  if (num_fields < 2 || num_fields > kFwfmMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_fwfm_backward: %d fields (supported 2..%d)", num_fields, kFwfmMaxFields);
+  if (!embeddings || !field_weight || !prob || !dprob || !d_emb || !dz || !d_field_weight || !d_bias ||
+      ld_demb < (int64_t)num_fields * dim)
+    return fail(RK_ERR_INVALID, "rk_fwfm_backward: bad arguments");
+  if (dim <= 0 || dim > 256) return fail(RK_ERR_UNSUPPORTED, "rk_fwfm_backward: dim %d (supported 1..256)", dim);
+  bool vec4 = dim % 4 == 0 && aligned16(d_emb) && ld_demb % 4 == 0;
+  FwfmTables t;
+  for (int f = 0; f < num_fields; ++f) {
+    const rk_segment& e = embeddings[f];
+    if (!e.src || !e.idx || e.rows <= 0 || e.dim != dim)
+      return fail(RK_ERR_INVALID, "rk_fwfm_backward: field %d table invalid", f);
+    vec4 = vec4 && aligned16(e.src) && e.src_ld % 4 == 0;
+    t.emb[f] = e;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int P = num_fields * (num_fields - 1) / 2;
+  if (hipMemsetAsync(d_field_weight, 0, (size_t)P * sizeof(float), st) != hipSuccess ||
+      hipMemsetAsync(d_bias, 0, sizeof(float), st) != hipSuccess)
+    return fail(RK_ERR_RUNTIME, "rk_fwfm_backward: memset failed");
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_fwfm_backward: negative batch");
+  const int vec = vec4 ? 4 : 1;
+  int G = 1;
+  while (G * vec < dim) G <<= 1;
+  if (G > 64) return fail(RK_ERR_UNSUPPORTED, "rk_fwfm_backward: dim %d needs 16-byte aligned rows", dim);
+  const int64_t per_block = 4 * (64 / G);
+  const int64_t blocks = (batch + per_block - 1) / per_block;
+  uint32_t* fl = device_flags();
+#define RK_FWFM_CASE(GG, VV)                                                                                   \
+  if (G == GG && vec == VV) {                                                                                  \
+    fwfm_backward_kernel<GG, VV><<<(unsigned)blocks, 256, 0, st>>>(t, num_fields, dim, batch, field_weight, prob, \
+                                                                   dprob, d_emb, ld_demb, dz, d_field_weight,   \
+                                                                   d_bias, fl);                                 \
+    return check_launch("rk_fwfm_backward");                                                                   \
+  }
+  RK_FWFM_CASE(1, 4)
+  RK_FWFM_CASE(2, 4)
+  RK_FWFM_CASE(4, 4)
+  RK_FWFM_CASE(8, 4)
+  RK_FWFM_CASE(16, 4)
+  RK_FWFM_CASE(32, 4)
+  RK_FWFM_CASE(64, 4)
+  RK_FWFM_CASE(1, 1)
+  RK_FWFM_CASE(2, 1)
+  RK_FWFM_CASE(4, 1)
+  RK_FWFM_CASE(8, 1)
+  RK_FWFM_CASE(16, 1)
+  RK_FWFM_CASE(32, 1)
+  RK_FWFM_CASE(64, 1)
+#undef RK_FWFM_CASE
+  return fail(RK_ERR_UNSUPPORTED, "rk_fwfm_backward: dim %d", dim);
 }

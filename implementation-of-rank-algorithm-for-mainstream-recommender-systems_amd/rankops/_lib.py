@@ -195,6 +195,8 @@ SIGNATURES = {
                                          c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_row_l2norm_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_void_p,
                                               c_void_p, c_int64, c_void_p]),
+    "rk_fwfm_backward": (ctypes.c_int, [POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, train
 from .common import EngineModule, check_eval
 
 FWFM_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
@@ -41,17 +41,22 @@ class FwFM(EngineModule):
         self.bias = nn.Parameter(torch.zeros(1))
 
     def forward(self, x, *, return_logit=False):
-        """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit)."""
-        check_eval(self)
+        """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit).
+        Under .train() with autograd on, the probabilities carry the HIP backward (rankops.train)."""
+        if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            check_eval(self)  # a train-mode forward without autograd is not implemented
         idx0 = ops.as_index(x[self.field_names[0]], f"x[{self.field_names[0]!r}]")
         B = idx0.shape[0]
-        emb, lin = [], []
+        emb, lin, idxs = [], [], []
         for f, name in enumerate(self.field_names):
             idx = ops.as_index(x[name], f"x[{name!r}]")
             if idx.shape != (B,):
                 raise ValueError(f"FwFM.forward: x[{name!r}] has shape {tuple(idx.shape)}, expected ({B},)")
             emb.append(ops.table_segment(self.embedding[f].weight, idx, 0))
             lin.append(ops.table_segment(self.linear[f].weight, idx, 0))
+            idxs.append(idx)
+        if self.training:
+            return train.fwfm_train_forward(self, idxs, return_logit)
         prob = torch.empty(B, device=idx0.device, dtype=torch.float32)
         logit = torch.empty(B, device=idx0.device, dtype=torch.float32) if return_logit else None
         ops.fwfm_forward(emb, lin, self.embed_dim, B, ops.as_f32(self.field_weight, "field_weight"),

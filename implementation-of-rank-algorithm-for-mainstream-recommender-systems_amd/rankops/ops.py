@@ -445,6 +445,13 @@ def row_l2norm_backward(x, col0, ncols, scale, grad_out, dx):
                                      ptr(dx), dx.stride(0), _lib.stream_of(dx)), "rk_row_l2norm_backward")
 
 
+def fwfm_backward(emb_segs, dim, batch, field_weight, prob, dprob, d_emb, dz, d_field_weight, d_bias):
+    lib = _lib.load()
+    check(lib.rk_fwfm_backward(_seg_array(emb_segs), len(emb_segs), dim, batch, ptr(field_weight), ptr(prob),
+                               ptr(dprob), ptr(d_emb), d_emb.stride(0), ptr(dz), ptr(d_field_weight), ptr(d_bias),
+                               _lib.stream_of(prob)), "rk_fwfm_backward")
+
+
 def fm_backward(deep_in, d_deep, dfm2, num_fields, dim, out):
     lib = _lib.load()
     check(lib.rk_fm_backward(ptr(deep_in), deep_in.stride(0), ptr(d_deep), d_deep.stride(0) if d_deep is not None else 0,

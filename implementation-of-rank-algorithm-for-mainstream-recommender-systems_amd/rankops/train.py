@@ -607,6 +607,56 @@ def din_train_forward(model, pl, att):
     return _DINTrain.apply(model, pl, att, (weights, looks), *weights, *_din_params(model, units))
 
 
+# ---------------------------------------------------------------- FwFM
+
+class _FwFMTrain(torch.autograd.Function):
+    """FwFM forward (rk_fwfm_forward, fwfm.py:114-139; no train/eval difference) + backward
+    (rk_fwfm_backward, then the table scatters).  Inputs after the fixed arguments: the linear
+    tables, the embedding tables, field_weight, bias."""
+
+    @staticmethod
+    def forward(ctx, model, idx, want_logit, *params):
+        F = model.num_fields
+        lin_w, emb_w = params[:F], params[F:2 * F]
+        field_weight, bias = params[2 * F], params[2 * F + 1]
+        B, dev = idx[0].shape[0], idx[0].device
+        emb = [ops.table_segment(w, i, 0) for w, i in zip(emb_w, idx)]
+        lin = [ops.table_segment(w, i, 0) for w, i in zip(lin_w, idx)]
+        prob = torch.empty(B, device=dev, dtype=torch.float32)
+        logit = torch.empty(B, device=dev, dtype=torch.float32) if want_logit else None
+        ops.fwfm_forward(emb, lin, model.embed_dim, B, field_weight, bias, logit, prob)
+        ctx.model, ctx.idx = model, idx
+        ctx.save_for_backward(prob, field_weight, *emb_w, *lin_w)
+        if want_logit:
+            ctx.mark_non_differentiable(logit)
+            return prob, logit
+        return prob
+
+    @staticmethod
+    def backward(ctx, dprob, *_):
+        model, idx = ctx.model, ctx.idx
+        F, D = model.num_fields, model.embed_dim
+        prob, field_weight, *tabs = ctx.saved_tensors
+        emb_w, lin_w = tabs[:F], tabs[F:]
+        B, dev = prob.shape[0], prob.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        d_emb = torch.empty(B, F * D, **f32)
+        dz = torch.empty(B, 1, **f32)
+        d_r = torch.empty_like(field_weight)
+        d_b = torch.empty(1, **f32)
+        ops.fwfm_backward([ops.table_segment(w, i, 0) for w, i in zip(emb_w, idx)], D, B, field_weight, prob,
+                          _grad_out(dprob, prob), d_emb, dz, d_r, d_b)
+        g_emb = embedding_grads(list(emb_w), idx, 0, d_emb)
+        g_lin = embedding_grads(list(lin_w), idx, 0, dz, cols=[0] * F)
+        return (None, None, None, *g_lin, *g_emb, d_r, d_b)
+
+
+def fwfm_train_forward(model, idx, want_logit):
+    params = ([m.weight for m in model.linear] + [m.weight for m in model.embedding]
+              + [model.field_weight, model.bias])
+    return _FwFMTrain.apply(model, idx, want_logit, *params)
+
+
 # ---------------------------------------------------------------- optimizer
 
 class Adam(torch.optim.Optimizer):

@@ -45,6 +45,7 @@
  *   rk_din_att_cross, rk_din_att_pool_forward, rk_din_att_pool_backward, rk_din_cross_fold
  *                      din_attention() train forward pieces and backward   din.py:42-84
  *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
+ *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -400,6 +401,14 @@ int rk_din_cross_fold(const float* dcross, const float* x, int64_t ldx, int32_t 
  * scale / rows, adds grad_out[0] * scale * x / ||x_r|| to dx[r, col0 + c] (0 for a zero row).   */
 int rk_row_l2norm_backward(const float* x, int64_t ldx, int64_t rows, int32_t col0, int32_t ncols,
                            float scale, const float* grad_out, float* dx, int64_t lddx, void* stream);
+
+/* FwFM backward from dL/dprob [B] (BCELoss on rk_fwfm_forward's probabilities, fwfm.py:150-156):
+ * dz = dprob * (1 - prob) * prob -> dz [B] (the first-order tables' gradient rows),
+ * d_emb[b, f*dim + c] = dz * sum_{j != f} r_{pair(f,j)} E_j[c] (scatter with rk_embedding_backward),
+ * d_field_weight [F(F-1)/2] and d_bias [1] (overwritten).                                   */
+int rk_fwfm_backward(const rk_segment* embeddings, int32_t num_fields, int32_t dim, int64_t batch,
+                     const float* field_weight, const float* prob, const float* dprob, float* d_emb,
+                     int64_t ld_demb, float* dz, float* d_field_weight, float* d_bias, void* stream);
 
 typedef struct rk_adam_tensor {
   float* param;

@@ -170,13 +170,15 @@ def test_fwfm_construction_matches_reference():
     assert m.num_pairs == 15
 
 
-def test_fwfm_requires_gpu_and_eval():
+def test_fwfm_requires_gpu_and_autograd_in_train():
     m = FwFM([3, 3, 3, 3, 3, 3], 8)
     x = {f: torch.zeros(4, dtype=torch.long) for f in of.FIELDS}
-    with pytest.raises(NotImplementedError):
+    with torch.no_grad(), pytest.raises(NotImplementedError):  # train mode without autograd
+        m(x)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # train mode: the HIP backward path, GPU only
         m(x)
     m.eval()
-    with pytest.raises(Exception):  # CPU tensors: the engine has no CPU path
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # CPU tensors: the engine has no CPU path
         m(x)
 
 

@@ -102,3 +102,53 @@ def test_fwfm_label_encode_to_forward():
         np.testing.assert_array_equal(enc, want)
         x[f] = torch.from_numpy(enc)
     _check(m, x, of.FIELDS)
+
+
+def _train_check(dims, D, fields, B, seed, steps=2):
+    """FwFM train steps (fwfm.py:141-160: forward, BCELoss, backward, Adam) against the oracle
+    forward differentiated by autograd; gradients within 5e-4 of each tensor's largest."""
+    torch.manual_seed(seed)
+    m = FwFM(dims, D, field_names=fields).cuda().train()
+    x = _inputs(dims, B, fields, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    params = dict(m.named_parameters())
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    opt = rankops.Adam(m.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in params], lr=1e-3)
+    crit = torch.nn.BCELoss()
+    xd = {f: t.cuda() for f, t in x.items()}
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        prob = m(xd)
+        crit(prob, label.cuda()).backward()
+        want, _ = of.forward(p, x, fields)
+        crit(want, label).backward()
+        torch.testing.assert_close(prob.detach().cpu(), want.detach(), rtol=0, atol=1e-5)
+        for n, prm in params.items():
+            scale = max(1e-4, float(p[n].grad.abs().max()))
+            torch.testing.assert_close(prm.grad.cpu(), p[n].grad, rtol=0, atol=5e-4 * scale,
+                                       msg=lambda msg: f"grad {n} step {step}: {msg}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in params.items():
+            torch.testing.assert_close(prm.detach().cpu(), p[n].detach(), rtol=1e-4, atol=2e-5,
+                                       msg=lambda msg: f"param {n} step {step}: {msg}")
+        with torch.no_grad():  # re-synchronise (Adam's sign flips on noise-level gradients)
+            for n, prm in params.items():
+                p[n].copy_(prm.detach().cpu())
+                for key in ("exp_avg", "exp_avg_sq"):
+                    ref_opt.state[p[n]][key].copy_(opt.state[prm][key].cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [8, 5, 32])
+def test_fwfm_train_steps_match_autograd(D):
+    _train_check([50, 70, 2, 40, 30, 60], D, of.FIELDS, 1024, seed=D)
+
+
+@pytest.mark.gpu
+def test_fwfm_train_wechat_and_16_fields():
+    _train_check(WECHAT_FWFM_DIMS, 8, of.FIELDS, 4096, seed=3, steps=1)
+    fields = tuple(f"field_{i}" for i in range(16))
+    _train_check([11 + 3 * i for i in range(16)], 16, fields, 777, seed=4)
