@@ -197,6 +197,14 @@ SIGNATURES = {
                                               c_void_p, c_int64, c_void_p]),
     "rk_fwfm_backward": (ctypes.c_int, [POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_afm_pairs": (ctypes.c_int, [POINTER(Segment), c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rk_afm_pool_forward": (ctypes.c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                                           c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_afm_pool_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
+                                            c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_afm_pair_fold": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

@@ -16,7 +16,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, train
 from .common import DENSE_FEATURES, EngineModule, check_eval
 
 
@@ -63,14 +63,18 @@ class AFM(EngineModule):
         self.p = nn.Linear(embedding_dim, 1)
 
     def forward(self, dense_input, category_input):
-        check_eval(self)
+        if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            check_eval(self)  # a train-mode forward without autograd is not implemented
         dense_input = ops.as_f32(dense_input, "dense_input")
         B = dense_input.shape[0]
         dev = dense_input.device
-        fields = []
+        fields, idxs = [], []
         for col in self.category_features:
             idx = ops.as_index(category_input[col], f"category_input[{col!r}]")
             fields.append(ops.table_segment(self.embeddings[col].weight, idx, 0))
+            idxs.append(idx)
+        if self.training:  # AFM has no BatchNorm / Dropout: the train forward is the eval math
+            return train.afm_train_forward(self, dense_input.contiguous(), idxs)
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
         pred = torch.empty(B, 1, device=dev, dtype=torch.float32)
         att1, att2 = self.attention[0], self.attention[2]

@@ -452,6 +452,34 @@ def fwfm_backward(emb_segs, dim, batch, field_weight, prob, dprob, d_emb, dz, d_
                                _lib.stream_of(prob)), "rk_fwfm_backward")
 
 
+def afm_pairs(fields, dim, batch, emb, pairs):
+    lib = _lib.load()
+    check(lib.rk_afm_pairs(_seg_array(fields), len(fields), dim, batch, ptr(emb), ptr(pairs), _lib.stream_of(emb)),
+          "rk_afm_pairs")
+
+
+def afm_pool_forward(a1, w2, b2, pairs, num_pairs, dim, dense, wd, bd, wp, bp, weights, ws, logit, pred):
+    lib = _lib.load()
+    check(lib.rk_afm_pool_forward(ptr(a1), a1.shape[1], ptr(w2), ptr(b2), ptr(pairs), num_pairs, dim, ptr(dense),
+                                  dense.stride(0), dense.shape[1], ptr(wd), ptr(bd), ptr(wp), ptr(bp), dense.shape[0],
+                                  ptr(weights), ptr(ws), ptr(logit), ptr(pred), _lib.stream_of(pred)),
+          "rk_afm_pool_forward")
+
+
+def afm_pool_backward(dpred, dtotal, pred, weights, ws, pairs, a1, w2, wp, dense, num_pairs, dim, d_pairs, da1, acc):
+    lib = _lib.load()
+    check(lib.rk_afm_pool_backward(ptr(dpred), ptr(dtotal), ptr(pred), ptr(weights), ptr(ws), ptr(pairs), ptr(a1),
+                                   a1.shape[1], ptr(w2), ptr(wp), ptr(dense), dense.stride(0), dense.shape[1],
+                                   dense.shape[0], num_pairs, dim, ptr(d_pairs), ptr(da1), ptr(acc),
+                                   _lib.stream_of(pred)), "rk_afm_pool_backward")
+
+
+def afm_pair_fold(d_pairs, emb, num_fields, dim, d_emb):
+    lib = _lib.load()
+    check(lib.rk_afm_pair_fold(ptr(d_pairs), ptr(emb), num_fields, dim, emb.shape[0], ptr(d_emb),
+                               _lib.stream_of(emb)), "rk_afm_pair_fold")
+
+
 def fm_backward(deep_in, d_deep, dfm2, num_fields, dim, out):
     lib = _lib.load()
     check(lib.rk_fm_backward(ptr(deep_in), deep_in.stride(0), ptr(d_deep), d_deep.stride(0) if d_deep is not None else 0,

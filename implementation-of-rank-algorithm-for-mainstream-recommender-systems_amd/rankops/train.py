@@ -607,6 +607,78 @@ def din_train_forward(model, pl, att):
     return _DINTrain.apply(model, pl, att, (weights, looks), *weights, *_din_params(model, units))
 
 
+# ---------------------------------------------------------------- AFM
+
+class _AFMTrain(torch.autograd.Function):
+    """AFM forward + backward (afm.py:92-119; no train/eval difference in the module).  Inputs
+    after the fixed arguments: dense_layer.{weight,bias}, the field embeddings, attention.0.{weight,
+    bias}, attention.2.{weight,bias}, p.{weight,bias}."""
+
+    @staticmethod
+    def forward(ctx, model, dense, idx, *params):
+        F, D = model.num_fields, model.embedding_dim
+        wd, bd = params[0], params[1]
+        tables = params[2:2 + F]
+        w1, b1, w2, b2, wp, bp = params[2 + F:]
+        B, dev = dense.shape[0], dense.device
+        P = F * (F - 1) // 2
+        f32 = dict(device=dev, dtype=torch.float32)
+        emb = torch.empty(B, F * D, **f32)
+        pairs = torch.empty(B * P, D, **f32)
+        ops.afm_pairs([ops.table_segment(t, i, 0) for t, i in zip(tables, idx)], D, B, emb, pairs)
+        a1 = torch.empty(B * P, w1.shape[0], **f32)
+        ops.linear(pairs, w1, a1, epilogue=ops.make_epilogue(bias=b1, act="relu"))
+        weights = torch.empty(B, P, **f32)
+        ws = torch.empty(B, D, **f32)
+        logit = torch.empty(B, 1, **f32)
+        pred = torch.empty(B, 1, **f32)
+        ops.afm_pool_forward(a1, w2.reshape(-1), b2, pairs, P, D, dense, wd.reshape(-1), bd, wp.reshape(-1), bp,
+                             weights, ws, logit, pred)
+        ctx.model, ctx.idx = model, idx
+        ctx.save_for_backward(dense, emb, pairs, a1, weights, ws, pred, w1, w2, wp, *tables)
+        return pred, logit
+
+    @staticmethod
+    def backward(ctx, dpred, dlogit):
+        model, idx = ctx.model, ctx.idx
+        dense, emb, pairs, a1, weights, ws, pred, w1, w2, wp, *tables = ctx.saved_tensors
+        F, D = model.num_fields, model.embedding_dim
+        B, dev = dense.shape[0], dense.device
+        P, A, nd = F * (F - 1) // 2, w1.shape[0], dense.shape[1]
+        f32 = dict(device=dev, dtype=torch.float32)
+        d_pairs = torch.empty(B * P, D, **f32)
+        da1 = torch.empty(B * P, A, **f32)
+        acc = torch.empty(nd + 1 + D + 1 + A + 1, **f32)
+        ops.afm_pool_backward(_grad_out(dpred, pred) if dpred is not None else None,
+                              _grad_out(dlogit, pred) if dlogit is not None else None, pred, weights, ws, pairs, a1,
+                              w2.reshape(-1), wp.reshape(-1), dense, P, D, d_pairs, da1, acc)
+        dW1 = torch.empty_like(w1)
+        db1 = torch.empty(A, **f32)
+        M = B * P
+        ops.gemm(True, True, A, D, M, da1, A, pairs, D, dW1, row_sums=db1)
+        ops.gemm(False, True, M, D, A, da1, A, w1, D, d_pairs, accumulate=True)
+        d_emb = torch.empty(B, F * D, **f32)
+        ops.afm_pair_fold(d_pairs, emb, F, D, d_emb)
+        g_emb = embedding_grads(list(tables), idx, 0, d_emb)
+        o = 0
+        dwd, dbd = acc[o:o + nd].view(1, nd), acc[o + nd:o + nd + 1]
+        o += nd + 1
+        dwp, dbp = acc[o:o + D].view(1, D), acc[o + D:o + D + 1]
+        o += D + 1
+        dw2, db2 = acc[o:o + A].view(1, A), acc[o + A:o + A + 1]
+        return (None, None, None, dwd, dbd, *g_emb, dW1, db1, dw2, db2, dwp, dbp)
+
+
+def afm_train_forward(model, dense, idx):
+    att1, att2 = model.attention[0], model.attention[2]
+    params = ([model.dense_layer.weight, model.dense_layer.bias]
+              + [model.embeddings[c].weight for c in model.category_features]
+              + [att1.weight, att1.bias, att2.weight, att2.bias, model.p.weight, model.p.bias])
+    if any(t is None for t in params):
+        raise NotImplementedError("rankops AFM training expects the reference's biased Linear layers")
+    return _AFMTrain.apply(model, dense, idx, *params)
+
+
 # ---------------------------------------------------------------- FwFM
 
 class _FwFMTrain(torch.autograd.Function):

@@ -46,6 +46,8 @@
  *                      din_attention() train forward pieces and backward   din.py:42-84
  *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
+ *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
+ *                      AFM train forward (activations kept) and backward  afm.py:92-119,173
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
 #ifndef RANKOPS_H
@@ -409,6 +411,29 @@ int rk_row_l2norm_backward(const float* x, int64_t ldx, int64_t rows, int32_t co
 int rk_fwfm_backward(const rk_segment* embeddings, int32_t num_fields, int32_t dim, int64_t batch,
                      const float* field_weight, const float* prob, const float* dprob, float* d_emb,
                      int64_t ld_demb, float* dz, float* d_field_weight, float* d_bias, void* stream);
+
+/* AFM training (afm.py:92-119).  pairs: emb [B, F*dim] (gathered rows) and pairs [B*P, dim]
+ * (P = F(F-1)/2, i-major), 2 <= F <= 16.  The attention's first layer a1 = relu(pairs W1^T + b1)
+ * runs on rk_linear; pool_forward: s = a1 . w2 + b2, softmax over the P pairs (weights [B, P]),
+ * ws = sum_p w_p pair_p [B, dim], logit = dense . wd + bd + ws . wp + bp, pred = sigmoid(logit)
+ * (dim, num_dense <= 64; logit may be NULL).  pool_backward from dpred and/or dtotal (either may
+ * be NULL): d_pairs (direct part, overwritten), da1 = d a1 [B*P, A] (masked by a1 > 0), and
+ * acc = [d wd (num_dense) | d bd | d wp (dim) | d bp | d w2 (A <= 256) | d b2] (overwritten).
+ * pair_fold: d_emb[b, i*dim + d] = sum_j d_pairs[b, pair(i,j), d] * emb[b, j*dim + d].          */
+int rk_afm_pairs(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch, float* emb,
+                 float* pairs, void* stream);
+int rk_afm_pool_forward(const float* a1, int32_t att_dim, const float* w2, const float* b2,
+                        const float* pairs, int32_t num_pairs, int32_t dim, const float* dense,
+                        int64_t ld_dense, int32_t num_dense, const float* wd, const float* bd,
+                        const float* wp, const float* bp, int64_t batch, float* weights, float* ws,
+                        float* logit, float* pred, void* stream);
+int rk_afm_pool_backward(const float* dpred, const float* dtotal, const float* pred,
+                         const float* weights, const float* ws, const float* pairs, const float* a1,
+                         int32_t att_dim, const float* w2, const float* wp, const float* dense,
+                         int64_t ld_dense, int32_t num_dense, int64_t batch, int32_t num_pairs,
+                         int32_t dim, float* d_pairs, float* da1, float* acc, void* stream);
+int rk_afm_pair_fold(const float* d_pairs, const float* emb, int32_t num_fields, int32_t dim,
+                     int64_t batch, float* d_emb, void* stream);
 
 typedef struct rk_adam_tensor {
   float* param;

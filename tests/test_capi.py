@@ -105,8 +105,11 @@ def test_python_layer_refuses_cpu_tensors():
         H.call_model(m, "dcn", inp)
     with pytest.raises(RuntimeError, match="ROCm GPU"):  # DCN trains on the engine, still GPU-only
         H.call_model(m.train(), "dcn", inp)
-    afm = H.build("afm", {}).train()  # no training path yet: refused, never a silent eager fallback
+    bst = H.build("bst", {"T": 8}).train()  # no training path yet: refused, never a silent eager fallback
     with pytest.raises(NotImplementedError):
+        H.call_model(bst, "bst", H.make_inputs("bst", {"T": 8}, 4))
+    afm = H.build("afm", {}).train()  # trains on the engine: GPU-only like the forward
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
         H.call_model(afm, "afm", H.make_inputs("afm", {}, 4))
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         rankops.cross_layer(torch.zeros(2, 50), torch.zeros(2, 50), 0)

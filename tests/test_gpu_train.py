@@ -569,6 +569,59 @@ def test_din_train_graph_capture_matches_eager():
         torch.testing.assert_close(results[1][n], results[0][n], rtol=1e-5, atol=1e-6, msg=n)
 
 
+AFM_CATS = ["userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list"]
+
+
+def _afm_step_check(cfg, B, seed, steps):
+    """AFM train steps (afm.py:158-180: forward, BCELoss(prediction), backward, Adam) against the
+    oracle's AFM.forward (afm.py:92-119) differentiated by autograd."""
+    model = H.build("afm", cfg).cuda().train()
+    inp = H.make_inputs("afm", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    params = dict(model.named_parameters())
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in params], lr=1e-3)
+    crit = torch.nn.BCELoss()
+    dinp = H.to_device(inp, "cuda")
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        out = H.call_model(model, "afm", dinp)
+        crit(out[0].squeeze(), label.cuda()).backward()
+        r = ref.afm_forward(p, inp["dense_input"], inp["category_input"], AFM_CATS)
+        crit(r[0].squeeze(), label).backward()
+        for i, (o, w) in enumerate(zip(out, r)):
+            torch.testing.assert_close(o.detach().cpu(), w.detach(), rtol=1e-4, atol=1e-4,
+                                       msg=lambda m: f"output {i} step {step}: {m}")
+        for n, prm in params.items():
+            want = p[n].grad
+            scale = max(1e-4, float(want.abs().max()))
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=5e-4 * scale,
+                                       msg=lambda m: f"grad {n} step {step}: {m}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in params.items():
+            if n == "attention.2.bias":
+                # the softmax over pairs is shift-invariant: this bias has a zero true gradient and
+                # both sides hold rounding noise, which Adam normalises to +-lr steps
+                continue
+            _assert_adam_params_close(prm.detach().cpu(), p[n].detach(), lr=1e-3, steps=1,
+                                      what=f"param {n} after step {step}")
+        with torch.no_grad():
+            for n, prm in params.items():
+                p[n].copy_(prm.detach().cpu())
+                for key in ("exp_avg", "exp_avg_sq"):
+                    ref_opt.state[p[n]][key].copy_(opt.state[prm][key].cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{}, {"dim": 32, "att": 64}, {"vocab": H.WECHAT_VOCAB, "dim": 16, "att": 256}],
+                         ids=["default", "dim32_att64", "wechat_att256"])
+def test_afm_train_steps_match_autograd(cfg):
+    _afm_step_check(cfg, 1024, seed=2500, steps=2)
+
+
 @pytest.mark.gpu
 def test_dropout_mask_rate_and_freshness():
     counter = torch.zeros(1, dtype=torch.int64, device="cuda")
