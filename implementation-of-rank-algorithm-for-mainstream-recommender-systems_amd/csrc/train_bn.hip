@@ -11,20 +11,10 @@
 // is read from device memory (rk_rng_next advances it), so a captured hipGraph draws a fresh
 // mask on every replay.  The mask is not torch's Philox stream: dropout masks (like torch's
 // CPU vs CUDA masks) are a random choice, parity tests feed the same mask to the oracle.
-#include "common.h"
+#include "train_common.h"
 
 namespace rk {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uint64_t i, uint32_t threshold) {
-  const uint64_t h = mix64(seed ^ mix64(stream * 0x9E3779B97F4A7C15ull + i));
-  return (uint32_t)(h >> 32) >= threshold;
-}
 
 constexpr int kBnCols = 64;   // columns per workgroup (one per lane)
 constexpr int kBnRows = 256;  // rows per workgroup
@@ -72,7 +62,8 @@ __device__ __forceinline__ BnCol bn_col(const double* sum, const double* sq, int
   return c;
 }
 
-// y = dropout(relu(gamma * (z + bias - mean) * invstd + beta)); with bn == 0: dropout(relu(z + bias)).
+// y = dropout(act(gamma * (z + bias - mean) * invstd + beta)); with bn == 0: dropout(act(z + bias)).
+// act: RK_ACT_NONE, RK_ACT_RELU or RK_ACT_LEAKY(slope) (BST's DNN units, bst.py:207-211).
 // Row block 0 also writes save_mean / save_invstd and updates the running statistics.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, int64_t ldz, int64_t B, int N,
                                                        const float* __restrict__ bias, int bn,
@@ -80,7 +71,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, float momentum, float* __restrict__ running_mean,
                                                        float* __restrict__ running_var, float* __restrict__ save_mean,
-                                                       float* __restrict__ save_invstd, int relu, uint32_t threshold,
+                                                       float* __restrict__ save_invstd, int act, float slope, uint32_t threshold,
                                                        float scale, uint64_t seed,
                                                        const int64_t* __restrict__ stream_slot,
                                                        float* __restrict__ y, int64_t ldy) {
@@ -112,18 +103,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   for (int64_t b = b0 + w; b < b1; b += 4) {
     float u = z[b * ldz + n] + bb;
     if (bn) u = (u - mean) * invstd * g + be;
-    if (relu) u = u < 0.f ? 0.f : u;
+    if (act == RK_ACT_RELU) u = u < 0.f ? 0.f : u;
+    else if (act == RK_ACT_LEAKY) u = u > 0.f ? u : u * slope;
     if (threshold) u = dropout_keep(seed, stream, (uint64_t)b * N + n, threshold) ? u * scale : 0.f;
     y[b * ldy + n] = u;
   }
 }
 
-// Backward statistics: du = dy * keep * scale * [relu: u > 0]; sum[n] += du; sq[n] += du * xhat.
+// Backward statistics: du = dy * keep * scale * act'(u); sum[n] += du; sq[n] += du * xhat.
 template <bool STATS>
 __global__ __launch_bounds__(256) void bn_backward_kernel(
     const float* __restrict__ dy, int64_t lddy, const float* __restrict__ z, int64_t ldz, int64_t B, int N,
     const float* __restrict__ bias, int bn, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
-    const float* __restrict__ gamma, const float* __restrict__ beta, int relu, uint32_t threshold, float scale,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int act, float slope, uint32_t threshold, float scale,
     uint64_t seed, const int64_t* __restrict__ stream_slot, double* __restrict__ sum, double* __restrict__ sq,
     float* __restrict__ dz, int64_t lddz) {
   __shared__ double red[2][4][kBnCols];
@@ -147,9 +139,9 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(
       const float xhat = xmu * invstd;
       float du = dy[b * lddy + n];
       if (threshold) du = dropout_keep(seed, stream, (uint64_t)b * N + n, threshold) ? du * scale : 0.f;
-      if (relu) {
+      if (act == RK_ACT_RELU || act == RK_ACT_LEAKY) {
         const float u = bn ? xhat * g + be : xmu;
-        du = u > 0.f ? du : 0.f;
+        du = u > 0.f ? du : (act == RK_ACT_RELU ? 0.f : du * slope);
       }
       if (STATS) {
         s += (double)du;
@@ -264,11 +256,6 @@ __global__ void dropout_mask_kernel(uint64_t seed, const int64_t* __restrict__ s
     out[i] = dropout_keep(seed, stream, (uint64_t)i, threshold) ? scale : 0.f;
 }
 
-static uint32_t dropout_threshold(double p) {
-  if (!(p > 0.0)) return 0;
-  const double t = p * 4294967296.0;
-  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-}
 
 
 // ---- DIN's Dice activation in train mode (din.py:26-36): x = z + bias, xhat = BatchNorm1d(affine
@@ -392,8 +379,8 @@ RK_API int rk_dropout_mask(uint64_t seed, const int64_t* stream_slot, int64_t ba
 RK_API int rk_bn_act_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
                                    int32_t batch_norm, const float* gamma, const float* beta, float eps,
                                    float momentum, float* running_mean, float* running_var, double* workspace,
-                                   float* save_mean, float* save_invstd, int32_t relu, double dropout_p,
-                                   uint64_t seed, const int64_t* stream_slot, float* y, int64_t ldy, void* stream) {
+                                   float* save_mean, float* save_invstd, int32_t act, float slope,
+                                   double dropout_p, uint64_t seed, const int64_t* stream_slot, float* y, int64_t ldy, void* stream) {
   if (!z || !y || batch <= 0 || n <= 0 || ldz < n || ldy < n || (batch_norm && (!workspace || !save_mean ||
       !save_invstd)) || !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot) ||
       (running_mean != nullptr) != (running_var != nullptr))
@@ -407,15 +394,15 @@ RK_API int rk_bn_act_train_forward(const float* z, int64_t ldz, int64_t batch, i
   const uint32_t thr = dropout_threshold(dropout_p);
   const float scale = (float)(1.0 / (1.0 - dropout_p));
   bn_apply_kernel<<<grid, 256, 0, st>>>(z, ldz, batch, n, bias, batch_norm, workspace, workspace + n, gamma, beta, eps,
-                                        momentum, running_mean, running_var, save_mean, save_invstd, relu, thr, scale,
+                                        momentum, running_mean, running_var, save_mean, save_invstd, act, slope, thr, scale,
                                         seed, stream_slot, y, ldy);
   return check_launch("rk_bn_act_train_forward");
 }
 
 RK_API int rk_bn_act_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch, int32_t n,
                               const float* bias, int32_t batch_norm, const float* gamma, const float* beta,
-                              const float* save_mean, const float* save_invstd, int32_t relu, double dropout_p,
-                              uint64_t seed, const int64_t* stream_slot, double* workspace, float* dz, int64_t lddz,
+                              const float* save_mean, const float* save_invstd, int32_t act, float slope,
+                              double dropout_p, uint64_t seed, const int64_t* stream_slot, double* workspace, float* dz, int64_t lddz,
                               float* dgamma, float* dbeta, void* stream) {
   if (!dy || !z || !dz || batch <= 0 || n <= 0 || (batch_norm && (!save_mean || !save_invstd || !workspace)) ||
       !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
@@ -427,13 +414,13 @@ RK_API int rk_bn_act_backward(const float* dy, int64_t lddy, const float* z, int
   if (batch_norm) {
     zero_f64_kernel<<<(2 * n + 255) / 256, 256, 0, st>>>(workspace, 2 * n);
     bn_backward_kernel<true><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, 1, save_mean, save_invstd, gamma,
-                                                   beta, relu, thr, scale, seed, stream_slot, workspace,
+                                                   beta, act, slope, thr, scale, seed, stream_slot, workspace,
                                                    workspace + n, nullptr, 0);
     if (dgamma || dbeta)
       bn_param_grads_kernel<<<(n + 255) / 256, 256, 0, st>>>(workspace, workspace + n, save_invstd, n, dgamma, dbeta);
   }
   bn_backward_kernel<false><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, batch_norm, save_mean,
-                                                  save_invstd, gamma, beta, relu, thr, scale, seed, stream_slot,
+                                                  save_invstd, gamma, beta, act, slope, thr, scale, seed, stream_slot,
                                                   workspace, batch_norm ? workspace + n : nullptr, dz, lddz);
   return check_launch("rk_bn_act_backward");
 }

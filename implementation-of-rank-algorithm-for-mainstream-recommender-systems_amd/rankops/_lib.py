@@ -167,10 +167,10 @@ SIGNATURES = {
                                        c_void_p]),
     "rk_bn_act_train_forward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32, c_void_p,
                                                c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
-                                               c_void_p, c_int32, ctypes.c_double, ctypes.c_uint64, c_void_p,
+                                               c_void_p, c_int32, c_float, ctypes.c_double, ctypes.c_uint64, c_void_p,
                                                c_void_p, c_int64, c_void_p]),
     "rk_bn_act_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32,
-                                          c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_double,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_float, ctypes.c_double,
                                           ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                           c_void_p]),
     "rk_fm_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32,
@@ -205,6 +205,23 @@ SIGNATURES = {
                                             c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
                                             c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_afm_pair_fold": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
+    "rk_bst_add_pos": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p]),
+    "rk_bst_attn_train_forward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p]),
+    "rk_bst_attn_train_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,
+                                                  c_void_p, c_void_p]),
+    "rk_bst_res_dropout_ln_forward": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, ctypes.c_double,
+                                                     ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                                                     c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_bst_ln_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                          ctypes.c_double, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p]),
+    "rk_bst_leaky_dropout": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, ctypes.c_double, ctypes.c_uint64,
+                                            c_void_p, c_int32, c_void_p, c_void_p]),
+    "rk_bst_pool": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_int64, c_int32,
+                                   c_void_p]),
+    "rk_bst_pool_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int64, c_int32, c_int32, c_void_p, c_int32,
+                                            c_void_p, c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

@@ -25,7 +25,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import common, ops
+from . import common, ops, train
 from .common import EngineModule, Layer, Packed, check_eval, run_tail, table_rows
 
 FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
@@ -140,12 +140,22 @@ class BSTModel(EngineModule):
             width = h
         layers.append(nn.Linear(width, 1))
         self.dnn = nn.Sequential(*layers)
+        self._dropout = train.DropoutStreams()
 
     def forward(self, dense, category, seq_feedid, seq_length):
-        check_eval(self)
+        if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            check_eval(self)  # a train-mode forward without autograd is not implemented
         dense = ops.as_f32(dense, "dense")
         seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
         seq_length = ops.as_index(seq_length, "seq_length")
+        if self.training:  # Dropout in the blocks and the dnn, BatchNorm batch statistics, HIP backward
+            if len(self.transformer_blocks) == 0:
+                raise NotImplementedError("BSTModel with zero transformer blocks")
+            for blk in self.transformer_blocks:
+                if seq_feedid.shape[1] > blk.position_embedding.num_embeddings:
+                    raise IndexError(f"BSTTransformer: sequence length {seq_feedid.shape[1]} exceeds max_len "
+                                     f"{blk.position_embedding.num_embeddings}")
+            return train.bst_train_forward(self, dense.contiguous(), category, seq_feedid, seq_length)
         B, T = seq_feedid.shape
         dev = dense.device
         d = self.d_model

@@ -369,8 +369,15 @@ def dropout_mask(seed: int, slot: torch.Tensor, batch: int, n: int, p: float) ->
     return out
 
 
-def bn_act_train_forward(z, bias, bn, relu, p, seed, slot, y, save_mean, save_invstd, workspace):
-    """bn: an nn.BatchNorm1d (train mode) or None."""
+def _act_code(act):
+    """True/False (ReLU or none) or an ACT name."""
+    if isinstance(act, str):
+        return ACT[act]
+    return _lib.RK_ACT_RELU if act else _lib.RK_ACT_NONE
+
+
+def bn_act_train_forward(z, bias, bn, act, p, seed, slot, y, save_mean, save_invstd, workspace, slope=0.0):
+    """bn: an nn.BatchNorm1d (train mode) or None; act: True (ReLU), False, or 'leaky' with `slope`."""
     lib = _lib.load()
     track = bn is not None and bn.track_running_stats and bn.running_mean is not None
     check(lib.rk_bn_act_train_forward(
@@ -378,16 +385,17 @@ def bn_act_train_forward(z, bias, bn, relu, p, seed, slot, y, save_mean, save_in
         ptr(bn.weight) if bn is not None else None, ptr(bn.bias) if bn is not None else None,
         float(bn.eps) if bn is not None else 0.0, float(bn.momentum) if bn is not None else 0.0,
         ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None, ptr(workspace),
-        ptr(save_mean), ptr(save_invstd), int(relu), float(p), seed, ptr(slot), ptr(y), y.stride(0),
-        _lib.stream_of(z)), "rk_bn_act_train_forward")
+        ptr(save_mean), ptr(save_invstd), _act_code(act), float(slope), float(p), seed, ptr(slot), ptr(y),
+        y.stride(0), _lib.stream_of(z)), "rk_bn_act_train_forward")
 
 
-def bn_act_backward(dy, z, bias, bn, relu, p, seed, slot, save_mean, save_invstd, workspace, dz, dgamma, dbeta):
+def bn_act_backward(dy, z, bias, bn, act, p, seed, slot, save_mean, save_invstd, workspace, dz, dgamma, dbeta,
+                    slope=0.0):
     lib = _lib.load()
     check(lib.rk_bn_act_backward(
         ptr(dy), dy.stride(0), ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), int(bn is not None),
         ptr(bn.weight) if bn is not None else None, ptr(bn.bias) if bn is not None else None, ptr(save_mean),
-        ptr(save_invstd), int(relu), float(p), seed, ptr(slot), ptr(workspace), ptr(dz), dz.stride(0), ptr(dgamma),
+        ptr(save_invstd), _act_code(act), float(slope), float(p), seed, ptr(slot), ptr(workspace), ptr(dz), dz.stride(0), ptr(dgamma),
         ptr(dbeta), _lib.stream_of(dy)), "rk_bn_act_backward")
 
 
@@ -478,6 +486,57 @@ def afm_pair_fold(d_pairs, emb, num_fields, dim, d_emb):
     lib = _lib.load()
     check(lib.rk_afm_pair_fold(ptr(d_pairs), ptr(emb), num_fields, dim, emb.shape[0], ptr(d_emb),
                                _lib.stream_of(emb)), "rk_afm_pair_fold")
+
+
+def bst_add_pos(x, pos, T, xp):
+    lib = _lib.load()
+    check(lib.rk_bst_add_pos(ptr(x), ptr(pos), T, x.shape[0], x.shape[1], ptr(xp), _lib.stream_of(x)),
+          "rk_bst_add_pos")
+
+
+def bst_attn_train_forward(qkv, B, T, d, heads, seq_len, probs, ctx):
+    lib = _lib.load()
+    check(lib.rk_bst_attn_train_forward(ptr(qkv), B, T, d, heads, ptr(seq_len), ptr(probs), ptr(ctx),
+                                        _lib.stream_of(qkv)), "rk_bst_attn_train_forward")
+
+
+def bst_attn_train_backward(qkv, probs, dctx, B, T, d, heads, dqkv):
+    lib = _lib.load()
+    check(lib.rk_bst_attn_train_backward(ptr(qkv), ptr(probs), ptr(dctx), B, T, d, heads, ptr(dqkv),
+                                         _lib.stream_of(qkv)), "rk_bst_attn_train_backward")
+
+
+def bst_res_dropout_ln_forward(base, o, p, seed, slot, ln, r, y, mean, rstd):
+    lib = _lib.load()
+    check(lib.rk_bst_res_dropout_ln_forward(ptr(base), ptr(o), base.shape[0], base.shape[1], float(p), seed,
+                                            ptr(slot), ptr(ln.weight), ptr(ln.bias), float(ln.eps), ptr(r), ptr(y),
+                                            ptr(mean), ptr(rstd), _lib.stream_of(base)),
+          "rk_bst_res_dropout_ln_forward")
+
+
+def bst_ln_backward(dy, r, mean, rstd, ln, p, seed, slot, dr, d_o, dgamma, dbeta):
+    lib = _lib.load()
+    check(lib.rk_bst_ln_backward(ptr(dy), ptr(r), ptr(mean), ptr(rstd), ptr(ln.weight), r.shape[0], r.shape[1],
+                                 float(p), seed, ptr(slot), ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta),
+                                 _lib.stream_of(dy)), "rk_bst_ln_backward")
+
+
+def bst_leaky_dropout(inp, f, slope, p, seed, slot, backward, out):
+    lib = _lib.load()
+    check(lib.rk_bst_leaky_dropout(ptr(inp), ptr(f), f.numel(), float(slope), float(p), seed, ptr(slot),
+                                   int(backward), ptr(out), _lib.stream_of(f)), "rk_bst_leaky_dropout")
+
+
+def bst_pool(x, B, T, seq_len, mean, row, col):
+    lib = _lib.load()
+    check(lib.rk_bst_pool(ptr(x), B, T, x.shape[1], ptr(seq_len), int(mean), ptr(row), row.stride(0), col,
+                          _lib.stream_of(x)), "rk_bst_pool")
+
+
+def bst_pool_backward(drow, col, B, T, d, seq_len, mean, dx):
+    lib = _lib.load()
+    check(lib.rk_bst_pool_backward(ptr(drow), drow.stride(0), col, B, T, d, ptr(seq_len), int(mean), ptr(dx),
+                                   _lib.stream_of(dx)), "rk_bst_pool_backward")
 
 
 def fm_backward(deep_in, d_deep, dfm2, num_fields, dim, out):

@@ -297,7 +297,9 @@ def deep_stack_forward(x, units, seed, slot):
     B, dev = x.shape[0], x.device
     saved = []
     h = x
-    for u, (lin, bn, relu, p) in enumerate(units):
+    for u, unit in enumerate(units):
+        lin, bn, act, p = unit[:4]
+        slope = unit[4] if len(unit) > 4 else 0.0
         n = lin.out_features
         z = torch.empty(B, n, device=dev, dtype=torch.float32)
         ops.gemm(False, False, B, n, lin.in_features, h, h.stride(0), lin.weight, lin.weight.stride(0), z)
@@ -305,7 +307,7 @@ def deep_stack_forward(x, units, seed, slot):
         mean = torch.empty(n, device=dev, dtype=torch.float32)
         invstd = torch.empty(n, device=dev, dtype=torch.float32)
         ws = torch.empty(2 * n, device=dev, dtype=torch.float64)
-        ops.bn_act_train_forward(z, lin.bias, bn, relu, p, seed + u, slot, y, mean, invstd, ws)
+        ops.bn_act_train_forward(z, lin.bias, bn, act, p, seed + u, slot, y, mean, invstd, ws, slope=slope)
         if bn is not None and bn.track_running_stats and bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(1)
         saved.append((z, y, mean, invstd))
@@ -319,7 +321,8 @@ def deep_stack_backward(dy, x, units, saved, seed, slot):
     B, dev = x.shape[0], x.device
     grads = [None] * len(units)
     for u in range(len(units) - 1, -1, -1):
-        lin, bn, relu, p = units[u]
+        lin, bn, act, p = units[u][:4]
+        slope = units[u][4] if len(units[u]) > 4 else 0.0
         z, y, mean, invstd = saved[u]
         n, K = lin.out_features, lin.in_features
         h_in = saved[u - 1][1] if u > 0 else x
@@ -327,7 +330,7 @@ def deep_stack_backward(dy, x, units, saved, seed, slot):
         ws = torch.empty(2 * n, device=dev, dtype=torch.float64)
         dg = torch.empty(n, device=dev, dtype=torch.float32) if bn is not None and bn.weight is not None else None
         dbt = torch.empty(n, device=dev, dtype=torch.float32) if bn is not None and bn.bias is not None else None
-        ops.bn_act_backward(dy, z, lin.bias, bn, relu, p, seed + u, slot, mean, invstd, ws, dz, dg, dbt)
+        ops.bn_act_backward(dy, z, lin.bias, bn, act, p, seed + u, slot, mean, invstd, ws, dz, dg, dbt, slope=slope)
         dW = torch.empty(n, K, device=dev, dtype=torch.float32)
         db = torch.empty(n, device=dev, dtype=torch.float32)
         ops.gemm(True, True, n, K, B, dz, dz.stride(0), h_in, h_in.stride(0), dW, row_sums=db)
@@ -343,7 +346,8 @@ def deep_stack_backward(dy, x, units, saved, seed, slot):
 
 def _unit_params(units):
     out = []
-    for lin, bn, _, _ in units:
+    for unit in units:
+        lin, bn = unit[0], unit[1]
         out += [lin.weight] + ([lin.bias] if lin.bias is not None else [])
         if bn is not None:
             out += [t for t in (bn.weight, bn.bias) if t is not None]
@@ -677,6 +681,230 @@ def afm_train_forward(model, dense, idx):
     if any(t is None for t in params):
         raise NotImplementedError("rankops AFM training expects the reference's biased Linear layers")
     return _AFMTrain.apply(model, dense, idx, *params)
+
+
+# ---------------------------------------------------------------- BST
+
+def bst_units(model):
+    """([Linear, BatchNorm1d or None, 'leaky', dropout p, slope] per dnn unit, last Linear)
+    (bst.py:203-213)."""
+    mods = list(model.dnn)
+    units = []
+    for m in mods[:-1]:
+        if isinstance(m, torch.nn.Linear):
+            units.append([m, None, "none", 0.0, 0.0])
+        elif isinstance(m, torch.nn.BatchNorm1d):
+            if m.momentum is None:
+                raise NotImplementedError("rankops BST training: BatchNorm1d needs a numeric momentum")
+            units[-1][1] = m
+        elif isinstance(m, torch.nn.LeakyReLU):
+            units[-1][2], units[-1][4] = "leaky", float(m.negative_slope)
+        elif isinstance(m, torch.nn.Dropout):
+            units[-1][3] = float(m.p) if m.training else 0.0
+        else:
+            raise NotImplementedError(f"rankops BST training: unsupported dnn layer {type(m).__name__}")
+    return units, mods[-1]
+
+
+def _block_params(blk):
+    return [blk.position_embedding.weight, blk.w_q.weight, blk.w_q.bias, blk.w_k.weight, blk.w_k.bias,
+            blk.w_v.weight, blk.w_v.bias, blk.w_o.weight, blk.w_o.bias, blk.norm1.weight, blk.norm1.bias,
+            blk.norm2.weight, blk.norm2.bias, blk.ffn[0].weight, blk.ffn[0].bias, blk.ffn[3].weight, blk.ffn[3].bias]
+
+
+def bst_dropout_seed(seed, block, site):
+    """Dropout stream seed of transformer block `block`, site 0 (w_o output), 1 (inside the FFN),
+    2 (FFN output); the dnn units use seed + unit."""
+    return seed + 100 + 3 * block + site
+
+
+def _lin_grads(dy, x, w, need_dx=True, dx=None, accumulate=False):
+    """y = x W^T + b backward with dy row stride dy.stride(0): (dW, db[, dx])."""
+    M, N = dy.shape[0], w.shape[0]
+    K = w.shape[1]
+    dW = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+    db = torch.empty(N, device=dy.device, dtype=torch.float32)
+    ops.gemm(True, True, N, K, M, dy, dy.stride(0), x, x.stride(0), dW, row_sums=db)
+    if need_dx:
+        if dx is None:
+            dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+        ops.gemm(False, True, M, K, N, dy, dy.stride(0), w, w.stride(0), dx, accumulate=accumulate)
+    return dW, db, dx
+
+
+class _BSTTrain(torch.autograd.Function):
+    """BSTModel forward + backward in train mode (bst.py:216-247 with BSTTransformer.forward
+    bst.py:66-91): Dropout in every block (w_o output, inside and after the FFN) and in the dnn,
+    BatchNorm1d with batch statistics.  Inputs after the fixed arguments: the distinct embedding
+    tables of `plan`, then per block `_block_params`, then the dnn unit parameters and the last
+    Linear."""
+
+    @staticmethod
+    def forward(ctx, model, plan, *params):
+        seq, seq_len, B, T, width, col = plan["seq"], plan["seq_len"], plan["B"], plan["T"], plan["width"], plan["col"]
+        dev, d = seq.device, model.d_model
+        M = B * T
+        f32 = dict(device=dev, dtype=torch.float32)
+        row = torch.empty(B, width, **f32)
+        ops.concat_gather(plan["segs"], B, row)
+        feed = model.embeddings["feedid"].weight
+        x = torch.empty(M, d, **f32)
+        ops.concat_gather([ops.table_segment(feed, seq.view(-1), 0)], M, x)
+        seed, slot = model._dropout.next(dev)
+        saves = []
+        for i, blk in enumerate(model.transformer_blocks):
+            p_o, p_f = float(blk.dropout.p) if blk.training else 0.0, float(blk.ffn[2].p) if blk.training else 0.0
+            h = blk.nhead
+            xp = torch.empty(M, d, **f32)
+            ops.bst_add_pos(x, blk.position_embedding.weight, T, xp)
+            qkv = torch.empty(M, 3 * d, **f32)
+            ops.linear(xp, blk.w_q.weight, None, y_ptr=qkv.data_ptr(), ldy=3 * d,
+                       epilogue=ops.make_epilogue(bias=blk.w_q.bias))
+            ops.linear(xp, blk.w_k.weight, None, y_ptr=ops._lib.fptr(qkv, d), ldy=3 * d,
+                       epilogue=ops.make_epilogue(bias=blk.w_k.bias))
+            ops.linear(x, blk.w_v.weight, None, y_ptr=ops._lib.fptr(qkv, 2 * d), ldy=3 * d,
+                       epilogue=ops.make_epilogue(bias=blk.w_v.bias))
+            probs = torch.empty(B * h * T * T, **f32)
+            cx = torch.empty(M, d, **f32)
+            ops.bst_attn_train_forward(qkv, B, T, d, h, seq_len, probs, cx)
+            o = torch.empty(M, d, **f32)
+            ops.linear(cx, blk.w_o.weight, o, epilogue=ops.make_epilogue(bias=blk.w_o.bias))
+            r1, out1 = torch.empty(M, d, **f32), torch.empty(M, d, **f32)
+            m1, s1 = torch.empty(M, **f32), torch.empty(M, **f32)
+            ops.bst_res_dropout_ln_forward(xp, o, p_o, bst_dropout_seed(seed, i, 0), slot, blk.norm1, r1, out1, m1, s1)
+            del o
+            f1 = torch.empty(M, d, **f32)
+            ops.linear(out1, blk.ffn[0].weight, f1, epilogue=ops.make_epilogue(bias=blk.ffn[0].bias))
+            a = torch.empty(M, d, **f32)
+            ops.bst_leaky_dropout(None, f1, blk.ffn[1].negative_slope, p_f, bst_dropout_seed(seed, i, 1), slot, False, a)
+            f2 = torch.empty(M, d, **f32)
+            ops.linear(a, blk.ffn[3].weight, f2, epilogue=ops.make_epilogue(bias=blk.ffn[3].bias))
+            r2, out = torch.empty(M, d, **f32), torch.empty(M, d, **f32)
+            m2, s2 = torch.empty(M, **f32), torch.empty(M, **f32)
+            ops.bst_res_dropout_ln_forward(out1, f2, p_o, bst_dropout_seed(seed, i, 2), slot, blk.norm2, r2, out, m2, s2)
+            saves.append((x, xp, qkv, probs, cx, r1, out1, m1, s1, f1, a, r2, m2, s2))
+            x = out
+        mean_pool = model.pooling_method != "sum"
+        ops.bst_pool(x, B, T, seq_len, mean_pool, row, col)
+        units, last = bst_units(model)
+        saved = deep_stack_forward(row, units, seed, slot)
+        hid = saved[-1][1] if saved else row
+        logit = torch.empty(B, 1, **f32)
+        prob = torch.empty(B, 1, **f32)
+        ops.mlp_forward(hid, [], ops.make_epilogue(head_w=last.weight, head_b=last.bias, head_logit=logit,
+                                                   head_prob=prob))
+        ctx.model, ctx.plan, ctx.units, ctx.seed, ctx.nsave = model, plan, units, seed, len(saves)
+        ctx.save_for_backward(row, prob, slot, *[t for sv in saves for t in sv], *[t for sv in saved for t in sv])
+        return prob, logit
+
+    @staticmethod
+    def backward(ctx, dprob, dlogit):
+        model, plan, units, seed = ctx.model, ctx.plan, ctx.units, ctx.seed
+        row, prob, slot, *flat = ctx.saved_tensors
+        nb = ctx.nsave
+        saves = [tuple(flat[14 * i:14 * i + 14]) for i in range(nb)]
+        flat = flat[14 * nb:]
+        saved = [tuple(flat[4 * u:4 * u + 4]) for u in range(len(units))]
+        seq, seq_len, B, T, col = plan["seq"], plan["seq_len"], plan["B"], plan["T"], plan["col"]
+        dev, d = row.device, model.d_model
+        M = B * T
+        f32 = dict(device=dev, dtype=torch.float32)
+        _, last = bst_units(model)
+        hid = saved[-1][1] if saved else row
+        dh = torch.empty_like(hid)
+        dw_last = torch.empty_like(last.weight)
+        db_last = torch.empty(1, **f32)
+        ops.logit_head_backward(_grad_out(dlogit, prob), _grad_out(dprob, prob), prob, hid, None, last.weight, dh,
+                                None, dw_last, db_last)
+        d_row, unit_grads = deep_stack_backward(dh, row, units, saved, seed, slot)
+        dx = torch.empty(M, d, **f32)
+        ops.bst_pool_backward(d_row, col, B, T, d, seq_len, model.pooling_method != "sum", dx)
+        tables, looks = plan["tables"], plan["looks"]
+        total = sum(w.numel() for w in tables)
+        gflat = torch.zeros(total, **f32)
+        tgrads, off = [], 0
+        for w in tables:
+            tgrads.append(gflat[off:off + w.numel()].view(w.shape))
+            off += w.numel()
+        block_grads = [None] * nb
+        pos_idx = plan["pos_idx"]
+        for i in range(nb - 1, -1, -1):
+            blk = model.transformer_blocks[i]
+            x, xp, qkv, probs, cx, r1, out1, m1, s1, f1, a, r2, m2, s2 = saves[i]
+            p_o, p_f = float(blk.dropout.p) if blk.training else 0.0, float(blk.ffn[2].p) if blk.training else 0.0
+            # out = LN2(out1 + dropout(f2))
+            d_out1 = torch.empty(M, d, **f32)
+            df2 = torch.empty(M, d, **f32)
+            dg2, dbe2 = torch.empty(d, **f32), torch.empty(d, **f32)
+            ops.bst_ln_backward(dx, r2, m2, s2, blk.norm2, p_o, bst_dropout_seed(seed, i, 2), slot, d_out1, df2, dg2,
+                                dbe2)
+            dW2, db2, da = _lin_grads(df2, a, blk.ffn[3].weight)
+            df1 = torch.empty(M, d, **f32)
+            ops.bst_leaky_dropout(da, f1, blk.ffn[1].negative_slope, p_f, bst_dropout_seed(seed, i, 1), slot, True, df1)
+            dW1, db1, _ = _lin_grads(df1, out1, blk.ffn[0].weight, dx=d_out1, accumulate=True)
+            # out1 = LN1(xp + dropout(o))
+            dxp = torch.empty(M, d, **f32)
+            do = torch.empty(M, d, **f32)
+            dg1, dbe1 = torch.empty(d, **f32), torch.empty(d, **f32)
+            ops.bst_ln_backward(d_out1, r1, m1, s1, blk.norm1, p_o, bst_dropout_seed(seed, i, 0), slot, dxp, do, dg1,
+                                dbe1)
+            dWo, dbo, dcx = _lin_grads(do, cx, blk.w_o.weight)
+            dqkv = torch.empty(M, 3 * d, **f32)
+            ops.bst_attn_train_backward(qkv, probs, dcx, B, T, d, blk.nhead, dqkv)
+            dQ, dK, dV = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
+            dWq, dbq, _ = _lin_grads(dQ, xp, blk.w_q.weight, dx=dxp, accumulate=True)
+            dWk, dbk, _ = _lin_grads(dK, xp, blk.w_k.weight, dx=dxp, accumulate=True)
+            # position embedding: every row m adds into pos[m % T]
+            gpos = torch.zeros_like(blk.position_embedding.weight)
+            ops.embedding_backward([ops.table_segment(gpos, pos_idx, 0)], M, dxp)
+            # keys/queries carry x + pos, values carry x: dL/dx = dL/dxp + dV Wv
+            dWv, dbv, _ = _lin_grads(dV, x, blk.w_v.weight, dx=dxp, accumulate=True)
+            block_grads[i] = [gpos, dWq, dbq, dWk, dbk, dWv, dbv, dWo, dbo, dg1, dbe1, dg2, dbe2, dW1, db1, dW2, db2]
+            dx = dxp
+        # embedding tables: the category lookups from the dnn input row, the behaviour sequence from dx
+        segs = [ops.table_segment(tgrads[k], idx, c) for k, idx, c in looks]
+        if segs:
+            ops.embedding_backward(segs, B, d_row)
+        ops.embedding_backward([ops.table_segment(tgrads[plan["feed_slot"]], seq.view(-1), 0)], M, dx)
+        flat_units = [t for g in unit_grads for t in g if t is not None]
+        return (None, None, *tgrads, *[t for g in block_grads for t in g], *flat_units, dw_last, db_last)
+
+
+def bst_train_forward(model, dense, category, seq, seq_len):
+    """BSTModel train-mode forward with autograd (rankops.BSTModel.forward in model.train())."""
+    B, T = seq.shape
+    d = model.d_model
+    for blk in model.transformer_blocks:
+        if T > 64 or d // blk.nhead > 64 or d % blk.nhead or d > 256:
+            raise NotImplementedError("rankops BST training: T <= 64, d_model <= 256, d_model / nhead <= 64")
+    segs = [ops.dense_segment(dense, model.num_dense_features, 0)]
+    col = model.num_dense_features
+    tables, looks = [], []
+
+    def slot_of(w):
+        for k, t in enumerate(tables):
+            if t is w:
+                return k
+        tables.append(w)
+        return len(tables) - 1
+
+    for name, emb in model.embeddings.items():
+        if name in category:
+            idx = ops.as_index(category[name], f"category[{name!r}]")
+            segs.append(ops.table_segment(emb.weight, idx, col))
+            looks.append((slot_of(emb.weight), idx, col))
+            col += emb.embedding_dim
+    feed_slot = slot_of(model.embeddings["feedid"].weight)
+    key = (B, T, seq.device)
+    if getattr(model, "_pos_idx_key", None) != key:  # row m -> position m % T, for the pos-table scatter
+        model._pos_idx = torch.arange(T, device=seq.device, dtype=torch.int64).repeat(B)
+        model._pos_idx_key = key
+    plan = dict(seq=seq, seq_len=seq_len, B=B, T=T, width=col + d, col=col, segs=segs, tables=tables, looks=looks,
+                feed_slot=feed_slot, pos_idx=model._pos_idx)
+    units, last = bst_units(model)
+    params = (tables + [t for blk in model.transformer_blocks for t in _block_params(blk)] + _unit_params(units)
+              + [last.weight, last.bias])
+    return _BSTTrain.apply(model, plan, *params)
 
 
 # ---------------------------------------------------------------- FwFM

@@ -47,6 +47,9 @@
  *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
+ *   rk_bst_add_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
+ *   rk_bst_ln_backward, rk_bst_leaky_dropout, rk_bst_pool / _backward
+ *                      BSTTransformer train forward (activations kept) and backward  bst.py:66-91,238-241
  *                      AFM train forward (activations kept) and backward  afm.py:92-119,173
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
  */
@@ -328,16 +331,17 @@ int rk_rng_next(int64_t* counter, int64_t* slot, void* stream);
 int rk_dropout_mask(uint64_t seed, const int64_t* stream_slot, int64_t batch, int32_t n,
                     double dropout_p, float* out, void* stream);
 
-/* y = Dropout_p(ReLU(BatchNorm1d_train(z + bias))) over [batch, n] (deepfm.py:101-108):
- * batch statistics (biased variance) in fp64, save_mean / save_invstd written, running_mean /
- * running_var updated with momentum and the unbiased variance (both may be NULL); batch_norm =
- * 0 skips the normalisation, relu = 0 the ReLU, dropout_p = 0 the dropout.  workspace: 2n
- * doubles.  gamma / beta may be NULL (affine = False).                                        */
+/* y = Dropout_p(act(BatchNorm1d_train(z + bias))) over [batch, n] (deepfm.py:101-108; BST's
+ * LeakyReLU units bst.py:207-211): batch statistics (biased variance) in fp64, save_mean /
+ * save_invstd written, running_mean / running_var updated with momentum and the unbiased variance
+ * (both may be NULL); batch_norm = 0 skips the normalisation, act = RK_ACT_NONE / RK_ACT_RELU /
+ * RK_ACT_LEAKY (negative slope `slope`), dropout_p = 0 the dropout.  workspace: 2n doubles.
+ * gamma / beta may be NULL (affine = False).                                                  */
 int rk_bn_act_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
                             int32_t batch_norm, const float* gamma, const float* beta, float eps,
                             float momentum, float* running_mean, float* running_var,
-                            double* workspace, float* save_mean, float* save_invstd, int32_t relu,
-                            double dropout_p, uint64_t seed, const int64_t* stream_slot, float* y,
+                            double* workspace, float* save_mean, float* save_invstd, int32_t act,
+                            float slope, double dropout_p, uint64_t seed, const int64_t* stream_slot, float* y,
                             int64_t ldy, void* stream);
 
 /* Backward of rk_bn_act_train_forward given dy: dz (gradient w.r.t. z, i.e. the Linear output
@@ -345,7 +349,8 @@ int rk_bn_act_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t 
 int rk_bn_act_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch,
                        int32_t n, const float* bias, int32_t batch_norm, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd,
-                       int32_t relu, double dropout_p, uint64_t seed, const int64_t* stream_slot,
+                       int32_t act, float slope, double dropout_p, uint64_t seed,
+                       const int64_t* stream_slot,
                        double* workspace, float* dz, int64_t lddz, float* dgamma, float* dbeta,
                        void* stream);
 
@@ -434,6 +439,42 @@ int rk_afm_pool_backward(const float* dpred, const float* dtotal, const float* p
                          int32_t dim, float* d_pairs, float* da1, float* acc, void* stream);
 int rk_afm_pair_fold(const float* d_pairs, const float* emb, int32_t num_fields, int32_t dim,
                      int64_t batch, float* d_emb, void* stream);
+
+/* BST training (bst.py:66-91, 238-241), rows = B*T of width d:
+ *   add_pos: xp[m] = x[m] + pos[m % T].
+ *   attn_train_forward: per (sample, head) P = softmax(mask(Q K^T / sqrt(dh))) saved to probs
+ *     [B, heads, T, T] and ctx = P V [rows, d]; qkv is [rows, 3d] = [Q | K | V].  T <= 64,
+ *     d / heads <= 64.  attn_train_backward: dqkv [rows, 3d] from dctx (overwritten).
+ *   res_dropout_ln_forward: r = base + Dropout_p(o) (saved), y = LayerNorm(r) (gamma, beta, eps),
+ *     mean / rstd [rows] saved.  d <= 256.
+ *   ln_backward: dr = LayerNorm backward of dy (overwritten), d_o = Dropout_p-masked dr (NULL:
+ *     skipped), dgamma / dbeta [d] (overwritten).
+ *   leaky_dropout: forward out = Dropout_p(LeakyReLU_slope(f)); backward (backward = 1)
+ *     out = in * keep * scale * (f > 0 ? 1 : slope).
+ *   pool: row[b, col:+d] = sum_t x[b*T + t] (/ seq_len[b] when mean); pool_backward broadcasts.
+ * Dropout masks: the counter hash of rk_dropout_mask with index m * d + k.                      */
+int rk_bst_add_pos(const float* x, const float* pos, int32_t T, int64_t rows, int32_t d, float* xp,
+                   void* stream);
+int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_t d, int32_t heads,
+                              const int64_t* seq_len, float* probs, float* ctx, void* stream);
+int rk_bst_attn_train_backward(const float* qkv, const float* probs, const float* dctx,
+                               int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
+                               void* stream);
+int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,
+                                  double dropout_p, uint64_t seed, const int64_t* stream_slot,
+                                  const float* gamma, const float* beta, float eps, float* r, float* y,
+                                  float* mean, float* rstd, void* stream);
+int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
+                       const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
+                       const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
+                       void* stream);
+int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, float slope, double dropout_p,
+                         uint64_t seed, const int64_t* stream_slot, int32_t backward, float* out,
+                         void* stream);
+int rk_bst_pool(const float* x, int64_t batch, int32_t T, int32_t d, const int64_t* seq_len,
+                int32_t mean, float* row, int64_t ld_row, int32_t col, void* stream);
+int rk_bst_pool_backward(const float* drow, int64_t ld_row, int32_t col, int64_t batch, int32_t T,
+                         int32_t d, const int64_t* seq_len, int32_t mean, float* dx, void* stream);
 
 typedef struct rk_adam_tensor {
   float* param;

@@ -346,6 +346,67 @@ def bst_block(p, prefix, queries, keys, values, nhead, key_padding_mask=None, ep
     return F.layer_norm(out1 + ffn, (d_model,), p[prefix + "norm2.weight"], p[prefix + "norm2.bias"], eps)
 
 
+def bst_block_train(p, prefix, queries, keys, values, nhead, key_padding_mask=None, masks=None, eps=1e-5):
+    """BSTTransformer.forward in model.train() (bst.py:66-91): the three Dropout sites as given
+    multiplier masks [B*T, d] (w_o output, inside the FFN, FFN output), or identity when None."""
+    batch_size, seq_len, d_model = queries.size()
+
+    def drop(t, k):
+        if masks is None or masks[k] is None:
+            return t
+        return t * masks[k].view(batch_size, seq_len, d_model)
+
+    pos_indices = torch.arange(seq_len).expand(batch_size, -1)
+    pos = F.embedding(pos_indices, p[prefix + "position_embedding.weight"])
+    queries = queries + pos
+    keys = keys + pos
+    q = _lin(queries, p, prefix + "w_q.").view(batch_size, seq_len, nhead, -1).transpose(1, 2)
+    k = _lin(keys, p, prefix + "w_k.").view(batch_size, seq_len, nhead, -1).transpose(1, 2)
+    v = _lin(values, p, prefix + "w_v.").view(batch_size, seq_len, nhead, -1).transpose(1, 2)
+    scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(q.size(-1))
+    if key_padding_mask is not None:
+        scores = scores.masked_fill(key_padding_mask.unsqueeze(1).unsqueeze(2), float("-inf"))
+    attn = F.softmax(scores, dim=-1)
+    context = torch.matmul(attn, v).transpose(1, 2).contiguous().view(batch_size, seq_len, -1)
+    out1 = F.layer_norm(queries + drop(_lin(context, p, prefix + "w_o."), 0), (d_model,), p[prefix + "norm1.weight"],
+                        p[prefix + "norm1.bias"], eps)
+    ffn = _lin(drop(F.leaky_relu(_lin(out1, p, prefix + "ffn.0."), 0.01), 1), p, prefix + "ffn.3.")
+    return F.layer_norm(out1 + drop(ffn, 2), (d_model,), p[prefix + "norm2.weight"], p[prefix + "norm2.bias"], eps)
+
+
+def bst_forward_train(p, dense, category, seq_feedid, seq_length, nhead=4, num_blocks=1, num_hidden=3,
+                      batch_norm=True, dropout_rate=0.1, pooling_method="sum", block_masks=None, dnn_masks=None,
+                      momentum=0.1, eps=1e-5):
+    """BSTModel.forward in model.train() (bst.py:216-247): BatchNorm1d with batch statistics (running
+    statistics in `p` updated), Dropout as the given multiplier masks; differentiable w.r.t. `p`."""
+    category_emb = torch.cat(_cat_fields(p, category, DCN_FIELDS + ["feedid"]), dim=1)
+    seq_emb = F.embedding(seq_feedid, p["embeddings.feedid.weight"])
+    max_len = seq_feedid.size(1)
+    mask = torch.arange(max_len).expand(len(seq_length), max_len) >= seq_length.unsqueeze(1)
+    out = seq_emb
+    for i in range(num_blocks):
+        out = bst_block_train(p, f"transformer_blocks.{i}.", out, out, out, nhead, mask,
+                              block_masks[i] if block_masks is not None else None)
+    if pooling_method == "sum":
+        out = torch.sum(out, dim=1)
+    else:
+        out = torch.sum(out, dim=1) / seq_length.unsqueeze(1).float()
+    h = torch.cat([dense, category_emb, out], dim=1)
+    layout, last = bst_dnn_layout(num_hidden, batch_norm, dropout_rate)
+    for u, (lin, bn) in enumerate(layout):
+        h = _lin(h, p, f"dnn.{lin}.")
+        if bn is not None:
+            pre = f"dnn.{bn}."
+            h = F.batch_norm(h, p[pre + "running_mean"], p[pre + "running_var"], p[pre + "weight"], p[pre + "bias"],
+                             training=True, momentum=momentum, eps=eps)
+            p[pre + "num_batches_tracked"] += 1
+        h = F.leaky_relu(h, 0.01)
+        if dnn_masks is not None and dnn_masks[u] is not None:
+            h = h * dnn_masks[u]
+    logits = _lin(h, p, f"dnn.{last}.")
+    return torch.sigmoid(logits), logits
+
+
 def bst_dnn_layout(num_hidden, batch_norm=True, dropout_rate=0.1):
     """Module indices of dnn (bst.py:203-213): Linear, [BN], LeakyReLU, [Dropout]; last Linear."""
     idx, out = 0, []

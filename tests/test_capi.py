@@ -105,8 +105,10 @@ def test_python_layer_refuses_cpu_tensors():
         H.call_model(m, "dcn", inp)
     with pytest.raises(RuntimeError, match="ROCm GPU"):  # DCN trains on the engine, still GPU-only
         H.call_model(m.train(), "dcn", inp)
-    bst = H.build("bst", {"T": 8}).train()  # no training path yet: refused, never a silent eager fallback
-    with pytest.raises(NotImplementedError):
+    bst = H.build("bst", {"T": 8}).train()  # train mode without autograd: refused, never a silent fallback
+    with torch.no_grad(), pytest.raises(NotImplementedError):
+        H.call_model(bst, "bst", H.make_inputs("bst", {"T": 8}, 4))
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # BST trains on the engine: GPU-only
         H.call_model(bst, "bst", H.make_inputs("bst", {"T": 8}, 4))
     afm = H.build("afm", {}).train()  # trains on the engine: GPU-only like the forward
     with pytest.raises(RuntimeError, match="ROCm GPU"):

@@ -195,11 +195,11 @@ def test_cpu_inputs_raise():
 
 @pytest.mark.gpu
 def test_training_mode_raises():
-    """Models whose backward is not built yet refuse a train-mode forward instead of silently
-    running eval semantics (DCN, DeepCrossing and DeepFM train: tests/test_gpu_train.py)."""
+    """A train-mode forward without autograd (no backward to attach) is refused instead of
+    silently running eval semantics; with autograd every model trains (tests/test_gpu_train.py)."""
     model = H.build("bst", {"T": 20}).cuda().train()
     inp = H.to_device(H.make_inputs("bst", {"T": 20}, 8), "cuda")
-    with pytest.raises(NotImplementedError):
+    with torch.no_grad(), pytest.raises(NotImplementedError):
         H.call_model(model, "bst", inp)
 
 

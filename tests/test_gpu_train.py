@@ -622,6 +622,93 @@ def test_afm_train_steps_match_autograd(cfg):
     _afm_step_check(cfg, 1024, seed=2500, steps=2)
 
 
+def _bst_masks(model, B, T):
+    from rankops import train as rt
+    seed, slot = model._dropout.seed, model._dropout.counter - 1
+    units, _ = rt.bst_units(model)
+    dnn = [ops.dropout_mask(seed + u, slot, B, un[0].out_features, un[3]).cpu() if un[3] > 0 else None
+           for u, un in enumerate(units)]
+    blocks = []
+    for i, blk in enumerate(model.transformer_blocks):
+        ps = (blk.dropout.p, blk.ffn[2].p, blk.dropout.p)
+        blocks.append([ops.dropout_mask(rt.bst_dropout_seed(seed, i, k), slot, B * T, model.d_model, ps[k]).cpu()
+                       if ps[k] > 0 else None for k in range(3)])
+    return blocks, dnn
+
+
+def _bst_step_check(cfg, B, seed, steps):
+    """BST train steps (bst.py:266-289: forward, BCELoss(prob), backward, Adam) against the oracle's
+    train-mode BSTModel.forward (blocks and dnn with the engine's dropout masks) differentiated by
+    autograd."""
+    model = H.build("bst", cfg).cuda().train()
+    T = cfg.get("T", 50)
+    inp = H.make_inputs("bst", cfg, B, seed=seed)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed)) < 0.3).float()
+    params = dict(model.named_parameters())
+    p = {k: (v.detach().cpu().clone().requires_grad_(True) if k in params else v.detach().cpu().clone())
+         for k, v in model.state_dict().items()}
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    ref_opt = torch.optim.Adam([p[n] for n in params], lr=1e-3)
+    crit = torch.nn.BCELoss()
+    dinp = H.to_device(inp, "cuda")
+    hidden = len(cfg.get("hidden", [512, 256, 128]))
+    bn_fed = {f"dnn.{i}.bias" for i, m in enumerate(model.dnn)
+              if isinstance(m, torch.nn.Linear) and i + 1 < len(model.dnn)
+              and isinstance(model.dnn[i + 1], torch.nn.BatchNorm1d)}
+    for step in range(steps):
+        opt.zero_grad()
+        ref_opt.zero_grad()
+        out = H.call_model(model, "bst", dinp)
+        crit(out[0].squeeze(), label.cuda()).backward()
+        bm, dm = _bst_masks(model, B, T)
+        r = ref.bst_forward_train(p, inp["dense"], inp["category"], inp["seq_feedid"], inp["seq_length"],
+                                  cfg.get("heads", 4), cfg.get("blocks", 1), hidden, cfg.get("batch_norm", True), 0.1,
+                                  cfg.get("pooling", "sum"), bm, dm)
+        crit(r[0].squeeze(), label).backward()
+        for i, (o, w) in enumerate(zip(out, r)):
+            torch.testing.assert_close(o.detach().cpu(), w.detach(), rtol=1e-4, atol=1e-4,
+                                       msg=lambda m: f"output {i} step {step}: {m}")
+        for k, v in model.state_dict().items():
+            if k not in params and (step == 0 or not k.endswith("running_mean")):
+                torch.testing.assert_close(v.cpu(), p[k], rtol=1e-4, atol=1e-5, msg=lambda m: f"buffer {k}: {m}")
+        for n, prm in params.items():
+            want = p[n].grad
+            if want is None:
+                assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, n
+                continue
+            scale = max(1e-3, float(want.abs().max()))  # floor: null-space parameters hold only noise
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=1e-3 * scale,
+                                       msg=lambda m: f"grad {n} step {step}: {m}")
+        opt.step()
+        ref_opt.step()
+        for n, prm in params.items():
+            # zero true gradients, rounding noise on both sides (Adam turns it into +-lr steps): a
+            # Linear bias feeding BatchNorm; w_k's bias (q.(k + b) shifts every key's score of a
+            # query by the same q.b, which the softmax removes); with sum pooling over a fixed T the
+            # last block's norm2.bias adds the same T * beta to every sample, which the dnn's first
+            # BatchNorm removes — caught generically as a numerically-zero oracle gradient
+            if (n in bn_fed or n.endswith("w_k.bias") or p[n].grad is None
+                    or float(p[n].grad.abs().max()) < 1e-6):
+                continue
+            _assert_adam_params_close(prm.detach().cpu(), p[n].detach(), lr=1e-3, steps=1,
+                                      what=f"param {n} after step {step}")
+        with torch.no_grad():
+            for k, v in model.state_dict().items():
+                p[k].copy_(v.cpu())
+            for n, prm in params.items():
+                if prm in opt.state and p[n] in ref_opt.state:
+                    for key in ("exp_avg", "exp_avg_sq"):
+                        ref_opt.state[p[n]][key].copy_(opt.state[prm][key].cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{"T": 20}, {"T": 20, "dim": 32, "blocks": 2, "pooling": "mean"},
+                                 {"T": 64, "dim": 128, "max_len": 64, "vocab": H.WECHAT_VOCAB}],
+                         ids=["reference", "two_blocks_mean", "bench_shape"])
+def test_bst_train_steps_match_autograd(cfg):
+    _bst_step_check(cfg, 256, seed=2600, steps=2)
+
+
 @pytest.mark.gpu
 def test_dropout_mask_rate_and_freshness():
     counter = torch.zeros(1, dtype=torch.int64, device="cuda")
