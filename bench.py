@@ -387,18 +387,27 @@ def bench_metrics(batch, batches=256):
 
 def bench_train(batch, steps, warmup, name="dcn"):
     """Training step (§8(f) #2) at `batch`, wechat tables: zero_grad, forward, the script's loss
-    (DCN BCEWithLogits on the logit, DeepFM BCE on the probability, DIN BCE + l2_reg), loss.backward()
-    (HIP backward kernels), Adam step — the reference's train() loop body (dcn.py:195-201,
-    deepfm.py:166-171, din.py:339-347) with the per-call H2 draws frozen; inputs in HBM.  Timed eagerly
+    (DCN / DeepCrossing / BST BCEWithLogits on the logit, DIN BCE + l2_reg, the others BCE on the
+    probability),
+    loss.backward() (HIP backward kernels), Adam step — the reference's train() loop body
+    (dcn.py:195-201, deepfm.py:166-171, din.py:339-347, afm.py:168-176, bst.py:276-284,
+    fwfm.py:150-157) with the per-call H2 draws frozen; inputs in HBM.  Timed eagerly
     (rankops.Adam) and as one captured hipGraph per step (rankops.Adam(capturable=True))."""
     import helpers as H
     import rankops
     cfg = {"dcn": {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"},
+           "deepcrossing": {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"},
            "deepfm": {"vocab": H.WECHAT_VOCAB},
-           "din": {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32, "interaction_weights": "frozen"}}[name]
+           "din": {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32, "interaction_weights": "frozen"},
+           "afm": {"vocab": H.WECHAT_VOCAB, "dim": 8, "att": 128},
+           "bst": {"vocab": H.WECHAT_VOCAB, "T": 64, "dim": 128, "heads": 4, "max_len": 64},
+           "fwfm": {"vocab": H.WECHAT_VOCAB, "dim": 8}}[name]
     inp = None
-    res = {"model": {"dcn": "DCN", "deepfm": "DeepFM", "din": "DIN"}[name], "batch": batch}
-    crit = torch.nn.BCEWithLogitsLoss() if name == "dcn" else torch.nn.BCELoss()
+    res = {"model": {"dcn": "DCN", "deepcrossing": "DeepCrossing", "deepfm": "DeepFM", "din": "DIN", "afm": "AFM",
+                     "bst": "BST", "fwfm": "FwFM"}[name], "batch": batch, "config": {k: v for k, v in cfg.items()
+                                                                                   if k != "vocab"}}
+    on_logit = name in ("dcn", "deepcrossing", "bst")  # BCEWithLogitsLoss (dcn.py:274, deepcrossing.py:256, bst.py:351)
+    crit = torch.nn.BCEWithLogitsLoss() if on_logit else torch.nn.BCELoss()
     for mode in ("eager", "graph"):
         torch.manual_seed(0)
         model = H.build(name, cfg).cuda().train()
@@ -409,8 +418,8 @@ def bench_train(batch, steps, warmup, name="dcn"):
 
         def step():
             opt.zero_grad(set_to_none=True)
-            out = H.call_model(model, name, inp)
-            loss = crit(out[1].squeeze(), label) if name == "dcn" else crit(out[0].squeeze(), label)
+            out = H.as_tuple(H.call_model(model, name, inp))
+            loss = crit(out[1].squeeze(), label) if on_logit else crit(out[0].squeeze(), label)
             if name == "din":  # ce_loss + l2_reg (din.py:343-344)
                 loss = loss + out[2]
             loss.backward()
@@ -555,8 +564,8 @@ def main():
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_extras:
         try:
-            result["train"] = {m: bench_train(args.batch, max(10, args.steps // 2), 3, m)
-                               for m in ("dcn", "deepfm", "din")}
+            result["train"] = {m: bench_train(2048 if m == "bst" else args.batch, max(10, args.steps // 2), 3, m)
+                               for m in ("dcn", "deepcrossing", "deepfm", "din", "afm", "bst", "fwfm")}
         except Exception as exc:  # reported, never fatal for the headline line
             result["train"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_loader:

@@ -35,13 +35,14 @@ __device__ __forceinline__ void bst_stage(float* __restrict__ dst, const float* 
   }
 }
 
-// Workgroup per (sample, head).  Wave w handles query rows w, w+4, ...; lane j = key position.
+// Workgroup per (sample, head).  Phase 1: wave w computes the probability rows w, w+4, ... (lane =
+// key position) into LDS and HBM; phase 2: ctx = P V with lane = (row in a group of 64/dh rows,
+// column), so every lane is busy at dh = 32.
 __global__ __launch_bounds__(256) void bst_attn_train_fwd_kernel(const float* __restrict__ qkv, int64_t B, int T,
                                                                  int d, int heads,
                                                                  const int64_t* __restrict__ seq_len,
                                                                  float* __restrict__ P, float* __restrict__ ctx) {
-  __shared__ float sQ[kBstTMax * kBstLd], sK[kBstTMax * kBstLd], sV[kBstTMax * kBstLd];
-  __shared__ float sP[4][kBstTMax];
+  __shared__ float sQ[kBstTMax * kBstLd], sK[kBstTMax * kBstLd], sV[kBstTMax * kBstLd], sP[kBstTMax * kBstLd];
   const int64_t b = blockIdx.x / heads;
   const int h = (int)(blockIdx.x - b * heads);
   const int dh = d / heads;
@@ -67,16 +68,18 @@ __global__ __launch_bounds__(256) void bst_attn_train_fwd_kernel(const float* __
     const float p = e / sum;
     if (lane < T) {
       Pb[(int64_t)i * T + lane] = p;
-      sP[wv][lane] = p;
+      sP[i * kBstLd + lane] = p;
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    if (lane < dh) {
+  }
+  __syncthreads();
+  const int R = 64 / dh, rr = lane / dh, k = lane - rr * dh;
+  for (int i0 = wv * R; i0 < T; i0 += 4 * R) {
+    const int i = i0 + rr;
+    if (rr < R && i < T) {
       float c = 0.f;
-      for (int j = 0; j < T; ++j) c = fmaf(sP[wv][j], sV[j * kBstLd + lane], c);
-      ctx[(row0 + i) * d + h * dh + lane] = c;
+      for (int j = 0; j < T; ++j) c = fmaf(sP[i * kBstLd + j], sV[j * kBstLd + k], c);
+      ctx[(row0 + i) * d + h * dh + k] = c;
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -111,15 +114,18 @@ __global__ __launch_bounds__(256) void bst_attn_train_bwd_kernel(const float* __
     if (lane < T) sS[i * kBstLd + lane] = p * (dp - D) / sq;
   }
   __syncthreads();
-  for (int i = wv; i < T; i += 4) {
-    if (lane < dh) {
+  // lane = (row in a group of 64/dh rows, column): every lane busy at dh = 32
+  const int R = 64 / dh, rr = lane / dh, c = lane - rr * dh;
+  for (int i0 = wv * R; i0 < T; i0 += 4 * R) {
+    const int i = i0 + rr;
+    if (rr < R && i < T) {
       float q = 0.f, kk = 0.f, v = 0.f;
       for (int j = 0; j < T; ++j) {
-        q = fmaf(sS[i * kBstLd + j], sK[j * kBstLd + lane], q);   // dQ[i] = sum_j dS[i, j] K[j]
-        kk = fmaf(sS[j * kBstLd + i], sQ[j * kBstLd + lane], kk);  // dK[i] = sum_j dS[j, i] Q[j]
-        v = fmaf(sP[j * kBstLd + i], sC[j * kBstLd + lane], v);    // dV[i] = sum_j P[j, i] dC[j]
+        q = fmaf(sS[i * kBstLd + j], sK[j * kBstLd + c], q);   // dQ[i] = sum_j dS[i, j] K[j]
+        kk = fmaf(sS[j * kBstLd + i], sQ[j * kBstLd + c], kk);  // dK[i] = sum_j dS[j, i] Q[j]
+        v = fmaf(sP[j * kBstLd + i], sC[j * kBstLd + c], v);    // dV[i] = sum_j P[j, i] dC[j]
       }
-      float* o = dqkv + (row0 + i) * ld + h * dh + lane;
+      float* o = dqkv + (row0 + i) * ld + h * dh + c;
       o[0] = q;
       o[d] = kk;
       o[2 * d] = v;
@@ -168,24 +174,28 @@ __global__ __launch_bounds__(256) void bst_res_dropout_ln_fwd_kernel(
   }
 }
 
-// LayerNorm backward (one wave per row) from dy: dr = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma;
-// d_o = dropout-masked dr (the residual branch's gradient); dgamma += dy xhat, dbeta += dy (LDS partials).
+// LayerNorm backward from dy: dr = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma; d_o =
+// dropout-masked dr (the residual branch's gradient).  Waves walk rows grid-stride; each lane keeps
+// its columns' dgamma = sum dy xhat and dbeta = sum dy in registers, the workgroup combines them
+// in LDS and writes one partial row per workgroup to ws [kLnBlocks][2d], summed in block order by
+// bst_ln_param_kernel (deterministic; per-row atomics on the same 2d addresses serialised).
+constexpr int kLnBlocks = 512;
+
 __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ r,
                                                          const float* __restrict__ mean_in,
                                                          const float* __restrict__ rstd_in,
                                                          const float* __restrict__ gamma, int64_t M, int d,
                                                          uint64_t seed, const int64_t* __restrict__ stream_slot,
                                                          uint32_t threshold, float scale, float* __restrict__ dr,
-                                                         float* __restrict__ d_o, float* __restrict__ dgamma,
-                                                         float* __restrict__ dbeta) {
-  __shared__ float red[2][256];
-  for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) red[i / 256][i % 256] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (m < M) {
+                                                         float* __restrict__ d_o, float* __restrict__ ws) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, gm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) gm[c] = lane + 64 * c < d ? gamma[lane + 64 * c] : 0.f;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wv; m < M; m += (int64_t)gridDim.x * 4) {
     const float mean = mean_in[m], rstd = rstd_in[m];
-    const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
     float g[4], xh[4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -195,11 +205,11 @@ __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict
       if (k < d) {
         const float dyv = dy[m * d + k];
         xh[c] = (r[m * d + k] - mean) * rstd;
-        g[c] = dyv * gamma[k];
+        g[c] = dyv * gm[c];
         s1 += g[c];
         s2 += g[c] * xh[c];
-        atomicAdd(&red[0][k], dyv * xh[c]);
-        atomicAdd(&red[1][k], dyv);
+        pg[c] = fmaf(dyv, xh[c], pg[c]);
+        pb[c] += dyv;
       }
     }
     const float k1 = wave_sum(s1) / (float)d, k2 = wave_sum(s2) / (float)d;
@@ -215,11 +225,53 @@ __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict
       }
     }
   }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    red[wv][0][lane + 64 * c] = pg[c];
+    red[wv][1][lane + 64 * c] = pb[c];
+  }
   __syncthreads();
   for (int k = threadIdx.x; k < d; k += blockDim.x) {
-    atomicAdd(dgamma + k, red[0][k]);
-    atomicAdd(dbeta + k, red[1][k]);
+    ws[(int64_t)blockIdx.x * 2 * d + k] = red[0][0][k] + red[1][0][k] + red[2][0][k] + red[3][0][k];
+    ws[(int64_t)blockIdx.x * 2 * d + d + k] = red[0][1][k] + red[1][1][k] + red[2][1][k] + red[3][1][k];
   }
+}
+
+// 16 waves per workgroup, each summing every 16th block partial of 64 columns; LDS combine.
+__global__ __launch_bounds__(1024) void bst_ln_param_kernel(const float* __restrict__ ws, int nblocks, int d,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (k < 2 * d)
+    for (int blk = wv; blk < nblocks; blk += 16) s += ws[(int64_t)blk * 2 * d + k];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && k < 2 * d) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    if (k < d)
+      dgamma[k] = t;
+    else
+      dbeta[k - d] = t;
+  }
+}
+
+// Position-embedding gradient: dpos[t, k] += sum over a chunk of samples of dxp[b*T + t, k] (rows
+// t < T; the caller zeroes dpos).  grid.y splits the batch into kPosChunks chunks (one float
+// atomic per chunk and element).
+constexpr int kPosChunks = 64;
+
+__global__ __launch_bounds__(256) void bst_pos_grad_kernel(const float* __restrict__ dxp, int64_t B, int T, int d,
+                                                           float* __restrict__ dpos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T * d) return;
+  const int64_t per = (B + gridDim.y - 1) / gridDim.y;
+  const int64_t b0 = blockIdx.y * per, b1 = min<int64_t>(B, b0 + per);
+  float s = 0.f;
+  for (int64_t b = b0; b < b1; ++b) s += dxp[b * T * d + i];
+  atomicAdd(dpos + i, s);
 }
 
 // a = dropout(leaky(f)) forward; backward df = da * keep * scale * (f > 0 ? 1 : slope).
@@ -322,19 +374,26 @@ RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int6
 RK_API int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
                               const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
                               const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
-                              void* stream) {
-  if (!dy || !r || !mean || !rstd || !gamma || !dr || !dgamma || !dbeta || rows < 0 || d <= 0 || d > 256 ||
-      !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
-    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: bad arguments (d <= 256)");
+                              float* workspace, void* stream) {
+  if (!dy || !r || !mean || !rstd || !gamma || !dr || !dgamma || !dbeta || !workspace || rows < 0 || d <= 0 ||
+      d > 256 || !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
+    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: bad arguments (d <= 256, workspace of %d * 2d floats)",
+                kLnBlocks);
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(dgamma, 0, (size_t)d * sizeof(float), st) != hipSuccess ||
-      hipMemsetAsync(dbeta, 0, (size_t)d * sizeof(float), st) != hipSuccess)
-    return fail(RK_ERR_RUNTIME, "rk_bst_ln_backward: memset failed");
-  if (rows == 0) return RK_OK;
-  bst_ln_bwd_kernel<<<grid_of(rows, 4), 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot,
-                                                      dropout_threshold(dropout_p), (float)(1.0 / (1.0 - dropout_p)),
-                                                      dr, d_o, dgamma, dbeta);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (rows + 3) / 4));
+  bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot,
+                                            dropout_threshold(dropout_p), (float)(1.0 / (1.0 - dropout_p)), dr, d_o,
+                                            workspace);
+  bst_ln_param_kernel<<<grid_of(2 * d, 64), 1024, 0, st>>>(workspace, blocks, d, dgamma, dbeta);
   return check_launch("rk_bst_ln_backward");
+}
+
+RK_API int rk_bst_pos_backward(const float* dxp, int64_t batch, int32_t T, int32_t d, float* dpos, void* stream) {
+  if (!dxp || !dpos || batch < 0 || T <= 0 || d <= 0) return fail(RK_ERR_INVALID, "rk_bst_pos_backward: bad arguments");
+  if (batch == 0) return RK_OK;
+  const dim3 grid(grid_of((int64_t)T * d), (unsigned)std::min<int64_t>(kPosChunks, batch));
+  bst_pos_grad_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(dxp, batch, T, d, dpos);
+  return check_launch("rk_bst_pos_backward");
 }
 
 RK_API int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, float slope, double dropout_p,

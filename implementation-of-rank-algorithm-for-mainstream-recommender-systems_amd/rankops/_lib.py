@@ -215,13 +215,17 @@ SIGNATURES = {
                                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_bst_ln_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                           ctypes.c_double, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                          c_void_p, c_void_p]),
+                                          c_void_p, c_void_p, c_void_p]),
+    "rk_bst_pos_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_bst_leaky_dropout": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, ctypes.c_double, ctypes.c_uint64,
                                             c_void_p, c_int32, c_void_p, c_void_p]),
     "rk_bst_pool": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_int64, c_int32,
                                    c_void_p]),
     "rk_bst_pool_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int64, c_int32, c_int32, c_void_p, c_int32,
                                             c_void_p, c_void_p]),
+    "rk_embedding_backward_sorted_workspace_size": (ctypes.c_int, [c_int64, POINTER(c_int64)]),
+    "rk_embedding_backward_sorted": (ctypes.c_int, [POINTER(Segment), c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                                    c_void_p]),
     "rk_relu_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "rk_dcn_cross_backward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
                                              c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p]),

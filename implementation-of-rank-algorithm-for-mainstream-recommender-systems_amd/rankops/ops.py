@@ -348,6 +348,17 @@ def embedding_backward(grad_segs, batch, dx):
                                     _lib.stream_of(dx)), "rk_embedding_backward")
 
 
+def embedding_backward_sorted(grad_seg, n, dx):
+    """rk_embedding_backward_sorted: one table segment over n index entries (sorted segment-reduce)."""
+    lib = _lib.load()
+    nbytes = ctypes.c_int64()
+    check(lib.rk_embedding_backward_sorted_workspace_size(n, ctypes.byref(nbytes)),
+          "rk_embedding_backward_sorted_workspace_size")
+    ws = torch.empty(max(1, nbytes.value), device=dx.device, dtype=torch.uint8)
+    check(lib.rk_embedding_backward_sorted(ctypes.byref(grad_seg), n, ptr(dx), dx.stride(0), ptr(ws), nbytes.value,
+                                           _lib.stream_of(dx)), "rk_embedding_backward_sorted")
+
+
 def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, stream):
     """entries: list of (param, grad, exp_avg, exp_avg_sq[, device step tensor]) float32 tensors."""
     lib = _lib.load()
@@ -514,11 +525,21 @@ def bst_res_dropout_ln_forward(base, o, p, seed, slot, ln, r, y, mean, rstd):
           "rk_bst_res_dropout_ln_forward")
 
 
+BST_LN_WORKSPACE = 1024  # floats per model column (rk_bst_ln_backward)
+
+
 def bst_ln_backward(dy, r, mean, rstd, ln, p, seed, slot, dr, d_o, dgamma, dbeta):
     lib = _lib.load()
+    ws = torch.empty(BST_LN_WORKSPACE * r.shape[1], device=r.device, dtype=torch.float32)
     check(lib.rk_bst_ln_backward(ptr(dy), ptr(r), ptr(mean), ptr(rstd), ptr(ln.weight), r.shape[0], r.shape[1],
-                                 float(p), seed, ptr(slot), ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta),
+                                 float(p), seed, ptr(slot), ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta), ptr(ws),
                                  _lib.stream_of(dy)), "rk_bst_ln_backward")
+
+
+def bst_pos_backward(dxp, B, T, dpos):
+    lib = _lib.load()
+    check(lib.rk_bst_pos_backward(ptr(dxp), B, T, dxp.shape[1], ptr(dpos), _lib.stream_of(dxp)),
+          "rk_bst_pos_backward")
 
 
 def bst_leaky_dropout(inp, f, slope, p, seed, slot, backward, out):

@@ -13,10 +13,13 @@ parameter gradients back to autograd — so `loss.backward()` fills every `.grad
 reference does and the unchanged loop works with `torch.optim.Adam` or with `rankops.Adam`
 (the same update as one fused launch over all tensors, `rk_adam_step`).
 
-Models with training support (no BatchNorm / Dropout in them, so their train and eval forwards
-coincide): DCNModel (`dcn.py:114-180`: embeddings, cross stack, ReLU MLP, output_layer +
-sigmoid) and DeepCrossingModel (`deepcrossing.py:106-163`: embeddings, residual units,
-output_layer + sigmoid).
+Every model trains: DCNModel (`dcn.py:114-180`), DeepCrossingModel (`deepcrossing.py:106-163`)
+and AFM (`afm.py:64-119`) — no BatchNorm / Dropout, train and eval forwards coincide —, DeepFM
+(`deepfm.py:73-151`: BatchNorm batch statistics, Dropout), DIN (`din.py:225-323`: Dice and
+BatchNorm batch statistics, Dropout, attention backward, l2 term), BSTModel (`bst.py:42-247`:
+Dropout inside the transformer blocks, LayerNorm, attention backward) and FwFM (`fwfm.py:87-139`).
+Dropout masks are a counter hash on the device (train_common.h): a random choice like torch's own
+masks, so parity tests hand the engine's masks to the oracle.
 """
 from __future__ import annotations
 
@@ -577,8 +580,9 @@ class _DINTrain(torch.autograd.Function):
             off += w.numel()
         segs = [ops.table_segment(grads[k], i, col) for k, i, col in looks]
         ops.embedding_backward(segs, B, dxr)
-        ops.embedding_backward([ops.table_segment(grads[pl["seq_slot"]], pl["seq"].reshape(-1), 0)], M,
-                               dkeys.view(M, H))
+        # the padded history positions all map to row 0: sorted segment-reduce instead of atomics
+        ops.embedding_backward_sorted(ops.table_segment(grads[pl["seq_slot"]], pl["seq"].reshape(-1), 0), M,
+                                      dkeys.view(M, H))
         flat = [t for g in unit_grads for t in g]
         return (None, None, None, None, *grads, *flat, dw_out, db_out)
 
@@ -827,7 +831,6 @@ class _BSTTrain(torch.autograd.Function):
             tgrads.append(gflat[off:off + w.numel()].view(w.shape))
             off += w.numel()
         block_grads = [None] * nb
-        pos_idx = plan["pos_idx"]
         for i in range(nb - 1, -1, -1):
             blk = model.transformer_blocks[i]
             x, xp, qkv, probs, cx, r1, out1, m1, s1, f1, a, r2, m2, s2 = saves[i]
@@ -856,7 +859,7 @@ class _BSTTrain(torch.autograd.Function):
             dWk, dbk, _ = _lin_grads(dK, xp, blk.w_k.weight, dx=dxp, accumulate=True)
             # position embedding: every row m adds into pos[m % T]
             gpos = torch.zeros_like(blk.position_embedding.weight)
-            ops.embedding_backward([ops.table_segment(gpos, pos_idx, 0)], M, dxp)
+            ops.bst_pos_backward(dxp, B, T, gpos)
             # keys/queries carry x + pos, values carry x: dL/dx = dL/dxp + dV Wv
             dWv, dbv, _ = _lin_grads(dV, x, blk.w_v.weight, dx=dxp, accumulate=True)
             block_grads[i] = [gpos, dWq, dbq, dWk, dbk, dWv, dbv, dWo, dbo, dg1, dbe1, dg2, dbe2, dW1, db1, dW2, db2]
@@ -865,7 +868,8 @@ class _BSTTrain(torch.autograd.Function):
         segs = [ops.table_segment(tgrads[k], idx, c) for k, idx, c in looks]
         if segs:
             ops.embedding_backward(segs, B, d_row)
-        ops.embedding_backward([ops.table_segment(tgrads[plan["feed_slot"]], seq.view(-1), 0)], M, dx)
+        # padded positions all map to row 0 and carry non-zero gradients: sorted segment-reduce
+        ops.embedding_backward_sorted(ops.table_segment(tgrads[plan["feed_slot"]], seq.view(-1), 0), M, dx)
         flat_units = [t for g in unit_grads for t in g if t is not None]
         return (None, None, *tgrads, *[t for g in block_grads for t in g], *flat_units, dw_last, db_last)
 
@@ -895,12 +899,8 @@ def bst_train_forward(model, dense, category, seq, seq_len):
             looks.append((slot_of(emb.weight), idx, col))
             col += emb.embedding_dim
     feed_slot = slot_of(model.embeddings["feedid"].weight)
-    key = (B, T, seq.device)
-    if getattr(model, "_pos_idx_key", None) != key:  # row m -> position m % T, for the pos-table scatter
-        model._pos_idx = torch.arange(T, device=seq.device, dtype=torch.int64).repeat(B)
-        model._pos_idx_key = key
     plan = dict(seq=seq, seq_len=seq_len, B=B, T=T, width=col + d, col=col, segs=segs, tables=tables, looks=looks,
-                feed_slot=feed_slot, pos_idx=model._pos_idx)
+                feed_slot=feed_slot)
     units, last = bst_units(model)
     params = (tables + [t for blk in model.transformer_blocks for t in _block_params(blk)] + _unit_params(units)
               + [last.weight, last.bias])

@@ -36,6 +36,8 @@
  *   rk_dcn_cross_backward   cross_layer backward w.r.t. x0        dcn.py:46-49
  *   rk_relu_backward   ReLU backward (residual_unit's outer ReLU) deepcrossing.py:41
  *   rk_embedding_backward   nn.Embedding dense weight gradient    dcn.py:131-138,163-166
+ *   rk_embedding_backward_sorted  the same for long, skewed index lists (behaviour sequences)
+ *                      as a sorted segment-reduce                din.py:300-303, bst.py:224
  *   rk_adam_step       torch.optim.Adam step (all tensors, one launch)  dcn.py:275
  *   rk_bn_act_train_forward / rk_bn_act_backward  Linear -> BatchNorm1d (train) -> ReLU -> Dropout
  *                      and its backward                       deepfm.py:100-109
@@ -48,7 +50,7 @@
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
  *   rk_bst_add_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
- *   rk_bst_ln_backward, rk_bst_leaky_dropout, rk_bst_pool / _backward
+ *   rk_bst_ln_backward, rk_bst_pos_backward, rk_bst_leaky_dropout, rk_bst_pool / _backward
  *                      BSTTransformer train forward (activations kept) and backward  bst.py:66-91,238-241
  *                      AFM train forward (activations kept) and backward  afm.py:92-119,173
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
@@ -310,6 +312,15 @@ int rk_logit_head_backward(const float* dlogit, const float* dprob, const float*
                            int32_t kb, const float* w, float* dxa, int64_t ld_dxa, float* dxb,
                            int64_t ld_dxb, float* dw, float* db, float* g_out, void* stream);
 
+/* Sorted segment-reduce form of rk_embedding_backward for ONE table segment and a long index list
+ * with hot rows (padded behaviour sequences): grad[idx[i]] += dx[i, out_col:+dim] for i < n, via a
+ * radix sort of the indices and one atomic per (distinct row in a 64-position chunk, column).
+ * workspace: rk_embedding_backward_sorted_workspace_size(n) bytes.  Out-of-range indices are skipped
+ * and raise RK_FLAG_INDEX_OOB.                                                               */
+int rk_embedding_backward_sorted_workspace_size(int64_t n, int64_t* bytes);
+int rk_embedding_backward_sorted(const rk_segment* grad, int64_t n, const float* dx, int64_t ld_dx,
+                                 void* workspace, int64_t ws_bytes, void* stream);
+
 /* Gradient of num_layers cross layers (rk_dcn_cross's stack, weights [L, width]) w.r.t. x0 given
  * dL/dx_L; written to dx0 (added when accumulate).  width <= 256, num_layers <= 8.           */
 int rk_dcn_cross_backward(const float* x0, int64_t ld_x0, int64_t batch, int32_t width,
@@ -448,7 +459,8 @@ int rk_afm_pair_fold(const float* d_pairs, const float* emb, int32_t num_fields,
  *   res_dropout_ln_forward: r = base + Dropout_p(o) (saved), y = LayerNorm(r) (gamma, beta, eps),
  *     mean / rstd [rows] saved.  d <= 256.
  *   ln_backward: dr = LayerNorm backward of dy (overwritten), d_o = Dropout_p-masked dr (NULL:
- *     skipped), dgamma / dbeta [d] (overwritten).
+ *     skipped), dgamma / dbeta [d] (overwritten, summed in a fixed order: workspace 1024 * d floats).
+ *   pos_backward: dpos[t] += sum_b dxp[b*T + t] for t < T (the position-embedding gradient; zero dpos first).
  *   leaky_dropout: forward out = Dropout_p(LeakyReLU_slope(f)); backward (backward = 1)
  *     out = in * keep * scale * (f > 0 ? 1 : slope).
  *   pool: row[b, col:+d] = sum_t x[b*T + t] (/ seq_len[b] when mean); pool_backward broadcasts.
@@ -467,7 +479,8 @@ int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t row
 int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
                        const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
                        const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
-                       void* stream);
+                       float* workspace, void* stream);
+int rk_bst_pos_backward(const float* dxp, int64_t batch, int32_t T, int32_t d, float* dpos, void* stream);
 int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, float slope, double dropout_p,
                          uint64_t seed, const int64_t* stream_slot, int32_t backward, float* out,
                          void* stream);

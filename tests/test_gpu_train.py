@@ -143,6 +143,36 @@ def test_embedding_backward_dense_grad():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,rows,dim", [(131072, 106445, 128), (204800, 106445, 32), (1000, 7, 5), (1, 3, 4)])
+def test_embedding_backward_sorted_matches_index_add(n, rows, dim):
+    """Sorted segment-reduce scatter against index_add_ (fp64) with half the ids on one hot row,
+    a strided dx segment and out-of-range ids (skipped, flagged)."""
+    g = torch.Generator().manual_seed(n + dim)
+    idx = torch.randint(0, rows, (n,), generator=g)
+    idx[::2] = 0  # padded history positions
+    ld = dim + 3
+    dx = torch.randn(n, ld, generator=g)
+    grad = torch.zeros(rows, dim, device="cuda")
+    rankops.error_flags(reset=True)
+    idx_d, dx_d = idx.cuda(), dx.cuda()
+    ops.embedding_backward_sorted(ops.table_segment(grad, idx_d, 2), n, dx_d)
+    want = torch.zeros(rows, dim, dtype=torch.float64).index_add_(0, idx, dx[:, 2:2 + dim].double())
+    torch.testing.assert_close(grad.cpu().double(), want, rtol=1e-5, atol=1e-4 * max(1.0, float(want.abs().max())))
+    assert rankops.error_flags() == 0
+    if n > 4:
+        bad = idx.clone()
+        bad[3] = rows + 5
+        bad[4] = -1
+        grad.zero_()
+        bad_d = bad.cuda()
+        ops.embedding_backward_sorted(ops.table_segment(grad, bad_d, 2), n, dx_d)
+        keep = (bad >= 0) & (bad < rows)
+        want = torch.zeros(rows, dim, dtype=torch.float64).index_add_(0, bad[keep], dx[keep, 2:2 + dim].double())
+        torch.testing.assert_close(grad.cpu().double(), want, rtol=1e-5, atol=1e-4 * max(1.0, float(want.abs().max())))
+        assert rankops.error_flags(reset=True) & 1
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("wd", [0.0, 0.01])
 def test_adam_matches_torch(wd):
     g = torch.Generator().manual_seed(11)
