@@ -42,7 +42,7 @@ PEAK_HBM = 8.0e12          # MI355X_MICROARCH.md: HBM3E peak BW (spec)
 METRIC = "forward samples/sec at batch 4096 (DCN, DIN, BST) on 1/2/4/8 MI355X"
 
 # Algorithmic work per sample
-DIN_ATT_FLOP = 2 * 50 * (128 * 64 + 64 * 32 + 32)  # 1,028,200: att-MLP of din_attention, T=50, H=32
+DIN_ATT_FLOP = 2 * 50 * (128 * 64 + 64 * 32 + 32)  # 1,027,200: att-MLP of din_attention, T=50, H=32
 DIN_FWD_FLOP = DIN_ATT_FLOP + 6_400 + 444_672       # whole DIN forward, reference formulation
 # what din_forward_kernel<32> issues per sample: split layer 1 (K=H) + layer 2 + layer 3 over 64 padded
 # positions, the per-sample bias u, and the fcn at padded widths (128->512->256->128)
@@ -62,8 +62,8 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the per-model extras")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--models", default="dcn,deepfm,bst,fwfm,din_per_call")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     return ap.parse_args()
 
@@ -106,8 +106,8 @@ def workload(name: str, batch: int, seed: int):
         cfg = {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32,
                "interaction_weights": "frozen" if name == "din" else "per_call"}
         model_name = "din"
-    elif name == "dcn":
-        cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    elif name in ("dcn", "dcn_per_call", "dcn_256_per_call"):
+        cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen" if name == "dcn" else "per_call"}
         model_name = "dcn"
     elif name == "deepfm":
         cfg = {"dim": 32, "fields": {f"field_{i:02d}": 1_000_000 for i in range(30)}}
@@ -198,28 +198,72 @@ def load_traffic(kernel: str, workload_name: str):
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
 
-def cpu_baseline(name, model, cfg, batch, budget_s):
-    """The oracle (CPU restatement of the reference forward, per-call draws included) on this
-    host, on a bounded sample: repeated forwards of batch `batch` until ~budget_s."""
+def _frozen_interaction(name, cfg):
+    """H2 weights drawn once in oracle form (the CPU counterpart of interaction_weights='frozen')."""
+    from oracle import reference_forward as ref
+    if name == "din":
+        return ref.draw_din_att(cfg.get("dim", 16))
+    if name == "dcn":
+        return ref.draw_cross(16 + 16 + 2 + 4 * 4, cfg.get("cross", 1))
+    return None
+
+
+def cpu_baseline(name, model, cfg, batch, budget_s, frozen):
+    """The oracle (CPU restatement of the reference forward) on this host, on a bounded sample:
+    repeated forwards of batch `batch` until ~budget_s.  `frozen` times the same H2 mode as the
+    GPU headline (interaction MLP drawn once); otherwise every call redraws it from the CPU
+    generator as the reference does."""
     import helpers as H
     n = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(n)
     p = H.cpu_params(model)
     cfg_cpu = dict(cfg)
     inp = H.make_inputs(name, cfg_cpu, batch, seed=2000)
+    inter = _frozen_interaction(name, cfg_cpu) if frozen else None
     with torch.no_grad():
-        H.call_oracle(name, cfg_cpu, p, inp)  # warm-up
+        H.call_oracle(name, cfg_cpu, p, inp, inter)  # warm-up
         t0 = time.perf_counter()
         iters = 0
         while True:
-            H.call_oracle(name, cfg_cpu, p, inp)
+            H.call_oracle(name, cfg_cpu, p, inp, inter)
             iters += 1
             el = time.perf_counter() - t0
-            if el >= budget_s or iters >= 200:
+            if el >= budget_s or iters >= 2000:
                 break
+    mode = "H2 weights frozen (drawn once)" if frozen else "per-call H2 draws included"
     return {"value": round(iters * batch / el, 1), "unit": "samples/s", "cores": n, "kind": "port",
-            "sample": f"{iters} oracle forwards of batch {batch} ({el:.1f} s, per-call H2 draws included, "
-                      f"fp32, torch {torch.__version__} CPU)"}
+            "sample": f"{iters} oracle {name.upper()} forwards of batch {batch} ({el:.1f} s, {mode}, fp32, "
+                      f"eval + no_grad, torch {torch.__version__} CPU)"}
+
+
+def cpu_baselines(model, cfg, head_value, extras, batch, budget_s):
+    """cpu_baseline for the headline (DIN configs[2], same frozen H2 mode as the GPU line), plus
+    the per-call mode beside din_per_call, DCN at batch 4096 (the north star's >= 10x target) in
+    both modes beside models.dcn / models.dcn_per_call, and configs[0] (DCN, wechat schema,
+    batch 256, the reference's CPU plumbing with per-call draws)."""
+    import helpers as H
+    out = cpu_baseline("din", model, cfg, batch, budget_s, frozen=True)
+    out["gpu_over_cpu"] = round(head_value / out["value"], 1)
+    out["mode"] = "frozen H2 beside the frozen GPU headline"
+    legs = {}
+    leg = cpu_baseline("din", model, cfg, batch, budget_s / 3, frozen=False)
+    if "din_per_call" in extras:
+        leg["gpu_samples_per_s"] = extras["din_per_call"]["samples_per_s"]
+        leg["gpu_over_cpu"] = round(leg["gpu_samples_per_s"] / leg["value"], 1)
+    legs["din_per_call"] = leg
+    dcn_cfg = {"vocab": H.WECHAT_VOCAB}
+    dcn = H.build("dcn", dcn_cfg, seed=42)
+    for key, b, frozen, gpu_key in (("dcn_4096", 4096, True, "dcn"), ("dcn_4096_per_call", 4096, False,
+                                                                       "dcn_per_call"),
+                                    ("configs0_dcn_256", 256, False, "dcn_256_per_call")):
+        leg = cpu_baseline("dcn", dcn, dcn_cfg, b, budget_s / (1.5 if key == "dcn_4096" else 3), frozen)
+        if gpu_key in extras:
+            leg["gpu_samples_per_s"] = extras[gpu_key]["samples_per_s"]
+            leg["gpu_over_cpu"] = round(leg["gpu_samples_per_s"] / leg["value"], 1)
+        legs[key] = leg
+    legs["dcn_4096"]["target"] = ">= 10x (BASELINE.json north star, DCN batch 4096, 1 MI355X)"
+    out["legs"] = legs
+    return out
 
 
 # ------------------------------------------------------------------ configs[4]: table-sharded DeepFM
@@ -484,7 +528,7 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
 
 def bench_one(name, batch, steps, warmup, world, rank):
     model, inp, fn, cfg, model_name = workload(name, batch, rank)
-    if name == "din_per_call":  # eager: per-call CPU draws + H2D are part of every forward
+    if name.endswith("per_call"):  # eager: per-call CPU draws + H2D are part of every forward
         def run():
             with torch.no_grad():
                 fn()
@@ -533,14 +577,14 @@ def main():
                               "achieved": round(achieved / 1e12, 3), "peak": PEAK_FP32_MFMA / 1e12,
                               "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
                               "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
-                              "flop_basis": "reference formulation per sample: att-MLP 1,028,200 + cross/"
+                              "flop_basis": "reference formulation per sample: att-MLP 1,027,200 + cross/"
                                             "weighted sum 6,400 + fcn 444,672 (SURVEY §8d)",
                               "executed_flop_per_launch": DIN_FWD_EXEC_FLOP * args.batch,
                               "traffic": load_traffic("din_forward_kernel", "din")}
     if rank == 0 and world == 1 and not args.no_extras:
         extras = {}
         for name in [m for m in args.models.split(",") if m]:
-            batch = 2048 if name == "bst" else args.batch
+            batch = {"bst": 2048, "dcn_256_per_call": 256}.get(name, args.batch)
             r, m2, inp2, cfg2, mn2 = bench_one(name, batch, args.steps, args.warmup, 1, 0)
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
@@ -581,8 +625,8 @@ def main():
             sh = {"error": f"{type(exc).__name__}: {exc}"[:300]}
         result["sharded_deepfm"] = sh
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(model_name, model.cpu(), cfg, args.batch, args.cpu_seconds)
-        result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        result["cpu_baseline"] = cpu_baselines(model.cpu(), cfg, result["value"], result.get("models", {}),
+                                               args.batch, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

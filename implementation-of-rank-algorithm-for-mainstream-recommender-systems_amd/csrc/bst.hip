@@ -5,8 +5,9 @@
 // Input is the packed projection buffer qkv [B*T, ld] holding Q | K | V column blocks of
 // width d_model (head h uses columns h*d_h .. (h+1)*d_h of each block).  One wave per
 // (sample, head): K_h and V_h are staged in LDS, lane = query position, the keys are swept
-// with an online softmax.  A sample whose length is 0 has every key masked; like torch's
-// softmax over an all -inf row this yields NaN context rows (bst.py:80-82).
+// with an online softmax.  The mask is either a length per sample (keys j >= len) or an
+// explicit [B, T] byte mask (nonzero = padding).  A sample whose keys are all masked yields NaN
+// context rows, like torch's softmax over an all -inf row (bst.py:80-82).
 #include "common.h"
 
 namespace rk {
@@ -15,6 +16,7 @@ template <int DH>
 __global__ __launch_bounds__(256) void bst_attention_kernel(const float* __restrict__ qkv, int64_t ld_qkv,
                                                             int64_t batch, int T, int d_model, int heads,
                                                             const int64_t* __restrict__ seq_len,
+                                                            const uint8_t* __restrict__ key_mask, int64_t ld_mask,
                                                             float* __restrict__ ctx, int64_t ld_ctx, int waves_per_wg) {
   extern __shared__ __attribute__((aligned(16))) float kv[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -36,8 +38,17 @@ __global__ __launch_bounds__(256) void bst_attention_kernel(const float* __restr
   __syncthreads();
   if (!live) return;
 
-  int64_t len = seq_len[b];
-  const int nvalid = (int)(len < 0 ? 0 : (len > T ? T : len));
+  // keys j >= seq_len[b] are masked (BSTModel's mask, bst.py:228-229); with an explicit
+  // key_padding_mask (BSTTransformer.forward, bst.py:79-80) key j is masked where it is nonzero;
+  // with neither nothing is masked
+  const int64_t len = seq_len ? seq_len[b] : (int64_t)T;
+  const int nkeys = (int)(len < 0 ? 0 : (len > T ? T : len));
+  const uint8_t* mrow = key_mask ? key_mask + b * ld_mask : nullptr;
+  int nvalid = nkeys;
+  if (mrow) {
+    nvalid = 0;
+    for (int j = 0; j < nkeys; ++j) nvalid += mrow[j] == 0;
+  }
   const float scale = (float)__builtin_sqrt((double)DH);
 
   for (int t0 = 0; t0 < T; t0 += 64) {
@@ -51,7 +62,8 @@ __global__ __launch_bounds__(256) void bst_attention_kernel(const float* __restr
       o[d] = 0.f;
     }
     float m = -INFINITY, l = 0.f;
-    for (int j = 0; j < nvalid; ++j) {
+    for (int j = 0; j < nkeys; ++j) {
+      if (mrow && mrow[j]) continue;
       float s = 0.f;
 #pragma unroll
       for (int d = 0; d < DH; ++d) s = fmaf(q[d], Ks[j * DH + d], s);
@@ -75,15 +87,16 @@ __global__ __launch_bounds__(256) void bst_attention_kernel(const float* __restr
 
 using namespace rk;
 
-RK_API int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T, int32_t d_model,
-                            int32_t heads, const int64_t* seq_len, float* ctx, int64_t ld_ctx, void* stream) {
-  if (!qkv || !seq_len || !ctx || T <= 0 || d_model <= 0 || heads <= 0 || d_model % heads != 0 ||
-      ld_qkv < 3 * d_model || ld_ctx < d_model || batch < 0)
-    return fail(RK_ERR_INVALID, "rk_bst_attention: bad arguments (T=%d d=%d heads=%d)", T, d_model, heads);
+static int launch_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T, int32_t d_model,
+                                int32_t heads, const int64_t* seq_len, const uint8_t* key_mask, int64_t ld_mask,
+                                float* ctx, int64_t ld_ctx, void* stream, const char* who) {
+  if (!qkv || !ctx || T <= 0 || d_model <= 0 || heads <= 0 || d_model % heads != 0 || ld_qkv < 3 * d_model ||
+      ld_ctx < d_model || batch < 0 || (key_mask && ld_mask < T))
+    return fail(RK_ERR_INVALID, "%s: bad arguments (T=%d d=%d heads=%d)", who, T, d_model, heads);
   if (batch == 0) return RK_OK;
   const int dh = d_model / heads;
   const size_t per_wave = (size_t)2 * T * dh * sizeof(float);
-  if (per_wave > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_bst_attention: T*d_h too large for LDS");
+  if (per_wave > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "%s: T*d_h too large for LDS", who);
   int wpg = 4;
   while (wpg > 1 && per_wave * wpg > 64 * 1024) wpg >>= 1;
   const int64_t items = batch * heads;
@@ -96,7 +109,7 @@ RK_API int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int
       (void)hipFuncSetAttribute((const void*)bst_attention_kernel<DD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           (int)shm);                                                                          \
     bst_attention_kernel<DD><<<blocks, 64 * wpg, shm, st>>>(qkv, ld_qkv, batch, T, d_model, heads, seq_len,   \
-                                                           ctx, ld_ctx, wpg);                                 \
+                                                           key_mask, ld_mask, ctx, ld_ctx, wpg);              \
     break;
   switch (dh) {
     RK_BST_CASE(1)
@@ -107,8 +120,22 @@ RK_API int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int
     RK_BST_CASE(32)
     RK_BST_CASE(64)
     default:
-      return fail(RK_ERR_UNSUPPORTED, "rk_bst_attention: head dim %d not in {1,2,4,8,16,32,64}", dh);
+      return fail(RK_ERR_UNSUPPORTED, "%s: head dim %d not in {1,2,4,8,16,32,64}", who, dh);
   }
 #undef RK_BST_CASE
-  return check_launch("rk_bst_attention");
+  return check_launch(who);
+}
+
+RK_API int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T, int32_t d_model,
+                            int32_t heads, const int64_t* seq_len, float* ctx, int64_t ld_ctx, void* stream) {
+  if (!seq_len) return fail(RK_ERR_INVALID, "rk_bst_attention: null seq_len");
+  return launch_bst_attention(qkv, ld_qkv, batch, T, d_model, heads, seq_len, nullptr, 0, ctx, ld_ctx, stream,
+                              "rk_bst_attention");
+}
+
+RK_API int rk_bst_attention_masked(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T, int32_t d_model,
+                                   int32_t heads, const uint8_t* key_padding_mask, int64_t ld_mask, float* ctx,
+                                   int64_t ld_ctx, void* stream) {
+  return launch_bst_attention(qkv, ld_qkv, batch, T, d_model, heads, nullptr, key_padding_mask, ld_mask, ctx,
+                              ld_ctx, stream, "rk_bst_attention_masked");
 }

@@ -24,7 +24,8 @@ constexpr int kDinH1 = 64, kDinH2 = 32;
 template <int H>
 __global__ __launch_bounds__(256) void din_attention_kernel(
     const float* __restrict__ query, int64_t ld_query, const float* __restrict__ key_table, int64_t key_rows,
-    int64_t ld_key, const int64_t* __restrict__ seq, int64_t ld_seq, int T, const int64_t* __restrict__ seq_len,
+    int64_t ld_key, const int64_t* __restrict__ seq, int64_t ld_seq, int64_t ld_kb, int T,
+    const int64_t* __restrict__ seq_len,
     int64_t batch, const float* __restrict__ w1, const float* __restrict__ b1, const float* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ w3, const float* __restrict__ b3, int use_softmax,
     float* __restrict__ out, int64_t ld_out, uint32_t* flags) {
@@ -74,11 +75,15 @@ __global__ __launch_bounds__(256) void din_attention_kernel(
       f32x4 k[NQ];
       const float* krow = nullptr;
       if (in_seq) {
-        const int64_t r = seq[b * ld_seq + t];
-        if (r >= 0 && r < key_rows)
-          krow = key_table + r * ld_key;
-        else
-          flag_oob(flags);
+        if (seq) {  // history gathered from the embedding table
+          const int64_t r = seq[b * ld_seq + t];
+          if (r >= 0 && r < key_rows)
+            krow = key_table + r * ld_key;
+          else
+            flag_oob(flags);
+        } else {  // dense keys [B, T, H]
+          krow = key_table + b * ld_kb + (int64_t)t * ld_key;
+        }
       }
 #pragma unroll
       for (int c = 0; c < NQ; ++c)
@@ -179,6 +184,35 @@ __global__ __launch_bounds__(256) void din_attention_kernel(
 
 using namespace rk;
 
+static int launch_din_attention(const float* query, int64_t ld_query, const float* key_table, int64_t key_rows,
+                                int64_t ld_key, const int64_t* seq, int64_t ld_seq, int64_t ld_kb, int32_t T,
+                                const int64_t* seq_len, int64_t batch, int32_t H, const float* w1, const float* b1,
+                                const float* w2, const float* b2, const float* w3, const float* b3,
+                                int32_t use_softmax, float* out, int64_t ld_out, void* stream, const char* who) {
+  if (batch == 0) return RK_OK;
+  const int64_t want = (batch + 3) / 4;
+  // persistent: W1/W2 are staged in LDS once per workgroup, which then walks many samples
+  const unsigned blocks = (unsigned)std::min<int64_t>(want, (int64_t)num_cus() * 2);
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* fl = device_flags();
+#define RK_DIN_CASE(HH)                                                                                         \
+  case HH:                                                                                                      \
+    din_attention_kernel<HH><<<blocks, 256, 0, st>>>(query, ld_query, key_table, key_rows, ld_key, seq, ld_seq, \
+                                                     ld_kb, T, seq_len, batch, w1, b1, w2, b2, w3, b3,          \
+                                                     use_softmax, out, ld_out, fl);                             \
+    break;
+  switch (H) {
+    RK_DIN_CASE(8)
+    RK_DIN_CASE(16)
+    RK_DIN_CASE(32)
+    RK_DIN_CASE(64)
+    default:
+      return fail(RK_ERR_UNSUPPORTED, "%s: embedding dim %d not in {8,16,32,64}", who, H);
+  }
+#undef RK_DIN_CASE
+  return check_launch(who);
+}
+
 RK_API int rk_din_attention(const float* query, int64_t ld_query, const float* key_table, int64_t key_rows,
                             int64_t ld_key, const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
                             int64_t batch, int32_t H, const float* w1, const float* b1, const float* w2,
@@ -190,26 +224,21 @@ RK_API int rk_din_attention(const float* query, int64_t ld_query, const float* k
     return fail(RK_ERR_INVALID, "rk_din_attention: bad shape T=%d H=%d", T, H);
   if (ld_key % 4 != 0 || ((uintptr_t)key_table & 15u))
     return fail(RK_ERR_UNSUPPORTED, "rk_din_attention: key table rows must be 16-B aligned");
-  if (batch == 0) return RK_OK;
-  const int64_t want = (batch + 3) / 4;
-  // persistent: W1/W2 are staged in LDS once per workgroup, which then walks many samples
-  const unsigned blocks = (unsigned)std::min<int64_t>(want, (int64_t)num_cus() * 2);
-  hipStream_t st = (hipStream_t)stream;
-  uint32_t* fl = device_flags();
-#define RK_DIN_CASE(HH)                                                                                         \
-  case HH:                                                                                                      \
-    din_attention_kernel<HH><<<blocks, 256, 0, st>>>(query, ld_query, key_table, key_rows, ld_key, seq, ld_seq, \
-                                                     T, seq_len, batch, w1, b1, w2, b2, w3, b3, use_softmax,    \
-                                                     out, ld_out, fl);                                          \
-    break;
-  switch (H) {
-    RK_DIN_CASE(8)
-    RK_DIN_CASE(16)
-    RK_DIN_CASE(32)
-    RK_DIN_CASE(64)
-    default:
-      return fail(RK_ERR_UNSUPPORTED, "rk_din_attention: embedding dim %d not in {8,16,32,64}", H);
-  }
-#undef RK_DIN_CASE
-  return check_launch("rk_din_attention");
+  return launch_din_attention(query, ld_query, key_table, key_rows, ld_key, seq, ld_seq, 0, T, seq_len, batch, H,
+                              w1, b1, w2, b2, w3, b3, use_softmax, out, ld_out, stream, "rk_din_attention");
+}
+
+RK_API int rk_din_attention_dense(const float* query, int64_t ld_query, const float* keys, int64_t ld_keys_b,
+                                  int64_t ld_keys_t, int32_t T, const int64_t* keys_length, int64_t batch,
+                                  int32_t H, const float* w1, const float* b1, const float* w2, const float* b2,
+                                  const float* w3, const float* b3, int32_t use_softmax, float* out,
+                                  int64_t ld_out, void* stream) {
+  if (!query || !keys || !keys_length || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !out)
+    return fail(RK_ERR_INVALID, "rk_din_attention_dense: null pointer");
+  if (T <= 0 || batch < 0 || ld_query < H || ld_out < H || ld_keys_t < H || ld_keys_b < (int64_t)T * ld_keys_t)
+    return fail(RK_ERR_INVALID, "rk_din_attention_dense: bad shape T=%d H=%d", T, H);
+  if (ld_keys_t % 4 != 0 || ld_keys_b % 4 != 0 || ((uintptr_t)keys & 15u))
+    return fail(RK_ERR_UNSUPPORTED, "rk_din_attention_dense: key rows must be 16-B aligned");
+  return launch_din_attention(query, ld_query, keys, 0, ld_keys_t, nullptr, 0, ld_keys_b, T, keys_length, batch, H,
+                              w1, b1, w2, b2, w3, b3, use_softmax, out, ld_out, stream, "rk_din_attention_dense");
 }

@@ -294,6 +294,24 @@ __global__ __launch_bounds__(256) void dice_apply_kernel(const float* __restrict
   }
 }
 
+// ---- Dice in eval (din.py:33-36): xhat = x * scale + shift (BatchNorm1d running statistics,
+// folded by rk_bn_fold), p = sigmoid(xhat), y = alpha * (1 - p) * x + p * x.  Thread per element,
+// rows over grid.y.
+__global__ __launch_bounds__(256) void dice_eval_kernel(const float* __restrict__ x, int64_t ldx, int64_t B, int N,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ alpha, float* __restrict__ y,
+                                                        int64_t ldy) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const float sc = scale[n], sh = shift[n], a = alpha[n];
+  for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
+    const float v = x[b * ldx + n];
+    const float p = 1.0f / (1.0f + expf(-(v * sc + sh)));
+    y[b * ldy + n] = a * (1.0f - p) * v + p * v;
+  }
+}
+
 // Dice backward.  With g = dy: dx = g * (alpha (1 - p) + p)  [direct]
 //   + invstd * (dxhat - mean_b dxhat - xhat * mean_b(dxhat * xhat))  [through the batch statistics],
 // dxhat = g * x * (1 - alpha) * p * (1 - p);  dalpha = sum_b g * x * (1 - p).
@@ -483,4 +501,14 @@ RK_API int rk_dice_backward(const float* dy, int64_t lddy, const float* z, int64
   dice_backward_kernel<false><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, alpha, save_mean, save_invstd,
                                                     workspace, dz, lddz);
   return check_launch("rk_dice_backward");
+}
+
+RK_API int rk_dice_forward(const float* x, int64_t ldx, int64_t rows, int32_t n, const float* bn_scale,
+                           const float* bn_shift, const float* alpha, float* y, int64_t ldy, void* stream) {
+  if (!x || !y || !bn_scale || !bn_shift || !alpha || rows < 0 || n <= 0 || ldx < n || ldy < n)
+    return fail(RK_ERR_INVALID, "rk_dice_forward: bad arguments");
+  if (rows == 0) return RK_OK;
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)std::min<int64_t>(rows, 4096));
+  dice_eval_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(x, ldx, rows, n, bn_scale, bn_shift, alpha, y, ldy);
+  return check_launch("rk_dice_forward");
 }

@@ -371,14 +371,18 @@ RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int6
   return check_launch("rk_bst_res_dropout_ln_forward");
 }
 
+RK_API int64_t rk_bst_ln_backward_workspace_floats(int32_t d) { return (int64_t)kLnBlocks * 2 * (d > 0 ? d : 0); }
+
 RK_API int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
                               const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
                               const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
-                              float* workspace, void* stream) {
+                              float* workspace, int64_t workspace_floats, void* stream) {
   if (!dy || !r || !mean || !rstd || !gamma || !dr || !dgamma || !dbeta || !workspace || rows < 0 || d <= 0 ||
       d > 256 || !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
-    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: bad arguments (d <= 256, workspace of %d * 2d floats)",
-                kLnBlocks);
+    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: bad arguments (d <= 256)");
+  if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
+    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: workspace of %lld floats, needs %lld (%d * 2d)",
+                (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d), kLnBlocks);
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (rows + 3) / 4));
   bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot,

@@ -27,7 +27,7 @@ from .bst import BSTModel, BSTTransformer  # noqa: F401
 from .dcn import DCNModel, cross_layer  # noqa: F401
 from .deepcrossing import DeepCrossingModel, residual_unit  # noqa: F401
 from .deepfm import DeepFM  # noqa: F401
-from .din import DIN, Dice, din_attention  # noqa: F401
+from .din import DIN, Dice, din_attention, din_attention_gather  # noqa: F401
 from .fwfm import FwFM  # noqa: F401
 from .loader import BatchAssembler, Vocabulary, label_encode, wechat_vocabularies  # noqa: F401
 from .metrics import EvalAccumulator, roc_auc  # noqa: F401
@@ -35,7 +35,7 @@ from .train import Adam  # noqa: F401
 
 __all__ = [
     "AFM", "BSTModel", "BSTTransformer", "BatchAssembler", "DCNModel", "DIN", "DeepCrossingModel", "DeepFM",
-    "Dice", "FwFM", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention",
+    "Dice", "FwFM", "RankOpsError", "Vocabulary", "create_feature_columns", "cross_layer", "din_attention", "din_attention_gather",
     "error_flags", "load_library", "residual_unit", "wechat_vocabularies", "EvalAccumulator", "roc_auc",
     "label_encode", "Adam",
 ]

@@ -135,8 +135,18 @@ SIGNATURES = {
         [_SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "rk_din_attention_dense": (
+        ctypes.c_int,
+        [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int32,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p],
+    ),
+    "rk_dice_forward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int64, c_void_p]),
     "rk_bst_attention": (
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_bst_attention_masked": (
+        ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64,
+                       c_void_p]),
     "rk_bst_forward_blocks": (
         ctypes.c_int,
         [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32, c_int32,
@@ -215,7 +225,8 @@ SIGNATURES = {
                                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_bst_ln_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                           ctypes.c_double, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                          c_void_p, c_void_p, c_void_p]),
+                                          c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_bst_ln_backward_workspace_floats": (c_int64, [c_int32]),
     "rk_bst_pos_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_bst_leaky_dropout": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, ctypes.c_double, ctypes.c_uint64,
                                             c_void_p, c_int32, c_void_p, c_void_p]),

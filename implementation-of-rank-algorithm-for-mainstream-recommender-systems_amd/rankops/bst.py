@@ -63,6 +63,76 @@ class BSTTransformer(EngineModule):
         self._wqk = Packed()
         self._bqk = Packed()
 
+    def forward(self, queries, keys, values, key_padding_mask=None):
+        """BSTTransformer.forward(queries, keys, values, key_padding_mask=None) (bst.py:66-91):
+        queries/keys/values [B, T, d]; key_padding_mask [B, T] bool (True = padding key) or None.
+        Eval semantics (Dropout identity).  rk_linear for Q (queries + positions), K (keys +
+        positions), V, W_o + residual + LayerNorm1 and the FFN + residual + LayerNorm2, and
+        rk_bst_attention_masked in between; a row whose keys are all masked gives NaN, as torch's
+        softmax over an all -inf row does."""
+        check_eval(self)
+        queries = ops.as_f32(queries, "queries")
+        keys = ops.as_f32(keys, "keys")
+        values = ops.as_f32(values, "values")
+        if queries.dim() != 3 or keys.shape != queries.shape or values.shape != queries.shape:
+            raise ValueError(f"BSTTransformer: queries {tuple(queries.shape)}, keys {tuple(keys.shape)} and values "
+                             f"{tuple(values.shape)} must all be [batch, seq_len, d_model]")
+        B, T, d = queries.shape
+        if d != self.d_model:
+            raise ValueError(f"BSTTransformer: d_model {self.d_model}, inputs have {d}")
+        pos = self.position_embedding.weight
+        if T > pos.shape[0]:
+            raise IndexError(f"BSTTransformer: sequence length {T} exceeds max_len {pos.shape[0]}")
+        dev = queries.device
+        out = torch.empty(B, T, d, device=dev, dtype=torch.float32)
+        if B == 0:
+            return out
+        mask = None
+        if key_padding_mask is not None:
+            require = ops.require_gpu(key_padding_mask, "key_padding_mask")
+            if require.dtype != torch.bool or tuple(require.shape) != (B, T):
+                raise ValueError(f"BSTTransformer: key_padding_mask must be a bool [{B}, {T}] tensor, got "
+                                 f"{require.dtype} {tuple(require.shape)}")
+            mask = require.contiguous().view(torch.uint8)
+        q2 = queries.reshape(B * T, d).contiguous()
+        k2 = q2 if keys is queries else keys.reshape(B * T, d).contiguous()
+        v2 = q2 if values is queries else values.reshape(B * T, d).contiguous()
+        qkv = torch.empty(B * T, 3 * d, device=dev, dtype=torch.float32)
+        if k2 is q2:  # self-attention: [W_q; W_k] as one GEMM with the positions added in the A loader
+            ops.linear(q2, self._wqk(self.w_q.weight, self.w_k.weight), None, x_periodic=pos, x_period=T,
+                       y_ptr=qkv.data_ptr(), ldy=3 * d, epilogue=ops.make_epilogue(bias=self._bqk(self.w_q.bias,
+                                                                                                  self.w_k.bias)))
+        else:
+            ops.linear(q2, self.w_q.weight, None, x_periodic=pos, x_period=T, y_ptr=qkv.data_ptr(), ldy=3 * d,
+                       epilogue=ops.make_epilogue(bias=self.w_q.bias))
+            ops.linear(k2, self.w_k.weight, None, x_periodic=pos, x_period=T, y_ptr=ops._lib.fptr(qkv, d),
+                       ldy=3 * d, epilogue=ops.make_epilogue(bias=self.w_k.bias))
+        ops.linear(v2, self.w_v.weight, None, y_ptr=ops._lib.fptr(qkv, 2 * d), ldy=3 * d,
+                   epilogue=ops.make_epilogue(bias=self.w_v.bias))
+        ctx = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+        ops.bst_attention_masked(qkv, B, T, d, self.nhead, mask, ctx)
+        self._tail(ctx, q2, pos, T, out.view(B * T, d))
+        return out
+
+    def _tail(self, ctx, x, pos, T, out, pool_out_ptr=None, ld_pool=0, pool_mean=False, seq_length=None):
+        """out1 = LN1((x + pos) + ctx W_o^T + b_o); out = LN2(out1 + FFN(out1)) (bst.py:86-90),
+        optionally summed / averaged per sample into pool_out_ptr (bst.py:238-241)."""
+        d = self.d_model
+        out1 = torch.empty(x.shape[0], d, device=x.device, dtype=torch.float32)
+        ops.linear(ctx, self.w_o.weight, out1, epilogue=ops.make_epilogue(
+            bias=self.w_o.bias, residual=x, ld_residual=x.stride(0), residual_periodic=pos, residual_period=T,
+            has_ln=1, ln_gamma=self.norm1.weight, ln_beta=self.norm1.bias, ln_eps=self.norm1.eps))
+        f1 = torch.empty(x.shape[0], d, device=x.device, dtype=torch.float32)
+        ops.linear(out1, self.ffn[0].weight, f1, epilogue=ops.make_epilogue(
+            bias=self.ffn[0].bias, act="leaky", slope=self.ffn[1].negative_slope))
+        ep = dict(bias=self.ffn[3].bias, residual=out1, ld_residual=out1.stride(0), has_ln=1,
+                  ln_gamma=self.norm2.weight, ln_beta=self.norm2.bias, ln_eps=self.norm2.eps)
+        if pool_out_ptr is not None:
+            ep.update(pool_out=pool_out_ptr, ld_pool=ld_pool, pool_rows=T, pool_mean=1 if pool_mean else 0,
+                      pool_len=seq_length)
+        ops.linear(f1, self.ffn[3].weight, out, epilogue=ops.make_epilogue(**ep))
+        return out
+
     def run(self, x: torch.Tensor, B: int, T: int, seq_length: torch.Tensor, out: torch.Tensor = None,
             pool_out_ptr: int = None, ld_pool: int = 0, pool_mean: bool = False):
         """x: [B*T, d] (queries = keys = values).  Writes the block output to `out`, or pools it
@@ -81,20 +151,7 @@ class BSTTransformer(EngineModule):
                    epilogue=ops.make_epilogue(bias=self.w_v.bias))
         ctx = torch.empty(B * T, d, device=dev, dtype=torch.float32)
         ops.bst_attention(qkv, B, T, d, self.nhead, seq_length, ctx)
-        out1 = torch.empty(B * T, d, device=dev, dtype=torch.float32)
-        ops.linear(ctx, self.w_o.weight, out1, epilogue=ops.make_epilogue(
-            bias=self.w_o.bias, residual=x, ld_residual=x.stride(0), residual_periodic=pos, residual_period=T,
-            has_ln=1, ln_gamma=self.norm1.weight, ln_beta=self.norm1.bias, ln_eps=self.norm1.eps))
-        f1 = torch.empty(B * T, d, device=dev, dtype=torch.float32)
-        ops.linear(out1, self.ffn[0].weight, f1, epilogue=ops.make_epilogue(
-            bias=self.ffn[0].bias, act="leaky", slope=self.ffn[1].negative_slope))
-        ep = dict(bias=self.ffn[3].bias, residual=out1, ld_residual=out1.stride(0), has_ln=1,
-                  ln_gamma=self.norm2.weight, ln_beta=self.norm2.bias, ln_eps=self.norm2.eps)
-        if pool_out_ptr is not None:
-            ep.update(pool_out=pool_out_ptr, ld_pool=ld_pool, pool_rows=T, pool_mean=1 if pool_mean else 0,
-                      pool_len=seq_length)
-        ops.linear(f1, self.ffn[3].weight, out, epilogue=ops.make_epilogue(**ep))
-        return out
+        return self._tail(ctx, x, pos, T, out, pool_out_ptr, ld_pool, pool_mean, seq_length)
 
 
 class BSTModel(EngineModule):

@@ -138,6 +138,14 @@ class EngineModule(nn.Module):
         _GENERATION[0] += 1
         return super()._apply(fn, *args, **kwargs)
 
+    def train(self, mode: bool = True):
+        # A mode switch also invalidates every derived cache: replays of a captured train step
+        # (hipGraph) update weights and BatchNorm running statistics without bumping tensor
+        # versions, and the reference's loop always calls model.eval() before evaluate()
+        # (dcn.py:215, din.py:442-446), so the first eval forward after training re-folds.
+        _GENERATION[0] += 1
+        return super().train(mode)
+
 
 def _key(tensors):
     return (_GENERATION[0],) + tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)

@@ -29,24 +29,93 @@ FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_i
 SEQ_KEY = "his_read_comment_7d_seq"
 
 
+class _DiceTrain(torch.autograd.Function):
+    """Dice with batch statistics (BatchNorm1d in train mode, running statistics updated):
+    rk_dice_train_forward / rk_dice_backward."""
+
+    @staticmethod
+    def forward(ctx, x, alpha, dice):
+        n = x.shape[1]
+        f32 = dict(device=x.device, dtype=torch.float32)
+        y = torch.empty_like(x)
+        mean, invstd = torch.empty(n, **f32), torch.empty(n, **f32)
+        ops.dice_train_forward(x, None, dice, y, mean, invstd, torch.empty(2 * n, device=x.device,
+                                                                          dtype=torch.float64))
+        ctx.save_for_backward(x, mean, invstd)
+        ctx.dice = dice
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        n = x.shape[1]
+        dx = torch.empty_like(x)
+        dalpha = torch.empty(n, device=x.device, dtype=torch.float32)
+        ops.dice_backward(dy, x, None, ctx.dice, mean, invstd, torch.empty(3 * n, device=x.device,
+                                                                          dtype=torch.float64), dx, dalpha)
+        return dx, dalpha, None
+
+
 class Dice(nn.Module):
-    """Dice activation (din.py:26-36).  Same parameters/buffers as the reference; its eval-mode
-    math runs inside the rk_linear epilogue."""
+    """Dice activation (din.py:26-36): alpha * (1 - p) * x + p * x, p = sigmoid(BatchNorm1d(x))
+    with an affine-free BatchNorm (its eps 1e-5; the module's own eps is unused, as in the
+    reference).  Same parameters/buffers as the reference.  Inside DIN it runs fused in the fcn
+    epilogue; called on its own, eval uses rk_dice_forward (running statistics folded by
+    rk_bn_fold) and train mode rk_dice_train_forward / rk_dice_backward (batch statistics)."""
 
     def __init__(self, num_features, eps=1e-9):
         super().__init__()
         self.eps = eps
         self.alpha = nn.Parameter(torch.zeros(num_features))
         self.bn = nn.BatchNorm1d(num_features, affine=False)
+        self._fold = common.FoldedBN()
 
     def forward(self, x):
-        raise RuntimeError("Dice runs fused inside the rankops fcn epilogue; call DIN.forward")
+        x = ops.as_f32(x, "Dice input")
+        if x.dim() != 2 or x.shape[1] != self.alpha.numel():
+            raise ValueError(f"rankops Dice: expected [batch, {self.alpha.numel()}], got {tuple(x.shape)}")
+        x = x.contiguous()
+        if self.bn.training or not self.bn.track_running_stats or self.bn.running_mean is None:
+            if self.bn.momentum is None:
+                raise NotImplementedError("rankops Dice: BatchNorm momentum=None (cumulative average)")
+            if x.shape[0] < 2:
+                raise ValueError("Expected more than 1 value per channel when training (BatchNorm1d)")
+            return _DiceTrain.apply(x, self.alpha, self)
+        scale, shift = self._fold(self.bn)
+        y = torch.empty_like(x)
+        ops.dice_forward(x, scale, shift, self.alpha, y)
+        return y
 
 
-def din_attention(query, keys_table, seq, keys_length, is_softmax=False, weights=None):
-    """Reference din_attention (din.py:42-84) with the history given as (table, index) —
-    the gather happens inside the kernel.  `weights` = (W1, b1, W2, b2, W3, b3) device tensors;
-    when None they are drawn from the CPU generator like the reference."""
+def din_attention(query, keys, keys_length, is_softmax=False, *, weights=None):
+    """din_attention(query[B,H], keys[B,T,H], keys_length[B], is_softmax=False) -> [B,H]
+    (din.py:42-84) on rk_din_attention_dense.  The attention MLP Linear(4H,64), Linear(64,32),
+    Linear(32,1) is drawn from the CPU generator on every call like the reference (din.py:61-67);
+    `weights` = (W1, b1, W2, b2, W3, b3) device tensors replaces the draw."""
+    query = ops.as_f32(query, "query")
+    keys = ops.as_f32(keys, "keys")
+    keys_length = ops.as_index(keys_length, "keys_length")
+    if keys.dim() != 3 or query.dim() != 2 or query.shape[0] != keys.shape[0] or query.shape[1] != keys.shape[2]:
+        raise ValueError(f"din_attention: query {tuple(query.shape)} and keys {tuple(keys.shape)} do not match")
+    B, T, H = keys.shape
+    if keys.stride(2) != 1 or keys.stride(1) % 4 or keys.stride(0) % 4 or keys.data_ptr() % 16:
+        keys = keys.contiguous()
+    if query.stride(1) != 1:
+        query = query.contiguous()
+    if weights is None:
+        weights = [t.to(keys.device) for t in draw_din_attention(H)]
+    out = torch.empty(B, H, device=keys.device, dtype=torch.float32)
+    if B == 0:
+        return out
+    ops.din_attention_dense(query, keys, keys_length.contiguous(), weights, is_softmax, out)
+    return out
+
+
+def din_attention_gather(query, keys_table, seq, keys_length, is_softmax=False, weights=None):
+    """din_attention with the history given as (embedding table, index [B,T]) — the gather
+    din.py:300-303 does before the call happens inside the kernel (rk_din_attention).
+    `weights` as for din_attention."""
     query = ops.as_f32(query, "query")
     seq = ops.as_index(seq, "keys index")
     keys_length = ops.as_index(keys_length, "keys_length")

@@ -115,6 +115,24 @@ def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, u
                                torch.cuda.current_stream(device).cuda_stream), "rk_din_attention")
 
 
+def din_attention_dense(query, keys, keys_length, weights, use_softmax, out):
+    """rk_din_attention_dense: keys [B, T, H] (rows 16-B aligned), query/out [B, H]."""
+    lib = _lib.load()
+    _lib.ensure_device(keys.device)
+    w1, b1, w2, b2, w3, b3 = weights
+    B, T, H = keys.shape
+    check(lib.rk_din_attention_dense(ptr(query), query.stride(0), ptr(keys), keys.stride(0), keys.stride(1), T,
+                                     ptr(keys_length), B, H, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3), ptr(b3),
+                                     1 if use_softmax else 0, ptr(out), out.stride(0), _lib.stream_of(keys)),
+          "rk_din_attention_dense")
+
+
+def dice_forward(x, scale, shift, alpha, y):
+    lib = _lib.load()
+    check(lib.rk_dice_forward(ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(scale), ptr(shift), ptr(alpha),
+                              ptr(y), y.stride(0), _lib.stream_of(x)), "rk_dice_forward")
+
+
 L2_WORKSPACE = 512  # RK_L2_WORKSPACE
 
 
@@ -148,6 +166,14 @@ def bst_attention(qkv, batch, T, d_model, heads, seq_len, ctx):
     lib = _lib.load()
     check(lib.rk_bst_attention(ptr(qkv), qkv.stride(0), batch, T, d_model, heads, ptr(seq_len), ptr(ctx),
                                ctx.stride(0), _lib.stream_of(qkv)), "rk_bst_attention")
+
+
+def bst_attention_masked(qkv, batch, T, d_model, heads, key_mask, ctx):
+    """key_mask: None or a [batch, T] uint8 view of the bool key_padding_mask (nonzero = masked)."""
+    lib = _lib.load()
+    check(lib.rk_bst_attention_masked(ptr(qkv), qkv.stride(0), batch, T, d_model, heads, ptr(key_mask),
+                                      key_mask.stride(0) if key_mask is not None else 0, ptr(ctx), ctx.stride(0),
+                                      _lib.stream_of(qkv)), "rk_bst_attention_masked")
 
 
 BST_BLOCK_PARAMS = 17
@@ -387,6 +413,15 @@ def _act_code(act):
     return _lib.RK_ACT_RELU if act else _lib.RK_ACT_NONE
 
 
+def _stats_updated(bn):
+    """After a train-mode kernel updated `bn`'s running statistics through raw pointers: count the
+    batch as torch's BatchNorm does and bump the buffers' versions so eval-mode folds
+    (common.FoldedBN) keyed on them recompute."""
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    torch.autograd.graph.increment_version([bn.running_mean, bn.running_var])
+
+
 def bn_act_train_forward(z, bias, bn, act, p, seed, slot, y, save_mean, save_invstd, workspace, slope=0.0):
     """bn: an nn.BatchNorm1d (train mode) or None; act: True (ReLU), False, or 'leaky' with `slope`."""
     lib = _lib.load()
@@ -398,6 +433,8 @@ def bn_act_train_forward(z, bias, bn, act, p, seed, slot, y, save_mean, save_inv
         ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None, ptr(workspace),
         ptr(save_mean), ptr(save_invstd), _act_code(act), float(slope), float(p), seed, ptr(slot), ptr(y),
         y.stride(0), _lib.stream_of(z)), "rk_bn_act_train_forward")
+    if track:
+        _stats_updated(bn)
 
 
 def bn_act_backward(dy, z, bias, bn, act, p, seed, slot, save_mean, save_invstd, workspace, dz, dgamma, dbeta,
@@ -420,8 +457,8 @@ def dice_train_forward(z, bias, dice, y, save_mean, save_invstd, workspace):
                                     float(bn.eps), float(bn.momentum), ptr(bn.running_mean) if track else None,
                                     ptr(bn.running_var) if track else None, ptr(workspace), ptr(save_mean),
                                     ptr(save_invstd), ptr(y), y.stride(0), _lib.stream_of(z)), "rk_dice_train_forward")
-    if track and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+    if track:
+        _stats_updated(bn)
 
 
 def dice_backward(dy, z, bias, dice, save_mean, save_invstd, workspace, dz, dalpha):
@@ -525,15 +562,13 @@ def bst_res_dropout_ln_forward(base, o, p, seed, slot, ln, r, y, mean, rstd):
           "rk_bst_res_dropout_ln_forward")
 
 
-BST_LN_WORKSPACE = 1024  # floats per model column (rk_bst_ln_backward)
-
-
 def bst_ln_backward(dy, r, mean, rstd, ln, p, seed, slot, dr, d_o, dgamma, dbeta):
     lib = _lib.load()
-    ws = torch.empty(BST_LN_WORKSPACE * r.shape[1], device=r.device, dtype=torch.float32)
+    nws = lib.rk_bst_ln_backward_workspace_floats(r.shape[1])
+    ws = torch.empty(nws, device=r.device, dtype=torch.float32)
     check(lib.rk_bst_ln_backward(ptr(dy), ptr(r), ptr(mean), ptr(rstd), ptr(ln.weight), r.shape[0], r.shape[1],
                                  float(p), seed, ptr(slot), ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta), ptr(ws),
-                                 _lib.stream_of(dy)), "rk_bst_ln_backward")
+                                 nws, _lib.stream_of(dy)), "rk_bst_ln_backward")
 
 
 def bst_pos_backward(dxp, B, T, dpos):

@@ -311,8 +311,6 @@ def deep_stack_forward(x, units, seed, slot):
         invstd = torch.empty(n, device=dev, dtype=torch.float32)
         ws = torch.empty(2 * n, device=dev, dtype=torch.float64)
         ops.bn_act_train_forward(z, lin.bias, bn, act, p, seed + u, slot, y, mean, invstd, ws, slope=slope)
-        if bn is not None and bn.track_running_stats and bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
         saved.append((z, y, mean, invstd))
         h = y
     return saved
@@ -498,8 +496,6 @@ class _DINTrain(torch.autograd.Function):
                 m2, s2 = torch.empty(n, **f32), torch.empty(n, **f32)
                 ops.bn_act_train_forward(y1, None, bn, False, p, seed + u, slot, y2, m2, s2,
                                          torch.empty(2 * n, device=dev, dtype=torch.float64))
-                if bn is not None and bn.track_running_stats and bn.num_batches_tracked is not None:
-                    bn.num_batches_tracked.add_(1)
             saved.append((z, y1, m1, s1, y2, m2, s2))
             h = y2
         logit = torch.empty(B, 1, **f32)

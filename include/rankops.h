@@ -22,10 +22,13 @@
  *                      LayerNorm, sum/mean pooling, final Linear(*,1)+sigmoid) dcn.py:144-152,175-180;
  *                      deepfm.py:100-112,143-151; din.py:26-36,272-285,312-316; deepcrossing.py:25-42,161-162;
  *                      bst.py:59-64,73-75,86-90,203-214,238-247
- *   rk_din_attention   din_attention()                       din.py:42-84
+ *   rk_din_attention   din_attention() with the history gathered from the table  din.py:42-84,300-305
+ *   rk_din_attention_dense  din_attention(query, keys[B,T,H], keys_length, is_softmax)  din.py:42-84
+ *   rk_dice_forward    Dice.forward() in eval (BatchNorm running statistics)           din.py:26-36
  *   rk_row_l2norm_mean DIN mini-batch-aware l2 term          din.py:318-322
  *   rk_afm_forward     AFM.forward()                         afm.py:92-119
- *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84
+ *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84 (mask from seq_length, bst.py:228-229)
+ *   rk_bst_attention_masked  the same with BSTTransformer.forward's key_padding_mask  bst.py:66-84
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
@@ -203,6 +206,19 @@ int rk_din_attention(const float* query, int64_t ld_query, const float* key_tabl
                      const float* w3, const float* b3, int32_t use_softmax, float* out,
                      int64_t ld_out, void* stream);
 
+/* din_attention(query, keys, keys_length, is_softmax) with a dense history tensor: key row t of
+ * sample b at keys + b * ld_keys_b + t * ld_keys_t (16-B aligned rows).  H in {8,16,32,64}.   */
+int rk_din_attention_dense(const float* query, int64_t ld_query, const float* keys, int64_t ld_keys_b,
+                           int64_t ld_keys_t, int32_t T, const int64_t* keys_length, int64_t batch,
+                           int32_t H, const float* w1, const float* b1, const float* w2,
+                           const float* b2, const float* w3, const float* b3, int32_t use_softmax,
+                           float* out, int64_t ld_out, void* stream);
+
+/* Dice (din.py:26-36) in eval: p = sigmoid(x * bn_scale + bn_shift) with the BatchNorm folded
+ * by rk_bn_fold, y = alpha * (1 - p) * x + p * x;  x, y: [rows, n].                          */
+int rk_dice_forward(const float* x, int64_t ldx, int64_t rows, int32_t n, const float* bn_scale,
+                    const float* bn_shift, const float* alpha, float* y, int64_t ldy, void* stream);
+
 /* out_scalar = scale * mean_r ||x[r, col0:col0+ncols]||_2, deterministic two-stage sum;
  * workspace: RK_L2_WORKSPACE floats of device scratch.                                   */
 #define RK_L2_WORKSPACE 512
@@ -234,6 +250,11 @@ int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, in
 int rk_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T,
                      int32_t d_model, int32_t heads, const int64_t* seq_len, float* ctx,
                      int64_t ld_ctx, void* stream);
+/* key_padding_mask: [batch, ld_mask] bytes, nonzero = masked key (torch bool); NULL = none.
+ * A row with every key masked gives NaN context, as torch's softmax over all -inf.          */
+int rk_bst_attention_masked(const float* qkv, int64_t ld_qkv, int64_t batch, int32_t T,
+                            int32_t d_model, int32_t heads, const uint8_t* key_padding_mask,
+                            int64_t ld_mask, float* ctx, int64_t ld_ctx, void* stream);
 
 /* Every transformer block of BSTModel.forward plus the pooling (bst.py:66-91, 224-241) in one
  * launch, one workgroup per sample, activations kept in LDS:
@@ -479,7 +500,9 @@ int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t row
 int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
                        const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
                        const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
-                       float* workspace, void* stream);
+                       float* workspace, int64_t workspace_floats, void* stream);
+/* Floats rk_bst_ln_backward needs in `workspace` for model width d. */
+int64_t rk_bst_ln_backward_workspace_floats(int32_t d);
 int rk_bst_pos_backward(const float* dxp, int64_t batch, int32_t T, int32_t d, float* dpos, void* stream);
 int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, float slope, double dropout_p,
                          uint64_t seed, const int64_t* stream_slot, int32_t backward, float* out,

@@ -205,8 +205,9 @@ def test_training_mode_raises():
 
 @pytest.mark.gpu
 def test_standalone_reference_functions():
-    """cross_layer, residual_unit and din_attention as module-level functions (dcn.py:25,
-    deepcrossing.py:25, din.py:42) draw per call like the reference."""
+    """cross_layer, residual_unit and din_attention_gather (din_attention with the history as
+    table + index) as module-level functions (dcn.py:25, deepcrossing.py:25, din.py:42) draw per
+    call like the reference."""
     from oracle import reference_forward as ref
     g = torch.Generator().manual_seed(3)
     x0 = torch.randn(40, 50, generator=g)
@@ -232,7 +233,7 @@ def test_standalone_reference_functions():
         torch.manual_seed(13)
         expect = ref.din_attention(q, table[seq], lens, sm)
         torch.manual_seed(13)
-        got = rankops.din_attention(q.cuda(), table.cuda(), seq.cuda(), lens.cuda(), sm)
+        got = rankops.din_attention_gather(q.cuda(), table.cuda(), seq.cuda(), lens.cuda(), sm)
         torch.testing.assert_close(got.cpu(), expect, atol=ATOL, rtol=RTOL)
 
 

@@ -707,7 +707,10 @@ def _bst_step_check(cfg, B, seed, steps):
                 assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, n
                 continue
             scale = max(1e-3, float(want.abs().max()))  # floor: null-space parameters hold only noise
-            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=1e-3 * scale,
+            # absolute floor 1e-5: gradients reaching the embeddings through the dnn's train-mode
+            # BatchNorm (a difference of batch means) carry fp32 cancellation noise of a few 1e-6
+            # on both sides (observed 3.5e-6 once on embeddings.userid at the bench shape)
+            torch.testing.assert_close(prm.grad.cpu(), want, rtol=0, atol=max(1e-3 * scale, 1e-5),
                                        msg=lambda m: f"grad {n} step {step}: {m}")
         opt.step()
         ref_opt.step()
@@ -752,3 +755,81 @@ def test_dropout_mask_rate_and_freshness():
     assert set(torch.unique(m1).tolist()) == {0.0, float(torch.tensor(1 / 0.9, dtype=torch.float32))}
     assert (m1 != m2).float().mean().item() > 0.1  # a new stream draws a new mask
     assert int(counter) == 2
+
+
+# ------------------------------------------------------------------ eval after training (cache invalidation)
+
+def _eval_vs_oracle(model, name, cfg, inp, interaction=None, seed=17):
+    model.eval()
+    p = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        out = H.as_tuple(H.call_model(model, name, inp))
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        want = H.as_tuple(H.call_oracle(name, cfg, p, H.to_device(inp, "cpu"), interaction))
+    for i, (o, r) in enumerate(zip(out, want)):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.detach().cpu(), r, rtol=1e-4, atol=1e-4, msg=lambda m: f"{name}[{i}] {m}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,cfg", [("din", {"T": 20}), ("deepfm", {}), ("bst", {"T": 12, "dim": 16})])
+@pytest.mark.parametrize("opt_kind", ["rankops", "torch"])
+def test_eval_train_eval_uses_updated_running_stats(name, cfg, opt_kind):
+    """The reference loop (din.py:442-446): evaluate, train an epoch, evaluate again.  The second
+    eval must fold the BatchNorm / Dice running statistics the train kernels updated (they are
+    written through raw pointers), not the fold cached at the first eval."""
+    B = 256
+    model = H.build(name, cfg).cuda()
+    inp = H.to_device(H.make_inputs(name, cfg, B, seed=41), "cuda")
+    _eval_vs_oracle(model, name, cfg, inp)  # caches the eval folds
+    model.train()
+    opt = rankops.Adam(model.parameters(), lr=1e-2) if opt_kind == "rankops" else \
+        torch.optim.Adam(model.parameters(), lr=1e-2)
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(3)) < 0.3).float().cuda()
+    for _ in range(3):
+        opt.zero_grad()
+        out = H.as_tuple(H.call_model(model, name, inp))
+        logit_loss = name == "bst"
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(out[1].squeeze(), label) if logit_loss else \
+            torch.nn.functional.binary_cross_entropy(out[0].squeeze(), label)
+        loss.backward()
+        opt.step()
+    stats = [m.running_mean for m in model.modules() if isinstance(m, torch.nn.BatchNorm1d)]
+    assert stats, "config has no BatchNorm"
+    _eval_vs_oracle(model, name, cfg, inp)
+
+
+@pytest.mark.gpu
+def test_graph_replayed_train_steps_then_eval():
+    """Replays of a captured DIN train step change weights and running statistics without any
+    tensor-version bump; model.eval() must still invalidate the eval folds and packed weights."""
+    cfg = {"T": 20, "interaction_weights": "frozen"}
+    B = 256
+    inp = H.to_device(H.make_inputs("din", cfg, B, seed=51), "cuda")
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(5)) < 0.3).float().cuda()
+    torch.manual_seed(0)
+    model = H.build("din", cfg).cuda()
+    _eval_vs_oracle(model, "din", cfg, inp)  # draws the frozen att_net (same seed on both sides)
+    att = [t.detach().cpu() for t in model.att_weights._cached[1]]
+    _eval_vs_oracle(model, "din", cfg, inp, interaction=att)
+    model.train()
+    opt = rankops.Adam(model.parameters(), lr=1e-2, capturable=True)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        out = H.call_model(model, "din", inp)
+        (torch.nn.functional.binary_cross_entropy(out[0].squeeze(), label) + out[2]).backward()
+        opt.step()
+
+    step()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(4):
+        g.replay()
+    torch.cuda.synchronize()
+    _eval_vs_oracle(model, "din", cfg, inp, interaction=att)
