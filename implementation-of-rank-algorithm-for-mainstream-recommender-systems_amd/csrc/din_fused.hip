@@ -37,6 +37,9 @@ struct DinArgs {
   const float *w1, *b1, *w2, *b2, *w3, *b3;
   int use_softmax;
   float* l2_part;
+  unsigned* l2_count;  // zero between launches: the last workgroup to finish phase A resets it
+  float* l2_out;
+  float l2_scale;
   uint32_t* flags;
   rk_mlp_layer L[RK_MLP_MAX_LAYERS];
   int nl;
@@ -54,6 +57,20 @@ struct DinLds {
   static constexpr int BUF0 = NORM + 16;
 };
 
+#ifdef RK_DIN_PHASES  // timing build only (tools/din_phases.py): per-workgroup wall-clock marks
+constexpr int kDinPhaseWG = 1024;
+__device__ unsigned long long g_din_ts[kDinPhaseWG][4];       // entry, staged, phase A done, phase B done
+__device__ unsigned long long g_din_wave[kDinPhaseWG][16];    // per-wave phase-A cycles (clock64)
+#define DIN_TS(i)                                                                       \
+  do {                                                                                  \
+    if (tid == 0 && blockIdx.x < kDinPhaseWG) g_din_ts[blockIdx.x][i] = wall_clock64(); \
+  } while (0)
+#else
+#define DIN_TS(i) \
+  do {            \
+  } while (0)
+#endif
+
 template <int H>
 __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   using Ly = DinLds<H>;
@@ -66,6 +83,21 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5, hk = 4 * half;
+  DIN_TS(0);
+
+  // ---- per-sample tile counts, issued first (their latency overlaps the staging below): a sample
+  // needs ceil(min(len, T) / 32) attention tiles — positions past its length contribute exactly 0
+  // (plain: masked weight 0; softmax: exp(pad / sqrt(H) - max) underflows to 0) — except with
+  // softmax and len <= 0, where every position carries the same pad score and all T count.
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
+  const int ntiles_all = (a.T + 31) / 32;
+  int my_tiles = -1;  // lanes 0..15: tiles of sample m0 + lane (-1: past the batch)
+  int64_t my_len = 0;
+  if (lane < rows) {
+    my_len = a.seq_len[m0 + lane];
+    my_tiles = my_len <= 0 ? (a.use_softmax ? ntiles_all : 0) : (int)((min<int64_t>(my_len, a.T) + 31) / 32);
+  }
 
   // ---- stage the split attention weights and the column map
   for (int i = tid; i < 64 * H; i += kMlpThreads) {
@@ -92,16 +124,31 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     col_off[c] = off;
   }
   __syncthreads();
+  DIN_TS(1);
+#ifdef RK_DIN_PHASES
+  const unsigned long long wave_t0 = clock64();
+#endif
 
-  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
-  const int64_t b = m0 + wave;
+  // ---- balance the attention work over the SIMDs: waves w, w+4, w+8, w+12 share one SIMD, so
+  // wave w takes the sample of rank w in descending tile count (the longest four samples land on
+  // four different SIMDs, and so on).  Every wave computes the same ranking in registers.
+  int rank = 0;
+#pragma unroll
+  for (int j = 0; j < kMlpRows; ++j) {
+    const int tj = __shfl(my_tiles, j, kWave);
+    rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
+  }
+  const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
+  const int loc = pick ? __builtin_ctzll(pick) : wave;  // this wave's sample within the workgroup
+  const int ntiles = max(0, __shfl(my_tiles, loc, kWave));
+  const int64_t len = __shfl(my_len, loc, kWave);
+  const int64_t b = m0 + loc;
 #ifdef RK_DIN_SKIP_A  // timing experiment only (tools/din_phase_time.py): phase B on zero rows
   const bool live = false;
 #else
-  const bool live = wave < rows;
+  const bool live = loc < rows;
 #endif
-  float* row = buf0 + wave * a.ld0;
+  float* row = buf0 + loc * a.ld0;
   uint32_t* flags = a.flags;
 
   // ---- Phase A.1: the feature row (zero padded to pad64(width))
@@ -134,15 +181,12 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
 
-    const int64_t len = a.seq_len[b];
     const float sqrt_h = (float)__builtin_sqrt((double)H);
     const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
     float m_run = -INFINITY, l_run = 0.f;
     f32x4_t o[NQ];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) o[c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    const int ntiles = (a.T + 31) / 32;
-
     for (int tt = 0; tt < ntiles; ++tt) {
       // the weight/bias LDS reads below are loop-invariant; hoisting them out of the tile loop
       // costs ~96 VGPRs and spills at the 128-register budget of a 16-wave workgroup
@@ -245,11 +289,22 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     }
   }
   if (lane == 0) sm[Ly::NORM + wave] = norm_part;
+#ifdef RK_DIN_PHASES
+  if (lane == 0 && blockIdx.x < kDinPhaseWG) g_din_wave[blockIdx.x][wave] = clock64() - wave_t0;
+#endif
   __syncthreads();
+  DIN_TS(2);
+  // l2 partials: the last workgroup to publish its partial also finishes the mean, after its own
+  // phase B (hand-off per MI355X_MICROARCH.md: sc1 partial stores, vmcnt(0), one agent atomic
+  // add per workgroup; the adder that returns n-1 reads every partial with sc1 loads)
+  int& l2_last = *reinterpret_cast<int*>(col_seg + 512);
   if (a.l2_part && tid == 0) {
     float t = 0.f;
     for (int w = 0; w < kMlpRows; ++w) t += sm[Ly::NORM + w];
-    a.l2_part[blockIdx.x] = t;
+    __hip_atomic_store(a.l2_part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(a.l2_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    l2_last = prev == gridDim.x - 1;
   }
 
   // ---- Phase B: fcn tail + head over the 16 rows
@@ -257,6 +312,18 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   return;
 #endif
   mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid);
+  DIN_TS(3);
+  // (mlp_rows' barriers order tid 0's l2_last store before these reads)
+  if (a.l2_part && tid < 64 && l2_last) {
+    float t = 0.f;
+    for (int i = tid; i < (int)gridDim.x; i += 64)
+      t += __hip_atomic_load(a.l2_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = wave_sum(t);  // the order of row_l2norm_final_kernel (embedding.hip)
+    if (tid == 0) {
+      a.l2_out[0] = a.l2_scale * (t / (float)a.batch);
+      __hip_atomic_store(a.l2_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 }  // namespace rk
@@ -279,8 +346,8 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
   if (width <= 0 || width > 255 || q_col < 0 || q_col + H > width || att_col < 0 || att_col + H > width ||
       T <= 0 || ld_seq < T || key_rows <= 0 || ld_key < H || ld_key % 4 || ((uintptr_t)key_table & 15u))
     return fail(RK_ERR_INVALID, "rk_din_forward: bad row/sequence layout (width=%d T=%d H=%d)", width, T, H);
-  if (l2_out && (!l2_workspace || l2_col0 < 0 || l2_col0 >= width))
-    return fail(RK_ERR_INVALID, "rk_din_forward: l2 term needs a workspace of ceil(batch/16) floats");
+  if (l2_out && (!l2_workspace || l2_col0 < 0 || l2_col0 >= width || ((uintptr_t)l2_workspace & 3u)))
+    return fail(RK_ERR_INVALID, "rk_din_forward: l2 term needs a workspace of ceil(batch/16) + 1 words");
   DinArgs a = {};
   for (int s = 0; s < nseg; ++s) {
     const rk_segment& g = row_segs[s];
@@ -314,6 +381,9 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
   a.b3 = b3;
   a.use_softmax = use_softmax;
   a.l2_part = l2_out ? l2_workspace : nullptr;
+  a.l2_count = l2_out ? reinterpret_cast<unsigned*>(l2_workspace + (batch + kMlpRows - 1) / kMlpRows) : nullptr;
+  a.l2_out = l2_out;
+  a.l2_scale = l2_scale;
   a.flags = device_flags();
   a.ld0 = need0 + 4;
   a.ld1 = need1 + 4;
@@ -326,7 +396,7 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
     case 16: base = DinLds<16>::BUF0; break;
     default: base = DinLds<32>::BUF0; break;
   }
-  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + 512;
+  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + 512 + 16;
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
   hipStream_t st = (hipStream_t)stream;
   static bool attr_set = false;
@@ -342,6 +412,19 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
     default: din_forward_kernel<32><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
   }
   if (int e = check_launch("rk_din_forward")) return e;
-  if (l2_out) return launch_l2_final(l2_workspace, (int)blocks, batch, l2_scale, l2_out, st);
   return RK_OK;
 }
+
+#ifdef RK_DIN_PHASES
+RK_API int rk_debug_din_phases(unsigned long long* ts, unsigned long long* waves, unsigned long long* mlp) {
+  if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_din_ts), sizeof(g_din_ts)) != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_din_wave), sizeof(g_din_wave)) != hipSuccess) return 1;
+#ifdef RK_MLP_PHASES
+  if (hipMemcpyFromSymbol(mlp, HIP_SYMBOL(g_mlp_phase), sizeof(g_mlp_phase)) != hipSuccess) return 1;
+  (void)hipMemset(mlp, 0, 0);
+#else
+  (void)mlp;
+#endif
+  return 0;
+}
+#endif

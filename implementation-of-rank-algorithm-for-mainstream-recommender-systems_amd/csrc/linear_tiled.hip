@@ -41,11 +41,11 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
   const bool col_live = n < pad64(L.n);
 
   // weight stream of this lane's row over the whole K (ring of 4 chunks)
-  const float* wrow = L.w + (int64_t)(col_live ? n : 0) * L.ldw + kq;
+  const float* wrow = wfrag(L, col_live ? (n >> 4) : 0, lane);
   const int kchunks = a.Kp / 16;
   f32x4_t ring[kMlpPD];
 #pragma unroll
-  for (int s = 0; s < kMlpPD; ++s) ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s);
+  for (int s = 0; s < kMlpPD; ++s) ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * s);
   const ColEpi ep = col_epi(L, n < L.n ? n : 0);
 
   // A staging: block b covers columns [256 b, min(256 b + 256, Kp)); thread tid moves float4s
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
 #pragma unroll
           for (int t = 0; t < 2; ++t) acc[t] = mfma16(av[t][e], bv[e], acc[t]);
         const int cn = min(c + s + kMlpPD, kchunks - 1);
-        ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * cn);
+        ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * cn);
         __builtin_amdgcn_sched_barrier(0);
       }
       c += kMlpPD;

@@ -84,12 +84,19 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
 #endif
 }
 
+// Fragment-major image (mlp_core.h wfrag): element i of the image is lane (i >> 2) & 63, component
+// i & 3 of chunk c of column tile t, i >> 8 = t * kp/16 + c; that lane's value is W[16 t + (lane & 15)]
+// [16 c + 4 (lane >> 4) + (i & 3)], zero outside [n, k).
 __global__ void mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int n, int k, int np, int kp,
                                 float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)np * kp) return;
-  const int r = (int)(i / kp), c = (int)(i % kp);
-  out[i] = (r < n && c < k) ? w[(int64_t)r * ldw + c] : 0.f;
+  const int e = (int)(i & 3), lane = (int)((i >> 2) & 63);
+  const int64_t blk = i >> 8;
+  const int kch = kp / 16;
+  const int t = (int)(blk / kch), c = (int)(blk % kch);
+  const int r = 16 * t + (lane & 15), col = 16 * c + 4 * (lane >> 4) + e;
+  out[i] = (r < n && col < k) ? w[(int64_t)r * ldw + col] : 0.f;
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

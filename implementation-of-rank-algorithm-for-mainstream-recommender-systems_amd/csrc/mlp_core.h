@@ -30,6 +30,15 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 __host__ __device__ constexpr int pad64(int v) { return (v + kMlpPad - 1) / kMlpPad * kMlpPad; }
 
+// Packed weights are fragment-major (rk_mlp_pack_weight): the float4 a lane of column tile t
+// feeds to the 4 MFMAs of K-chunk c (16 k) sits at wfrag(L, t, lane) + kFragStep * c, so a wave's
+// chunk load is one contiguous, fully coalesced 1 KiB (8 whole cache lines) rather than sixteen
+// half lines of sixteen weight rows.  ldw is pad64(K), the image holds pad64(n) x pad64(K) floats.
+constexpr int kFragStep = 256;
+__device__ __forceinline__ const float* wfrag(const rk_mlp_layer& L, int tile, int lane) {
+  return L.w + (int64_t)tile * (L.ldw / 16) * kFragStep + 4 * lane;
+}
+
 __device__ __forceinline__ f32x4_t mfma16(float a, float b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -112,17 +121,17 @@ struct LayerPipe {
   f32x4_t ring[PD][TPW];
   ColEpi ep[TPW];
   __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int wave, int lane) {
-    const int li = lane & 15, kq = 4 * (lane >> 4);
+    const int li = lane & 15;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int n = 16 * (wave + kMlpWaves * j) + li;
-      wrow[j] = L.w + (int64_t)n * L.ldw + kq;
+      wrow[j] = wfrag(L, wave + kMlpWaves * j, lane);
       ep[j] = col_epi(L, n < L.n ? n : 0);
     }
 #pragma unroll
     for (int s = 0; s < PD; ++s)
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + 16 * s);
+      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * s);
   }
 };
 
@@ -165,7 +174,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_la
       // refill this slot with chunk c + PD (clamped: the tail re-reads the last chunk, unused)
       const int cn = min(c + PD, kchunks - 1);
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) P.ring[s][j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + 16 * cn);
+      for (int j = 0; j < TPW; ++j) P.ring[s][j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + kFragStep * cn);
       // keep the refill here: sinking it to the end of the unrolled body would leave each
       // slot's latency uncovered by the other slots' MFMAs
       __builtin_amdgcn_sched_barrier(0);

@@ -273,6 +273,23 @@ def linear_tiled(x: torch.Tensor, layer: "_lib.MlpLayer", out: torch.Tensor, K: 
     return out
 
 
+_DIN_L2_WS = {}
+
+
+def _din_l2_workspace(device, batch):
+    """rk_din_forward's l2 workspace: ceil(batch/16) partials + a completion counter that starts at
+    zero and that every launch leaves at zero, so it is allocated (zeroed) once per device and
+    size and reused, also by a hipGraph captured after a warm-up call.  DIN forwards of one batch
+    size on one device therefore must not run concurrently on two streams."""
+    n = (batch + 15) // 16 + 1
+    key = (str(torch.device(device)), n)
+    ws = _DIN_L2_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(n, device=device, dtype=torch.float32)
+        _DIN_L2_WS[key] = ws
+    return ws
+
+
 def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
                 head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None):
     """Whole DIN eval forward (row gather, attention, fcn tail, head, l2 partials) in one launch."""
@@ -283,7 +300,7 @@ def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_wei
     larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
     ws = None
     if l2_out is not None:
-        ws = torch.empty((batch + 15) // 16, device=device, dtype=torch.float32)
+        ws = _din_l2_workspace(device, batch)
     check(lib.rk_din_forward(arr, len(segs), width, q_col, att_col, ptr(key_table), key_table.shape[0],
                              key_table.stride(0), ptr(seq), seq.stride(0), seq.shape[1], ptr(seq_len), batch, H,
                              ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3), ptr(b3), 1 if use_softmax else 0, larr,

@@ -225,12 +225,14 @@ int rk_dice_forward(const float* x, int64_t ldx, int64_t rows, int32_t n, const 
 int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols,
                        float scale, float* workspace, float* out_scalar, void* stream);
 
-/* Whole DIN eval forward (din.py:294-323) in one launch + a one-wave l2 finish:
+/* Whole DIN eval forward (din.py:294-323) in one launch:
  *   row[b] = concat(row_segs)  (width <= 255; target query at q_col, attention written at att_col)
  *   row[b, att_col:+H] = din_attention(row[b, q_col:+H], key_table[seq[b]], seq_len[b])
  *   head outputs = fcn layers (rk_mlp_layer, packed) + head (head_w/head_b/head_logit/head_prob)
- *   l2_out = l2_scale * mean_b ||row[b, l2_col0:width]||_2 when l2_out != NULL
- *     (l2_workspace: ceil(batch/16) floats).  H in {8, 16, 32}.                            */
+ *   l2_out = l2_scale * mean_b ||row[b, l2_col0:width]||_2 when l2_out != NULL, finished in
+ *     the same launch by the last workgroup.  l2_workspace: ceil(batch/16) floats of partials
+ *     followed by one uint32 counter that must be 0 before the first call (the kernel leaves it
+ *     0 again; keep one workspace per stream).  H in {8, 16, 32}.                          */
 int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col,
                    int32_t att_col, const float* key_table, int64_t key_rows, int64_t ld_key,
                    const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
@@ -277,8 +279,11 @@ int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_pe
               const float* w, int64_t ldw, int64_t M, int32_t N, int32_t K,
               const rk_epilogue* ep, float* y, int64_t ldy, void* stream);
 
-/* Packed layout of a fused-MLP weight: [pad64(n), pad64(k)], zero filled (rows and K padded to
- * 64 so the kernel's loads are unconditional aligned float4s).  Pack once at load time.    */
+/* Packed layout of a fused-MLP weight: pad64(n) x pad64(k) floats, zero filled (rows and K
+ * padded to 64 so the kernel's loads are unconditional aligned float4s), fragment-major: the
+ * 16-column x 16-k block (t, c) is 256 contiguous floats in the order the MFMA lanes load it
+ * (float i of the block = W[16t + ((i>>2)&15)][16c + 4((i>>2)>>4) + (i&3)]).  Pack once at load
+ * time; rows/cols of rk_mlp_packed_size give the size and ldw = cols.                       */
 int rk_mlp_packed_size(int32_t n, int32_t k, int64_t* rows, int64_t* cols);
 int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k, float* out, void* stream);
 

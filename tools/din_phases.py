@@ -1,0 +1,55 @@
+"""Phase split of din_forward_kernel<32> at the bench's DIN configs[2] workload, from a timing
+build of the library (make EXTRA=-DRK_DIN_PHASES OUT=<lib> BUILD=build_phases; point RANKOPS_LIB
+at it).  Per workgroup: wall-clock (100 MHz) marks at entry, after staging, after phase A
+(attention), after phase B (fcn tail); per wave: phase-A cycles.  Prints the distributions."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+import torch  # noqa: E402
+
+batch = int(os.environ.get("BATCH", "4096"))
+model, inp, fn, cfg, name = bench.workload("din", batch, 0)
+launch = model.fused_kernel_launcher(inp["dense"], inp["category"], inp["sequence"], inp["target"])
+us = 1e3 * bench.kernel_avg_ms(launch)
+torch.cuda.synchronize()
+n_launch = 5 + 50 + 1  # kernel_avg_ms warm-up + timed, and the launch below (RK_MLP_PHASES accumulates)
+launch()
+torch.cuda.synchronize()
+from rankops import _lib  # noqa: E402
+lib = _lib.load()
+ts = (ctypes.c_ulonglong * (1024 * 4))()
+wv = (ctypes.c_ulonglong * (1024 * 16))()
+ml = (ctypes.c_ulonglong * (3 * 8 + 2))()
+lib.rk_debug_din_phases.argtypes = [ctypes.c_void_p] * 3
+assert lib.rk_debug_din_phases(ts, wv, ml) == 0
+nwg = min(1024, (batch + 15) // 16)
+t = np.array(ts, dtype=np.int64).reshape(1024, 4)[:nwg] * 10  # ns
+w = np.array(wv, dtype=np.int64).reshape(1024, 16)[:nwg]
+t0 = t[:, 0].min()
+rel = (t - t0) / 1e3  # us from the first workgroup's entry
+lens = inp["sequence"]["his_read_comment_7d_seq_length"].cpu().numpy()
+
+
+def q(x):
+    return f"min {np.min(x):7.2f}  med {np.median(x):7.2f}  max {np.max(x):7.2f}"
+
+
+print(f"kernel avg {us:.2f} us (events), {nwg} workgroups")
+print("entry        ", q(rel[:, 0]))
+print("staging      ", q((t[:, 1] - t[:, 0]) / 1e3))
+print("phase A      ", q((t[:, 2] - t[:, 1]) / 1e3))
+print("phase B      ", q((t[:, 3] - t[:, 2]) / 1e3))
+print("end          ", q(rel[:, 3]))
+print("wave A cycles", q(w.reshape(-1) / 1e3), "(k cycles)")
+print("wave A max/mean per WG", q(w.max(1) / np.maximum(w.mean(1), 1)))
+print("lengths: mean", lens.mean(), "frac <= 32:", (lens <= 32).mean())
+mlp = np.array(ml, dtype=np.float64)
+if mlp.any():
+    per = mlp / (n_launch * nwg) / 1e3
+    for l in range(3):
+        print(f"layer {l}: mfma done {per[3*l]:6.2f}  epilogue stored {per[3*l+1]:6.2f}  barrier {per[3*l+2]:6.2f} (k cycles, wave 0)")
