@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step legs")
     return ap.parse_args()
 
 
@@ -293,23 +294,29 @@ def bench_sharded(world, rank, steps, warmup):
     out_r, in_r = model.row_splits(B_l)
     recv_idx = torch.empty(sum(out_i), dtype=torch.int64, device=dev)
     recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
-    g1, send = graph_of(lambda: model.pack_indices(cat))
-    g2, rows = graph_of(lambda: model.gather_local(recv_idx, world * B_l))
-    g3, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_l))
+    if world == 1:  # nothing to exchange: one packed FM gather + the tail, one hipGraph
+        g0, _ = graph_of(lambda: model.run_steps(cat))
+        step = g0.replay
+    else:
+        g1, send = graph_of(lambda: model.pack_indices(cat))
+        g2, rows = graph_of(lambda: model.gather_local(recv_idx, world * B_l))
+        g3, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_l))
 
-    def step():
-        g1.replay()
-        model._exchange(recv_idx, send, out_i, in_i)
-        g2.replay()
-        model._exchange(recv_rows, rows.reshape(-1), out_r, in_r)
-        g3.replay()
+        def step():
+            g1.replay()
+            model._exchange(recv_idx, send, out_i, in_i)
+            g2.replay()
+            model._exchange(recv_rows, rows.reshape(-1), out_r, in_r)
+            g3.replay()
 
     t = max_over_ranks(world, time_replays(step, steps, warmup, world))
     wire = B_l * SHARDED_FIELDS * (8 + 4 * row_stride(32)) * (world - 1) / world
     return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
             "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
-            "scaling": "strong", "mode": "3 hipGraph segments + eager RCCL all_to_all_single"}
+            "scaling": "strong",
+            "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
+                     "3 hipGraph segments + eager RCCL all_to_all_single")}
 
 
 # ------------------------------------------------------------------ host input path
@@ -606,7 +613,7 @@ def main():
             result["loader"] = bench_loader(model, args.batch)
         except Exception as exc:  # reported, never fatal for the headline line
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
-    if rank == 0 and world == 1 and not args.no_extras:
+    if rank == 0 and world == 1 and not args.no_extras and not args.no_train:
         try:
             result["train"] = {m: bench_train(2048 if m == "bst" else args.batch, max(10, args.steps // 2), 3, m)
                                for m in ("dcn", "deepcrossing", "deepfm", "din", "afm", "bst", "fwfm")}

@@ -166,8 +166,11 @@ struct FmTables {
 // Modes: kFmTables — embedding tables, any index/row strides; kFmPacked — embedding tables with
 // one shared unit-stride index array per field (first- and second-order) and contiguous rows
 // (nn.Embedding's layout, DeepFM's call): 5 descriptor words per field instead of 11;
-// kFmDense — row b of src (the sharded path's received rows).
-constexpr int kFmTables = 0, kFmPacked = 1, kFmDense = 2;
+// kFmDense — row b of src (the sharded path's received rows); kFmRowPacked — one packed
+// [V, RS] table per field (rk_fm_pack_table: the dim second-order floats, then the first-order
+// weight at column dim), one unit-stride index array: the weight shares the row's line pair
+// instead of costing a lone 4-B load (and its own 128-B line) in a separate [V, 1] table.
+constexpr int kFmTables = 0, kFmPacked = 1, kFmDense = 2, kFmRowPacked = 3;
 template <int G, int MODE>  // G = quads per row = dim / 4
 __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64_t batch, float* __restrict__ deep_in,
                                                         int64_t ld_deep, float* __restrict__ fm1,
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64
     for (int i = 0; i < CH; ++i) {
       if constexpr (MODE == kFmDense) {
         r2[i] = r1[i] = b;
-      } else if constexpr (MODE == kFmPacked) {
+      } else if constexpr (MODE == kFmPacked || MODE == kFmRowPacked) {
         r2[i] = r1[i] = t.idx2[fi[i]][b];
       } else {
         r2[i] = t.idx2[fi[i]][b * t.istride2[fi[i]]];
@@ -207,14 +210,18 @@ __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64
     float w1[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      constexpr bool kDense = MODE == kFmDense, kPacked = MODE == kFmPacked;
+      constexpr bool kDense = MODE == kFmDense, kPacked = MODE == kFmPacked, kRow = MODE == kFmRowPacked;
       const bool ok2 = kDense || (uint64_t)r2[i] < (uint64_t)t.rows2[fi[i]];
-      const bool ok1 = kDense || kPacked ? ok2 : (uint64_t)r1[i] < (uint64_t)t.rows1[fi[i]];
+      const bool ok1 = kDense || kPacked || kRow ? ok2 : (uint64_t)r1[i] < (uint64_t)t.rows1[fi[i]];
       oob |= live[i] && !(ok2 && ok1);
       const int64_t ld2 = kPacked ? 4 * G : t.ld2[fi[i]], ld1 = kPacked ? 1 : t.ld1[fi[i]];
       // (nontemporal row loads measured no faster: 143 vs 144 us at batch 65536)
-      v[i] = *reinterpret_cast<const f32x4*>(t.src2[fi[i]] + (ok2 ? r2[i] : 0) * ld2 + 4 * q);
-      w1[i] = t.src1[fi[i]][(ok1 ? r1[i] : 0) * ld1];
+      const float* row = t.src2[fi[i]] + (ok2 ? r2[i] : 0) * ld2;
+      v[i] = *reinterpret_cast<const f32x4*>(row + 4 * q);
+      if constexpr (kRow)
+        w1[i] = row[4 * G];  // the first-order weight sits right after the row's dim floats
+      else
+        w1[i] = t.src1[fi[i]][(ok1 ? r1[i] : 0) * ld1];
       if (!(live[i] && ok2)) v[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
       if (!(live[i] && ok1) || q != 0) w1[i] = 0.f;
     }
@@ -281,6 +288,26 @@ __global__ __launch_bounds__(64) void row_l2norm_final_kernel(const float* __res
   if (threadIdx.x == 0) out[0] = scale * (t / (float)rows);
 }
 
+// Packed FM table: out[r, 0:dim] = second[r, :], out[r, dim] = first[r, 0], zero pad to ld_out.
+// One thread per float4 of the output (ld_out % 4 == 0), a one-off layout pass per weight version.
+__global__ __launch_bounds__(256) void fm_pack_table_kernel(const float* __restrict__ second, int64_t ld2,
+                                                            const float* __restrict__ first, int64_t ld1,
+                                                            int64_t rows, int dim, float* __restrict__ out,
+                                                            int64_t ld_out) {
+  const int quads = (int)(ld_out / 4);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * quads) return;
+  const int64_t r = i / quads;
+  const int c0 = (int)(i - r * quads) * 4;
+  f32x4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + k;
+    v[k] = c < dim ? second[r * ld2 + c] : c == dim ? first[r * ld1] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(out + r * ld_out + c0) = v;
+}
+
 __global__ void bn_fold_kernel(const float* __restrict__ mean, const float* __restrict__ var,
                                const float* __restrict__ weight, const float* __restrict__ bias, float eps, int n,
                                float* __restrict__ scale, float* __restrict__ shift) {
@@ -309,6 +336,9 @@ static int check_segments(const rk_segment* segs, int nseg, const char* what) {
   }
   return RK_OK;
 }
+
+int launch_fm_gather(const FmTables& t, int mode, int num_fields, int G, int64_t batch, float* deep_in,
+                     int64_t ld_deep, float* fm1, float* fm2, hipStream_t st);
 
 }  // namespace rk
 
@@ -414,8 +444,53 @@ RK_API int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_
     for (int f = 0; f < num_fields; ++f) t.rows2[f] = std::min(t.rows2[f], t.rows1[f]);
   const int mode = dense ? kFmDense : packed ? kFmPacked : kFmTables;
   if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_fm_gather: negative batch");
+  return launch_fm_gather(t, mode, num_fields, G, batch, deep_in, ld_deep, fm1, fm2, (hipStream_t)stream);
+}
+
+RK_API int rk_fm_pack_table(const float* second, int64_t ld_second, const float* first, int64_t ld_first,
+                            int64_t rows, int32_t dim, float* out, int64_t ld_out, void* stream) {
+  if (!second || !first || !out || rows < 0 || dim <= 0 || ld_second < dim || ld_first < 1 || ld_out < dim + 1 ||
+      ld_out % 4 != 0 || !aligned16(out))
+    return fail(RK_ERR_INVALID, "rk_fm_pack_table: bad arguments (dim %d, ld_out %lld)", dim, (long long)ld_out);
+  if (rows == 0) return RK_OK;
+  const int64_t n = rows * (ld_out / 4);
+  fm_pack_table_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(second, ld_second, first,
+                                                                                    ld_first, rows, dim, out, ld_out);
+  return check_launch("rk_fm_pack_table");
+}
+
+RK_API int rk_fm_gather_packed(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                               float* deep_in, int64_t ld_deep, float* fm1, float* fm2, void* stream) {
+  if (num_fields <= 0 || num_fields > kFmMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather_packed: %d fields (max %d)", num_fields, kFmMaxFields);
+  if (int e = check_segments(fields, num_fields, "rk_fm_gather_packed")) return e;
+  if (!deep_in || !fm1 || !fm2 || ld_deep % 4 != 0 || !aligned16(deep_in))
+    return fail(RK_ERR_INVALID, "rk_fm_gather_packed: outputs must be non-null, 16-B aligned, ld %% 4 == 0");
+  if (dim % 4 != 0 || dim < 4 || dim > 256 || ((dim / 4) & (dim / 4 - 1)))
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather_packed: dim %d must be 4 * a power of two <= 256", dim);
+  FmTables t;
+  for (int f = 0; f < num_fields; ++f) {
+    const rk_segment& s = fields[f];
+    if (!s.idx || s.idx_stride != 1 || s.dim != dim || s.src_ld < dim + 1 || s.src_ld % 4 || !aligned16(s.src) ||
+        s.out_col % 4 || s.out_col + dim > ld_deep)
+      return fail(RK_ERR_INVALID, "rk_fm_gather_packed: field %d is not a unit-stride packed [rows, >= dim+1] table",
+                  f);
+    t.src2[f] = t.src1[f] = s.src;
+    t.idx2[f] = t.idx1[f] = s.idx;
+    t.istride2[f] = t.istride1[f] = 1;
+    t.ld2[f] = t.ld1[f] = s.src_ld;
+    t.rows2[f] = t.rows1[f] = s.rows;
+    t.col[f] = s.out_col;
+  }
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_fm_gather_packed: negative batch");
+  return launch_fm_gather(t, kFmRowPacked, num_fields, dim / 4, batch, deep_in, ld_deep, fm1, fm2,
+                          (hipStream_t)stream);
+}
+
+namespace rk {
+int launch_fm_gather(const FmTables& t, int mode, int num_fields, int G, int64_t batch, float* deep_in,
+                     int64_t ld_deep, float* fm1, float* fm2, hipStream_t st) {
   const int64_t blocks = (batch + 3) / 4;  // one wave per sample, 4 waves per workgroup
-  hipStream_t st = (hipStream_t)stream;
   uint32_t* fl = device_flags();
 #define RK_FM_LAUNCH(GG, MM) \
   fm_gather_kernel<GG, MM><<<(unsigned)blocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl)
@@ -425,6 +500,8 @@ RK_API int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_
       RK_FM_LAUNCH(GG, kFmDense);                        \
     else if (mode == kFmPacked)                          \
       RK_FM_LAUNCH(GG, kFmPacked);                       \
+    else if (mode == kFmRowPacked)                       \
+      RK_FM_LAUNCH(GG, kFmRowPacked);                    \
     else                                                 \
       RK_FM_LAUNCH(GG, kFmTables);                       \
     break;
@@ -437,12 +514,13 @@ RK_API int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_
     RK_FM_CASE(32)
     RK_FM_CASE(64)
     default:
-      return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim %d", dim);
+      return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim %d", 4 * G);
   }
 #undef RK_FM_CASE
 #undef RK_FM_LAUNCH
   return check_launch("rk_fm_gather");
 }
+}  // namespace rk
 
 RK_API int rk_row_l2norm_mean(const float* x, int64_t ld, int64_t rows, int32_t col0, int32_t ncols, float scale,
                               float* workspace, float* out_scalar, void* stream) {

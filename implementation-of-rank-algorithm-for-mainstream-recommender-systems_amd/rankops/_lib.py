@@ -123,6 +123,10 @@ SIGNATURES = {
         ctypes.c_int,
         [_SEG_P, _SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     ),
+    "rk_fm_pack_table": (
+        ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p]),
+    "rk_fm_gather_packed": (
+        ctypes.c_int, [_SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rk_din_attention": (
         ctypes.c_int,
         [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32,

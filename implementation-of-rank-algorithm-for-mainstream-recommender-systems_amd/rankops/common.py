@@ -185,6 +185,25 @@ class Packed:
         return self._val
 
 
+class PackedFMTable:
+    """One field's [V, D] second-order and [V, 1] first-order embedding weights as one packed
+    [V, pad4(D+1)] table (rk_fm_pack_table), rebuilt only when either weight's storage or version
+    changes or the module moved / switched mode (_GENERATION)."""
+
+    def __init__(self):
+        self._key = None
+        self._val = None
+
+    def __call__(self, second: torch.Tensor, first: torch.Tensor) -> torch.Tensor:
+        k = _key((second, first)) + (tuple(second.shape),)
+        if k != self._key:
+            self._val = None  # release the stale image before allocating its replacement
+            D = second.shape[1]
+            self._val = ops.fm_pack_table(second.detach(), first.detach(), (D + 1 + 3) // 4 * 4)
+            self._key = k
+        return self._val
+
+
 _CONST = {}
 
 

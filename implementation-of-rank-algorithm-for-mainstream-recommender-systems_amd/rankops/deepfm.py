@@ -10,7 +10,9 @@ Beyond the reference's six wechat fields the constructor takes `vocab_sizes={fie
 (any field names, dict order = field order) so the 30-field benchmark configuration runs
 through the same class; with the default wechat vocabulary it is the reference model.
 
-Launches: rk_fm_gather (both embedding orders, fm1, fm2 and the deep input in one pass), then
+Launches: rk_fm_gather_packed (both embedding orders, fm1, fm2 and the deep input in one pass over
+one packed [V, pad4(D+1)] table per field, built once per weight version by rk_fm_pack_table;
+PACKED_TABLES = False gathers from the two nn.Embedding weights with rk_fm_gather), then
 the deep layers on rk_linear with BatchNorm folded into the epilogue; the last one also
 evaluates deep_output_layer, final_layer(3->1) and the sigmoid.
 """
@@ -20,9 +22,12 @@ import torch
 import torch.nn as nn
 
 from . import ops, train
-from .common import EngineModule, Layer, check_eval, load_vocabulary, run_tail, table_rows
+from .common import EngineModule, Layer, PackedFMTable, check_eval, load_vocabulary, run_tail, table_rows
 
 WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
+# Eval gather from packed [V, pad4(D+1)] tables (one line pair per row instead of a row line plus
+# a separate line for the 4-B first-order weight; costs one extra table copy in HBM).
+PACKED_TABLES = True
 
 
 class DeepFM(EngineModule):
@@ -59,37 +64,60 @@ class DeepFM(EngineModule):
         self.deep_output_layer = nn.Linear(width, 1)
         self.final_layer = nn.Linear(3, 1)
         self._dropout = train.DropoutStreams()
+        self._fm_packs = {}  # field -> PackedFMTable (eval gather layout, not part of the state_dict)
 
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
+
+    def packed_table(self, name):
+        """The packed [V, pad4(D+1)] eval table of field `name` (cached per weight version)."""
+        pk = self._fm_packs.get(name)
+        if pk is None:
+            pk = self._fm_packs[name] = PackedFMTable()
+        return pk(self.second_order_embeddings[name].weight, self.first_order_embeddings[name].weight)
 
     def _gather_plan(self, names, category):
         D = self.embedding_dim
         first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
         B, dev = first.shape[0], first.device
+        packed = PACKED_TABLES and D % 4 == 0 and (D // 4) & (D // 4 - 1) == 0 and D <= 256
         second_segs, first_segs = [], []
         for f, name in enumerate(names):
             idx = ops.as_index(category[name], f"category[{name!r}]")
-            second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
-            first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
+            if packed:
+                if idx.stride(0) != 1:
+                    idx = idx.contiguous()
+                second_segs.append(ops.packed_segment(self.packed_table(name), idx, D, f * D))
+                first_segs.append(idx)  # keeps a contiguous copy alive for the launch
+            else:
+                second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
+                first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
         deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32)
         fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        return (second_segs, first_segs, D, B, deep_in, fm1, fm2)
+        return (packed, second_segs, first_segs, D, B, deep_in, fm1, fm2)
+
+    @staticmethod
+    def _launch(plan):
+        packed, second, first, D, B, deep_in, fm1, fm2 = plan
+        if packed:
+            ops.fm_gather_packed(second, D, B, deep_in, fm1, fm2)
+        else:
+            ops.fm_gather(second, first, D, B, deep_in, fm1, fm2)
 
     def _gather_fm(self, names, category):
-        """rk_fm_gather: both embedding orders, fm1, fm2 and the deep input row in one pass
-        (deepfm.py:122-140,142)."""
+        """rk_fm_gather_packed / rk_fm_gather: both embedding orders, fm1, fm2 and the deep input
+        row in one pass (deepfm.py:122-140,142)."""
         plan = self._gather_plan(names, category)
-        ops.fm_gather(*plan)
-        return plan[4], plan[5], plan[6]
+        self._launch(plan)
+        return plan[5], plan[6], plan[7]
 
     def gather_launcher(self, category):
-        """Zero-argument re-launch of this forward's rk_fm_gather kernel, for kernel-level timing
+        """Zero-argument re-launch of this forward's FM gather kernel, for kernel-level timing
         (bench.py gather roofline)."""
         names = [c for c in self.second_order_embeddings if c in category]
         plan = self._gather_plan(names, category)
-        return lambda: ops.fm_gather(*plan)
+        return lambda: self._launch(plan)
 
     def forward(self, category):
         if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):

@@ -57,6 +57,13 @@ def table_segment(weight: torch.Tensor, idx: torch.Tensor, out_col: int, idx_str
                    weight.shape[1], out_col)
 
 
+def packed_segment(packed: torch.Tensor, idx: torch.Tensor, dim: int, out_col: int) -> Segment:
+    """Packed FM-table segment (rk_fm_gather_packed): row packed[idx[b]], D floats + weight at D."""
+    if idx.dim() != 1 or idx.stride(0) != 1:
+        raise ValueError("rankops: packed FM gather needs unit-stride 1-D indices")
+    return Segment(packed.data_ptr(), idx.data_ptr(), 1, packed.stride(0), packed.shape[0], dim, out_col)
+
+
 def dense_segment(src: torch.Tensor, dim: int, out_col: int, col_offset: int = 0) -> Segment:
     """Dense segment: src[b, col_offset:col_offset+dim] -> out[b, out_col:+dim] (src is [B] or [B, *])."""
     if src.dim() == 1:
@@ -102,6 +109,28 @@ def fm_gather(second, first, dim, batch, deep_in, fm1, fm2):
     a2, a1 = _seg_array(second), _seg_array(first)
     check(lib.rk_fm_gather(a2, a1, len(second), dim, batch, ptr(deep_in), deep_in.stride(0), ptr(fm1), ptr(fm2),
                            _lib.stream_of(deep_in)), "rk_fm_gather")
+
+
+def fm_pack_table(second: torch.Tensor, first: torch.Tensor, row_stride: int) -> torch.Tensor:
+    """rk_fm_pack_table: [V, D] + [V, 1] -> one [V, row_stride] table (row, then the weight at D)."""
+    lib = _lib.load()
+    _lib.ensure_device(second.device)
+    V, D = second.shape
+    if first.shape[0] != V or second.stride(1) != 1:
+        raise ValueError("rankops.fm_pack_table: tables of one field must have the same rows")
+    out = torch.empty(V, row_stride, device=second.device, dtype=torch.float32)
+    check(lib.rk_fm_pack_table(ptr(second), second.stride(0), ptr(first), first.stride(0), V, D, ptr(out),
+                               row_stride, _lib.stream_of(out)), "rk_fm_pack_table")
+    return out
+
+
+def fm_gather_packed(fields, dim, batch, deep_in, fm1, fm2):
+    """rk_fm_gather_packed: fields = table_segment(packed table, idx, out_col) per field."""
+    lib = _lib.load()
+    _lib.ensure_device(deep_in.device)
+    arr = _seg_array(fields)
+    check(lib.rk_fm_gather_packed(arr, len(fields), dim, batch, ptr(deep_in), deep_in.stride(0), ptr(fm1),
+                                  ptr(fm2), _lib.stream_of(deep_in)), "rk_fm_gather_packed")
 
 
 def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, use_softmax, out_ptr, ld_out,

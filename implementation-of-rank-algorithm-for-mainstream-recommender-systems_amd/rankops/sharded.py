@@ -7,14 +7,16 @@ rank holds a data-parallel slice of B_l samples with the indices of all F fields
 
   1. index exchange   all_to_all_single: rank r receives, from every source s, the indices of
                       r's fields for s's samples, laid out [s][b][f_r] (int64)
-  2. local gather     rk_concat_gather on r's tables -> rows [s][b][f_r][RS] with the D
-                      second-order floats at 0..D-1 and the first-order weight at D
-                      (RS = D + 1 rounded up to 4 floats so every row stays 16-B aligned)
+  2. local gather     one rk_concat_gather from r's packed tables (rk_fm_pack_table: per field
+                      one [V_f, RS] table, the D second-order floats at 0..D-1 and the
+                      first-order weight at D, RS = D + 1 rounded up to 4 floats so every row
+                      stays 16-B aligned) -> rows [s][b][f_r][RS], one contiguous read per row
   3. row exchange     all_to_all_single back: each source gets [r][b][f_r][RS] from every owner
   4. FM + MLP         rk_fm_gather over the received rows (dense segments, field order restored
                       through out_col = f * D), then the fused MLP tail exactly as DeepFM
 
-At P = 1 both exchanges are skipped and the path equals `DeepFM.forward` on the same weights.
+At P = 1 there is nothing to exchange: the forward is one rk_fm_gather_packed pass over the
+packed tables plus the tail, i.e. `DeepFM.forward` on the same weights.
 The exchange volume per rank and step is B_l * F * (8 + 4 * RS) bytes, (P-1)/P of it on the
 wire.  Reference: DeepFM.forward, deepfm.py:121-151 (the reference is single-device; the
 sharding is the MI355X build's own).
@@ -26,7 +28,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
-from .common import EngineModule, Layer, check_eval, run_tail
+from .common import EngineModule, Layer, PackedFMTable, check_eval, run_tail
 
 
 def row_stride(dim: int) -> int:
@@ -77,6 +79,11 @@ class ShardedDeepFM(EngineModule):
             width = unit
         self.deep_output_layer = nn.Linear(width, 1)
         self.final_layer = nn.Linear(3, 1)
+        self._fm_packs = {f: PackedFMTable() for f in self.local_fields}
+
+    def packed_table(self, f):
+        """This rank's packed [V_f, RS] table of field f (cached per weight version)."""
+        return self._fm_packs[f](self.second_order_embeddings[f].weight, self.first_order_embeddings[f].weight)
 
     @classmethod
     def from_deepfm(cls, model, *, group=None, rank=None, world_size=None):
@@ -137,13 +144,11 @@ class ShardedDeepFM(EngineModule):
         out = torch.empty(rows_total, F_me * RS, device=recv_idx.device, dtype=torch.float32)
         if F_me == 0 or rows_total == 0:
             return out
-        second, first = [], []
+        segs = []
         for j, f in enumerate(self.local_fields):
             idx = recv_idx[j:]  # element (R, j) sits at R * F_me + j
-            second.append(ops.table_segment(self.second_order_embeddings[f].weight, idx, j * RS, idx_stride=F_me))
-            first.append(ops.table_segment(self.first_order_embeddings[f].weight, idx, j * RS + D, idx_stride=F_me))
-        ops.concat_gather(second, rows_total, out)  # 16-B rows: vectorised path
-        ops.concat_gather(first, rows_total, out)
+            segs.append(ops.table_segment(self.packed_table(f), idx, j * RS, idx_stride=F_me))
+        ops.concat_gather(segs, rows_total, out)  # whole packed rows, 16-B vectorised path
         return out
 
     def exchange_rows(self, rows: torch.Tensor, B_l: int) -> torch.Tensor:
@@ -171,6 +176,25 @@ class ShardedDeepFM(EngineModule):
         fm1 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
         ops.fm_gather(second, first, D, B_l, deep_in, fm1, fm2)
+        return self._tail_of(deep_in, fm1, fm2)
+
+    def local_fm_and_tail(self, cat: dict):
+        """P = 1: the FM gather straight from the packed tables (one pass), then the tail."""
+        D = self.embedding_dim
+        B_l = cat[self.fields[0]].shape[0]
+        dev = self._device()
+        segs = []
+        for i, f in enumerate(self.fields):
+            idx = cat[f] if cat[f].stride(0) == 1 else cat[f].contiguous()
+            segs.append(ops.packed_segment(self.packed_table(f), idx, D, i * D))
+        deep_in = torch.empty(B_l, len(self.fields) * D, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        ops.fm_gather_packed(segs, D, B_l, deep_in, fm1, fm2)
+        return self._tail_of(deep_in, fm1, fm2)
+
+    def _tail_of(self, deep_in, fm1, fm2):
+        B_l, dev = deep_in.shape[0], deep_in.device
         deep = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
         total = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
@@ -192,6 +216,8 @@ class ShardedDeepFM(EngineModule):
         return self.run_steps(cat)
 
     def run_steps(self, cat: dict):
+        if self.world == 1:
+            return self.local_fm_and_tail(cat)
         B_l = cat[self.fields[0]].shape[0]
         recv_idx = self.exchange_indices(cat, B_l)
         rows = self.gather_local(recv_idx, self.world * B_l)

@@ -18,6 +18,7 @@
  *                                                            din.py:296-305,310, bst.py:218-224,243
  *   rk_dcn_cross       cross_layer() loop + output_layer part dcn.py:25-50,171-173,177-178
  *   rk_fm_gather       DeepFM first/second-order FM + concat deepfm.py:122-142
+ *   rk_fm_pack_table, rk_fm_gather_packed  the same over one packed [V, pad4(D+1)] table per field
  *   rk_linear          nn.Linear (+BatchNorm1d eval, ReLU/LeakyReLU/Dice/PReLU, residual,
  *                      LayerNorm, sum/mean pooling, final Linear(*,1)+sigmoid) dcn.py:144-152,175-180;
  *                      deepfm.py:100-112,143-151; din.py:26-36,272-285,312-316; deepcrossing.py:25-42,161-162;
@@ -198,6 +199,20 @@ int rk_dcn_cross(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t wi
 int rk_fm_gather(const rk_segment* second_order, const rk_segment* first_order,
                  int32_t num_fields, int32_t dim, int64_t batch, float* deep_in,
                  int64_t ld_deep, float* fm1, float* fm2, void* stream);
+
+/* One field's DeepFM tables packed into one row-major [rows, ld_out] table (ld_out % 4 == 0,
+ * ld_out >= dim + 1): second-order row at columns 0..dim-1, first-order weight at column dim,
+ * zero padding.  Replaces the pair nn.Embedding(V, dim) + nn.Embedding(V, 1) of one field
+ * (deepfm.py:90-98) as the storage the eval gather reads; a layout pass run once per weight
+ * version (the host layer caches it like the packed MLP weights).                            */
+int rk_fm_pack_table(const float* second, int64_t ld_second, const float* first, int64_t ld_first,
+                     int64_t rows, int32_t dim, float* out, int64_t ld_out, void* stream);
+
+/* rk_fm_gather over packed tables (deepfm.py:122-142): segment f = {packed table of field f,
+ * its [B] int64 indices (unit stride), src_ld = the packed row stride, rows, dim, out_col}.  One
+ * contiguous row read per (sample, field) gives both embedding orders.                          */
+int rk_fm_gather_packed(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                        float* deep_in, int64_t ld_deep, float* fm1, float* fm2, void* stream);
 
 int rk_din_attention(const float* query, int64_t ld_query, const float* key_table,
                      int64_t key_rows, int64_t ld_key, const int64_t* seq, int64_t ld_seq,
