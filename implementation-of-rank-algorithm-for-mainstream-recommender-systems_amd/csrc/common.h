@@ -48,6 +48,12 @@ __device__ __forceinline__ float half_sum(float v) {
 }
 
 __device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Sigmoid on the transcendental unit: v_exp_f32 (2^x) and v_rcp_f32, each ~1 ulp, 4 instructions
+// instead of the ~25 of expf + an IEEE divide; saturates to exactly 0 / 1 where the reference
+// formula does.  Used in the hot eval epilogues (Dice); relative error ~1e-7 against 1e-4 parity.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
+}
 
 __device__ __forceinline__ void flag_oob(uint32_t* flags) {
   if (flags) atomicOr(flags, RK_FLAG_INDEX_OOB);

@@ -15,17 +15,22 @@
 //   * the attention output goes into the LDS row; the row's l2 norm (din.py:318-322) is taken.
 //  Phase B: the fcn tail + output layer + sigmoid over the 16 LDS rows (mlp_core.h).
 // The l2 term is finished by a one-wave reduction over the per-workgroup partial sums.
+#include <new>
+
 #include "mlp_core.h"
 
 namespace rk {
 
 constexpr int kDinSegs = 32;
+constexpr int kDinSegLdsOff = 528;  // bytes past the column map: 256 + 256 map bytes, l2_last int, pad to 16
 struct DinSegs {
   rk_segment s[kDinSegs];
 };
 
 struct DinArgs {
   DinSegs segs;
+  uint8_t col_seg[256], col_off[256];  // column -> (segment, offset) map, built by the host wrapper
+  const float* att_image;              // rk_din_pack_attention image (the first DinLds::U floats of LDS)
   int nseg, width, q_col, att_col, l2_col0;
   const float* key_table;
   int64_t key_rows, ld_key;
@@ -80,6 +85,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   float* const buf1 = buf0 + kMlpRows * a.ld0;
   uint8_t* const col_seg = reinterpret_cast<uint8_t*>(buf1 + kMlpRows * a.ld1);
   uint8_t* const col_off = col_seg + 256;
+  // the row segments' descriptors, copied to LDS so that the per-column lookups of the row
+  // gather read them from LDS instead of the kernel-argument segment (one global round trip less)
+  rk_segment* const lsegs = reinterpret_cast<rk_segment*>(col_seg + kDinSegLdsOff);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5, hk = 4 * half;
@@ -99,30 +107,44 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     my_tiles = my_len <= 0 ? (a.use_softmax ? ntiles_all : 0) : (int)((min<int64_t>(my_len, a.T) + 31) / 32);
   }
 
-  // ---- stage the split attention weights and the column map
-  for (int i = tid; i < 64 * H; i += kMlpThreads) {
-    const int j = i / H, h = i % H;
-    const float* r = a.w1 + (int64_t)j * 4 * H;
-    sm[Ly::WQ + j * Ly::LDH + h] = r[h] + r[2 * H + h];
-    sm[Ly::WK + j * Ly::LDH + h] = r[H + h] - r[2 * H + h];
-    sm[Ly::WQK + j * Ly::LDH + h] = r[3 * H + h];
+  // ---- stage the split attention weights and the column map: with a packed image
+  // (rk_din_pack_attention) one round of coalesced float4 copies, all loads in flight at once
+  if (a.att_image) {
+    static_assert(Ly::U % 4 == 0, "image of whole float4s");
+    constexpr int kImg4 = Ly::U / 4, kPer = (kImg4 + kMlpThreads - 1) / kMlpThreads;
+    f32x4_t v[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = tid + r * kMlpThreads;
+      if (i < kImg4) v[r] = reinterpret_cast<const f32x4_t*>(a.att_image)[i];
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = tid + r * kMlpThreads;
+      if (i < kImg4) reinterpret_cast<f32x4_t*>(sm)[i] = v[r];
+    }
+  } else {
+    for (int i = tid; i < 64 * H; i += kMlpThreads) {
+      const int j = i / H, h = i % H;
+      const float* r = a.w1 + (int64_t)j * 4 * H;
+      sm[Ly::WQ + j * Ly::LDH + h] = r[h] + r[2 * H + h];
+      sm[Ly::WK + j * Ly::LDH + h] = r[H + h] - r[2 * H + h];
+      sm[Ly::WQK + j * Ly::LDH + h] = r[3 * H + h];
+    }
+    for (int i = tid; i < 32 * 64; i += kMlpThreads) sm[Ly::W2 + (i / 64) * 68 + (i % 64)] = a.w2[i];
+    if (tid < 64) sm[Ly::B1 + tid] = a.b1[tid];
+    if (tid < 32) {
+      sm[Ly::B2 + tid] = a.b2[tid];
+      sm[Ly::W3 + tid] = a.w3[tid];
+    }
   }
-  for (int i = tid; i < 32 * 64; i += kMlpThreads) sm[Ly::W2 + (i / 64) * 68 + (i % 64)] = a.w2[i];
-  if (tid < 64) sm[Ly::B1 + tid] = a.b1[tid];
-  if (tid < 32) {
-    sm[Ly::B2 + tid] = a.b2[tid];
-    sm[Ly::W3 + tid] = a.w3[tid];
+  if (tid < 256) {
+    col_seg[tid] = a.col_seg[tid];
+    col_off[tid] = a.col_off[tid];
   }
-  for (int c = tid; c < a.width; c += kMlpThreads) {
-    uint8_t hit = 255, off = 0;
-    for (int s = 0; s < a.nseg; ++s)
-      if (c >= a.segs.s[s].out_col && c < a.segs.s[s].out_col + a.segs.s[s].dim) {
-        hit = (uint8_t)s;
-        off = (uint8_t)(c - a.segs.s[s].out_col);
-      }
-    col_seg[c] = hit;
-    col_off[c] = off;
-  }
+  static_assert(sizeof(rk_segment) % 4 == 0, "segment descriptor of whole words");
+  if (tid < a.nseg * (int)(sizeof(rk_segment) / 4))
+    reinterpret_cast<int*>(lsegs)[tid] = reinterpret_cast<const int*>(&a.segs)[tid];
   __syncthreads();
   DIN_TS(1);
 #ifdef RK_DIN_PHASES
@@ -139,8 +161,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
   }
   const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
-  const int loc = pick ? __builtin_ctzll(pick) : wave;  // this wave's sample within the workgroup
-  const int ntiles = max(0, __shfl(my_tiles, loc, kWave));
+  // wave-uniform values in scalar registers (readfirstlane): the sample's addresses stay scalar
+  const int loc = __builtin_amdgcn_readfirstlane(pick ? __builtin_ctzll(pick) : wave);  // sample in the WG
+  const int ntiles = __builtin_amdgcn_readfirstlane(max(0, __shfl(my_tiles, loc, kWave)));
   const int64_t len = __shfl(my_len, loc, kWave);
   const int64_t b = m0 + loc;
 #ifdef RK_DIN_SKIP_A  // timing experiment only (tools/din_phase_time.py): phase B on zero rows
@@ -151,20 +174,68 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   float* row = buf0 + loc * a.ld0;
   uint32_t* flags = a.flags;
 
-  // ---- Phase A.1: the feature row (zero padded to pad64(width))
+  // ---- Phase A.1: the feature row (zero padded to pad64(width)) and the first attention tile's
+  // keys, with the loads ordered so that the two dependent rounds (indices, then rows) of the
+  // row and of the keys overlap: history indices of the first two tiles, the row's segment
+  // indices, the row values, the first tile's key rows — then the row goes to LDS while the
+  // key rows are still in flight.
   const int wp = pad64(a.width);
-  for (int c = lane; c < wp; c += 64) {
-    float v = 0.f;
-    if (live && c < a.width) {
-      const int s = col_seg[c];
-      if (s != 255) {
-        const float* src = segment_row(a.segs.s[s], b, flags);
-        if (src) v = src[col_off[c]];
-      }
-    }
-    row[c] = v;
+  int64_t kidx[2] = {0, 0};  // history index of position tt * 32 + l32, tiles 0 and 1
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = tt * 32 + l32;
+    if (live && tt < ntiles && t < a.T) kidx[tt] = a.seq[b * a.ld_seq + t];
   }
-  __builtin_amdgcn_s_waitcnt(0);
+  // tile 1's index waits in LDS (a register across tile 0 spills at the 128-VGPR budget)
+  int64_t* const kpre = reinterpret_cast<int64_t*>(col_seg + kDinSegLdsOff + sizeof(rk_segment) * kDinSegs) + 32 * wave;
+  constexpr int kColIt = 4;  // width <= 255: at most four 64-column passes
+  int64_t cidx[kColIt];
+  int cseg[kColIt];
+#pragma unroll
+  for (int i = 0; i < kColIt; ++i) {
+    const int c = lane + 64 * i;
+    cseg[i] = (live && c < a.width) ? col_seg[c] : 255;
+    cidx[i] = b;
+    if (cseg[i] != 255 && lsegs[cseg[i]].idx) cidx[i] = lsegs[cseg[i]].idx[b * lsegs[cseg[i]].idx_stride];
+  }
+  float cval[kColIt];
+#pragma unroll
+  for (int i = 0; i < kColIt; ++i) {
+    const int c = lane + 64 * i;
+    cval[i] = 0.f;
+    if (cseg[i] != 255) {
+      const rk_segment& g = lsegs[cseg[i]];
+      if (g.idx && (cidx[i] < 0 || cidx[i] >= g.rows))
+        flag_oob(flags);
+      else
+        cval[i] = g.src[cidx[i] * g.src_ld + col_off[c]];
+    }
+  }
+  f32x4_t k[NQ];
+  // key rows of position t (index r) into k; positions past T read as zeros
+  auto load_keys = [&](int64_t r, int t) {
+    const float* krow = nullptr;
+    if (t < a.T) {
+      if (r >= 0 && r < a.key_rows)
+        krow = a.key_table + r * a.ld_key;
+      else
+        flag_oob(flags);
+#ifdef RK_DIN_NO_GATHER  // timing experiment only: the keys come from 32 cache-resident rows
+      krow = a.key_table + (int64_t)l32 * a.ld_key;
+#endif
+    }
+#pragma unroll
+    for (int c = 0; c < NQ; ++c)
+      k[c] = krow ? *reinterpret_cast<const f32x4_t*>(krow + 8 * c + hk) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  };
+  if (live && ntiles > 0) load_keys(kidx[0], l32);
+  if (half == 0) kpre[l32] = kidx[1];
+#pragma unroll
+  for (int i = 0; i < kColIt; ++i) {
+    const int c = lane + 64 * i;
+    if (c < wp) row[c] = cval[i];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 
   float norm_part = 0.f;
@@ -193,21 +264,8 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       asm volatile("" ::: "memory");
       const int t = tt * 32 + l32;
       const bool in_seq = t < a.T;
-      const float* krow = nullptr;
-      if (in_seq) {
-        const int64_t r = a.seq[b * a.ld_seq + t];
-        if (r >= 0 && r < a.key_rows)
-          krow = a.key_table + r * a.ld_key;
-        else
-          flag_oob(flags);
-#ifdef RK_DIN_NO_GATHER  // timing experiment only: the keys come from 32 cache-resident rows
-        krow = a.key_table + (int64_t)l32 * a.ld_key;
-#endif
-      }
-      f32x4_t k[NQ];
-#pragma unroll
-      for (int c = 0; c < NQ; ++c)
-        k[c] = krow ? *reinterpret_cast<const f32x4_t*>(krow + 8 * c + hk) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      if (tt > 0)  // tile 0's keys were loaded with the row; tile 1's index was prefetched
+        load_keys(tt == 1 ? kpre[l32] : (in_seq ? a.seq[b * a.ld_seq + t] : 0), t);
 
       // layer 1 (transposed) one 32-row block jt at a time, each folded straight into layer 2
       // (acc2 = W2 . h1^T with the layer-1 accumulator as the B operand): one layer-1
@@ -326,17 +384,81 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
 }
 
+// The LDS image of the split attention weights (see the layout above): WK = W1b - W1c,
+// WQK = W1d, WQ = W1a + W1c (rows of H, stride H + 4), W2 (32 x 64, stride 68), b1, b2, w3.
+template <int H>
+__global__ __launch_bounds__(256) void din_pack_attention_kernel(const float* __restrict__ w1,
+                                                                 const float* __restrict__ b1,
+                                                                 const float* __restrict__ w2,
+                                                                 const float* __restrict__ b2,
+                                                                 const float* __restrict__ w3, float* __restrict__ img) {
+  using Ly = DinLds<H>;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < Ly::U; i += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (i < Ly::W2) {
+      const int which = i / (64 * Ly::LDH), rem = i % (64 * Ly::LDH), j = rem / Ly::LDH, h = rem % Ly::LDH;
+      if (h < H) {
+        const float* r = w1 + (int64_t)j * 4 * H;
+        v = which == 0 ? r[H + h] - r[2 * H + h] : which == 1 ? r[3 * H + h] : r[h] + r[2 * H + h];
+      }
+    } else if (i < Ly::B1) {
+      const int k = i - Ly::W2, j = k / 68, c = k % 68;
+      v = c < 64 ? w2[j * 64 + c] : 0.f;
+    } else if (i < Ly::B2) {
+      v = b1[i - Ly::B1];
+    } else if (i < Ly::W3) {
+      v = b2[i - Ly::B2];
+    } else {
+      v = w3[i - Ly::W3];
+    }
+    img[i] = v;
+  }
+}
+
 }  // namespace rk
 
 using namespace rk;
 
-RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
+RK_API int64_t rk_din_attention_image_floats(int32_t H) {
+  switch (H) {
+    case 8: return DinLds<8>::U;
+    case 16: return DinLds<16>::U;
+    case 32: return DinLds<32>::U;
+    default: return 0;
+  }
+}
+
+RK_API int rk_din_pack_attention(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                                 int32_t H, float* image, void* stream) {
+  if (!w1 || !b1 || !w2 || !b2 || !w3 || !image || ((uintptr_t)image & 15u))
+    return fail(RK_ERR_INVALID, "rk_din_pack_attention: null or misaligned pointer");
+  hipStream_t st = (hipStream_t)stream;
+  switch (H) {
+    case 8: din_pack_attention_kernel<8><<<8, 256, 0, st>>>(w1, b1, w2, b2, w3, image); break;
+    case 16: din_pack_attention_kernel<16><<<16, 256, 0, st>>>(w1, b1, w2, b2, w3, image); break;
+    case 32: din_pack_attention_kernel<32><<<36, 256, 0, st>>>(w1, b1, w2, b2, w3, image); break;
+    default: return fail(RK_ERR_UNSUPPORTED, "rk_din_pack_attention: embedding dim %d not in {8,16,32}", H);
+  }
+  return check_launch("rk_din_pack_attention");
+}
+
+namespace rk {
+// A prepared launch of din_forward_kernel: validated arguments, grid and LDS size.
+struct DinPlan {
+  DinArgs a;
+  int64_t blocks;
+  size_t shm;
+  int H;
+};
+}  // namespace rk
+
+static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
                           const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
                           int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
                           const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
                           const float* b3, int32_t use_softmax, const rk_mlp_layer* layers, int32_t nlayers,
                           const rk_epilogue* head, int32_t l2_col0, float l2_scale, float* l2_workspace,
-                          float* l2_out, void* stream) {
+                          float* l2_out, const float* att_image, DinPlan* plan) {
   if (!row_segs || nseg <= 0 || nseg > kDinSegs)
     return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %d row segments (max %d)", nseg, kDinSegs);
   if (!key_table || !seq || !seq_len || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !head || !head->head_w)
@@ -348,12 +470,26 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
     return fail(RK_ERR_INVALID, "rk_din_forward: bad row/sequence layout (width=%d T=%d H=%d)", width, T, H);
   if (l2_out && (!l2_workspace || l2_col0 < 0 || l2_col0 >= width || ((uintptr_t)l2_workspace & 3u)))
     return fail(RK_ERR_INVALID, "rk_din_forward: l2 term needs a workspace of ceil(batch/16) + 1 words");
-  DinArgs a = {};
+  *plan = DinPlan{};
+  DinArgs& a = plan->a;
+  plan->H = H;
   for (int s = 0; s < nseg; ++s) {
     const rk_segment& g = row_segs[s];
     if (!g.src || g.dim <= 0 || g.out_col < 0 || g.out_col + g.dim > width || g.dim > 255 || (g.idx && g.rows <= 0))
       return fail(RK_ERR_INVALID, "rk_din_forward: row segment %d invalid", s);
     a.segs.s[s] = g;
+  }
+  if (att_image && ((uintptr_t)att_image & 15u)) return fail(RK_ERR_INVALID, "rk_din_forward: att_image not 16-B aligned");
+  a.att_image = att_image;
+  for (int c = 0; c < 256; ++c) {  // column map (rk_concat_gather semantics: the last covering segment wins)
+    uint8_t hit = 255, off = 0;
+    for (int s = 0; s < nseg && c < width; ++s)
+      if (c >= row_segs[s].out_col && c < row_segs[s].out_col + row_segs[s].dim) {
+        hit = (uint8_t)s;
+        off = (uint8_t)(c - row_segs[s].out_col);
+      }
+    a.col_seg[c] = hit;
+    a.col_off[c] = off;
   }
   a.head = *head;
   int need0 = 0, need1 = 0;
@@ -387,18 +523,24 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
   a.flags = device_flags();
   a.ld0 = need0 + 4;
   a.ld1 = need1 + 4;
+  static_assert(sizeof(DinArgs) <= 4096, "kernel arguments beyond 4 KiB");
   if (batch < 0) return fail(RK_ERR_INVALID, "rk_din_forward: negative batch");
-  if (batch == 0) return RK_OK;
-  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  plan->blocks = (batch + kMlpRows - 1) / kMlpRows;
   size_t base = 0;
   switch (H) {
     case 8: base = DinLds<8>::BUF0; break;
     case 16: base = DinLds<16>::BUF0; break;
     default: base = DinLds<32>::BUF0; break;
   }
-  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + 512 + 16;
+  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
+                     sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 32 * kMlpWaves;
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
-  hipStream_t st = (hipStream_t)stream;
+  plan->shm = shm;
+  return RK_OK;
+}
+
+static int din_launch(const DinPlan& p, hipStream_t st) {
+  if (p.blocks == 0) return RK_OK;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)din_forward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -406,14 +548,56 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
     (void)hipFuncSetAttribute((const void*)din_forward_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  switch (H) {
-    case 8: din_forward_kernel<8><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
-    case 16: din_forward_kernel<16><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
-    default: din_forward_kernel<32><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a); break;
+  const unsigned blocks = (unsigned)p.blocks;
+  switch (p.H) {
+    case 8: din_forward_kernel<8><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
+    case 16: din_forward_kernel<16><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
+    default: din_forward_kernel<32><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
   }
-  if (int e = check_launch("rk_din_forward")) return e;
+  return check_launch("rk_din_forward");
+}
+
+#define RK_DIN_ARG_NAMES                                                                                          \
+  row_segs, nseg, width, q_col, att_col, key_table, key_rows, ld_key, seq, ld_seq, T, seq_len, batch, H, w1, b1, \
+      w2, b2, w3, b3, use_softmax, layers, nlayers, head, l2_col0, l2_scale, l2_workspace, l2_out, att_image
+
+RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
+                          const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
+                          int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
+                          const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                          const float* b3, int32_t use_softmax, const rk_mlp_layer* layers, int32_t nlayers,
+                          const rk_epilogue* head, int32_t l2_col0, float l2_scale, float* l2_workspace,
+                          float* l2_out, const float* att_image, void* stream) {
+  DinPlan p;
+  if (int e = din_prepare(RK_DIN_ARG_NAMES, &p)) return e;
+  return din_launch(p, (hipStream_t)stream);
+}
+
+RK_API int rk_din_forward_plan(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
+                          const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
+                          int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
+                          const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                          const float* b3, int32_t use_softmax, const rk_mlp_layer* layers, int32_t nlayers,
+                          const rk_epilogue* head, int32_t l2_col0, float l2_scale, float* l2_workspace,
+                          float* l2_out, const float* att_image, void** plan_out) {
+  if (!plan_out) return fail(RK_ERR_INVALID, "rk_din_forward_plan: null plan_out");
+  *plan_out = nullptr;
+  DinPlan* p = new (std::nothrow) DinPlan;
+  if (!p) return fail(RK_ERR_RUNTIME, "rk_din_forward_plan: out of host memory");
+  if (int e = din_prepare(RK_DIN_ARG_NAMES, p)) {
+    delete p;
+    return e;
+  }
+  *plan_out = p;
   return RK_OK;
 }
+
+RK_API int rk_din_plan_launch(const void* plan, void* stream) {
+  if (!plan) return fail(RK_ERR_INVALID, "rk_din_plan_launch: null plan");
+  return din_launch(*static_cast<const DinPlan*>(plan), (hipStream_t)stream);
+}
+
+RK_API void rk_din_plan_destroy(void* plan) { delete static_cast<DinPlan*>(plan); }
 
 #ifdef RK_DIN_PHASES
 RK_API int rk_debug_din_phases(unsigned long long* ts, unsigned long long* waves, unsigned long long* mlp) {

@@ -80,7 +80,7 @@ __device__ __forceinline__ float col_apply(const ColEpi& e, int act, float slope
       z = z > 0.f ? z : z * slope;
       break;
     case RK_ACT_DICE: {
-      const float p = 1.0f / (1.0f + expf(-(z * e.act_s + e.act_b)));
+      const float p = sigmoid_fast(z * e.act_s + e.act_b);
       z = e.alpha * (1.0f - p) * z + p * z;
       break;
     }

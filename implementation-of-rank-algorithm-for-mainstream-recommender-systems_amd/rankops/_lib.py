@@ -164,7 +164,17 @@ SIGNATURES = {
         ctypes.c_int,
         [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
          c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
-         c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
+         c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_din_forward_plan": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
+         c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
+         c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p, POINTER(c_void_p)]),
+    "rk_din_plan_launch": (ctypes.c_int, [c_void_p, c_void_p]),
+    "rk_din_plan_destroy": (None, [c_void_p]),
+    "rk_din_attention_image_floats": (c_int64, [c_int32]),
+    "rk_din_pack_attention": (
+        ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rk_mlp_packed_size": (ctypes.c_int, [c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_mlp_forward": (

@@ -218,15 +218,65 @@ class DIN(EngineModule):
                     seq=seq, seq_len=seq_len, fused=fused, keep=(dense_cols, category, target), lookups=lookups,
                     seq_key=SEQ_KEY, want_l2=self.mini_batch_aware_regularization and self.l2_lambda > 0)
 
+    def _att_image(self, w, H):
+        """The attention weights pre-split into din_forward_kernel's LDS image: cached for frozen
+        H2 weights (they live on the device for good), packed per call otherwise."""
+        if self.att_weights.mode != "frozen":
+            return ops.din_pack_attention(w, H)
+        k = common._key(w) + (H,)
+        if getattr(self, "_att_img", None) is None or self._att_img[0] != k:
+            self._att_img = (k, ops.din_pack_attention(w, H))
+        return self._att_img[1]
+
     def _launch_fused(self, pl, w, logit, prob, l2_reg):
         layers = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs())
                   for l in self._tail]
+        img = self._att_image(w, pl["H"])
         head = ops.make_epilogue(head_w=self.output_layer.weight, head_b=self.output_layer.bias,
                                  head_logit=logit, head_prob=prob)
         ops.din_forward(pl["segs"], pl["width"], pl["q_col"], pl["att_col"], self.embeddings[SEQ_KEY].weight,
                         pl["seq"], pl["seq_len"], pl["H"], w, self.use_softmax, layers, head, pl["B"], pl["dev"],
                         l2_col0=pl["cat_col0"], l2_scale=float(self.l2_lambda),
-                        l2_out=l2_reg if isinstance(l2_reg, torch.Tensor) else None)
+                        l2_out=l2_reg if isinstance(l2_reg, torch.Tensor) else None, att_image=img)
+
+    def prepare(self, dense, category, sequence, target):
+        """An eval forward bound to these input tensors (the single-kernel analogue of capturing
+        the forward in a hipGraph): returns `run()` that recomputes the whole forward from the
+        current contents of the inputs with one kernel launch (rk_din_forward_plan /
+        rk_din_plan_launch) and returns the same (prob, logit, l2_reg) tensors each time.  Like a
+        captured graph it binds the current weights: prepare again after changing them."""
+        if self.training:
+            raise RuntimeError("DIN.prepare: eval mode only (call .eval() first)")
+        pl = self._plan(dense, category, sequence, target)
+        if not pl["fused"]:
+            raise RuntimeError("DIN.prepare: configuration outside rk_din_forward's envelope")
+        B, dev = pl["B"], pl["dev"]
+        w = self.att_weights.get(dev)
+        if self.att_weights.mode != "frozen":
+            raise RuntimeError("DIN.prepare: per-call interaction weights are redrawn every forward; "
+                               "use interaction_weights='frozen'")
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        want_l2 = pl["want_l2"]
+        l2_reg = torch.empty((), device=dev, dtype=torch.float32) if want_l2 else None
+        packed = [PACKED(l.linear.weight) for l in self._tail]
+        layers = [ops.make_mlp_layer(l.linear.weight, pk, **l.epilogue_kwargs()) for l, pk in zip(self._tail, packed)]
+        head = ops.make_epilogue(head_w=self.output_layer.weight, head_b=self.output_layer.bias,
+                                 head_logit=logit, head_prob=prob)
+        img = self._att_image(w, pl["H"])
+        keep = (pl, w, img, packed, [l.epilogue_kwargs() for l in self._tail], logit, prob, l2_reg,
+                self.embeddings[SEQ_KEY].weight)
+        plan = ops.din_forward_plan(pl["segs"], pl["width"], pl["q_col"], pl["att_col"],
+                                    self.embeddings[SEQ_KEY].weight, pl["seq"], pl["seq_len"], pl["H"], w,
+                                    self.use_softmax, layers, head, B, dev, l2_col0=pl["cat_col0"],
+                                    l2_scale=float(self.l2_lambda), l2_out=l2_reg, att_image=img, keep=keep)
+        out = (prob, logit, l2_reg if want_l2 else 0.0)
+
+        def run():
+            plan.launch()
+            return out
+        run.plan = plan
+        return run
 
     def fused_kernel_launcher(self, dense, category, sequence, target):
         """Zero-argument re-launch of this forward's rk_din_forward kernel (no l2 finish), for

@@ -319,22 +319,74 @@ def _din_l2_workspace(device, batch):
     return ws
 
 
-def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
-                head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None):
-    """Whole DIN eval forward (row gather, attention, fcn tail, head, l2 partials) in one launch."""
+def din_pack_attention(att_weights, H: int) -> torch.Tensor:
+    """rk_din_pack_attention: the split attention weights as din_forward_kernel's LDS image."""
     lib = _lib.load()
-    _lib.ensure_device(device)
+    w1, b1, w2, b2, w3, _ = att_weights
+    _lib.ensure_device(w1.device)
+    n = lib.rk_din_attention_image_floats(H)
+    if n <= 0:
+        raise ValueError(f"rankops.din_pack_attention: H={H} not in (8, 16, 32)")
+    img = torch.empty(n, device=w1.device, dtype=torch.float32)
+    check(lib.rk_din_pack_attention(ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3), H, ptr(img),
+                                    _lib.stream_of(img)), "rk_din_pack_attention")
+    return img
+
+
+def _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
+                      head: Epilogue, batch, device, l2_col0, l2_scale, l2_out, att_image):
+    """The rk_din_forward argument list (without the stream) and the ctypes arrays it points into."""
     w1, b1, w2, b2, w3, b3 = att_weights
     arr = _seg_array(segs)
     larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
-    ws = None
-    if l2_out is not None:
-        ws = _din_l2_workspace(device, batch)
-    check(lib.rk_din_forward(arr, len(segs), width, q_col, att_col, ptr(key_table), key_table.shape[0],
-                             key_table.stride(0), ptr(seq), seq.stride(0), seq.shape[1], ptr(seq_len), batch, H,
-                             ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3), ptr(b3), 1 if use_softmax else 0, larr,
-                             len(layers), ctypes.byref(head), l2_col0, float(l2_scale), ptr(ws), ptr(l2_out),
-                             torch.cuda.current_stream(device).cuda_stream), "rk_din_forward")
+    ws = _din_l2_workspace(device, batch) if l2_out is not None else None
+    args = (arr, len(segs), width, q_col, att_col, ptr(key_table), key_table.shape[0], key_table.stride(0), ptr(seq),
+            seq.stride(0), seq.shape[1], ptr(seq_len), batch, H, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3),
+            ptr(b3), 1 if use_softmax else 0, larr, len(layers), ctypes.byref(head), l2_col0, float(l2_scale),
+            ptr(ws), ptr(l2_out), ptr(att_image))
+    return args, (arr, larr, head, ws)
+
+
+def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
+                head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None, att_image=None):
+    """Whole DIN eval forward (row gather, attention, fcn tail, head, l2 partials) in one launch."""
+    lib = _lib.load()
+    _lib.ensure_device(device)
+    args, _keep = _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights,
+                                    use_softmax, layers, head, batch, device, l2_col0, l2_scale, l2_out, att_image)
+    check(lib.rk_din_forward(*args, torch.cuda.current_stream(device).cuda_stream), "rk_din_forward")
+
+
+class DinPlan:
+    """rk_din_forward_plan: the fused DIN forward with its arguments validated once; calling it
+    launches the kernel on the current stream (one launch, no per-call host work besides the
+    ctypes call).  Binds the pointers it was made with — `keep` holds every tensor it reads or
+    writes alive for the plan's lifetime."""
+
+    def __init__(self, args, keep, device):
+        self._lib = _lib.load()
+        self._device = device
+        self._handle = ctypes.c_void_p()
+        check(self._lib.rk_din_forward_plan(*args, ctypes.byref(self._handle)), "rk_din_forward_plan")
+        self._keep = keep
+
+    def launch(self):
+        check(self._lib.rk_din_plan_launch(self._handle, torch.cuda.current_stream(self._device).cuda_stream),
+              "rk_din_plan_launch")
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            self._lib.rk_din_plan_destroy(h)
+            h.value = None
+
+
+def din_forward_plan(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
+                     head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None, att_image=None, keep=()):
+    _lib.ensure_device(device)
+    args, k = _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax,
+                                layers, head, batch, device, l2_col0, l2_scale, l2_out, att_image)
+    return DinPlan(args, (k, tuple(keep)), device)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M: int = None, K: int = None,

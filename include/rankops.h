@@ -255,7 +255,32 @@ int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, int3
                    const float* b2, const float* w3, const float* b3, int32_t use_softmax,
                    const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head,
                    int32_t l2_col0, float l2_scale, float* l2_workspace, float* l2_out,
-                   void* stream);
+                   const float* att_image, void* stream);
+
+/* att_image (optional, NULL = split in the kernel from w1..w3): the attention weights pre-split
+ * into the kernel's LDS layout by rk_din_pack_attention (rk_din_attention_image_floats(H)
+ * floats, 16-B aligned), so the launch stages them with one round of coalesced copies.  The
+ * layout splits W1 = [W1a | W1b | W1c | W1d] over [q, k, q-k, q*k] (din.py:56-64): WK = W1b - W1c,
+ * WQK = W1d, WQ = W1a + W1c, then W2, b1, b2, w3 (b3 is read from its pointer).              */
+int64_t rk_din_attention_image_floats(int32_t H);
+int rk_din_pack_attention(const float* w1, const float* b1, const float* w2, const float* b2,
+                          const float* w3, int32_t H, float* image, void* stream);
+
+/* A prepared rk_din_forward: the same arguments, validated once, launched later by
+ * rk_din_plan_launch on any stream at the cost of one kernel launch — the one-kernel analogue of
+ * a captured hipGraph without the graph's per-replay launch gap (~9 us on this forward).  Like a
+ * graph, a plan binds the pointers it was made with: keep every buffer alive, and make a new plan
+ * after the weights move or their packed images are rebuilt.                                  */
+int rk_din_forward_plan(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col,
+                        int32_t att_col, const float* key_table, int64_t key_rows, int64_t ld_key,
+                        const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
+                        int64_t batch, int32_t H, const float* w1, const float* b1, const float* w2,
+                        const float* b2, const float* w3, const float* b3, int32_t use_softmax,
+                        const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head,
+                        int32_t l2_col0, float l2_scale, float* l2_workspace, float* l2_out,
+                        const float* att_image, void** plan);
+int rk_din_plan_launch(const void* plan, void* stream);
+void rk_din_plan_destroy(void* plan);
 
 int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                    const float* dense, int64_t ld_dense, int32_t num_dense,

@@ -1,0 +1,86 @@
+"""GPU: the prepared DIN forward (DIN.prepare -> rk_din_forward_plan / rk_din_plan_launch) equals
+the eager forward bit for bit and follows new input contents like a captured graph; the packed
+attention image path (rk_din_pack_attention) equals the in-kernel split and the oracle."""
+import pytest
+import torch
+
+import helpers as H
+from rankops import ops
+
+ATOL = RTOL = 1e-4
+
+
+def _cfg(**kw):
+    cfg = {"T": 50, "dim": 32, "interaction_weights": "frozen"}
+    cfg.update(kw)
+    return cfg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("softmax", [False, True])
+def test_prepared_equals_eager_and_follows_inputs(softmax):
+    cfg = _cfg(softmax=softmax)
+    model = H.build("din", cfg).cuda().eval()
+    inp = H.to_device(H.make_inputs("din", cfg, 300), "cuda")
+    with torch.no_grad():
+        eager = H.as_tuple(H.call_model(model, "din", inp))
+        run = model.prepare(inp["dense"], inp["category"], inp["sequence"], inp["target"])
+        out = run()
+        torch.cuda.synchronize()
+        for e, o in zip(eager, out):
+            assert torch.equal(e, o)
+        # new batch contents in the same input buffers: the plan recomputes from them
+        new = H.to_device(H.make_inputs("din", cfg, 300, seed=4242), "cuda")
+        inp["sequence"]["his_read_comment_7d_seq"].copy_(new["sequence"]["his_read_comment_7d_seq"])
+        inp["sequence"]["his_read_comment_7d_seq_length"].copy_(new["sequence"]["his_read_comment_7d_seq_length"])
+        inp["target"]["feedid"].copy_(new["target"]["feedid"])
+        out2 = tuple(x.clone() if isinstance(x, torch.Tensor) else x for x in run())
+        eager2 = H.as_tuple(H.call_model(model, "din", inp))
+        torch.cuda.synchronize()
+        for e, o in zip(eager2, out2):
+            assert torch.equal(e, o)
+        assert not torch.equal(out2[0], eager[0])
+
+
+@pytest.mark.gpu
+def test_prepared_matches_oracle_with_edge_lengths():
+    cfg = _cfg()
+    model = H.build("din", cfg)
+    inp = H.make_inputs("din", cfg, 128)
+    L = inp["sequence"]["his_read_comment_7d_seq_length"]
+    L[:6] = torch.tensor([0, 1, 31, 32, 33, 50])
+    p = H.cpu_params(model)
+    model = model.cuda().eval()
+    d = H.to_device(inp, "cuda")
+    torch.manual_seed(5)  # the frozen H2 draw happens on the first forward, as the oracle's per-call draw
+    with torch.no_grad():
+        out = model.prepare(d["dense"], d["category"], d["sequence"], d["target"])()
+        torch.manual_seed(5)
+        ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
+    for o, r in zip(out, ref):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.cpu(), r, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H_", [8, 16, 32])
+def test_attention_image_layout(H_):
+    """rk_din_pack_attention writes WK = W1b - W1c, WQK = W1d, WQ = W1a + W1c (rows padded to H+4),
+    W2 (rows padded to 68), b1, b2, w3 — the layout din_forward_kernel stages."""
+    g = torch.Generator().manual_seed(H_)
+    w1 = torch.randn(64, 4 * H_, generator=g)
+    b1, w2, b2 = torch.randn(64, generator=g), torch.randn(32, 64, generator=g), torch.randn(32, generator=g)
+    w3, b3 = torch.randn(1, 32, generator=g), torch.randn(1, generator=g)
+    img = ops.din_pack_attention(tuple(t.cuda() for t in (w1, b1, w2, b2, w3, b3)), H_).cpu()
+    L = H_ + 4
+    wa, wb, wc, wd = w1[:, :H_], w1[:, H_:2 * H_], w1[:, 2 * H_:3 * H_], w1[:, 3 * H_:]
+    blk = 64 * L
+    for i, want in enumerate((wb - wc, wd, wa + wc)):
+        got = img[i * blk:(i + 1) * blk].view(64, L)
+        assert torch.equal(got[:, :H_], want) and not got[:, H_:].any()
+    o = 3 * blk
+    got = img[o:o + 32 * 68].view(32, 68)
+    assert torch.equal(got[:, :64], w2) and not got[:, 64:].any()
+    o += 32 * 68
+    assert torch.equal(img[o:o + 64], b1) and torch.equal(img[o + 64:o + 96], b2)
+    assert torch.equal(img[o + 96:o + 128], w3[0])
