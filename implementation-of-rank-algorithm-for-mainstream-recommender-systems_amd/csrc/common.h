@@ -27,6 +27,11 @@ int num_cus();
 // out[0] = scale * (sum of part[0..n)) / rows, one wave, fixed order (embedding.hip).
 int launch_l2_final(const float* part, int n, int64_t rows, float scale, float* out, hipStream_t st);
 
+// Tall-skinny FP32-MFMA GEMM (gemm_rows.hip); returns false when the shape is not its case.
+bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float* Ap, int aperiod, const float* B,
+                   int64_t ldb, int b_trans, int64_t M, int N, int K, float* C, int64_t ldc, int accumulate,
+                   const rk_epilogue* ep, hipStream_t st);
+
 // ---- device helpers ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1,0 +1,298 @@
+// Tall-skinny GEMM for the training shapes (BST projections and FFN, DIN attention MLP):
+//   C[m, n] (+)= epilogue( sum_k opA(m, k) opB(n, k) ),  M large, N any, reduction K <= 128,
+//   opA(m, k) = (A[m, k] + Ap[m % period, k]) * [mask(m, k) > 0]   (addend and mask optional)
+//   opB(n, k) = b_trans ? B[k, n] : B[n, k]
+// Used by rk_linear (Y = X W^T) and rk_gemm without transposed A (dX = dY W) when M spans many
+// workgroups.  The generic kernels stage both operands through LDS per 32-deep step with a barrier
+// in between and run at 2 waves/SIMD: at M = 131072, N = K = 128 that is 41-52 TFLOP/s.
+//
+// Here a workgroup stages its 128-column slice of opB ONCE (the whole reduction, [128][K8 + 4] in
+// LDS) and then never synchronises again: each wave walks 32-row slabs of A grid-stride, reading
+// its A operand straight from global memory into registers (lane = row, float4 along k — the layout
+// v_mfma_f32_32x32x2_f32 consumes, no LDS round trip) with the NEXT slab's loads issued before the
+// current slab's 4 x K/2 MFMAs, so the HBM stream overlaps the matrix work.  Exact f32 products in a
+// k-ordered fma chain per output (permuted k within a chunk, like the other FP32-MFMA kernels).
+#include <cstdlib>
+
+#include "common.h"
+
+namespace rk {
+
+constexpr int kRowsKMax = 128;  // reduction envelope (all of it resident in registers and LDS)
+constexpr int kRowsWaves = 4;
+
+struct RowsArgs {
+  const float* A;
+  int64_t lda;
+  const float* A_mask;
+  const float* Ap;
+  int aperiod;
+  const float* B;
+  int64_t ldb;
+  int b_trans;
+  int64_t M;
+  int N;
+  int K;
+  float* C;
+  int64_t ldc;
+  int accumulate;
+  int c_vec;  // C rows 16-B aligned (float4 stores)
+  int b_vec;  // B rows 16-B aligned (float4 staging loads)
+  rk_epilogue ep;
+};
+
+// Linear epilogue handled here: bias and ReLU / LeakyReLU (the training layers); anything else
+// (residual, affine, Dice, PReLU) stays on linear_kernel.
+__device__ __forceinline__ float rows_act(const RowsArgs& a, float z) {
+  if (a.ep.act == RK_ACT_RELU) return z < 0.f ? 0.f : z;  // keeps NaN, like torch.relu
+  if (a.ep.act == RK_ACT_LEAKY) return z > 0.f ? z : z * a.ep.slope;
+  return z;
+}
+
+// A-operand modes: plain, ReLU-masked (opA = A [mask > 0]), periodic addend (opA = A + Ap[m % period]).
+enum { kRowsPlain = 0, kRowsMask = 1, kRowsPeriodic = 2 };
+
+// A-operand stream of one wave: chunk (slab s, j) is the float4 of row s*32 + (l & 31) at k = 8j + hk
+// (hk = 4 (l >> 5)), the layout v_mfma_f32_32x32x2_f32 consumes; rows past M read row M - 1 (their
+// outputs are never stored).  A ring of PD chunks runs PD chunks (PD x 4 NT MFMAs) ahead of the
+// MFMAs, across slab boundaries, so the HBM stream overlaps the matrix work without a whole
+// second slab in registers.
+template <int AM>
+struct RowsChunk {
+  f32x4 x, aux;  // aux: mask (kRowsMask) or periodic addend (kRowsPeriodic)
+};
+
+template <int AM>
+__device__ __forceinline__ RowsChunk<AM> rows_fetch(const RowsArgs& a, int64_t s, int j, int l32, int hk) {
+  const int64_t m = s * 32 + l32;
+  const int64_t mr = m < a.M ? m : a.M - 1;
+  RowsChunk<AM> c;
+  c.x = *reinterpret_cast<const f32x4*>(a.A + mr * a.lda + hk + 8 * j);
+  if (AM == kRowsMask) c.aux = *reinterpret_cast<const f32x4*>(a.A_mask + mr * a.lda + hk + 8 * j);
+  if (AM == kRowsPeriodic) c.aux = *reinterpret_cast<const f32x4*>(a.Ap + (mr % a.aperiod) * (int64_t)a.K + hk + 8 * j);
+  return c;
+}
+
+template <int AM>
+__device__ __forceinline__ f32x4 rows_operand(const RowsChunk<AM>& c) {
+  f32x4 v = c.x;
+  if (AM == kRowsPeriodic) v += c.aux;
+  if (AM == kRowsMask) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = c.aux[e] > 0.f ? v[e] : 0.f;
+  }
+  return v;
+}
+
+template <int NK8, int NT, bool EPI, int AM>
+__global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sB[];
+  constexpr int K8 = 8 * NK8, ldb = K8 + 4, BN = 32 * NT;
+  constexpr int PD = NK8 < 8 ? NK8 : 8;  // ring depth in chunks (divides NK8)
+  const int n0 = blockIdx.y * BN;
+  const int bn = min(BN, a.N - n0);
+  const int tid = threadIdx.x;
+  // opB slice [bn][K] -> LDS [BN][K8 + 4], zero-padded.  Every thread issues all of its float4
+  // loads (coalesced along the contiguous dim) before the first LDS write: a loop of dependent
+  // 4-B load -> store pairs put one L2 round trip per element in front of the first MFMA.
+  constexpr int NV = BN * K8 / 4 / 256;  // float4 per thread (BN * K8 is a multiple of 1024)
+  f32x4 bvals[NV];
+  if (a.b_trans) {  // B is [K][N]: float4 = 4 consecutive n at one k
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + 256 * i, k = idx / (BN / 4), n = 4 * (idx % (BN / 4));
+      const float* src = a.B + (int64_t)k * a.ldb + n0 + n;
+      if (a.b_vec && n + 3 < bn) {
+        bvals[i] = *reinterpret_cast<const f32x4*>(src);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bvals[i][e] = n + e < bn ? src[e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + 256 * i, k = idx / (BN / 4), n = 4 * (idx % (BN / 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sB[(n + e) * ldb + k] = bvals[i][e];
+    }
+  } else {  // B is [N][K]: float4 = 4 consecutive k of one row
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + 256 * i, n = idx / (K8 / 4), k = 4 * (idx % (K8 / 4));
+      const float* src = a.B + (int64_t)(n0 + (n < bn ? n : 0)) * a.ldb + k;
+      if (a.b_vec) {
+        bvals[i] = *reinterpret_cast<const f32x4*>(src);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bvals[i][e] = src[e];
+      }
+      if (n >= bn) bvals[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + 256 * i, n = idx / (K8 / 4), k = 4 * (idx % (K8 / 4));
+      *reinterpret_cast<f32x4*>(sB + n * ldb + k) = bvals[i];
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hk = 4 * (lane >> 5);
+  const int64_t nslabs = (a.M + 31) / 32;
+  const int64_t stride = (int64_t)gridDim.x * kRowsWaves;
+  int64_t s = (int64_t)blockIdx.x * kRowsWaves + wave;
+  if (s >= nslabs) return;
+  const float* bbase = sB + l32 * ldb + hk;
+  RowsChunk<AM> ring[PD];
+#pragma unroll
+  for (int j = 0; j < PD; ++j) ring[j] = rows_fetch<AM>(a, s, j, l32, hk);
+  for (; s < nslabs; s += stride) {
+    const int64_t sn = s + stride < nslabs ? s + stride : s;  // past the end: re-read (unused)
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NK8; ++j) {
+      const f32x4 av = rows_operand<AM>(ring[j % PD]);
+      // refill the slot with the chunk PD ahead (this slab's j + PD, else the next slab's)
+      ring[j % PD] = j + PD < NK8 ? rows_fetch<AM>(a, s, j + PD, l32, hk)
+                                  : rows_fetch<AM>(a, sn, j + PD - NK8, l32, hk);
+      f32x4 bv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const f32x4*>(bbase + 32 * t * ldb + 8 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma32(bv[t][e], av[e], acc[t]);  // C^T tile: see below
+      // keep each chunk's B fragments and refill in their own step: hoisting every step's LDS reads
+      // to the top of the unrolled loop (the scheduler's default) needs 4 NT x NK8 registers
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // The product is formed transposed (opB as the MFMA A operand), so lane l holds row
+    // m = 32 s + (l & 31) and, in registers 4q..4q+3 of tile t, the 4 consecutive columns
+    // n = 32 t + 8 q + 4 (l >> 5) + 0..3: one float4 store each, 4 NT stores per slab (the waitcnt
+    // pass can still count the ring loads across them; 64 scalar stores overflowed its counter).
+    const int64_t m = s * 32 + l32;
+    if (m < a.M) {
+      float* crow = a.C + m * a.ldc;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + 32 * t + 8 * q + hk;
+          f32x4 z = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+          if (a.c_vec && n + 3 < a.N) {
+            f32x4* c = reinterpret_cast<f32x4*>(crow + n);
+            if (EPI) {
+              if (a.ep.bias) z += *reinterpret_cast<const f32x4*>(a.ep.bias + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) z[e] = rows_act(a, z[e]);
+            } else if (a.accumulate) {
+              z += *c;
+            }
+            *c = z;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < a.N) {
+                float* c = crow + n + e;
+                float v = z[e];
+                if (EPI)
+                  v = rows_act(a, a.ep.bias ? v + a.ep.bias[n + e] : v);
+                else if (a.accumulate)
+                  v = *c + v;
+                *c = v;
+              }
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one float4 of epilogue loads live at a time
+        }
+    }
+  }
+}
+
+static bool rows_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Host: true (and launched) when the shape suits the kernel; false leaves the call to the caller's
+// generic path.  `ep` null: plain product (accumulate honoured); non-null: linear epilogue.
+bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float* Ap, int aperiod, const float* B,
+                   int64_t ldb, int b_trans, int64_t M, int N, int K, float* C, int64_t ldc, int accumulate,
+                   const rk_epilogue* ep, hipStream_t st) {
+  // reduction exactly 32, 64 or 128 deep (no k bounds in the load path)
+  if ((K != 32 && K != 64 && K != 128) || (lda & 3) || !rows_aligned16(A) || M <= 0) return false;
+  if (A_mask && !rows_aligned16(A_mask)) return false;
+  if (Ap && (!rows_aligned16(Ap) || aperiod <= 0)) return false;
+  const int64_t nslabs = (M + 31) / 32;
+  // enough 32-row slabs for every resident wave to get a few (prefetch overlap)
+  if (nslabs < (int64_t)16 * num_cus()) return false;
+  RowsArgs a = {};
+  a.A = A;
+  a.lda = lda;
+  a.A_mask = A_mask;
+  a.Ap = Ap;
+  a.aperiod = aperiod;
+  a.B = B;
+  a.ldb = ldb;
+  a.b_trans = b_trans;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.C = C;
+  a.ldc = ldc;
+  a.accumulate = accumulate;
+  if (ep) a.ep = *ep;
+  a.c_vec = (ldc % 4 == 0) && rows_aligned16(C);
+  a.b_vec = (ldb % 4 == 0) && rows_aligned16(B);
+  const int nk8 = K / 8;
+  const int nt = N <= 32 ? 1 : N <= 64 ? 2 : 4;       // 32-column accumulator tiles per workgroup
+  const int am = A_mask ? kRowsMask : Ap ? kRowsPeriodic : kRowsPlain;
+  if (A_mask && Ap) return false;
+  if (ep && (ep->residual || ep->pre_scale || ep->post_scale ||
+             (ep->act != RK_ACT_NONE && ep->act != RK_ACT_RELU && ep->act != RK_ACT_LEAKY) ||
+             (ep->bias && !rows_aligned16(ep->bias))))
+    return false;  // linear_kernel's general epilogue
+  if (ep && am == kRowsMask) return false;
+  const int ntile = (N + 32 * nt - 1) / (32 * nt);
+  if (ntile > 65535) return false;
+  const size_t shm = sizeof(float) * (size_t)(32 * nt) * (8 * nk8 + 4);
+  const int64_t per_tile = std::min<int64_t>((nslabs + kRowsWaves - 1) / kRowsWaves, (int64_t)2 * num_cus());
+  dim3 grid((unsigned)std::max<int64_t>(1, per_tile / ntile), (unsigned)ntile);
+  bool done = false;
+  auto go = [&](void (*kern)(RowsArgs)) {
+    static const void* raised[64];  // kernels whose dynamic-LDS limit is raised (> 64 KiB at nt 4, K 128)
+    static int nraised = 0;
+    bool seen = false;
+    for (int i = 0; i < nraised; ++i) seen |= raised[i] == (const void*)kern;
+    if (!seen && nraised < 64) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      raised[nraised++] = (const void*)kern;
+    }
+    kern<<<grid, 256, shm, st>>>(a);
+    done = true;
+  };
+#define RK_ROWS_NT(NK, NT)                                                      \
+  if (nk8 == NK && nt == NT) {                                                  \
+    if (ep) {                                                                   \
+      if (am == kRowsPeriodic)                                                  \
+        go(gemm_rows_kernel<NK, NT, true, kRowsPeriodic>);                      \
+      else                                                                      \
+        go(gemm_rows_kernel<NK, NT, true, kRowsPlain>);                         \
+    } else {                                                                    \
+      if (am == kRowsMask)                                                      \
+        go(gemm_rows_kernel<NK, NT, false, kRowsMask>);                         \
+      else if (am == kRowsPeriodic)                                             \
+        go(gemm_rows_kernel<NK, NT, false, kRowsPeriodic>);                     \
+      else                                                                      \
+        go(gemm_rows_kernel<NK, NT, false, kRowsPlain>);                        \
+    }                                                                           \
+  }
+  RK_ROWS_NT(4, 1) RK_ROWS_NT(4, 2) RK_ROWS_NT(4, 4)
+  RK_ROWS_NT(8, 1) RK_ROWS_NT(8, 2) RK_ROWS_NT(8, 4)
+  RK_ROWS_NT(16, 1) RK_ROWS_NT(16, 2) RK_ROWS_NT(16, 4)
+#undef RK_ROWS_NT
+  if (!done) return false;
+  return true;
+}
+
+}  // namespace rk

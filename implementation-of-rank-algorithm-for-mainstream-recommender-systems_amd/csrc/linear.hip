@@ -309,6 +309,8 @@ RK_API int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32
     else
       launch<1, 4, true>(vec, grid, st, x, ldx, x_periodic, x_period, w, ldw, M, N, K, ep, y, ldy, rpt);
   } else {
+    if (gemm_rows_try(x, ldx, nullptr, x_periodic, x_period, w, ldw, 0, M, N, K, y, ldy, 0, &ep, st))
+      return check_launch("rk_linear");
     const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128);
     if (big_tiles >= 2 * num_cus()) {
       dim3 grid((unsigned)((M + 127) / 128), (unsigned)((N + 127) / 128));

@@ -454,6 +454,9 @@ RK_API int rk_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64
   if (M == 0 || N == 0) return RK_OK;
   const int64_t tm = (M + kGT - 1) / kGT, tn = (N + kGT - 1) / kGT;
   if (tm > INT32_MAX || tn > 65535) return fail(RK_ERR_UNSUPPORTED, "rk_gemm: output too large");
+  if (!trans_a && !row_sums && split <= 1 &&
+      gemm_rows_try(A, lda, A_mask, nullptr, 0, B, ldb, trans_b, M, (int)N, (int)R, C, ldc, accumulate, nullptr, st))
+    return check_launch("rk_gemm");
   if (split <= 0) {  // enough workgroups to cover the CUs twice, >= 256 reduction values each
     const int64_t want = (2 * num_cus() + tm * tn - 1) / (tm * tn);
     split = (int32_t)std::max<int64_t>(1, std::min<int64_t>({want, R / 256, 1024}));

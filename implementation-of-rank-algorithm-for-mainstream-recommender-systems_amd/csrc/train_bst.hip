@@ -15,7 +15,6 @@ namespace rk {
 
 constexpr int kBstTMax = 64;   // sequence length envelope of the train kernels
 constexpr int kBstDhMax = 64;  // head width envelope
-constexpr int kBstLd = 65;     // LDS row pitch (bank-conflict padding)
 
 __global__ __launch_bounds__(256) void bst_add_pos_kernel(const float* __restrict__ x, const float* __restrict__ pos,
                                                           int T, int64_t M, int d, float* __restrict__ xp) {
@@ -26,110 +25,276 @@ __global__ __launch_bounds__(256) void bst_add_pos_kernel(const float* __restric
   xp[i] = x[i] + pos[(int64_t)(m % T) * d + k];
 }
 
-// Stage a [T, dh] head slice of a row-major [M, ld] matrix (columns col0..col0+dh) into LDS.
-__device__ __forceinline__ void bst_stage(float* __restrict__ dst, const float* __restrict__ src, int64_t ld,
-                                          int64_t row0, int col0, int T, int dh) {
-  for (int i = threadIdx.x; i < T * dh; i += blockDim.x) {
-    const int t = i / dh, k = i - t * dh;
-    dst[t * kBstLd + k] = src[(row0 + t) * ld + col0 + k];
+// Attention train kernels on FP32 MFMA (v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k] and
+// B[k][l&15] with hardware k = l>>4; accumulator register r of lane l is D[4*(l>>4) + r][l&15]).
+// One 256-thread workgroup per (sample, head); T is padded to TP = 16*ceil(T/16) <= 64 positions and
+// the head width to DP = 16*ceil(dh/16) <= 64 columns, zero-filled in LDS.  Wave w owns the 16-row
+// strip w of the TP x TP score matrix.  Scores are formed transposed (S^T = K Q^T), so a lane's
+// accumulators hold S[i = l&15][j = 16*jt + 4*(l>>4) + r]: the row-softmax reduces over registers
+// and the lane pairs l^16, l^32, and the probabilities are already the A operand of P V (k = j) —
+// no LDS round trip between the two products.
+// LDS (dynamic): the [TP][DP + 4] operand tiles, and in the backward two [TP][TP + 4] tiles (P, dS).
+__host__ __device__ constexpr int att_pad16(int v) { return (v + 15) & ~15; }
+static size_t att_lds_bytes(int T, int dh, bool bwd) {
+  const int TP = att_pad16(T), DP = att_pad16(dh);
+  return sizeof(float) * (size_t)(bwd ? 4 * TP * (DP + 4) + 2 * TP * (TP + 4) : 3 * TP * (DP + 4));
+}
+
+
+__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+
+// Stage a [T, dh] head slice (columns col0..col0+dh of a row-major [M, ld] matrix) into a zero-padded
+// [TP][DP] LDS tile of pitch ldt.
+__device__ __forceinline__ void att_stage(float* __restrict__ dst, int ldt, const float* __restrict__ src, int64_t ld,
+                                          int64_t row0, int col0, int T, int dh, int TP, int DP) {
+  if (((dh | ld | col0) & 3) == 0) {  // float4 path (16-B aligned rows, dh a multiple of 4)
+    const int q = DP / 4;
+    for (int i = threadIdx.x; i < TP * q; i += blockDim.x) {
+      const int t = i / q, k = 4 * (i - t * q);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (t < T && k < dh) v = *reinterpret_cast<const f32x4*>(src + (row0 + t) * ld + col0 + k);
+      *reinterpret_cast<f32x4*>(dst + t * ldt + k) = v;
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < TP * DP; i += blockDim.x) {
+    const int t = i / DP, k = i - t * DP;
+    dst[t * ldt + k] = (t < T && k < dh) ? src[(row0 + t) * ld + col0 + k] : 0.f;
   }
 }
 
-// Workgroup per (sample, head).  Phase 1: wave w computes the probability rows w, w+4, ... (lane =
-// key position) into LDS and HBM; phase 2: ctx = P V with lane = (row in a group of 64/dh rows,
-// column), so every lane is busy at dh = 32.
+// acc[jt] += rows(16*jt ..) of X  .  rows(16*w ..) of Y, contracted over DP columns (both [TP][ldt] LDS
+// tiles): lane ends with D[j = 16*jt + 4*(l>>4) + r][i = l&15] = sum_c X[j][c] Y[i][c].
+__device__ __forceinline__ void att_rowdot(f32x4 (&acc)[4], const float* __restrict__ X, const float* __restrict__ Y,
+                                           int ldt, int w, int NS, int ND, int lane) {
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) acc[jt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c >= ND) break;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(Y + (16 * w + li) * ldt + 16 * c + kq);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      if (jt >= NS) break;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(X + (16 * jt + li) * ldt + 16 * c + kq);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[jt] = mfma16x4(a[e], b[e], acc[jt]);
+    }
+  }
+}
+
+// out[ct] = A (registers: lane holds A[i = l&15][k = 16*kt + 4*(l>>4) + e] in a[kt][e]) . B[k][16*ct + (l&15)]
+// with B a [TP][ldb] LDS tile; lane ends with D[i = 4*(l>>4) + r][c = 16*ct + (l&15)].
+__device__ __forceinline__ void att_regmm(f32x4 (&out)[4], const f32x4 (&a)[4], const float* __restrict__ B, int ldb,
+                                         int NS, int ND, int lane) {
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) out[ct] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt >= NS) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float* brow = B + (16 * kt + kq + e) * ldb + li;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        if (ct >= ND) break;
+        out[ct] = mfma16x4(a[kt][e], brow[16 * ct], out[ct]);
+      }
+    }
+  }
+}
+
+// out[ct] = sum_i At[i][16*w + (l&15)] . B[i][16*ct + (l&15)] over i < TP: the transposed-A product
+// (dK = dS^T Q, dV = P^T dC) for the 16 output rows of strip w; At is [TP][lda], B is [TP][ldb] in LDS.
+__device__ __forceinline__ void att_tmm(f32x4 (&out)[4], const float* __restrict__ At, int lda,
+                                       const float* __restrict__ B, int ldb, int w, int NS, int ND, int lane) {
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) out[ct] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt >= NS) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 16 * kt + kq + e;
+      const float a = At[i * lda + 16 * w + li];
+      const float* brow = B + i * ldb + li;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        if (ct >= ND) break;
+        out[ct] = mfma16x4(a, brow[16 * ct], out[ct]);
+      }
+    }
+  }
+}
+
+// Store a strip result (lane holds D[16*w + 4*(l>>4) + r][16*ct + (l&15)]) into rows row0.. of a
+// row-major matrix at column col0 (rows < T, columns < dh only).
+__device__ __forceinline__ void att_store(const f32x4 (&v)[4], float* __restrict__ dst, int64_t ld, int64_t row0,
+                                          int col0, int w, int T, int dh, int ND, int lane) {
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    if (ct >= ND) break;
+    const int c = 16 * ct + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * w + kq + r;
+      if (i < T && c < dh) dst[(row0 + i) * ld + col0 + c] = v[ct][r];
+    }
+  }
+}
+
+// P = softmax(mask(Q K^T / sqrt(dh))) (saved, [B, h, T, T]) and ctx = P V.
 __global__ __launch_bounds__(256) void bst_attn_train_fwd_kernel(const float* __restrict__ qkv, int64_t B, int T,
                                                                  int d, int heads,
                                                                  const int64_t* __restrict__ seq_len,
                                                                  float* __restrict__ P, float* __restrict__ ctx) {
-  __shared__ float sQ[kBstTMax * kBstLd], sK[kBstTMax * kBstLd], sV[kBstTMax * kBstLd], sP[kBstTMax * kBstLd];
+  extern __shared__ __attribute__((aligned(16))) float att_sm[];
   const int64_t b = blockIdx.x / heads;
   const int h = (int)(blockIdx.x - b * heads);
   const int dh = d / heads;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int TP = (T + 15) & ~15, DP = (dh + 15) & ~15, ldt = DP + 4;
+  const int NS = TP / 16, ND = DP / 16;
+  float* const sQ = att_sm;
+  float* const sK = sQ + TP * ldt;
+  float* const sV = sK + TP * ldt;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t row0 = b * T, ld = 3 * (int64_t)d;
-  bst_stage(sQ, qkv, ld, row0, h * dh, T, dh);
-  bst_stage(sK, qkv, ld, row0, d + h * dh, T, dh);
-  bst_stage(sV, qkv, ld, row0, 2 * d + h * dh, T, dh);
+  att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
+  att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
+  att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
   __syncthreads();
+  if (w >= NS) return;
+  const int li = lane & 15, kq = 4 * (lane >> 4);
   const int64_t len = seq_len[b];
   const float sq = sqrtf((float)dh);  // scores / math.sqrt(q.size(-1)), bst.py:77
-  float* Pb = P + (b * heads + h) * (int64_t)T * T;
-  for (int i = wv; i < T; i += 4) {
-    float s = -INFINITY;
-    if (lane < T) {
-      float acc = 0.f;
-      for (int k = 0; k < dh; ++k) acc = fmaf(sQ[i * kBstLd + k], sK[lane * kBstLd + k], acc);
-      s = (int64_t)lane < len ? acc / sq : -INFINITY;  // masked_fill(key_padding_mask, -inf)
+  f32x4 s[4];
+  att_rowdot(s, sK, sQ, ldt, w, NS, ND, lane);  // s[jt][r] = S[i = 16w + li][j = 16jt + kq + r]
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      const float v = (jt < NS && j < T) ? ((int64_t)j < len ? s[jt][r] / sq : -INFINITY) : -INFINITY;
+      s[jt][r] = v;  // masked_fill(key_padding_mask, -inf), bst.py:80
+      mx = fmaxf(mx, v);
     }
-    const float mx = wave_max(s);
-    const float e = lane < T ? expf(s - mx) : 0.f;
-    const float sum = wave_sum(e);
-    const float p = e / sum;
-    if (lane < T) {
-      Pb[(int64_t)i * T + lane] = p;
-      sP[i * kBstLd + lane] = p;
+  mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  float sum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      const float e = (jt < NS && j < T) ? expf(s[jt][r] - mx) : 0.f;
+      s[jt][r] = e;
+      sum += e;
     }
+  sum += __shfl_xor(sum, 16, kWave);
+  sum += __shfl_xor(sum, 32, kWave);
+  const int i = 16 * w + li;
+  float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
+  const bool vec = (T & 3) == 0;  // rows of P are 16-B aligned: one float4 store per key tile
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    if (jt >= NS) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      const float p = s[jt][r] / sum;
+      s[jt][r] = j < T ? p : 0.f;
+      if (!vec && i < T && j < T) Pi[j] = p;
+    }
+    if (vec && i < T && 16 * jt + kq < T) *reinterpret_cast<f32x4*>(Pi + 16 * jt + kq) = s[jt];
   }
-  __syncthreads();
-  const int R = 64 / dh, rr = lane / dh, k = lane - rr * dh;
-  for (int i0 = wv * R; i0 < T; i0 += 4 * R) {
-    const int i = i0 + rr;
-    if (rr < R && i < T) {
-      float c = 0.f;
-      for (int j = 0; j < T; ++j) c = fmaf(sP[i * kBstLd + j], sV[j * kBstLd + k], c);
-      ctx[(row0 + i) * d + h * dh + k] = c;
-    }
-  }
+  f32x4 c[4];
+  att_regmm(c, s, sV, ldt, NS, ND, lane);
+  att_store(c, ctx, d, row0, h * dh, w, T, dh, ND, lane);
 }
 
 // Backward of the above from dctx [M, d]: dqkv [M, 3d] (overwritten).
 //   dP = dC V^T;  dS = P (dP - rowsum(P dP)) / sqrt(dh);  dQ = dS K;  dK = dS^T Q;  dV = P^T dC.
+// Phase 1 (wave = query strip): dP (transposed form, as S above), P from HBM in the same register
+// layout, dS, dQ = dS K with dS as the register A operand; P and dS go to LDS.  Phase 2 (wave = key
+// strip): dK and dV from the LDS copies (transposed-A products).
 __global__ __launch_bounds__(256) void bst_attn_train_bwd_kernel(const float* __restrict__ qkv,
                                                                  const float* __restrict__ P,
                                                                  const float* __restrict__ dctx, int64_t B, int T,
                                                                  int d, int heads, float* __restrict__ dqkv) {
-  __shared__ float sQ[kBstTMax * kBstLd], sK[kBstTMax * kBstLd], sV[kBstTMax * kBstLd];
-  __shared__ float sC[kBstTMax * kBstLd], sP[kBstTMax * kBstLd], sS[kBstTMax * kBstLd];
+  extern __shared__ __attribute__((aligned(16))) float att_sm[];
   const int64_t b = blockIdx.x / heads;
   const int h = (int)(blockIdx.x - b * heads);
   const int dh = d / heads;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int TP = (T + 15) & ~15, DP = (dh + 15) & ~15, ldt = DP + 4, ldp = TP + 4;
+  const int NS = TP / 16, ND = DP / 16;
+  float* const sQ = att_sm;
+  float* const sK = sQ + TP * ldt;
+  float* const sV = sK + TP * ldt;
+  float* const sC = sV + TP * ldt;
+  float* const sP = sC + TP * ldt;
+  float* const sS = sP + TP * ldp;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, kq = 4 * (lane >> 4);
   const int64_t row0 = b * T, ld = 3 * (int64_t)d;
-  bst_stage(sQ, qkv, ld, row0, h * dh, T, dh);
-  bst_stage(sK, qkv, ld, row0, d + h * dh, T, dh);
-  bst_stage(sV, qkv, ld, row0, 2 * d + h * dh, T, dh);
-  bst_stage(sC, dctx, d, row0, h * dh, T, dh);
-  const float* Pb = P + (b * heads + h) * (int64_t)T * T;
-  for (int i = threadIdx.x; i < T * T; i += blockDim.x) sP[(i / T) * kBstLd + i % T] = Pb[i];
+  att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
+  att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
+  att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
+  att_stage(sC, ldt, dctx, d, row0, h * dh, T, dh, TP, DP);
   __syncthreads();
   const float sq = sqrtf((float)dh);
-  for (int i = wv; i < T; i += 4) {
-    float dp = 0.f, p = 0.f;
-    if (lane < T) {
-      for (int k = 0; k < dh; ++k) dp = fmaf(sC[i * kBstLd + k], sV[lane * kBstLd + k], dp);
-      p = sP[i * kBstLd + lane];
+  if (w < NS) {
+    f32x4 g[4];
+    att_rowdot(g, sV, sC, ldt, w, NS, ND, lane);  // g[jt][r] = dP[i = 16w + li][j = 16jt + kq + r]
+    const int i = 16 * w + li;
+    const float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
+    f32x4 p[4];
+    const bool vec = (T & 3) == 0;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      p[jt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (jt >= NS || i >= T) continue;
+      if (vec) {
+        if (16 * jt + kq < T) p[jt] = *reinterpret_cast<const f32x4*>(Pi + 16 * jt + kq);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * jt + kq + r < T) p[jt][r] = Pi[16 * jt + kq + r];
+      }
     }
-    const float D = wave_sum(p * dp);
-    if (lane < T) sS[i * kBstLd + lane] = p * (dp - D) / sq;
+    float D = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) D += p[jt][r] * g[jt][r];
+    D += __shfl_xor(D, 16, kWave);
+    D += __shfl_xor(D, 32, kWave);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      if (jt >= NS) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[jt][r] = p[jt][r] * (g[jt][r] - D) / sq;
+      *reinterpret_cast<f32x4*>(sP + i * ldp + 16 * jt + kq) = p[jt];
+      *reinterpret_cast<f32x4*>(sS + i * ldp + 16 * jt + kq) = g[jt];
+    }
+    f32x4 q[4];
+    att_regmm(q, g, sK, ldt, NS, ND, lane);  // dQ[i] = sum_j dS[i, j] K[j]
+    att_store(q, dqkv, ld, row0, h * dh, w, T, dh, ND, lane);
   }
   __syncthreads();
-  // lane = (row in a group of 64/dh rows, column): every lane busy at dh = 32
-  const int R = 64 / dh, rr = lane / dh, c = lane - rr * dh;
-  for (int i0 = wv * R; i0 < T; i0 += 4 * R) {
-    const int i = i0 + rr;
-    if (rr < R && i < T) {
-      float q = 0.f, kk = 0.f, v = 0.f;
-      for (int j = 0; j < T; ++j) {
-        q = fmaf(sS[i * kBstLd + j], sK[j * kBstLd + c], q);   // dQ[i] = sum_j dS[i, j] K[j]
-        kk = fmaf(sS[j * kBstLd + i], sQ[j * kBstLd + c], kk);  // dK[i] = sum_j dS[j, i] Q[j]
-        v = fmaf(sP[j * kBstLd + i], sC[j * kBstLd + c], v);    // dV[i] = sum_j P[j, i] dC[j]
-      }
-      float* o = dqkv + (row0 + i) * ld + h * dh + c;
-      o[0] = q;
-      o[d] = kk;
-      o[2 * d] = v;
-    }
+  if (w < NS) {
+    f32x4 o[4];
+    att_tmm(o, sS, ldp, sQ, ldt, w, NS, ND, lane);  // dK[j] = sum_i dS[i, j] Q[i]
+    att_store(o, dqkv, ld, row0, d + h * dh, w, T, dh, ND, lane);
+    att_tmm(o, sP, ldp, sC, ldt, w, NS, ND, lane);  // dV[j] = sum_i P[i, j] dC[i]
+    att_store(o, dqkv, ld, row0, 2 * d + h * dh, w, T, dh, ND, lane);
   }
 }
 
@@ -322,6 +487,17 @@ __global__ __launch_bounds__(256) void bst_pool_bwd_kernel(const float* __restri
 
 static inline unsigned grid_of(int64_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
 
+// Dynamic LDS above the 64 KiB default: up to 104 KiB (T = 64, dh = 64 backward).
+static void att_set_attrs() {
+  static bool done = false;
+  if (done) return;
+  (void)hipFuncSetAttribute((const void*)bst_attn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  (void)hipFuncSetAttribute((const void*)bst_attn_train_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  done = true;
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -341,7 +517,9 @@ RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T,
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_forward: T <= %d, d %% heads == 0, d/heads <= %d", kBstTMax,
                 kBstDhMax);
   if (batch == 0) return RK_OK;
-  bst_attn_train_fwd_kernel<<<(unsigned)(batch * heads), 256, 0, (hipStream_t)stream>>>(qkv, batch, T, d, heads,
+  att_set_attrs();
+  bst_attn_train_fwd_kernel<<<(unsigned)(batch * heads), 256, att_lds_bytes(T, d / heads, false),
+                              (hipStream_t)stream>>>(qkv, batch, T, d, heads,
                                                                                         seq_len, probs, ctx);
   return check_launch("rk_bst_attn_train_forward");
 }
@@ -352,7 +530,9 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
       d / heads > kBstDhMax)
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_backward: T <= %d, d/heads <= %d", kBstTMax, kBstDhMax);
   if (batch == 0) return RK_OK;
-  bst_attn_train_bwd_kernel<<<(unsigned)(batch * heads), 256, 0, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T,
+  att_set_attrs();
+  bst_attn_train_bwd_kernel<<<(unsigned)(batch * heads), 256, att_lds_bytes(T, d / heads, true),
+                              (hipStream_t)stream>>>(qkv, probs, dctx, batch, T,
                                                                                         d, heads, dqkv);
   return check_launch("rk_bst_attn_train_backward");
 }

@@ -833,3 +833,114 @@ def test_graph_replayed_train_steps_then_eval():
         g.replay()
     torch.cuda.synchronize()
     _eval_vs_oracle(model, "din", cfg, inp, interaction=att)
+
+
+def _attn_reference(qkv, B, T, d, heads, seq_len, dctx):
+    """bst.py:72-83 in float64 autograd: softmax(mask(Q K^T / sqrt(dh))) V, mask = positions >= len."""
+    dh = d // heads
+    x = qkv.detach().double().requires_grad_(True)
+    q, k, v = (x[:, i * d:(i + 1) * d].view(B, T, heads, dh).transpose(1, 2) for i in range(3))
+    s = torch.matmul(q, k.transpose(-2, -1)) / np.sqrt(dh)
+    mask = torch.arange(T)[None, :] >= seq_len.cpu()[:, None]
+    s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    ctx = torch.matmul(p, v).transpose(1, 2).reshape(B * T, d)
+    ctx.backward(dctx.double())
+    return p, ctx, x.grad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,d,heads", [(64, 128, 4), (50, 32, 4), (20, 32, 4), (1, 16, 2), (17, 48, 1), (33, 256, 4),
+                                       (64, 256, 4), (7, 12, 3)])
+def test_bst_attention_train_kernels_match_autograd(T, d, heads):
+    """rk_bst_attn_train_forward / _backward (MFMA, T and dh zero-padded to 16) against float64 autograd
+    over every padding case: T < 16, T = 16k + 1, dh = 4, 12, 16, 48, 64; lengths 1..T (length 0 gives
+    NaN rows in the reference and here, checked separately)."""
+    g = torch.Generator().manual_seed(T * 1000 + d)
+    B = 37
+    qkv = torch.randn(B * T, 3 * d, generator=g)
+    dctx = torch.randn(B * T, d, generator=g)
+    seq_len = torch.randint(1, T + 1, (B,), generator=g)
+    seq_len[0], seq_len[-1] = 1, T
+    p_ref, c_ref, dx_ref = _attn_reference(qkv, B, T, d, heads, seq_len, dctx)
+    dev = torch.device("cuda")
+    qkv_d, dctx_d, len_d = qkv.to(dev), dctx.to(dev), seq_len.to(dev)
+    probs = torch.full((B, heads, T, T), float("nan"), device=dev)
+    ctx = torch.full((B * T, d), float("nan"), device=dev)
+    dqkv = torch.full((B * T, 3 * d), float("nan"), device=dev)
+    ops.bst_attn_train_forward(qkv_d, B, T, d, heads, len_d, probs, ctx)
+    ops.bst_attn_train_backward(qkv_d, probs, dctx_d, B, T, d, heads, dqkv)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(probs.cpu().double(), p_ref.detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(ctx.cpu().double(), c_ref.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dqkv.cpu().double(), dx_ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_bst_attention_train_length_zero_is_nan():
+    """A sample with no valid key: the reference's softmax over an all -inf row is NaN (bst.py:80-82)."""
+    B, T, d, heads = 3, 20, 32, 4
+    qkv = torch.randn(B * T, 3 * d, device="cuda")
+    seq_len = torch.tensor([5, 0, 20], device="cuda")
+    probs = torch.empty(B, heads, T, T, device="cuda")
+    ctx = torch.empty(B * T, d, device="cuda")
+    ops.bst_attn_train_forward(qkv, B, T, d, heads, seq_len, probs, ctx)
+    torch.cuda.synchronize()
+    assert torch.isnan(probs[1]).all() and torch.isnan(ctx[T:2 * T]).all()
+    assert torch.isfinite(probs[0]).all() and torch.isfinite(ctx[:T]).all() and torch.isfinite(ctx[2 * T:]).all()
+
+
+# Tall-skinny shapes (gemm_rows.hip: M >= 32 x 16 x CUs rows, reduction <= 128) — the BST / DIN training
+# GEMMs.  M is deliberately not a multiple of 32.
+ROWS_M = 131072 + 77
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("TB", [0, 1])
+@pytest.mark.parametrize("N,R", [(128, 128), (64, 128), (200, 36), (7, 12), (384, 64), (32, 100)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_gemm_rows_tall_skinny_matches_fp64(TB, N, R, masked):
+    M = ROWS_M
+    A, B, mask, want, _ = _gemm_case(0, TB, M, N, R, masked, seed=N * 13 + R + TB)
+    C = torch.full((M, N), 7.0, device="cuda")
+    Ad, Bd = A.cuda(), B.cuda()
+    md = mask.cuda() if mask is not None else None
+    ops.gemm(0, TB, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md)
+    tol = 1e-4 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
+    ops.gemm(0, TB, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md, accumulate=True)
+    torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K,act,periodic,residual", [(128, 128, "none", True, False), (128, 128, "relu", False, True),
+                                                       (64, 128, "relu", False, False), (32, 64, "none", False, False),
+                                                       (200, 40, "leaky", False, False), (5, 8, "none", True, True)])
+def test_linear_tall_skinny_matches_fp64(N, K, act, periodic, residual):
+    """rk_linear over M = 131149 rows (gemm_rows path): bias, x + periodic addend (BST positions),
+    residual, activation, strided output (ldy > N)."""
+    M = ROWS_M
+    g = torch.Generator().manual_seed(N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    per = torch.randn(64, K, generator=g) if periodic else None
+    res = torch.randn(M, N, generator=g) if residual else None
+    xin = x.double() + (per.double().repeat(M // 64 + 1, 1)[:M] if periodic else 0)
+    want = xin @ w.double().t() + b.double()
+    if residual:
+        want = res.double() + want
+    if act == "relu":
+        want = want.clamp_min(0)
+    elif act == "leaky":
+        want = torch.where(want > 0, want, want * 0.01)
+    out = torch.full((M, N + 3), 7.0, device="cuda")
+    bd = b.cuda()
+    rd = res.cuda() if residual else None
+    ep = ops.make_epilogue(bias=bd, act=act if act != "none" else None, slope=0.01, residual=rd,
+                           ld_residual=N if residual else 0)
+    ops.linear(x.cuda(), w.cuda(), None, y_ptr=out.data_ptr(), ldy=N + 3,
+               x_periodic=per.cuda() if periodic else None, x_period=64 if periodic else 0, epilogue=ep)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out[:, :N].cpu().double(), want, rtol=1e-4, atol=1e-4)
+    assert float((out[:, N:] - 7.0).abs().max()) == 0.0
