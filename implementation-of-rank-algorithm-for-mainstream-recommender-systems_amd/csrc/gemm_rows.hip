@@ -295,4 +295,5 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
   return true;
 }
 
+
 }  // namespace rk

@@ -944,3 +944,24 @@ def test_linear_tall_skinny_matches_fp64(N, K, act, periodic, residual):
     torch.cuda.synchronize()
     torch.testing.assert_close(out[:, :N].cpu().double(), want, rtol=1e-4, atol=1e-4)
     assert float((out[:, N:] - 7.0).abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(128, 128), (64, 128), (200, 36), (7, 12), (256, 512)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_gemm_cols_weight_gradient_matches_fp64(M, N, masked):
+    """rk_gemm(trans_a, trans_b) over R = 131149 rows (the weight-gradient shape: split reduction + atomics):
+    C = opA^T-reduction and the bias row sums, fresh and accumulated."""
+    R = ROWS_M
+    A, B, mask, want, rs = _gemm_case(1, 1, M, N, R, masked, seed=M + 3 * N)
+    C = torch.full((M, N), 7.0, device="cuda")
+    sums = torch.full((M,), 7.0, device="cuda")
+    Ad, Bd = A.cuda(), B.cuda()
+    md = mask.cuda() if mask is not None else None
+    ops.gemm(1, 1, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md, row_sums=sums)
+    tol = 2e-4 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
+    torch.testing.assert_close(sums.cpu().double(), rs, rtol=0, atol=tol)
+    ops.gemm(1, 1, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md, row_sums=sums, accumulate=True)
+    torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
+    torch.testing.assert_close(sums.cpu().double(), 2 * rs, rtol=0, atol=2 * tol)
