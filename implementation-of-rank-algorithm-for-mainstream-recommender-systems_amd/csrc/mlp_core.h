@@ -114,13 +114,19 @@ __device__ unsigned g_mlp_wg[8192][4];  // per workgroup: HW_ID, XCC_ID, wall du
 // Weight ring and per-column epilogue parameters of one layer for a wave owning TPW column tiles
 // (t = wave + 16*j).  prepare() issues the first PD weight chunks and the parameter loads; it runs
 // before the barrier that closes the previous layer, so that latency overlaps the previous
-// layer's tail instead of opening this one.
-template <int TPW, int PD = kMlpPD>
+// layer's tail instead of opening this one.  One register set serves both layer shapes: chunk s of
+// tile j sits in ring[s * TPW + j], so a one-tile layer (n <= 256) runs 8 chunks ahead instead of 4
+// (at 4 waves per SIMD, 4 chunks of one tile were ~2k cycles of cover against the L2 latency of
+// 256 CUs streaming the same weights: tools/mlp_phases.hip layer 1 waited ~9k cycles at its barrier).
+constexpr int kMlpRing = 8;  // f32x4 ring slots per lane
+
 struct LayerPipe {
-  const float* wrow[TPW];
-  f32x4_t ring[PD][TPW];
-  ColEpi ep[TPW];
+  const float* wrow[2];
+  f32x4_t ring[kMlpRing];
+  ColEpi ep[2];
+  template <int TPW, int PD>
   __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int wave, int lane) {
+    static_assert(TPW * PD <= kMlpRing, "ring overflow");
     const int li = lane & 15;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
@@ -131,18 +137,18 @@ struct LayerPipe {
 #pragma unroll
     for (int s = 0; s < PD; ++s)
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) ring[s][j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * s);
+      for (int j = 0; j < TPW; ++j) ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * s);
   }
 };
 
 // One layer (weights already in flight in P) over RT row tiles of 16 rows: each weight float4
-// feeds RT x 4 MFMAs.
-template <int TPW, int RT = 1, int PD = kMlpPD>
-__device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_layer& L, const float* __restrict__ in,
+// feeds RT x 4 MFMAs.  kchunks = Kp / 16 must be a multiple of PD.
+template <int TPW, int RT, int PD>
+__device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, const float* __restrict__ in,
                                           int ldin, float* __restrict__ out, int ldout, int Kp, int wave, int lane,
                                           int64_t m0, int rows, int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
   const int li = lane & 15, kq = 4 * (lane >> 4);
-  const int kchunks = Kp / 16;  // multiple of PD
+  const int kchunks = Kp / 16;
   f32x4_t acc[TPW][RT];
 #pragma unroll
   for (int j = 0; j < TPW; ++j)
@@ -170,11 +176,12 @@ __device__ __forceinline__ void mlp_layer(LayerPipe<TPW, PD>& P, const rk_mlp_la
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
 #pragma unroll
-          for (int t = 0; t < RT; ++t) acc[j][t] = mfma16(av[t][e], P.ring[s][j][e], acc[j][t]);
+          for (int t = 0; t < RT; ++t) acc[j][t] = mfma16(av[t][e], P.ring[s * TPW + j][e], acc[j][t]);
       // refill this slot with chunk c + PD (clamped: the tail re-reads the last chunk, unused)
       const int cn = min(c + PD, kchunks - 1);
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) P.ring[s][j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + kFragStep * cn);
+      for (int j = 0; j < TPW; ++j)
+        P.ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + kFragStep * cn);
       // keep the refill here: sinking it to the end of the unrolled body would leave each
       // slot's latency uncovered by the other slots' MFMAs
       __builtin_amdgcn_sched_barrier(0);
@@ -231,18 +238,42 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
                                          const rk_epilogue& h, float* y, int64_t ldy, int tid,
                                          Stage stage = Stage()) {
   const int lane = tid & 63, wave = tid >> 6;
-  LayerPipe<2> p2;
-  LayerPipe<1> p1;
+  LayerPipe pipe;
+  // one-tile layers with a reduction of a multiple of 128 run the 8-deep ring
+  auto deep = [&](int l) { return (pad64(l ? layers[l - 1].n : K0) / 16) % 8 == 0; };
   auto prepare = [&](int l) {
     const int nt = pad64(layers[l].n) / 16;  // multiple of 4
     if (wave + kMlpWaves < nt)
-      p2.prepare(layers[l], wave, lane);
-    else if (wave < nt)
-      p1.prepare(layers[l], wave, lane);
+      pipe.prepare<2, 4>(layers[l], wave, lane);
+    else if (wave < nt) {
+      if (deep(l))
+        pipe.prepare<1, 8>(layers[l], wave, lane);
+      else
+        pipe.prepare<1, 4>(layers[l], wave, lane);
+    }
   };
+  // The head's operands (head_w for this lane's columns, this wave's row scalars) are loaded while
+  // the last layer runs: fetched after the final barrier they put two dependent L2 round trips
+  // (~10k cycles at 256 busy CUs, tools/mlp_phases.hip) between the last MFMA and the logits.
+  const int Kh = nl ? layers[nl - 1].n : K0;
+  const bool hpre = h.head_w != nullptr && Kh <= 128;
+  float hw[2] = {0.f, 0.f};
+  float hp = 0.f;
+  auto head_prefetch = [&]() {
+    if (!hpre) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (lane + 64 * c < Kh) hw[c] = h.head_w[lane + 64 * c];
+    if (wave < rows && h.head_partial) hp = h.head_partial[m0 + wave];
+  };
+#ifdef RK_MLP_PHASES
+  const unsigned long long t_start = clock64();
+#endif
   if (nl > 0) prepare(0);
+  if (nl <= 1) head_prefetch();
   stage();
   mlp_lds_barrier();
+  MLP_MARK(3 * RK_MLP_MAX_LAYERS, t_start);  // prologue: input staged, layer 0 weights in flight
   int Kp = pad64(K0);
   for (int l = 0; l < nl; ++l) {
     const unsigned long long t0 =
@@ -257,10 +288,15 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
     if (wave + kMlpWaves < ntiles)
-      mlp_layer<2, RT>(p2, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
-    else if (wave < ntiles)
-      mlp_layer<1, RT>(p1, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
+      mlp_layer<2, RT, 4>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
+    else if (wave < ntiles) {
+      if (deep(l))
+        mlp_layer<1, RT, 8>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
+      else
+        mlp_layer<1, RT, 4>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
+    }
     if (l + 1 < nl) prepare(l + 1);
+    if (l + 2 == nl) head_prefetch();
     MLP_MARK(3 * l + 1, t0);
     mlp_lds_barrier();
     MLP_MARK(3 * l + 2, t0);
@@ -271,13 +307,20 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
   const int K = nl ? layers[nl - 1].n : K0;
   if (h.head_w) {
     for (int r = wave; r < rows; r += kMlpWaves) {
+      const bool pre = hpre && r == wave;  // operands prefetched for the wave's first row
       float p = 0.f;
-      for (int n = lane; n < K; n += 64) p = fmaf(fin[r * ldf + n], h.head_w[n], p);
+      if (pre) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (lane + 64 * c < K) p = fmaf(fin[r * ldf + lane + 64 * c], hw[c], p);
+      } else {
+        for (int n = lane; n < K; n += 64) p = fmaf(fin[r * ldf + n], h.head_w[n], p);
+      }
       p = wave_sum(p);
       if (lane == 0) {
         const int64_t m = m0 + r;
         float logit = p + h.head_b[0];
-        if (h.head_partial) logit = h.head_partial[m] + logit;
+        if (h.head_partial) logit = (pre ? hp : h.head_partial[m]) + logit;
         if (h.fm1) {
           if (h.head_aux) h.head_aux[m] = logit;
           logit = h.fm1[m] * h.final_w[0] + h.fm2[m] * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];
