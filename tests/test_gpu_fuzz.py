@@ -1,0 +1,104 @@
+"""Shape / edge fuzzing of the HIP forward path against the CPU oracle (random batch,
+sequence length, field counts and widths; behaviour lengths 0..T; all-OOV ids), driven by
+hypothesis with a fixed example database seed (derandomize) so the suite is deterministic.
+
+Every example builds a seeded model, runs the oracle and the rankops model on the same inputs and
+per-call draws, and compares all outputs at the north-star tolerance (atol 1e-4 + rtol 1e-4, NaN
+where the reference is NaN: a softmax over an empty history)."""
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import helpers as H
+from test_gpu_parity import _compare, run_pair
+
+FUZZ = settings(max_examples=60, deadline=None, derandomize=True, database=None,
+                suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+
+
+def _all_oov(inp):
+    """Every id -> 0 (the bucket an unknown token maps to, din.py:207 / dcn.py:101 vocab.get(.., 0));
+    lengths are kept, so histories of OOV items are attended over."""
+    if isinstance(inp, dict):
+        return {k: (v if "length" in k else _all_oov(v)) for k, v in inp.items()}
+    if isinstance(inp, torch.Tensor) and inp.dtype == torch.int64:
+        return torch.zeros_like(inp)
+    return inp
+
+
+@st.composite
+def din_case(draw):
+    T = draw(st.integers(1, 100))
+    cfg = {"T": T, "dim": draw(st.sampled_from([8, 16, 32])), "softmax": draw(st.booleans()),
+           "min_len": draw(st.sampled_from([0, 1, T])), "activation": draw(st.sampled_from(["dice", "prelu"])),
+           "batch_norm": draw(st.booleans()), "hidden": draw(st.sampled_from([[512, 256, 128], [64], [200, 80]]))}
+    return "din", cfg
+
+
+@st.composite
+def bst_case(draw):
+    dim, heads = draw(st.sampled_from([(16, 4), (32, 4), (128, 4), (24, 3), (8, 1)]))
+    T = draw(st.integers(1, 64))
+    cfg = {"T": T, "dim": dim, "heads": heads, "max_len": 64, "blocks": draw(st.integers(1, 2)),
+           "pooling": draw(st.sampled_from(["sum", "mean"])), "min_len": draw(st.sampled_from([1, T])),
+           "batch_norm": draw(st.booleans())}
+    return "bst", cfg
+
+
+@st.composite
+def deepfm_case(draw):
+    F = draw(st.integers(2, 30))
+    sizes = draw(st.lists(st.integers(1, 3000), min_size=F, max_size=F))
+    cfg = {"dim": draw(st.sampled_from([4, 8, 16, 32])), "fields": {f"f{i:02d}": n for i, n in enumerate(sizes)},
+           "batch_norm": draw(st.booleans())}
+    return "deepfm", cfg
+
+
+@st.composite
+def dense_case(draw):
+    name = draw(st.sampled_from(["dcn", "deepcrossing", "afm"]))
+    if name == "dcn":
+        cfg = {"cross": draw(st.integers(0, 3)), "hidden": draw(st.sampled_from([[512, 256, 128], [64], [300, 32]]))}
+    elif name == "deepcrossing":
+        cfg = {"units": draw(st.integers(1, 3)), "internal": draw(st.sampled_from([32, 64, 128]))}
+    else:
+        cfg = {"dim": draw(st.sampled_from([4, 8, 16])), "att": draw(st.sampled_from([16, 64, 128]))}
+    return name, cfg
+
+
+def _check(case, B, seed, oov):
+    name, cfg = case
+    inp = H.make_inputs(name, cfg, B, seed=seed)
+    if oov:
+        inp = _all_oov(inp)
+    out, ref = run_pair(name, cfg, B, seed=seed, inputs=inp)
+    _compare(out, ref, f"{name} {cfg} B={B} oov={oov}")
+
+
+@pytest.mark.gpu
+@FUZZ
+@given(case=din_case(), B=st.integers(1, 300), seed=st.integers(0, 10_000), oov=st.booleans())
+def test_fuzz_din(case, B, seed, oov):
+    _check(case, B, seed, oov)
+
+
+@pytest.mark.gpu
+@FUZZ
+@given(case=bst_case(), B=st.integers(1, 200), seed=st.integers(0, 10_000), oov=st.booleans())
+def test_fuzz_bst(case, B, seed, oov):
+    _check(case, B, seed, oov)
+
+
+@pytest.mark.gpu
+@FUZZ
+@given(case=deepfm_case(), B=st.integers(1, 300), seed=st.integers(0, 10_000), oov=st.booleans())
+def test_fuzz_deepfm(case, B, seed, oov):
+    _check(case, B, seed, oov)
+
+
+@pytest.mark.gpu
+@FUZZ
+@given(case=dense_case(), B=st.integers(1, 300), seed=st.integers(0, 10_000), oov=st.booleans())
+def test_fuzz_dcn_deepcrossing_afm(case, B, seed, oov):
+    _check(case, B, seed, oov)
