@@ -18,7 +18,7 @@ FUZZ = settings(max_examples=60, deadline=None, derandomize=True, database=None,
 
 
 def _all_oov(inp):
-    """Every id -> 0 (the bucket an unknown token maps to, din.py:207 / dcn.py:101 vocab.get(.., 0));
+    """Every id -> 0 (the index an unknown token maps to: din.py:140-143,152-155, dcn.py:101-104);
     lengths are kept, so histories of OOV items are attended over."""
     if isinstance(inp, dict):
         return {k: (v if "length" in k else _all_oov(v)) for k, v in inp.items()}
