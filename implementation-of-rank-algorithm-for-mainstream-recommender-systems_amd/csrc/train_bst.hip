@@ -345,6 +345,7 @@ __global__ __launch_bounds__(256) void bst_res_dropout_ln_fwd_kernel(
 // in LDS and writes one partial row per workgroup to ws [kLnBlocks][2d], summed in block order by
 // bst_ln_param_kernel (deterministic; per-row atomics on the same 2d addresses serialised).
 constexpr int kLnBlocks = 512;
+constexpr int kLnRows = 4;  // rows in flight per wave
 
 __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ r,
                                                          const float* __restrict__ mean_in,
@@ -359,34 +360,55 @@ __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict
   float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, gm[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) gm[c] = lane + 64 * c < d ? gamma[lane + 64 * c] : 0.f;
-  for (int64_t m = (int64_t)blockIdx.x * 4 + wv; m < M; m += (int64_t)gridDim.x * 4) {
-    const float mean = mean_in[m], rstd = rstd_in[m];
-    float g[4], xh[4];
-    float s1 = 0.f, s2 = 0.f;
+  // kLnRows rows per step, all of their loads issued before the first reduction: one row at a
+  // time left each wave (2 per SIMD at 512 workgroups) waiting a full memory round trip per row
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t m0 = (int64_t)blockIdx.x * 4 + wv; m0 < M; m0 += stride * kLnRows) {
+    float dyv[kLnRows][4], rv[kLnRows][4], mean[kLnRows], rstd[kLnRows];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = lane + 64 * c;
-      g[c] = xh[c] = 0.f;
-      if (k < d) {
-        const float dyv = dy[m * d + k];
-        xh[c] = (r[m * d + k] - mean) * rstd;
-        g[c] = dyv * gm[c];
-        s1 += g[c];
-        s2 += g[c] * xh[c];
-        pg[c] = fmaf(dyv, xh[c], pg[c]);
-        pb[c] += dyv;
+    for (int i = 0; i < kLnRows; ++i) {
+      const int64_t m = m0 + i * stride;
+      const int64_t mm = m < M ? m : M - 1;
+      mean[i] = mean_in[mm];
+      rstd[i] = rstd_in[mm];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = lane + 64 * c;
+        dyv[i][c] = k < d ? dy[mm * d + k] : 0.f;
+        rv[i][c] = k < d ? r[mm * d + k] : 0.f;
       }
     }
-    const float k1 = wave_sum(s1) / (float)d, k2 = wave_sum(s2) / (float)d;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = lane + 64 * c;
-      if (k < d) {
-        const float v = rstd * (g[c] - k1 - xh[c] * k2);
-        dr[m * d + k] = v;
-        if (d_o)
-          d_o[m * d + k] = threshold ? (dropout_keep(seed, stream, (uint64_t)m * d + k, threshold) ? v * scale : 0.f)
-                                     : v;
+    for (int i = 0; i < kLnRows; ++i) {
+      const int64_t m = m0 + i * stride;
+      if (m >= M) break;
+      float g[4], xh[4];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = lane + 64 * c;
+        g[c] = xh[c] = 0.f;
+        if (k < d) {
+          xh[c] = (rv[i][c] - mean[i]) * rstd[i];
+          g[c] = dyv[i][c] * gm[c];
+          s1 += g[c];
+          s2 += g[c] * xh[c];
+          pg[c] = fmaf(dyv[i][c], xh[c], pg[c]);
+          pb[c] += dyv[i][c];
+        }
+      }
+      const float k1 = wave_sum(s1) / (float)d, k2 = wave_sum(s2) / (float)d;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = lane + 64 * c;
+        if (k < d) {
+          const float v = rstd[i] * (g[c] - k1 - xh[c] * k2);
+          dr[m * d + k] = v;
+          if (d_o)
+            d_o[m * d + k] = threshold
+                                 ? (dropout_keep(seed, stream, (uint64_t)m * d + k, threshold) ? v * scale : 0.f)
+                                 : v;
+        }
       }
     }
   }
