@@ -276,8 +276,9 @@ SHARDED_GLOBAL_BATCH = 65536
 
 def bench_sharded(world, rank, steps, warmup):
     """Strong scaling: global batch 65536 split over the ranks, 1e8 embedding rows split by field.
-    Local compute runs as three captured hipGraph segments; the two RCCL all-to-alls run eagerly
-    between them (at world 1 they are plain device copies)."""
+    At world > 1 the local batch runs as ShardedDeepFM's exchange pipeline (pipeline_chunks
+    chunks; per chunk three captured hipGraph segments with asynchronous RCCL all-to-alls between
+    them); at world 1 the forward is one hipGraph (nothing to exchange)."""
     import helpers as H
     from rankops.sharded import ShardedDeepFM, row_stride
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -290,24 +291,39 @@ def bench_sharded(world, rank, steps, warmup):
     B_l = SHARDED_GLOBAL_BATCH // world
     rng = np.random.default_rng(5000 + rank)
     cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l, dtype=np.int64)).to(dev) for f in fields}
-    out_i, in_i = model.index_splits(B_l)
-    out_r, in_r = model.row_splits(B_l)
-    recv_idx = torch.empty(sum(out_i), dtype=torch.int64, device=dev)
-    recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
     if world == 1:  # nothing to exchange: one packed FM gather + the tail, one hipGraph
         g0, _ = graph_of(lambda: model.run_steps(cat))
         step = g0.replay
     else:
-        g1, send = graph_of(lambda: model.pack_indices(cat))
-        g2, rows = graph_of(lambda: model.gather_local(recv_idx, world * B_l))
-        g3, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_l))
+        # the exchange pipeline of ShardedDeepFM.run_steps with each chunk's local segments
+        # (index pack, gather, FM + tail) captured as hipGraphs and the RCCL all-to-alls issued
+        # asynchronously between them: chunk c's rows travel while chunk c+1 gathers
+        segs = []
+        for b0, b1 in model.chunk_bounds(B_l):
+            Bc = b1 - b0
+            cc = {f: v[b0:b1] for f, v in cat.items()}
+            out_i, in_i = model.index_splits(Bc)
+            out_r, in_r = model.row_splits(Bc)
+            recv_idx = torch.empty(sum(out_i), dtype=torch.int64, device=dev)
+            recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
+            g1, send = graph_of(lambda cc=cc: model.pack_indices(cc))
+            g2, rows = graph_of(lambda ri=recv_idx, Bc=Bc: model.gather_local(ri, world * Bc))
+            g3, _ = graph_of(lambda rr=recv_rows, Bc=Bc: model.fm_and_tail(rr, Bc))
+            segs.append((g1, send, g2, rows, g3, recv_idx, recv_rows, out_i, in_i, out_r, in_r))
 
         def step():
-            g1.replay()
-            model._exchange(recv_idx, send, out_i, in_i)
-            g2.replay()
-            model._exchange(recv_rows, rows.reshape(-1), out_r, in_r)
-            g3.replay()
+            works = []
+            for g1, send, _, _, _, recv_idx, _, out_i, in_i, _, _ in segs:
+                g1.replay()
+                works.append(model._exchange(recv_idx, send, out_i, in_i, async_op=True)[1])
+            rworks = []
+            for (_, _, g2, rows, _, _, recv_rows, _, _, out_r, in_r), w in zip(segs, works):
+                w.wait()
+                g2.replay()
+                rworks.append(model._exchange(recv_rows, rows.reshape(-1), out_r, in_r, async_op=True)[1])
+            for (_, _, _, _, g3, _, _, _, _, _, _), w in zip(segs, rworks):
+                w.wait()
+                g3.replay()
 
     t = max_over_ranks(world, time_replays(step, steps, warmup, world))
     wire = B_l * SHARDED_FIELDS * (8 + 4 * row_stride(32)) * (world - 1) / world
@@ -316,7 +332,8 @@ def bench_sharded(world, rank, steps, warmup):
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
             "scaling": "strong",
             "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
-                     "3 hipGraph segments + eager RCCL all_to_all_single")}
+                     f"{len(model.chunk_bounds(B_l))}-chunk pipeline: per chunk 3 hipGraph segments + async RCCL "
+                     "all_to_all_single (row exchange of chunk c overlaps the gather of c+1)")}
 
 
 # ------------------------------------------------------------------ host input path

@@ -15,6 +15,8 @@ rank holds a data-parallel slice of B_l samples with the indices of all F fields
   4. FM + MLP         rk_fm_gather over the received rows (dense segments, field order restored
                       through out_col = f * D), then the fused MLP tail exactly as DeepFM
 
+At P > 1 the steps run per chunk of the local batch (run_steps): each chunk's row all-to-all is
+issued asynchronously and overlaps the next chunk's gather and the previous chunk's FM + tail.
 At P = 1 there is nothing to exchange: the forward is one rk_fm_gather_packed pass over the
 packed tables plus the tail, i.e. `DeepFM.forward` on the same weights.
 The exchange volume per rank and step is B_l * F * (8 + 4 * RS) bytes, (P-1)/P of it on the
@@ -58,6 +60,8 @@ class ShardedDeepFM(EngineModule):
         self.owner = field_owner(len(self.fields), world_size)
         self.fields_of = [[f for i, f in enumerate(self.fields) if self.owner[i] == r] for r in range(world_size)]
         self.local_fields = self.fields_of[rank]
+        self.pipeline_chunks = 4  # exchange pipeline depth at P > 1 (chunk_bounds)
+        self.min_chunk = 512
         self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
                                                      for f in self.local_fields})
         self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
@@ -105,12 +109,14 @@ class ShardedDeepFM(EngineModule):
 
     # ------------------------------------------------------------------ exchange steps
 
-    def _exchange(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+    def _exchange(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, async_op: bool = False):
+        """all_to_all_single (RCCL on ROCm); with async_op the collective runs on the process
+        group's stream and the returned work's wait() orders the caller's stream after it."""
         if self.world == 1:
             out.copy_(inp)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
-        return out
+            return (out, None) if async_op else out
+        work = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=async_op)
+        return (out, work) if async_op else out
 
     def index_splits(self, B_l: int):
         """(output_split_sizes, input_split_sizes) of the index all-to-all, in int64 elements."""
@@ -131,12 +137,12 @@ class ShardedDeepFM(EngineModule):
                 blocks.append(torch.stack([category[f] for f in fr], 1).reshape(-1))
         return torch.cat(blocks) if blocks else torch.empty(0, dtype=torch.int64, device=self._device())
 
-    def exchange_indices(self, category: dict, B_l: int) -> torch.Tensor:
+    def exchange_indices(self, category: dict, B_l: int, async_op: bool = False):
         """Step 1: send [r][b][f_r] index blocks; receive [s][b][f_me]."""
         send = self.pack_indices(category)
         out_s, in_s = self.index_splits(B_l)
         recv = torch.empty(sum(out_s), dtype=torch.int64, device=send.device)
-        return self._exchange(recv, send, out_s, in_s)
+        return self._exchange(recv, send, out_s, in_s, async_op)
 
     def gather_local(self, recv_idx: torch.Tensor, rows_total: int) -> torch.Tensor:
         """Step 2: rows [s*B_l + b][f_me][RS] from this rank's tables (rk_concat_gather)."""
@@ -151,11 +157,11 @@ class ShardedDeepFM(EngineModule):
         ops.concat_gather(segs, rows_total, out)  # whole packed rows, 16-B vectorised path
         return out
 
-    def exchange_rows(self, rows: torch.Tensor, B_l: int) -> torch.Tensor:
+    def exchange_rows(self, rows: torch.Tensor, B_l: int, async_op: bool = False):
         """Step 3: send [s][b][f_me][RS] back to every source; receive [r][b][f_r][RS]."""
         out_s, in_s = self.row_splits(B_l)
         recv = torch.empty(sum(out_s), device=rows.device, dtype=torch.float32)
-        return self._exchange(recv, rows.reshape(-1), out_s, in_s)
+        return self._exchange(recv, rows.reshape(-1), out_s, in_s, async_op)
 
     def fm_and_tail(self, recv_rows: torch.Tensor, B_l: int):
         """Step 4: FM + deep tail on the received rows (field order restored by out_col)."""
@@ -215,14 +221,40 @@ class ShardedDeepFM(EngineModule):
         cat = {f: ops.as_index(category[f], f"category[{f!r}]") for f in self.fields}
         return self.run_steps(cat)
 
-    def run_steps(self, cat: dict):
+    def chunk_bounds(self, B_l: int, chunks: int = None):
+        """Sample ranges of the exchange pipeline (overlap the row all-to-all with
+        compute): `pipeline_chunks` contiguous slices of the local batch, none under `min_chunk` samples."""
+        C = self.pipeline_chunks if chunks is None else chunks
+        C = max(1, min(C, B_l // self.min_chunk))
+        edges = [B_l * i // C for i in range(C + 1)]
+        return [(edges[i], edges[i + 1]) for i in range(C)]
+
+    def run_steps(self, cat: dict, chunks: int = None):
+        """P > 1: the four steps per chunk of the local batch, pipelined — every chunk's index
+        all-to-all is issued first; then each chunk's gather runs on the compute stream while the
+        previous chunk's row all-to-all is in flight on the collective stream; the FM + tail of a
+        chunk waits only for its own rows.  Outputs are the chunks' results in sample order (each
+        sample's math is independent of the chunking)."""
         if self.world == 1:
             return self.local_fm_and_tail(cat)
         B_l = cat[self.fields[0]].shape[0]
-        recv_idx = self.exchange_indices(cat, B_l)
-        rows = self.gather_local(recv_idx, self.world * B_l)
-        recv_rows = self.exchange_rows(rows, B_l)
-        return self.fm_and_tail(recv_rows, B_l)
+        parts = self.chunk_bounds(B_l, chunks)
+        sub = [{f: v[b0:b1] for f, v in cat.items()} for b0, b1 in parts]
+        idx = [self.exchange_indices(c, b1 - b0, async_op=True) for c, (b0, b1) in zip(sub, parts)]
+        rows = []
+        for (recv_idx, work), (b0, b1) in zip(idx, parts):
+            if work is not None:
+                work.wait()
+            rows.append(self.exchange_rows(self.gather_local(recv_idx, self.world * (b1 - b0)), b1 - b0,
+                                           async_op=True))
+        outs = []
+        for (recv_rows, work), (b0, b1) in zip(rows, parts):
+            if work is not None:
+                work.wait()
+            outs.append(self.fm_and_tail(recv_rows, b1 - b0))
+        if len(outs) == 1:
+            return outs[0]
+        return tuple(torch.cat([o[i] for o in outs], 0) for i in range(len(outs[0])))
 
 
 def _lib_dense(buf: torch.Tensor, offset: int, ld: int, dim: int, out_col: int):

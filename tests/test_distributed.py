@@ -65,7 +65,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, B, q):
+def _worker(rank, world, port, B, q, chunks=1):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         full = H.build("deepfm", CFG, seed=42)
@@ -78,9 +78,11 @@ def _worker(rank, world, port, B, q):
               if not k.startswith(("first_order", "second_order")) or k.split(".")[1] in sh.local_fields}
         sh.load_state_dict(sd, strict=True)
         sh.eval()
+        sh.min_chunk = 4  # pipeline the exchange even at this small batch
         mine = {f: v[rank * B:(rank + 1) * B].contiguous() for f, v in inp["category"].items()}
+        assert len(sh.chunk_bounds(B, chunks)) == chunks
         with torch.no_grad():
-            got = sh.run_steps(mine)
+            got = sh.run_steps(mine, chunks=chunks)
         for g, e in zip(got, expect):
             torch.testing.assert_close(g, e[rank * B:(rank + 1) * B], atol=1e-5, rtol=1e-5)
         # every rank only holds its own fields' tables
@@ -94,12 +96,14 @@ def _worker(rank, world, port, B, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_deepfm_exchange_gloo(world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 3), (3, 4)])
+def test_sharded_deepfm_exchange_gloo(world, chunks):
+    """Exchange routing at world 2 / 3, unpipelined and with the batch split into 3-4 chunks whose
+    all-to-alls run asynchronously (async_op work objects waited in pipeline order)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 24, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 24, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
