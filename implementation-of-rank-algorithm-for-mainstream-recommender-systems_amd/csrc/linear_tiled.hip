@@ -122,13 +122,12 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
 
   // epilogue: bias, BatchNorm affine, activation; rows < M, columns < n
   if (n < L.n) {
-    const bool has_pre = L.pre_scale != nullptr, has_post = L.post_scale != nullptr;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + 32 * rh + 16 * t + 4 * (lane >> 4) + r;
-        if (m < a.M) a.y[m * a.ldy + n] = col_apply(ep, L.act, L.slope, acc[t][r], false, 0.f, has_pre, has_post);
+        if (m < a.M) a.y[m * a.ldy + n] = col_apply(ep, L.act == RK_ACT_DICE, acc[t][r], false, 0.f);
       }
   }
 }

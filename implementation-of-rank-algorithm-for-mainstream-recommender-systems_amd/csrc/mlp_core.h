@@ -48,9 +48,12 @@ __device__ __forceinline__ f32x4_t mfma16(float a, float b, f32x4_t c) {
 // prove the generic output pointer does not alias them), each fetch waiting on the whole vmcnt
 // queue of weight loads.
 struct ColEpi {
-  float bias, pre_s, pre_b, act_s, act_b, alpha, post_s, post_b;
+  float bias, pre_s, pre_b, act_s, act_b, alpha, neg, post_s, post_b;
 };
 
+// Absent affine parts default to the identity (z * 1 + 0 is exact), and the piecewise-linear
+// activations to one negative-side slope `neg` (ReLU 0, LeakyReLU slope, PReLU alpha, none 1), so
+// the epilogue runs as straight-line code with one wave-uniform branch (Dice).
 __device__ __forceinline__ ColEpi col_epi(const rk_mlp_layer& L, int n) {
   ColEpi e;
   e.bias = L.bias ? L.bias[n] : 0.f;
@@ -62,36 +65,24 @@ __device__ __forceinline__ ColEpi col_epi(const rk_mlp_layer& L, int n) {
   e.act_b = L.act == RK_ACT_DICE ? L.act_shift[n] : 0.f;
   e.alpha = L.act == RK_ACT_DICE ? L.act_alpha[n]
           : L.act == RK_ACT_PRELU ? L.act_alpha[L.act_alpha_len == 1 ? 0 : n] : 0.f;
+  e.neg = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? e.alpha : 1.f;
   return e;
 }
 
 // The element-wise epilogue in the reference's order (bias, residual, pre-BN, activation,
-// post-BN); `act` is wave-uniform.
-__device__ __forceinline__ float col_apply(const ColEpi& e, int act, float slope, float z, bool has_res, float res,
-                                           bool has_pre, bool has_post) {
+// post-BN); `dice` and `has_res` are wave-uniform.  ReLU of a negative value gives -0 here
+// (z * 0), equal to torch.relu's +0 in every later use; NaN stays NaN as in torch.relu.
+__device__ __forceinline__ float col_apply(const ColEpi& e, bool dice, float z, bool has_res, float res) {
   z += e.bias;
   if (has_res) z = res + z;
-  if (has_pre) z = z * e.pre_s + e.pre_b;
-  switch (act) {
-    case RK_ACT_RELU:
-      z = z < 0.f ? 0.f : z;
-      break;
-    case RK_ACT_LEAKY:
-      z = z > 0.f ? z : z * slope;
-      break;
-    case RK_ACT_DICE: {
-      const float p = sigmoid_fast(z * e.act_s + e.act_b);
-      z = e.alpha * (1.0f - p) * z + p * z;
-      break;
-    }
-    case RK_ACT_PRELU:
-      z = z > 0.f ? z : e.alpha * z;
-      break;
-    default:
-      break;
+  z = z * e.pre_s + e.pre_b;
+  if (dice) {
+    const float p = sigmoid_fast(z * e.act_s + e.act_b);
+    z = e.alpha * (1.0f - p) * z + p * z;
+  } else {
+    z = z > 0.f ? z : z * e.neg;
   }
-  if (has_post) z = z * e.post_s + e.post_b;
-  return z;
+  return z * e.post_s + e.post_b;
 }
 
 // Optional per-layer shader-clock counters (tools/mlp_phases.hip builds with RK_MLP_PHASES):
@@ -191,9 +182,8 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
 #ifdef RK_MLP_PHASES
   if (wave == 0 && lane == 0) atomicAdd(&g_mlp_phase[dbg_mark], clock64() - dbg_t0);
 #endif
-  const int act = L.act;
-  const float slope = L.slope;
-  const bool has_res = L.residual != 0, has_pre = L.pre_scale != nullptr, has_post = L.post_scale != nullptr;
+  const bool dice = L.act == RK_ACT_DICE;
+  const bool has_res = L.residual != 0;
   float* const store = L.store;
   const int64_t ld_store = L.ld_store;
 #pragma unroll
@@ -212,7 +202,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * t + (lane >> 4) * 4 + r;
         const float z =
-            real ? col_apply(P.ep[j], act, slope, acc[j][t][r], has_res, res[t][r], has_pre, has_post) : 0.f;
+            real ? col_apply(P.ep[j], dice, acc[j][t][r], has_res, res[t][r]) : 0.f;
         out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
         if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
       }
