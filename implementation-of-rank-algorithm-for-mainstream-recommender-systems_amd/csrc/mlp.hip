@@ -84,6 +84,84 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
 #endif
 }
 
+// Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): per 16-row tile, wave w
+// gathers row m0 + w (dense + category embeddings, dcn.py:163-169) straight into the MLP's LDS
+// input buffer while layer 0's weights are already in flight, runs the cross stack on the row in
+// registers (x_{l+1} = x0 (x_l . w_l) + b_l + x_l, dcn.py:25-50,171-173) and leaves the cross half of
+// output_layer (x_L . W_out[:, :width]) in LDS; then the MLP tail and the head (the dnn half,
+// + bias, + the cross partial, sigmoid: dcn.py:175-180) as in mlp_kernel.  Replaces rk_dcn_cross +
+// rk_mlp_forward (two launches and an x0 / partial round trip through HBM).
+constexpr int kDcnSegs = 8;
+constexpr int kDcnPerLane = 4;  // width <= 256
+
+struct DcnArgs {
+  MlpArgs m;
+  rk_segment segs[kDcnSegs];
+  int nseg;
+  const float* cross_w;
+  const float* cross_b;
+  int num_layers;
+  const float* cross_head_w;
+  uint32_t* flags;
+};
+
+__global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.m.off1;
+  float* const part = buf1 + kMlpRows * a.m.ld1;
+  const int width = a.m.K0;
+  auto stage = [&]() {
+    const int64_t b = m0 + wave;
+    const bool live = wave < rows;
+    const int K0p = pad64(width);
+    float x0[kDcnPerLane], xl[kDcnPerLane];
+#pragma unroll
+    for (int j = 0; j < kDcnPerLane; ++j) {
+      const int c = lane + 64 * j;
+      float v = 0.f;
+      if (live && c < width) {
+        int s = 0;
+        for (int t = 1; t < a.nseg; ++t) s = c >= a.segs[t].out_col ? t : s;  // out_col ascending
+        const float* row = segment_row(a.segs[s], b, a.flags);
+        if (row) v = row[c - a.segs[s].out_col];
+      }
+      x0[j] = xl[j] = v;
+      if (c < K0p) buf0[wave * a.m.ld0 + c] = v;
+    }
+    for (int l = 0; l < a.num_layers; ++l) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < kDcnPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) d = fmaf(xl[j], a.cross_w[(int64_t)l * width + c], d);
+      }
+      d = wave_sum(d);
+#pragma unroll
+      for (int j = 0; j < kDcnPerLane; ++j) {
+        const int c = lane + 64 * j;
+        if (c < width) {
+          float t = x0[j] * d;                        // torch.mul(x0, xl_wl)
+          t = t + a.cross_b[(int64_t)l * width + c];  // + bl.t()
+          xl[j] = t + xl[j];                          // + xl
+        }
+      }
+    }
+    float p = 0.f;
+#pragma unroll
+    for (int j = 0; j < kDcnPerLane; ++j) {
+      const int c = lane + 64 * j;
+      if (c < width) p = fmaf(xl[j], a.cross_head_w[c], p);
+    }
+    p = wave_sum(p);
+    if (lane == 0) part[wave] = p;
+  };
+  mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid, stage, part);
+}
+
 // Fragment-major image (mlp_core.h wfrag): element i of the image is lane (i >> 2) & 63, component
 // i & 3 of chunk c of column tile t, i >> 8 = t * kp/16 + c; that lane's value is W[16 t + (lane & 15)]
 // [16 c + 4 (lane >> 4) + (i & 3)], zero outside [n, k).
@@ -201,4 +279,53 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   else
     mlp_kernel<1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   return check_launch("rk_mlp_forward");
+}
+
+RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t width, const float* cross_w,
+                          const float* cross_b, int32_t num_layers, const float* cross_head_w,
+                          const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, void* stream) {
+  if (!segs || nseg <= 0 || nseg > kDcnSegs || batch < 0 || width <= 0 || width > 64 * kDcnPerLane ||
+      num_layers < 0 || (num_layers > 0 && (!cross_w || !cross_b)) || !cross_head_w || !head || !head->head_w)
+    return fail(RK_ERR_INVALID, "rk_dcn_forward: bad arguments (nseg %d <= %d, width %d <= %d, head required)", nseg,
+                kDcnSegs, width, 64 * kDcnPerLane);
+  DcnArgs a = {};
+  a.m.head = *head;
+  if (a.m.head.head_partial || a.m.head.fm1)
+    return fail(RK_ERR_INVALID, "rk_dcn_forward: the cross partial comes from the kernel (no head_partial / fm1)");
+  int need0 = 0, need1 = 0;
+  if (int e = mlp_validate(layers, nlayers, width, a.m.head, &need0, &need1, "rk_dcn_forward")) return e;
+  int prev = -1;
+  for (int i = 0; i < nseg; ++i) {
+    const rk_segment& g = segs[i];
+    if (!g.src || g.dim <= 0 || g.out_col <= prev || g.out_col + g.dim > width || (g.idx && g.rows <= 0))
+      return fail(RK_ERR_INVALID, "rk_dcn_forward: segment %d (out_col ascending, inside width)", i);
+    prev = g.out_col;
+    a.segs[i] = g;
+  }
+  if (segs[0].out_col != 0) return fail(RK_ERR_INVALID, "rk_dcn_forward: segments must start at column 0");
+  for (int l = 0; l < nlayers; ++l) a.m.L[l] = layers[l];
+  a.m.nl = nlayers;
+  a.m.ld0 = need0 + 4;
+  a.m.ld1 = need1 + 4;
+  a.m.off1 = kMlpRows * a.m.ld0;
+  a.m.M = batch;
+  a.m.K0 = width;
+  a.nseg = nseg;
+  a.cross_w = cross_w;
+  a.cross_b = cross_b;
+  a.num_layers = num_layers;
+  a.cross_head_w = cross_head_w;
+  a.flags = device_flags();
+  const size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
+  if (batch == 0) return RK_OK;
+  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)dcn_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  dcn_fused_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  return check_launch("rk_dcn_forward");
 }

@@ -222,11 +222,13 @@ struct NoStage {
   __device__ void operator()() const {}
 };
 
+// `lds_partial` (optional): per-row head partials the stage left in LDS (DCN's cross half of
+// output_layer), used instead of h.head_partial.
 template <int RT = 1, class Stage = NoStage>
 __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers, int nl, int K0, float* buf0,
                                          int ld0, float* buf1, int ld1, int64_t m0, int rows,
                                          const rk_epilogue& h, float* y, int64_t ldy, int tid,
-                                         Stage stage = Stage()) {
+                                         Stage stage = Stage(), const float* lds_partial = nullptr) {
   const int lane = tid & 63, wave = tid >> 6;
   LayerPipe pipe;
   // one-tile layers with a reduction of a multiple of 128 run the 8-deep ring
@@ -254,7 +256,7 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       if (lane + 64 * c < Kh) hw[c] = h.head_w[lane + 64 * c];
-    if (wave < rows && h.head_partial) hp = h.head_partial[m0 + wave];
+    if (wave < rows && h.head_partial && !lds_partial) hp = h.head_partial[m0 + wave];
   };
 #ifdef RK_MLP_PHASES
   const unsigned long long t_start = clock64();
@@ -310,7 +312,10 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
       if (lane == 0) {
         const int64_t m = m0 + r;
         float logit = p + h.head_b[0];
-        if (h.head_partial) logit = (pre ? hp : h.head_partial[m]) + logit;
+        if (lds_partial)
+          logit = lds_partial[r] + logit;
+        else if (h.head_partial)
+          logit = (pre ? hp : h.head_partial[m]) + logit;
         if (h.fm1) {
           if (h.head_aux) h.head_aux[m] = logit;
           logit = h.fm1[m] * h.final_w[0] + h.fm2[m] * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];

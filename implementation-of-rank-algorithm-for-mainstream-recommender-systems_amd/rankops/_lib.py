@@ -119,6 +119,10 @@ SIGNATURES = {
         [_SEG_P, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p,
          c_int64, c_void_p, c_int64, c_void_p, c_void_p],
     ),
+    "rk_dcn_forward": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, _MLP_P, c_int32, _EPI_P, c_void_p],
+    ),
     "rk_fm_gather": (
         ctypes.c_int,
         [_SEG_P, _SEG_P, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],

@@ -5,12 +5,12 @@ constructor, parameter creation order (so a seeded construction gives the same w
 `state_dict` keys (dcn.py:130-152: no cross-layer keys) and `forward(dense, category) ->
 (probability, logit)` (dcn.py:161-180).  In train mode with autograd recording, the same
 forward runs under `rankops.train._DCNTrain`, whose backward is HIP too (loss.backward() fills
-every .grad).  The forward is three kinds of HIP launch:
-
-  rk_dcn_cross   gather the 6 fields + dense into x0 [B, 50], run the cross layers, and
-                 produce the cross half of output_layer (dcn.py:163-173, 177-178)
-  rk_linear      dnn Linear+ReLU x2 (dcn.py:175)
-  rk_linear      last dnn layer with output_layer + sigmoid fused in its epilogue
+every .grad).  The eval forward is one launch, rk_dcn_forward: per 16-row tile the gather of the
+6 fields + dense (dcn.py:163-169) straight into the MLP's LDS input, the cross layers in registers
+(dcn.py:25-50,171-173) with the cross half of output_layer, the dnn tail (dcn.py:175) and the head
+(output_layer + sigmoid, dcn.py:177-180).  Shapes outside its envelope (more than 8 segments,
+width > 256, hidden widths past the fused MLP's) run rk_dcn_cross + the rk_mlp_forward / rk_linear
+tail instead.
 
 The cross weights are drawn per call from the CPU generator like the reference
 (`interaction_weights="per_call"`, dcn.py:37-45) or drawn once and kept on the device
@@ -21,7 +21,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops, train
+from . import common, ops, train
 from .common import EngineModule, InteractionWeights, Layer, draw_cross_layers, load_vocabulary, run_tail, table_rows
 
 
@@ -90,12 +90,22 @@ class DCNModel(EngineModule):
         cw, cb = self.cross_weights.get(dev)
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             return train.dcn_train_forward(self, dense, idx_keep, cw, cb)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        if (common.FUSED_MLP and len(segs) <= 8 and self.input_dim <= 256
+                and common.fused_mlp_fits(self.input_dim, [l.linear.out_features for l in self._tail])):
+            # one launch: gather + cross stack + MLP tail + head (rk_dcn_forward)
+            mls = [ops.make_mlp_layer(l.linear.weight, common.PACKED(l.linear.weight), **l.epilogue_kwargs())
+                   for l in self._tail]
+            head = _HeadView(self.output_layer, self.input_dim)
+            ep = ops.make_epilogue(head_w=head.weight, head_b=head.bias, head_logit=logit, head_prob=prob)
+            ops.dcn_forward(segs, B, self.input_dim, cw, cb, self.num_cross_layer, self.output_layer.weight, mls, ep,
+                            dev)
+            return prob, logit
         x0 = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
         partial = torch.empty(B, device=dev, dtype=torch.float32)
         head_w = self.output_layer.weight
         ops.dcn_cross(segs, B, self.input_dim, cw, cb, self.num_cross_layer, head_w.data_ptr(), x0, partial, dev)
-        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
         head = _HeadView(self.output_layer, self.input_dim)
         run_tail(x0, self._tail, head, dict(head_partial=partial), logit, prob)
         return prob, logit

@@ -103,6 +103,18 @@ def dcn_cross(segs, batch, width, cross_w, cross_b, num_layers, head_w_ptr, x0, 
                            ptr(partial), torch.cuda.current_stream(device).cuda_stream), "rk_dcn_cross")
 
 
+def dcn_forward(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head: Epilogue,
+                device):
+    """rk_dcn_forward: gather + cross stack + MLP tail + head in one launch (DCNModel eval forward)."""
+    lib = _lib.load()
+    _lib.ensure_device(device)
+    arr = _seg_array(segs)
+    mls = (_lib.MlpLayer * max(1, len(layers)))(*layers)
+    check(lib.rk_dcn_forward(arr, len(segs), batch, width, ptr(cross_w), ptr(cross_b), num_layers,
+                             cross_head_w.data_ptr(), mls, len(layers), ctypes.byref(head),
+                             torch.cuda.current_stream(device).cuda_stream), "rk_dcn_forward")
+
+
 def fm_gather(second, first, dim, batch, deep_in, fm1, fm2):
     lib = _lib.load()
     _lib.ensure_device(deep_in.device)

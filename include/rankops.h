@@ -334,6 +334,15 @@ int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k, float*
 int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_mlp_layer* layers,
                    int32_t nlayers, const rk_epilogue* head, float* y, int64_t ldy, void* stream);
 
+/* Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): gather of the row from
+ * segs (out_col ascending from 0, at most 8 segments, width <= 256), num_layers cross layers
+ * (weights [L, width] as rk_dcn_cross), the MLP tail as rk_mlp_forward (layers packed) and the head:
+ * logit = x_L . cross_head_w + (h . head->head_w + head->head_b), prob = sigmoid(logit), written to
+ * head->head_logit / head->head_prob.  cross_head_w = output_layer.weight[0, :width].           */
+int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t width, const float* cross_w,
+                   const float* cross_b, int32_t num_layers, const float* cross_head_w,
+                   const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, void* stream);
+
 /* One MLP layer as a 2D-tiled GEMM (64-row x 128-column tiles): y[M, n] = epilogue(x . W^T) with
  * W packed by rk_mlp_pack_weight (ldw = pad64(K)) and the element-wise part of the rk_mlp_layer
  * epilogue (bias, BatchNorm affines, activation; no residual).  For a wide first layer
