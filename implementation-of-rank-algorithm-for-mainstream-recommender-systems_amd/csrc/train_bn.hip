@@ -17,7 +17,7 @@ namespace rk {
 
 
 constexpr int kBnCols = 64;   // columns per workgroup (one per lane)
-constexpr int kBnRows = 256;  // rows per workgroup
+constexpr int kBnRows = 64;   // rows per workgroup (16 per wave: B = 4096 gives 64 row blocks)
 
 // sum[n] += sum_b (z[b, n] + bias[n]); sq[n] += sum_b (z + bias)^2   (fp64)
 __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ z, int64_t ldz, int64_t B, int N,
@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
   double s = 0.0, q = 0.0;
   if (n < N) {
     const float bb = bias ? bias[n] : 0.f;
+    #pragma unroll 4
     for (int64_t b = b0 + w; b < b1; b += 4) {
       const double v = (double)(z[b * ldz + n] + bb);
       s += v;
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     }
   }
   const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
-  for (int64_t b = b0 + w; b < b1; b += 4) {
+  #pragma unroll 4
+    for (int64_t b = b0 + w; b < b1; b += 4) {
     float u = z[b * ldz + n] + bb;
     if (bn) u = (u - mean) * invstd * g + be;
     if (act == RK_ACT_RELU) u = u < 0.f ? 0.f : u;
@@ -134,6 +136,7 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(
       k2 = (float)(sq[n] / (double)B);
     }
     const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
+    #pragma unroll 4
     for (int64_t b = b0 + w; b < b1; b += 4) {
       const float xmu = z[b * ldz + n] + bb - mean;
       const float xhat = xmu * invstd;
@@ -287,7 +290,8 @@ __global__ __launch_bounds__(256) void dice_apply_kernel(const float* __restrict
       running_var[n] = momentum * unbiased + (1.f - momentum) * running_var[n];
     }
   }
-  for (int64_t b = b0 + w; b < b1; b += 4) {
+  #pragma unroll 4
+    for (int64_t b = b0 + w; b < b1; b += 4) {
     const float x = z[b * ldz + n] + bb;
     const float p = 1.0f / (1.0f + expf(-((x - c.mean) * c.invstd)));
     y[b * ldy + n] = a * (1.0f - p) * x + p * x;
@@ -339,6 +343,7 @@ __global__ __launch_bounds__(256) void dice_backward_kernel(const float* __restr
       k1 = (float)(ws[n] / (double)B);
       k2 = (float)(ws[N + n] / (double)B);
     }
+    #pragma unroll 4
     for (int64_t b = b0 + w; b < b1; b += 4) {
       const float x = z[b * ldz + n] + bb;
       const float xhat = (x - mean) * invstd;
