@@ -229,7 +229,16 @@ class BSTModel(EngineModule):
         ops.concat_gather(segs, B, row)
         nblk = len(self.transformer_blocks)
         if nblk == 0:
-            raise NotImplementedError("BSTModel with zero transformer blocks")
+            # no transformer blocks (bst.py:228-235 leaves transformer_output = seq_emb): gather the
+            # history rows, then sum / mean pooling over all T positions into the DNN row
+            seq = torch.empty(B * T, d, device=dev, dtype=torch.float32)
+            ops.concat_gather([ops.table_segment(self.embeddings['feedid'].weight, seq_feedid.view(-1), 0)], B * T,
+                              seq)
+            ops.bst_pool(seq, B, T, seq_length, self.pooling_method != 'sum', row, col)
+            logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
+            probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
+            run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
+            return probs, logits
         for blk in self.transformer_blocks:
             if T > blk.position_embedding.num_embeddings:
                 raise IndexError(f"BSTTransformer: sequence length {T} exceeds max_len "

@@ -40,7 +40,7 @@ def din_case(draw):
 def bst_case(draw):
     dim, heads = draw(st.sampled_from([(16, 4), (32, 4), (128, 4), (24, 3), (8, 1)]))
     T = draw(st.integers(1, 64))
-    cfg = {"T": T, "dim": dim, "heads": heads, "max_len": 64, "blocks": draw(st.integers(1, 2)),
+    cfg = {"T": T, "dim": dim, "heads": heads, "max_len": 64, "blocks": draw(st.integers(0, 2)),
            "pooling": draw(st.sampled_from(["sum", "mean"])), "min_len": draw(st.sampled_from([1, T])),
            "batch_norm": draw(st.booleans())}
     return "bst", cfg

@@ -36,6 +36,8 @@ CASES = [
     ("bst", {"T": 64, "dim": 128, "max_len": 64, "heads": 4}),
     ("bst", {"T": 20, "blocks": 2, "batch_norm": False}),
     ("bst", {"T": 1}),
+    ("bst", {"T": 20, "blocks": 0}),  # no transformer block: pooling straight over the history rows
+    ("bst", {"T": 33, "blocks": 0, "pooling": "mean"}),
     # rk_bst_forward_blocks envelope (d_model 128, 4 heads, T <= 64)
     ("bst", {"T": 50, "dim": 128, "pooling": "mean"}),
     ("bst", {"T": 37, "dim": 128, "blocks": 2, "max_len": 40}),
