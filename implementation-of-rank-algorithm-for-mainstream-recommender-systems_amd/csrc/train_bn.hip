@@ -377,6 +377,66 @@ __global__ void f64_to_f32_kernel(const double* __restrict__ src, int n, float* 
   if (i < n) dst[i] = (float)src[i];
 }
 
+// ---- DIN's PReLU alternative (din.py:277-279, nn.PReLU(): one shared weight, or one per column
+// when nw == N): x = z + bias, y = x > 0 ? x : a x.
+__global__ __launch_bounds__(256) void prelu_apply_kernel(const float* __restrict__ z, int64_t ldz, int64_t B, int N,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ weight, int nw,
+                                                          float* __restrict__ y, int64_t ldy) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * kBnCols + lane;
+  if (n >= N) return;
+  const int64_t b0 = (int64_t)blockIdx.y * kBnRows;
+  const int64_t b1 = min<int64_t>(B, b0 + kBnRows);
+  const float bb = bias ? bias[n] : 0.f;
+  const float a = weight[nw == 1 ? 0 : n];
+  #pragma unroll 4
+  for (int64_t b = b0 + w; b < b1; b += 4) {
+    const float x = z[b * ldz + n] + bb;
+    y[b * ldy + n] = x > 0.f ? x : a * x;
+  }
+}
+
+// PReLU backward: dz = dy * (x > 0 ? 1 : a); ws[nw == 1 ? 0 : n] += sum_b dy * min(x, 0)  (fp64;
+// with one shared weight the columns are first summed across the wave).
+__global__ __launch_bounds__(256) void prelu_backward_kernel(const float* __restrict__ dy, int64_t lddy,
+                                                             const float* __restrict__ z, int64_t ldz, int64_t B,
+                                                             int N, const float* __restrict__ bias,
+                                                             const float* __restrict__ weight, int nw,
+                                                             double* __restrict__ ws, float* __restrict__ dz,
+                                                             int64_t lddz) {
+  __shared__ double red[4][kBnCols];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * kBnCols + lane;
+  const int64_t b0 = (int64_t)blockIdx.y * kBnRows;
+  const int64_t b1 = min<int64_t>(B, b0 + kBnRows);
+  double s = 0.0;
+  if (n < N) {
+    const float bb = bias ? bias[n] : 0.f;
+    const float a = weight[nw == 1 ? 0 : n];
+    #pragma unroll 4
+    for (int64_t b = b0 + w; b < b1; b += 4) {
+      const float x = z[b * ldz + n] + bb;
+      const float g = dy[b * lddy + n];
+      const bool pos = x > 0.f;
+      dz[b * lddz + n] = pos ? g : g * a;
+      s += pos ? 0.0 : (double)(g * x);
+    }
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0) {
+    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (nw == 1) {
+      #pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      if (lane == 0) atomicAdd(ws, s);
+    } else if (n < N) {
+      atomicAdd(ws + n, s);
+    }
+  }
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -506,6 +566,30 @@ RK_API int rk_dice_backward(const float* dy, int64_t lddy, const float* z, int64
   dice_backward_kernel<false><<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, alpha, save_mean, save_invstd,
                                                     workspace, dz, lddz);
   return check_launch("rk_dice_backward");
+}
+
+RK_API int rk_prelu_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
+                                  const float* weight, int32_t num_weights, float* y, int64_t ldy, void* stream) {
+  if (!z || !y || !weight || batch <= 0 || n <= 0 || ldz < n || ldy < n || (num_weights != 1 && num_weights != n))
+    return fail(RK_ERR_INVALID, "rk_prelu_train_forward: bad arguments");
+  dim3 grid((unsigned)((n + kBnCols - 1) / kBnCols), (unsigned)((batch + kBnRows - 1) / kBnRows));
+  prelu_apply_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(z, ldz, batch, n, bias, weight, num_weights, y, ldy);
+  return check_launch("rk_prelu_train_forward");
+}
+
+RK_API int rk_prelu_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch, int32_t n,
+                             const float* bias, const float* weight, int32_t num_weights, double* workspace,
+                             float* dz, int64_t lddz, float* dweight, void* stream) {
+  if (!dy || !z || !dz || !weight || !workspace || batch <= 0 || n <= 0 || ldz < n || lddy < n || lddz < n ||
+      (num_weights != 1 && num_weights != n))
+    return fail(RK_ERR_INVALID, "rk_prelu_backward: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((n + kBnCols - 1) / kBnCols), (unsigned)((batch + kBnRows - 1) / kBnRows));
+  zero_f64_kernel<<<(num_weights + 255) / 256, 256, 0, st>>>(workspace, num_weights);
+  prelu_backward_kernel<<<grid, 256, 0, st>>>(dy, lddy, z, ldz, batch, n, bias, weight, num_weights, workspace, dz,
+                                              lddz);
+  if (dweight) f64_to_f32_kernel<<<(num_weights + 255) / 256, 256, 0, st>>>(workspace, num_weights, dweight);
+  return check_launch("rk_prelu_backward");
 }
 
 RK_API int rk_dice_forward(const float* x, int64_t ldx, int64_t rows, int32_t n, const float* bn_scale,

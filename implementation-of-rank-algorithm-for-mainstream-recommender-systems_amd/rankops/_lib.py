@@ -211,6 +211,10 @@ SIGNATURES = {
                                              c_int64, c_void_p]),
     "rk_dice_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rk_prelu_train_forward": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_int32,
+                                              c_void_p, c_int64, c_void_p]),
+    "rk_prelu_backward": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p,
+                                         c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rk_din_att_cross": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                         c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "rk_din_att_pool_forward": (ctypes.c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,

@@ -578,6 +578,22 @@ def dice_backward(dy, z, bias, dice, save_mean, save_invstd, workspace, dz, dalp
                                dz.stride(0), ptr(dalpha), _lib.stream_of(dy)), "rk_dice_backward")
 
 
+def prelu_train_forward(z, bias, prelu, y):
+    """nn.PReLU (din.py:277-279) on z + bias; `prelu` is the module (its weight stays on the device)."""
+    lib = _lib.load()
+    w = prelu.weight
+    check(lib.rk_prelu_train_forward(ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), ptr(w), w.numel(),
+                                     ptr(y), y.stride(0), _lib.stream_of(z)), "rk_prelu_train_forward")
+
+
+def prelu_backward(dy, z, bias, prelu, workspace, dz, dweight):
+    lib = _lib.load()
+    w = prelu.weight
+    check(lib.rk_prelu_backward(ptr(dy), dy.stride(0), ptr(z), z.stride(0), z.shape[0], z.shape[1], ptr(bias), ptr(w),
+                                w.numel(), ptr(workspace), ptr(dz), dz.stride(0), ptr(dweight), _lib.stream_of(dy)),
+          "rk_prelu_backward")
+
+
 def din_att_cross(x, q_col, key_table, seq, T, H, keys, cross):
     lib = _lib.load()
     check(lib.rk_din_att_cross(ptr(x), x.stride(0), q_col, ptr(key_table), key_table.shape[0], key_table.stride(0),

@@ -431,7 +431,7 @@ def deepfm_train_forward(model, names, idx):
 # ---------------------------------------------------------------- DIN
 
 def din_units(model):
-    """(Linear, Dice module, BatchNorm1d or None, dropout p) per fcn unit (din.py:272-284)."""
+    """(Linear, Dice or PReLU module, BatchNorm1d or None, dropout p) per fcn unit (din.py:272-284)."""
     units = []
     for m in model.fcn:
         if isinstance(m, torch.nn.Linear):
@@ -440,14 +440,12 @@ def din_units(model):
             units[-1][2] = m
         elif isinstance(m, torch.nn.Dropout):
             units[-1][3] = float(m.p) if m.training else 0.0
-        elif isinstance(m, torch.nn.PReLU):
-            raise NotImplementedError("rankops DIN training: activation='prelu' is not implemented (use 'dice')")
-        else:  # Dice
+        else:  # Dice, or nn.PReLU with activation='prelu' (din.py:275-279)
             units[-1][1] = m
     for lin, act, bn, _ in units:
         if lin.bias is None or act is None:
-            raise NotImplementedError("rankops DIN training expects the reference's Linear + Dice units")
-        if act.bn.momentum is None or (bn is not None and bn.momentum is None):
+            raise NotImplementedError("rankops DIN training expects the reference's Linear + Dice / PReLU units")
+        if (not isinstance(act, torch.nn.PReLU) and act.bn.momentum is None) or (bn is not None and bn.momentum is None):
             raise NotImplementedError("rankops DIN training: BatchNorm1d needs a numeric momentum")
     return units
 
@@ -455,7 +453,7 @@ def din_units(model):
 class _DINTrain(torch.autograd.Function):
     """DIN forward + backward in train mode (din.py:294-323): gather, din_attention (att_net's
     layers as GEMMs on rk_linear with the activations kept for the backward, the weights drawn per
-    call like the reference and not trained), fcn units Linear -> Dice -> BatchNorm1d -> Dropout
+    call like the reference and not trained), fcn units Linear -> Dice / PReLU -> BatchNorm1d -> Dropout
     with batch statistics, output_layer + sigmoid, and the mini-batch-aware l2 term.
     Inputs after the fixed arguments are the parameters in `_din_params` order."""
 
@@ -489,7 +487,11 @@ class _DINTrain(torch.autograd.Function):
             ops.gemm(False, False, B, n, K, h, h.stride(0), lin.weight, lin.weight.stride(0), z)
             y1 = torch.empty(B, n, **f32)
             m1, s1 = torch.empty(n, **f32), torch.empty(n, **f32)
-            ops.dice_train_forward(z, lin.bias, dice, y1, m1, s1, torch.empty(2 * n, device=dev, dtype=torch.float64))
+            if isinstance(dice, torch.nn.PReLU):
+                ops.prelu_train_forward(z, lin.bias, dice, y1)
+            else:
+                ops.dice_train_forward(z, lin.bias, dice, y1, m1, s1,
+                                       torch.empty(2 * n, device=dev, dtype=torch.float64))
             y2, m2, s2 = y1, m1, s1
             if bn is not None or p > 0:
                 y2 = torch.empty(B, n, **f32)
@@ -540,9 +542,14 @@ class _DINTrain(torch.autograd.Function):
                 ops.bn_act_backward(dy, y1, None, bn, False, p, ctx.seed + u, slot, m2, s2,
                                     torch.empty(2 * n, device=dev, dtype=torch.float64), dy1, dg, dbt)
             dz = torch.empty(B, n, **f32)
-            dalpha = torch.empty(n, **f32)
-            ops.dice_backward(dy1, z, lin.bias, dice, m1, s1, torch.empty(3 * n, device=dev, dtype=torch.float64), dz,
-                              dalpha)
+            if isinstance(dice, torch.nn.PReLU):
+                dalpha = torch.empty_like(dice.weight)
+                ops.prelu_backward(dy1, z, lin.bias, dice, torch.empty(dice.weight.numel(), device=dev,
+                                                                       dtype=torch.float64), dz, dalpha)
+            else:
+                dalpha = torch.empty(n, **f32)
+                ops.dice_backward(dy1, z, lin.bias, dice, m1, s1, torch.empty(3 * n, device=dev, dtype=torch.float64),
+                                  dz, dalpha)
             dW = torch.empty(n, K, **f32)
             db = torch.empty(n, **f32)
             ops.gemm(True, True, n, K, B, dz, dz.stride(0), h_in, h_in.stride(0), dW, row_sums=db)
@@ -585,8 +592,8 @@ class _DINTrain(torch.autograd.Function):
 
 def _din_params(model, units):
     out = []
-    for lin, dice, bn, _ in units:
-        out += [lin.weight, lin.bias, dice.alpha]
+    for lin, act, bn, _ in units:
+        out += [lin.weight, lin.bias, act.weight if isinstance(act, torch.nn.PReLU) else act.alpha]
         if bn is not None:
             out += [t for t in (bn.weight, bn.bias) if t is not None]
     return out + [model.output_layer.weight, model.output_layer.bias]

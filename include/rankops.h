@@ -469,6 +469,16 @@ int rk_dice_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz,
                      const float* save_invstd, double* workspace, float* dz, int64_t lddz,
                      float* dalpha, void* stream);
 
+/* DIN's PReLU activation option (din.py:277-279, nn.PReLU()) in train mode: x = z + bias,
+ * y = x > 0 ? x : a x, with one shared weight (num_weights == 1, the reference's nn.PReLU()) or
+ * one per column (num_weights == n).  Backward writes dz = dL/d(z + bias) and dweight[num_weights]
+ * (when non-NULL); workspace: num_weights doubles.                                              */
+int rk_prelu_train_forward(const float* z, int64_t ldz, int64_t batch, int32_t n, const float* bias,
+                           const float* weight, int32_t num_weights, float* y, int64_t ldy, void* stream);
+int rk_prelu_backward(const float* dy, int64_t lddy, const float* z, int64_t ldz, int64_t batch,
+                      int32_t n, const float* bias, const float* weight, int32_t num_weights,
+                      double* workspace, float* dz, int64_t lddz, float* dweight, void* stream);
+
 /* din_attention train pieces (din.py:42-84).  keys [B, T, H] = key_table[seq] (gathered), cross
  * [B*T, 4H] = [q, k, q-k, q*k] with q = x[b, q_col:+H]; the att_net layers run on rk_linear.
  * pool_forward: s = a2 . w3 + b3, masked (softmax: padded with -2^32+1, / sqrt(H)) weights saved

@@ -250,10 +250,11 @@ def dice_train(x, p, prefix, momentum=0.1, eps=1e-5):
 
 def din_forward_train(p, dense, category, sequence, target, num_hidden=3, batch_norm=True, dropout_rate=0.1,
                       use_softmax=False, l2_lambda=0.2, mini_batch_aware_regularization=True, att=None, masks=None,
-                      momentum=0.1, eps=1e-5):
-    """DIN.forward in model.train() (din.py:294-323, activation='dice'): Dice and BatchNorm1d with batch
-    statistics (running statistics in `p` updated in place), Dropout as the given per-unit multiplier
-    masks (0 or 1/(1-p)); differentiable w.r.t. the tensors in `p`."""
+                      momentum=0.1, eps=1e-5, activation="dice"):
+    """DIN.forward in model.train() (din.py:294-323): Dice (or nn.PReLU with activation='prelu',
+    din.py:275-279) and BatchNorm1d with batch statistics (running statistics in `p` updated in
+    place), Dropout as the given per-unit multiplier masks (0 or 1/(1-p)); differentiable w.r.t. the
+    tensors in `p`."""
     dense_input = torch.cat([dense[c].unsqueeze(1) for c in dense], dim=1)
     category_emb = [F.embedding(category[c], p[f"embeddings.{c}.weight"]) for c in DIN_EMB if c in category]
     target_feed_emb = F.embedding(target["feedid"], p["embeddings.feedid.weight"])
@@ -261,9 +262,12 @@ def din_forward_train(p, dense, category, sequence, target, num_hidden=3, batch_
     seq_length = sequence["his_read_comment_7d_seq_length"]
     attention_output = din_attention(target_feed_emb, seq_emb, seq_length, use_softmax, att)
     net = torch.cat([dense_input] + category_emb + [target_feed_emb, attention_output], dim=1)
-    for u, (lin, act, bn) in enumerate(din_layout(num_hidden, "dice", batch_norm, dropout_rate)):
+    for u, (lin, act, bn) in enumerate(din_layout(num_hidden, activation, batch_norm, dropout_rate)):
         net = _lin(net, p, f"fcn.{lin}.")
-        net = dice_train(net, p, f"fcn.{act}.", momentum, eps)
+        if activation == "dice":
+            net = dice_train(net, p, f"fcn.{act}.", momentum, eps)
+        else:
+            net = F.prelu(net, p[f"fcn.{act}.weight"])
         if bn is not None:
             pre = f"fcn.{bn}."
             net = F.batch_norm(net, p[pre + "running_mean"], p[pre + "running_var"], p[pre + "weight"],

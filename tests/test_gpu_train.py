@@ -516,7 +516,7 @@ def _din_step_check(cfg, B, seed, steps):
         masks = _din_masks(model, B)
         r = ref.din_forward_train(p, inp["dense"], inp["category"], inp["sequence"], inp["target"], hidden,
                                   cfg.get("batch_norm", True), 0.1, cfg.get("softmax", False), cfg.get("l2", 0.2),
-                                  True, att, masks)
+                                  True, att, masks, activation=cfg.get("activation", "dice"))
         rloss = crit(r[0].squeeze(), label) + r[2]
         rloss.backward()
         for i, (o, w) in enumerate(zip(out, r)):
@@ -555,8 +555,11 @@ def _din_step_check(cfg, B, seed, steps):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [{"T": 20}, {"T": 20, "softmax": True}, {"T": 12, "batch_norm": False, "l2": 0.0},
-                                 {"T": 50, "dim": 32, "vocab": H.WECHAT_VOCAB}, {"T": 70, "min_len": 0}],
-                         ids=["default", "softmax", "no_bn_no_l2", "bench_shape", "long_empty"])
+                                 {"T": 50, "dim": 32, "vocab": H.WECHAT_VOCAB}, {"T": 70, "min_len": 0},
+                                 {"T": 20, "activation": "prelu"},
+                                 {"T": 16, "activation": "prelu", "batch_norm": False, "softmax": True}],
+                         ids=["default", "softmax", "no_bn_no_l2", "bench_shape", "long_empty", "prelu",
+                              "prelu_no_bn_softmax"])
 def test_din_train_steps_match_autograd(cfg):
     _din_step_check(cfg, 512, seed=2400, steps=2)
 
