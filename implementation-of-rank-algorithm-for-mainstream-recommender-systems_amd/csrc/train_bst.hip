@@ -339,6 +339,78 @@ __global__ __launch_bounds__(256) void bst_res_dropout_ln_fwd_kernel(
   }
 }
 
+// Row-group layout of the float4 LayerNorm kernels (d % 4 == 0, d <= 4L): a row is held by L lanes
+// of 4 consecutive columns (lane li: columns 4li..4li+3), so a wave holds 64 / L rows at once, and
+// each wave keeps NR such row groups in flight (all loads issued before the first reduction).
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+constexpr int kLnNR = 4;  // row groups in flight per wave
+
+template <int L>
+__global__ __launch_bounds__(256) void bst_res_dropout_ln_fwd4_kernel(
+    const float* __restrict__ base, const float* __restrict__ o, int64_t M, int d, uint64_t seed,
+    const int64_t* __restrict__ stream_slot, uint32_t threshold, float scale, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ r_out, float* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int RPW = 64 / L;
+  const int lane = threadIdx.x & 63, sub = lane / L, li = lane % L;
+  const int k = 4 * li;
+  const bool on = k < d;
+  const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
+  const f32x4 g4 = on ? ld4(gamma + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 b4 = on ? ld4(beta + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t step = nw * RPW;  // rows between a wave's consecutive row groups
+  const float inv_d = 1.0f / (float)d;
+  for (int64_t m0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub; m0 - sub < M; m0 += step * kLnNR) {
+    f32x4 v[kLnNR];
+#pragma unroll
+    for (int i = 0; i < kLnNR; ++i) {
+      const int64_t m = m0 + i * step;
+      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (on && m < M) {
+        const f32x4 ov = ld4(o + m * d + k), bv = ld4(base + m * d + k);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float t = ov[c];
+          if (threshold) t = dropout_keep(seed, stream, (uint64_t)m * d + k + c, threshold) ? t * scale : 0.f;
+          v[i][c] = bv[c] + t;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kLnNR; ++i) {
+      const int64_t m = m0 + i * step;
+      const float mean = group_sum<L>(v[i][0] + v[i][1] + v[i][2] + v[i][3]) * inv_d;
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) q += on ? (v[i][c] - mean) * (v[i][c] - mean) : 0.f;
+      const float rstd = 1.0f / sqrtf(group_sum<L>(q) * inv_d + eps);
+      if (m < M) {
+        if (on) {
+          f32x4 out;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) out[c] = (v[i][c] - mean) * rstd * g4[c] + b4[c];
+          st4(r_out + m * d + k, v[i]);
+          st4(y + m * d + k, out);
+        }
+        if (li == 0) {
+          mean_out[m] = mean;
+          rstd_out[m] = rstd;
+        }
+      }
+    }
+  }
+}
+
 // LayerNorm backward from dy: dr = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma; d_o =
 // dropout-masked dr (the residual branch's gradient).  Waves walk rows grid-stride; each lane keeps
 // its columns' dgamma = sum dy xhat and dbeta = sum dy in registers, the workgroup combines them
@@ -421,6 +493,107 @@ __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict
   for (int k = threadIdx.x; k < d; k += blockDim.x) {
     ws[(int64_t)blockIdx.x * 2 * d + k] = red[0][0][k] + red[1][0][k] + red[2][0][k] + red[3][0][k];
     ws[(int64_t)blockIdx.x * 2 * d + d + k] = red[0][1][k] + red[1][1][k] + red[2][1][k] + red[3][1][k];
+  }
+}
+
+// float4 row-group form of bst_ln_bwd_kernel (same math, same workspace layout: one [2d] partial
+// per workgroup).  When drow is non-NULL the incoming gradient is the pooling backward's broadcast
+// dy[m] = drow[m / T, col:] (/ seq_len for mean pooling, bst.py:238-241) instead of dy.
+template <int L>
+__global__ __launch_bounds__(256) void bst_ln_bwd4_kernel(const float* __restrict__ dy,
+                                                          const float* __restrict__ drow, int64_t ld_row, int col,
+                                                          int T, const int64_t* __restrict__ seq_len, int mean_pool,
+                                                          const float* __restrict__ r,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in,
+                                                          const float* __restrict__ gamma, int64_t M, int d,
+                                                          uint64_t seed, const int64_t* __restrict__ stream_slot,
+                                                          uint32_t threshold, float scale, float* __restrict__ dr,
+                                                          float* __restrict__ d_o, float* __restrict__ ws) {
+  constexpr int RPW = 64 / L;
+  __shared__ f32x4 red[4][2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane / L, li = lane % L;
+  const int k = 4 * li;
+  const bool on = k < d;
+  const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 gm = on ? ld4(gamma + k) : zero;
+  f32x4 pg = zero, pb = zero;
+  const int64_t step = (int64_t)gridDim.x * 4 * RPW;
+  const float inv_d = 1.0f / (float)d;
+  for (int64_t m0 = ((int64_t)blockIdx.x * 4 + wv) * RPW + sub; m0 - sub < M; m0 += step * kLnNR) {
+    f32x4 dyv[kLnNR], rv[kLnNR];
+    float mean[kLnNR], rstd[kLnNR];
+#pragma unroll
+    for (int i = 0; i < kLnNR; ++i) {
+      const int64_t m = m0 + i * step;
+      const int64_t mm = m < M ? m : M - 1;
+      mean[i] = mean_in[mm];
+      rstd[i] = rstd_in[mm];
+      dyv[i] = rv[i] = zero;
+      if (on) {
+        if (drow) {
+          const int64_t b = mm / T;
+          dyv[i] = ld4(drow + b * ld_row + col + k);
+          if (mean_pool) {
+            const float inv = 1.0f / (float)seq_len[b];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) dyv[i][c] = dyv[i][c] * inv;
+          }
+        } else {
+          dyv[i] = ld4(dy + mm * d + k);
+        }
+        rv[i] = ld4(r + mm * d + k);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kLnNR; ++i) {
+      const int64_t m = m0 + i * step;
+      const bool live = m < M;
+      f32x4 g, xh;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xh[c] = (rv[i][c] - mean[i]) * rstd[i];
+        g[c] = dyv[i][c] * gm[c];
+        s1 += g[c];
+        s2 += g[c] * xh[c];
+        if (live) {
+          pg[c] = fmaf(dyv[i][c], xh[c], pg[c]);
+          pb[c] += dyv[i][c];
+        }
+      }
+      const float k1 = group_sum<L>(s1) * inv_d, k2 = group_sum<L>(s2) * inv_d;
+      if (live && on) {
+        f32x4 v, vo;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          v[c] = rstd[i] * (g[c] - k1 - xh[c] * k2);
+          vo[c] = threshold ? (dropout_keep(seed, stream, (uint64_t)m * d + k + c, threshold) ? v[c] * scale : 0.f)
+                            : v[c];
+        }
+        st4(dr + m * d + k, v);
+        if (d_o) st4(d_o + m * d + k, vo);
+      }
+    }
+  }
+  // fold the wave's row groups (lanes li, li + L, ... hold the same columns), then the 4 waves
+#pragma unroll
+  for (int off = L; off < 64; off <<= 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      pg[c] += __shfl_xor(pg[c], off);
+      pb[c] += __shfl_xor(pb[c], off);
+    }
+  if (sub == 0) {
+    red[wv][0][li] = pg;
+    red[wv][1][li] = pb;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * (d / 4); t += blockDim.x) {
+    const int which = t / (d / 4), q = t % (d / 4);
+    const f32x4 s = red[0][which][q] + red[1][which][q] + red[2][which][q] + red[3][which][q];
+    st4(ws + (int64_t)blockIdx.x * 2 * d + which * d + 4 * q, s);
   }
 }
 
@@ -520,6 +693,45 @@ static void att_set_attrs() {
   done = true;
 }
 
+// Lanes per row of the float4 LayerNorm kernels (0: use the scalar kernels): d % 4 == 0 and every
+// row pointer 16-B aligned.
+static int ln_lanes(int d, std::initializer_list<const float*> ptrs) {
+  if (d % 4 || d > 256) return 0;
+  for (const float* p : ptrs)
+    if (p && (reinterpret_cast<uintptr_t>(p) & 15)) return 0;
+  int L = 8;
+  while (4 * L < d) L *= 2;
+  return L;
+}
+
+static int ln_backward(const float* dy, const float* drow, int64_t ld_row, int col, int T, const int64_t* seq_len,
+                       int mean_pool, const float* r, const float* mean, const float* rstd, const float* gamma,
+                       int64_t rows, int d, double dropout_p, uint64_t seed, const int64_t* stream_slot, float* dr,
+                       float* d_o, float* dgamma, float* dbeta, float* workspace, hipStream_t st, const char* what) {
+  const uint32_t thr = dropout_threshold(dropout_p);
+  const float scale = (float)(1.0 / (1.0 - dropout_p));
+  const int L = ln_lanes(d, {dy, drow ? drow + col : nullptr, r, gamma, dr, d_o, workspace});
+  int blocks;
+  if (L) {
+    const int64_t groups = (rows + 64 / L - 1) / (64 / L);
+    blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (groups + 3) / 4));
+#define RK_LN_BWD(L_)                                                                                             \
+  case L_:                                                                                                        \
+    bst_ln_bwd4_kernel<L_><<<blocks, 256, 0, st>>>(dy, drow, ld_row, col, T, seq_len, mean_pool, r, mean, rstd,   \
+                                                   gamma, rows, d, seed, stream_slot, thr, scale, dr, d_o,        \
+                                                   workspace);                                                    \
+    break;
+    switch (L) { RK_LN_BWD(8) RK_LN_BWD(16) RK_LN_BWD(32) RK_LN_BWD(64) }
+#undef RK_LN_BWD
+  } else {
+    blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (rows + 3) / 4));
+    bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot, thr, scale, dr,
+                                              d_o, workspace);
+  }
+  bst_ln_param_kernel<<<grid_of(2 * d, 64), 1024, 0, st>>>(workspace, blocks, d, dgamma, dbeta);
+  return check_launch(what);
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -567,9 +779,25 @@ RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int6
       !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
     return fail(RK_ERR_INVALID, "rk_bst_res_dropout_ln_forward: bad arguments (d <= 256)");
   if (rows == 0) return RK_OK;
-  bst_res_dropout_ln_fwd_kernel<<<grid_of(rows, 4), 256, 0, (hipStream_t)stream>>>(
-      base, o, rows, d, seed, stream_slot, dropout_threshold(dropout_p), (float)(1.0 / (1.0 - dropout_p)), gamma,
-      beta, eps, r, y, mean, rstd);
+  const uint32_t thr = dropout_threshold(dropout_p);
+  const float scale = (float)(1.0 / (1.0 - dropout_p));
+  hipStream_t st = (hipStream_t)stream;
+  const int L = ln_lanes(d, {base, o, gamma, beta, r, y});
+  if (L) {
+    const int64_t groups = (rows + 64 / L - 1) / (64 / L);  // row groups; kLnNR per wave
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 4 * kLnNR - 1) / (4 * kLnNR),
+                                                                            16 * num_cus()));
+#define RK_LN_FWD(L_)                                                                                             \
+  case L_:                                                                                                        \
+    bst_res_dropout_ln_fwd4_kernel<L_><<<blocks, 256, 0, st>>>(base, o, rows, d, seed, stream_slot, thr, scale,   \
+                                                               gamma, beta, eps, r, y, mean, rstd);               \
+    break;
+    switch (L) { RK_LN_FWD(8) RK_LN_FWD(16) RK_LN_FWD(32) RK_LN_FWD(64) }
+#undef RK_LN_FWD
+  } else {
+    bst_res_dropout_ln_fwd_kernel<<<grid_of(rows, 4), 256, 0, st>>>(base, o, rows, d, seed, stream_slot, thr, scale,
+                                                                    gamma, beta, eps, r, y, mean, rstd);
+  }
   return check_launch("rk_bst_res_dropout_ln_forward");
 }
 
@@ -585,13 +813,26 @@ RK_API int rk_bst_ln_backward(const float* dy, const float* r, const float* mean
   if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
     return fail(RK_ERR_INVALID, "rk_bst_ln_backward: workspace of %lld floats, needs %lld (%d * 2d)",
                 (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d), kLnBlocks);
-  hipStream_t st = (hipStream_t)stream;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (rows + 3) / 4));
-  bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot,
-                                            dropout_threshold(dropout_p), (float)(1.0 / (1.0 - dropout_p)), dr, d_o,
-                                            workspace);
-  bst_ln_param_kernel<<<grid_of(2 * d, 64), 1024, 0, st>>>(workspace, blocks, d, dgamma, dbeta);
-  return check_launch("rk_bst_ln_backward");
+  return ln_backward(dy, nullptr, 0, 0, 1, nullptr, 0, r, mean, rstd, gamma, rows, d, dropout_p, seed, stream_slot,
+                     dr, d_o, dgamma, dbeta, workspace, (hipStream_t)stream, "rk_bst_ln_backward");
+}
+
+RK_API int rk_bst_pool_ln_backward(const float* drow, int64_t ld_row, int32_t col, int32_t T,
+                                   const int64_t* seq_len, int32_t mean_pool, const float* r, const float* mean,
+                                   const float* rstd, const float* gamma, int64_t rows, int32_t d, double dropout_p,
+                                   uint64_t seed, const int64_t* stream_slot, float* dr, float* d_o, float* dgamma,
+                                   float* dbeta, float* workspace, int64_t workspace_floats, void* stream) {
+  if (!drow || !r || !mean || !rstd || !gamma || !dr || !dgamma || !dbeta || !workspace || rows < 0 || T <= 0 ||
+      rows % T || d <= 0 || d > 256 || col < 0 || col + d > ld_row || (mean_pool && !seq_len) ||
+      !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
+    return fail(RK_ERR_INVALID, "rk_bst_pool_ln_backward: bad arguments (d <= 256, rows = batch * T)");
+  if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
+    return fail(RK_ERR_INVALID, "rk_bst_pool_ln_backward: workspace of %lld floats, needs %lld",
+                (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d));
+  if (ln_lanes(d, {drow + col, r, gamma, dr, d_o}) == 0 || ld_row % 4)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_pool_ln_backward: needs d %% 4 == 0, 16-B aligned rows");
+  return ln_backward(nullptr, drow, ld_row, col, T, seq_len, mean_pool, r, mean, rstd, gamma, rows, d, dropout_p, seed,
+                     stream_slot, dr, d_o, dgamma, dbeta, workspace, (hipStream_t)stream, "rk_bst_pool_ln_backward");
 }
 
 RK_API int rk_bst_pos_backward(const float* dxp, int64_t batch, int32_t T, int32_t d, float* dpos, void* stream) {

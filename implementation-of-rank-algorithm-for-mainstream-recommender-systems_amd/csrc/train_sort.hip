@@ -108,6 +108,8 @@ RK_API int rk_embedding_backward_sorted(const rk_segment* grad, int64_t n, const
   size_t tb = p.sort_bytes;
   if (rocprim::radix_sort_pairs(ws + p.off_tmp, tb, k0, k1, p0, p1, (unsigned)n, 0, bits, st) != hipSuccess)
     return fail(RK_ERR_LAUNCH, "rk_embedding_backward_sorted: radix sort failed");
+  // (a wave-per-64-positions float2 variant measured 100 us vs 76 us here at BST configs[3]: the
+  // padding row's per-column atomics, not the row loads, bound this kernel)
   emb_sorted_reduce_kernel<<<(unsigned)((n + kSortChunk - 1) / kSortChunk), 256, 0, st>>>(
       k1, p1, n, dx, ld_dx, grad->out_col, grad->dim, (uint32_t)grad->rows, const_cast<float*>(grad->src),
       grad->src_ld);

@@ -248,7 +248,14 @@ SIGNATURES = {
     "rk_bst_ln_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                           ctypes.c_double, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_bst_pool_ln_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p,
+                                               c_void_p, c_void_p, c_void_p, c_int64, c_int32, ctypes.c_double,
+                                               ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_int64, c_void_p]),
     "rk_bst_ln_backward_workspace_floats": (c_int64, [c_int32]),
+    "rk_gemm_wgrad": (ctypes.c_int, [c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                                     c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
+    "rk_gemm_wgrad_workspace_floats": (c_int64, [c_int64, c_int64, c_int64]),
     "rk_bst_pos_backward": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_bst_leaky_dropout": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, ctypes.c_double, ctypes.c_uint64,
                                             c_void_p, c_int32, c_void_p, c_void_p]),

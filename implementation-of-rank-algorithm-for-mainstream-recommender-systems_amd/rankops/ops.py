@@ -426,8 +426,18 @@ def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M
 def gemm(trans_a: bool, trans_b: bool, M: int, N: int, R: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
          C: torch.Tensor, ldc: int = None, *, A_mask: torch.Tensor = None, row_sums: torch.Tensor = None,
          accumulate: bool = False, split: int = 0):
-    """C[m, n] (+)= sum_r opA(m, r) opB(n, r) (rk_gemm; layouts in include/rankops.h)."""
+    """C[m, n] (+)= sum_r opA(m, r) opB(n, r) (rk_gemm; layouts in include/rankops.h).  Weight
+    gradients (both operands transposed: dW = dZ^T X over the batch rows) go to rk_gemm_wgrad when
+    the layout allows it."""
     lib = _lib.load()
+    ldc_ = C.stride(0) if ldc is None else ldc
+    if (trans_a and trans_b and split <= 0 and R >= 512 and (M | N | lda | ldb | ldc_) % 4 == 0
+            and all(t is None or t.data_ptr() % 16 == 0 for t in (A, B, A_mask, C, row_sums))):
+        nws = lib.rk_gemm_wgrad_workspace_floats(M, N, R)
+        ws = torch.empty(nws, device=C.device, dtype=torch.float32)
+        check(lib.rk_gemm_wgrad(M, N, R, ptr(A), lda, ptr(A_mask), ptr(B), ldb, ptr(C), ldc_, ptr(row_sums),
+                                int(accumulate), ptr(ws), nws, _lib.stream_of(C)), "rk_gemm_wgrad")
+        return C
     check(lib.rk_gemm(int(trans_a), int(trans_b), M, N, R, ptr(A), lda, ptr(A_mask), ptr(B), ldb, ptr(C),
                       C.stride(0) if ldc is None else ldc, ptr(row_sums), int(accumulate), split,
                       _lib.stream_of(C)), "rk_gemm")
@@ -695,6 +705,24 @@ def bst_ln_backward(dy, r, mean, rstd, ln, p, seed, slot, dr, d_o, dgamma, dbeta
     check(lib.rk_bst_ln_backward(ptr(dy), ptr(r), ptr(mean), ptr(rstd), ptr(ln.weight), r.shape[0], r.shape[1],
                                  float(p), seed, ptr(slot), ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta), ptr(ws),
                                  nws, _lib.stream_of(dy)), "rk_bst_ln_backward")
+
+
+def bst_pool_ln_backward(drow, col, T, seq_len, mean_pool, r, mean, rstd, ln, p, seed, slot, dr, d_o, dgamma,
+                         dbeta):
+    """bst_ln_backward whose incoming gradient is the pooling backward's broadcast of drow
+    (rk_bst_pool_ln_backward); returns False (nothing launched) when the layout does not allow it."""
+    lib = _lib.load()
+    d = r.shape[1]
+    if d % 4 or drow.stride(0) % 4 or col % 4 or any(t is not None and t.data_ptr() % 16
+                                                     for t in (drow, r, ln.weight, dr, d_o)):
+        return False
+    nws = lib.rk_bst_ln_backward_workspace_floats(d)
+    ws = torch.empty(nws, device=r.device, dtype=torch.float32)
+    check(lib.rk_bst_pool_ln_backward(ptr(drow), drow.stride(0), col, T, ptr(seq_len), int(mean_pool), ptr(r),
+                                      ptr(mean), ptr(rstd), ptr(ln.weight), r.shape[0], d, float(p), seed, ptr(slot),
+                                      ptr(dr), ptr(d_o), ptr(dgamma), ptr(dbeta), ptr(ws), nws, _lib.stream_of(r)),
+          "rk_bst_pool_ln_backward")
+    return True
 
 
 def bst_pos_backward(dxp, B, T, dpos):

@@ -80,20 +80,27 @@ def mlp_relu_backward(dh, hs, linears):
     return dh, grads
 
 
+def zero_grads(weights, device):
+    """Zero-filled gradient tensors shaped like `weights`, carved from one flat buffer (one fill) at
+    256-B aligned offsets, so the row-vector (float4) scatter kernels apply to every table."""
+    offs, total = [], 0
+    for w in weights:
+        offs.append(total)
+        total += (w.numel() + 63) // 64 * 64
+    flat = torch.zeros(max(total, 1), device=device, dtype=torch.float32)
+    return [flat[o:o + w.numel()].view(w.shape) for o, w in zip(offs, weights)]
+
+
 def embedding_grads(weights, idx, col0, dx, cols=None):
     """Dense nn.Embedding gradients of the tables whose rows sit side by side in dx from column
     col0 on (or at the given `cols`): one zero-filled flat buffer for all tables (one fill),
     then rk_embedding_backward."""
-    total = sum(w.numel() for w in weights)
-    flat = torch.zeros(total, device=dx.device, dtype=torch.float32)
-    grads, segs = [], []
-    off, col = 0, col0
-    for k, (w, i) in enumerate(zip(weights, idx)):
-        g = flat[off:off + w.numel()].view(w.shape)
-        grads.append(g)
+    grads = zero_grads(weights, dx.device)
+    segs = []
+    col = col0
+    for k, (g, i) in enumerate(zip(grads, idx)):
         segs.append(ops.table_segment(g, i, col if cols is None else cols[k]))
-        off += w.numel()
-        col += w.shape[1]
+        col += g.shape[1]
     ops.embedding_backward(segs, dx.shape[0], dx)
     return grads
 
@@ -575,12 +582,7 @@ class _DINTrain(torch.autograd.Function):
         del dcross
         # nn.Embedding gradients: one zeroed buffer per distinct table, every lookup scattered into it
         weights, looks = ctx.emb_plan
-        total = sum(w.numel() for w in weights)
-        flat_g = torch.zeros(total, **f32)
-        grads, off = [], 0
-        for w in weights:
-            grads.append(flat_g[off:off + w.numel()].view(w.shape))
-            off += w.numel()
+        grads = zero_grads(weights, dev)
         segs = [ops.table_segment(grads[k], i, col) for k, i, col in looks]
         ops.embedding_backward(segs, B, dxr)
         # the padded history positions all map to row 0: sorted segment-reduce instead of atomics
@@ -824,15 +826,10 @@ class _BSTTrain(torch.autograd.Function):
         ops.logit_head_backward(_grad_out(dlogit, prob), _grad_out(dprob, prob), prob, hid, None, last.weight, dh,
                                 None, dw_last, db_last)
         d_row, unit_grads = deep_stack_backward(dh, row, units, saved, seed, slot)
-        dx = torch.empty(M, d, **f32)
-        ops.bst_pool_backward(d_row, col, B, T, d, seq_len, model.pooling_method != "sum", dx)
+        mean_pool = model.pooling_method != "sum"
+        dx = None  # the last block's LN2 backward reads the pooling gradient d_row directly
         tables, looks = plan["tables"], plan["looks"]
-        total = sum(w.numel() for w in tables)
-        gflat = torch.zeros(total, **f32)
-        tgrads, off = [], 0
-        for w in tables:
-            tgrads.append(gflat[off:off + w.numel()].view(w.shape))
-            off += w.numel()
+        tgrads = zero_grads(tables, dev)
         block_grads = [None] * nb
         for i in range(nb - 1, -1, -1):
             blk = model.transformer_blocks[i]
@@ -842,8 +839,14 @@ class _BSTTrain(torch.autograd.Function):
             d_out1 = torch.empty(M, d, **f32)
             df2 = torch.empty(M, d, **f32)
             dg2, dbe2 = torch.empty(d, **f32), torch.empty(d, **f32)
-            ops.bst_ln_backward(dx, r2, m2, s2, blk.norm2, p_o, bst_dropout_seed(seed, i, 2), slot, d_out1, df2, dg2,
-                                dbe2)
+            if dx is None and not ops.bst_pool_ln_backward(d_row, col, T, seq_len, mean_pool, r2, m2, s2, blk.norm2,
+                                                           p_o, bst_dropout_seed(seed, i, 2), slot, d_out1, df2, dg2,
+                                                           dbe2):
+                dx = torch.empty(M, d, **f32)
+                ops.bst_pool_backward(d_row, col, B, T, d, seq_len, mean_pool, dx)
+            if dx is not None:
+                ops.bst_ln_backward(dx, r2, m2, s2, blk.norm2, p_o, bst_dropout_seed(seed, i, 2), slot, d_out1, df2,
+                                    dg2, dbe2)
             dW2, db2, da = _lin_grads(df2, a, blk.ffn[3].weight)
             df1 = torch.empty(M, d, **f32)
             ops.bst_leaky_dropout(da, f1, blk.ffn[1].negative_slope, p_f, bst_dropout_seed(seed, i, 1), slot, True, df1)

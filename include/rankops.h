@@ -36,6 +36,7 @@
  *   rk_fwfm_forward    FwFM.forward()                        fwfm.py:114-139
  *   training (loss.backward() + optimizer.step() of the train() loops, dcn.py:196-201):
  *   rk_gemm            the Linear backward GEMMs (dX = dZ W, dW = dZ^T X, db)   dcn.py:147-150
+ *   rk_gemm_wgrad      dW = dZ^T X, db over long reductions (one tile owner per row slab)
  *   rk_logit_head_backward  output_layer + sigmoid backward      dcn.py:177-179
  *   rk_dcn_cross_backward   cross_layer backward w.r.t. x0        dcn.py:46-49
  *   rk_relu_backward   ReLU backward (residual_unit's outer ReLU) deepcrossing.py:41
@@ -48,13 +49,15 @@
  *   rk_fm_backward, rk_fm_combine_backward  FM and final_layer + sigmoid backward  deepfm.py:122-151
  *   rk_rng_next, rk_dropout_mask  dropout stream counter / explicit mask
  *   rk_dice_train_forward / rk_dice_backward  Dice with batch statistics and its backward  din.py:26-36
+ *   rk_prelu_train_forward / rk_prelu_backward  the activation='prelu' option (nn.PReLU)  din.py:277-279
  *   rk_din_att_cross, rk_din_att_pool_forward, rk_din_att_pool_backward, rk_din_cross_fold
  *                      din_attention() train forward pieces and backward   din.py:42-84
  *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
  *   rk_bst_add_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
- *   rk_bst_ln_backward, rk_bst_pos_backward, rk_bst_leaky_dropout, rk_bst_pool / _backward
+ *   rk_bst_ln_backward, rk_bst_pool_ln_backward, rk_bst_pos_backward, rk_bst_leaky_dropout,
+ *   rk_bst_pool / _backward
  *                      BSTTransformer train forward (activations kept) and backward  bst.py:66-91,238-241
  *                      AFM train forward (activations kept) and backward  afm.py:92-119,173
  *   rk_bn_fold         BatchNorm1d eval affine (running stats) deepfm.py:105, din.py:31,281, bst.py:208
@@ -374,6 +377,18 @@ int rk_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t R, c
             int64_t lda, const float* A_mask, const float* B, int64_t ldb, float* C, int64_t ldc,
             float* row_sums, int32_t accumulate, int32_t split, void* stream);
 
+/* Weight-gradient GEMM (every nn.Linear's dW / db in loss.backward(), e.g. bst.py:59-64,73-90,
+ * dcn.py:147-150): C[n, k] (+)= sum_r opA(r, n) B[r * ldb + k] and row_sums[n] (+)= sum_r opA(r, n),
+ * opA(r, n) = A[r * lda + n] (times [A_mask[r * lda + n] > 0] when A_mask != NULL), for a long
+ * reduction R.  Same result as rk_gemm(1, 1, N, K, R, ...) but each 128 x 128 output tile is owned
+ * by one workgroup per row slab and the slabs' partials are summed in a fixed order
+ * (deterministic).  Needs N, K, lda, ldb, ldc % 4 == 0 and 16-B aligned pointers
+ * (RK_ERR_UNSUPPORTED otherwise); workspace: rk_gemm_wgrad_workspace_floats(N, K, R) floats.  */
+int rk_gemm_wgrad(int64_t N, int64_t K, int64_t R, const float* A, int64_t lda, const float* A_mask,
+                  const float* B, int64_t ldb, float* C, int64_t ldc, float* row_sums,
+                  int32_t accumulate, float* workspace, int64_t workspace_floats, void* stream);
+int64_t rk_gemm_wgrad_workspace_floats(int64_t N, int64_t K, int64_t R);
+
 /* out[i] (+)= dy[i] * [y[i] > 0] over n contiguous floats (ReLU backward from its output; the
  * residual path of residual_unit, deepcrossing.py:41).                                        */
 int rk_relu_backward(const float* dy, const float* y, float* out, int64_t n, int32_t accumulate,
@@ -565,7 +580,17 @@ int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const
                        const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
                        const int64_t* stream_slot, float* dr, float* d_o, float* dgamma, float* dbeta,
                        float* workspace, int64_t workspace_floats, void* stream);
-/* Floats rk_bst_ln_backward needs in `workspace` for model width d. */
+/* rk_bst_ln_backward of the last block fused with the pooling backward (bst.py:238-241): the
+ * incoming gradient of row m is drow[m / T, col:col+d] (/ seq_len[m / T] when mean_pool), so the
+ * [rows, d] broadcast is never written.  rows = batch * T; needs d % 4 == 0 and 16-B aligned rows
+ * (RK_ERR_UNSUPPORTED otherwise: use rk_bst_pool_backward + rk_bst_ln_backward).               */
+int rk_bst_pool_ln_backward(const float* drow, int64_t ld_row, int32_t col, int32_t T,
+                            const int64_t* seq_len, int32_t mean_pool, const float* r,
+                            const float* mean, const float* rstd, const float* gamma, int64_t rows,
+                            int32_t d, double dropout_p, uint64_t seed, const int64_t* stream_slot,
+                            float* dr, float* d_o, float* dgamma, float* dbeta, float* workspace,
+                            int64_t workspace_floats, void* stream);
+/* Floats rk_bst_ln_backward / rk_bst_pool_ln_backward need in `workspace` for model width d. */
 int64_t rk_bst_ln_backward_workspace_floats(int32_t d);
 int rk_bst_pos_backward(const float* dxp, int64_t batch, int32_t T, int32_t d, float* dpos, void* stream);
 int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, float slope, double dropout_p,

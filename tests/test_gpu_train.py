@@ -968,3 +968,24 @@ def test_gemm_cols_weight_gradient_matches_fp64(M, N, masked):
     ops.gemm(1, 1, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md, row_sums=sums, accumulate=True)
     torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
     torch.testing.assert_close(sums.cpu().double(), 2 * rs, rtol=0, atol=2 * tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K,R,col", [(128, 128, 70001, 128), (256, 128, 4099, 0), (132, 260, 65, 4), (8, 4, 1, 0)])
+def test_gemm_wgrad_strided_views_match_fp64(N, K, R, col):
+    """rk_gemm_wgrad (ops.gemm with both operands transposed) on column views of a wider matrix
+    (dK = dqkv[:, d:2d] as in the BST backward): row pitch lda > N, ragged R, N/K off the 128 tile."""
+    g = torch.Generator().manual_seed(N + K + R)
+    wide = torch.randn(R, col + N + 8, generator=g)
+    X = torch.randn(R, K, generator=g)
+    A = wide[:, col:col + N]
+    want = A.double().t() @ X.double()
+    rs = A.double().sum(0)
+    wd, Xd = wide.cuda(), X.cuda()
+    Ad = wd[:, col:col + N]
+    C = torch.full((N, K), 7.0, device="cuda")
+    sums = torch.full((N,), 7.0, device="cuda")
+    ops.gemm(1, 1, N, K, R, Ad, wd.stride(0), Xd, Xd.stride(0), C, row_sums=sums)
+    tol = 2e-4 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
+    torch.testing.assert_close(sums.cpu().double(), rs, rtol=0, atol=tol)
