@@ -25,6 +25,29 @@ __global__ __launch_bounds__(256) void bst_add_pos_kernel(const float* __restric
   xp[i] = x[i] + pos[(int64_t)(m % T) * d + k];
 }
 
+// Behaviour-sequence gather fused with the position add (bst.py:224 + 73-75): x[m] = table[idx[m]]
+// (out-of-range -> zeros, flagged), xp[m] = x[m] + pos[m % T]; float4 per lane, d % 4 == 0.
+__global__ __launch_bounds__(256) void bst_gather_pos_kernel(const float* __restrict__ table, int64_t rows,
+                                                             int64_t ld_table, const int64_t* __restrict__ idx,
+                                                             int64_t M, int T, int d, const float* __restrict__ pos,
+                                                             float* __restrict__ x, float* __restrict__ xp,
+                                                             uint32_t* flags) {
+  const int q = d / 4;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M * q) return;
+  const int64_t m = e / q;
+  const int k = 4 * (int)(e - m * q);
+  const int64_t r = idx[m];
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (r >= 0 && r < rows)
+    v = *reinterpret_cast<const f32x4*>(table + r * ld_table + k);
+  else if (k == 0)
+    flag_oob(flags);
+  const f32x4 pv = *reinterpret_cast<const f32x4*>(pos + (int64_t)(m % T) * d + k);
+  *reinterpret_cast<f32x4*>(x + m * d + k) = v;
+  *reinterpret_cast<f32x4*>(xp + m * d + k) = v + pv;
+}
+
 // Attention train kernels on FP32 MFMA (v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k] and
 // B[k][l&15] with hardware k = l>>4; accumulator register r of lane l is D[4*(l>>4) + r][l&15]).
 // One 256-thread workgroup per (sample, head); T is padded to TP = 16*ceil(T/16) <= 64 positions and
@@ -64,6 +87,34 @@ __device__ __forceinline__ void att_stage(float* __restrict__ dst, int ldt, cons
     const int t = i / DP, k = i - t * DP;
     dst[t * ldt + k] = (t < T && k < dh) ? src[(row0 + t) * ld + col0 + k] : 0.f;
   }
+}
+
+// Stage NT head slices at once (float4 path only: dh, ld and col0 multiples of 4): every tile's
+// global loads are issued before the first LDS store, so the NT round trips overlap instead of
+// running one after another.  TP * DP / 4 <= 1024 float4 per tile (4 per thread at 256 threads).
+template <int NT>
+__device__ __forceinline__ void att_stage_all(float* const (&dst)[NT], const float* const (&src)[NT],
+                                              const int64_t (&ld)[NT], const int (&col0)[NT], int ldt, int64_t row0,
+                                              int T, int dh, int TP, int DP) {
+  const int q = DP / 4, n = TP * q;
+  f32x4 v[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int r = i / q, k = 4 * (i - r * q);
+      v[t][u] = (i < n && r < T && k < dh) ? *reinterpret_cast<const f32x4*>(src[t] + (row0 + r) * ld[t] + col0[t] + k)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int r = i / q, k = 4 * (i - r * q);
+      if (i < n) *reinterpret_cast<f32x4*>(dst[t] + r * ldt + k) = v[t][u];
+    }
 }
 
 // acc[jt] += rows(16*jt ..) of X  .  rows(16*w ..) of Y, contracted over DP columns (both [TP][ldt] LDS
@@ -166,9 +217,17 @@ __global__ __launch_bounds__(256) void bst_attn_train_fwd_kernel(const float* __
   float* const sV = sK + TP * ldt;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t row0 = b * T, ld = 3 * (int64_t)d;
-  att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
-  att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
-  att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
+  if (((dh | d) & 3) == 0) {
+    float* const dst[3] = {sQ, sK, sV};
+    const float* const src[3] = {qkv, qkv, qkv};
+    const int64_t lds[3] = {ld, ld, ld};
+    const int c0[3] = {h * dh, d + h * dh, 2 * d + h * dh};
+    att_stage_all<3>(dst, src, lds, c0, ldt, row0, T, dh, TP, DP);
+  } else {
+    att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
+    att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
+    att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
+  }
   __syncthreads();
   if (w >= NS) return;
   const int li = lane & 15, kq = 4 * (lane >> 4);
@@ -244,31 +303,41 @@ __global__ __launch_bounds__(256) void bst_attn_train_bwd_kernel(const float* __
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const int64_t row0 = b * T, ld = 3 * (int64_t)d;
-  att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
-  att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
-  att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
-  att_stage(sC, ldt, dctx, d, row0, h * dh, T, dh, TP, DP);
+  // this wave's P strip (register layout of the dP tile below) is loaded first, so its round trip
+  // overlaps the operand staging
+  const int i = 16 * w + li;
+  const float* Pi = P + ((b * heads + h) * (int64_t)T + min(i, T - 1)) * T;
+  f32x4 p[4];
+  const bool pvec = (T & 3) == 0;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    p[jt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (jt >= NS || i >= T || w >= NS) continue;
+    if (pvec) {
+      if (16 * jt + kq < T) p[jt] = *reinterpret_cast<const f32x4*>(Pi + 16 * jt + kq);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * jt + kq + r < T) p[jt][r] = Pi[16 * jt + kq + r];
+    }
+  }
+  if (((dh | d) & 3) == 0) {
+    float* const dst[4] = {sQ, sK, sV, sC};
+    const float* const src[4] = {qkv, qkv, qkv, dctx};
+    const int64_t lds[4] = {ld, ld, ld, (int64_t)d};
+    const int c0[4] = {h * dh, d + h * dh, 2 * d + h * dh, h * dh};
+    att_stage_all<4>(dst, src, lds, c0, ldt, row0, T, dh, TP, DP);
+  } else {
+    att_stage(sQ, ldt, qkv, ld, row0, h * dh, T, dh, TP, DP);
+    att_stage(sK, ldt, qkv, ld, row0, d + h * dh, T, dh, TP, DP);
+    att_stage(sV, ldt, qkv, ld, row0, 2 * d + h * dh, T, dh, TP, DP);
+    att_stage(sC, ldt, dctx, d, row0, h * dh, T, dh, TP, DP);
+  }
   __syncthreads();
   const float sq = sqrtf((float)dh);
   if (w < NS) {
     f32x4 g[4];
     att_rowdot(g, sV, sC, ldt, w, NS, ND, lane);  // g[jt][r] = dP[i = 16w + li][j = 16jt + kq + r]
-    const int i = 16 * w + li;
-    const float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
-    f32x4 p[4];
-    const bool vec = (T & 3) == 0;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      p[jt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (jt >= NS || i >= T) continue;
-      if (vec) {
-        if (16 * jt + kq < T) p[jt] = *reinterpret_cast<const f32x4*>(Pi + 16 * jt + kq);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (16 * jt + kq + r < T) p[jt][r] = Pi[16 * jt + kq + r];
-      }
-    }
     float D = 0.f;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
@@ -295,6 +364,217 @@ __global__ __launch_bounds__(256) void bst_attn_train_bwd_kernel(const float* __
     att_store(o, dqkv, ld, row0, d + h * dh, w, T, dh, ND, lane);
     att_tmm(o, sP, ldp, sC, ldt, w, NS, ND, lane);  // dV[j] = sum_i P[i, j] dC[i]
     att_store(o, dqkv, ld, row0, 2 * d + h * dh, w, T, dh, ND, lane);
+  }
+}
+
+// ---- Persistent forms of the two attention train kernels (T % 4 == 0, dh % 4 == 0: float4 rows).
+// A workgroup walks (sample, head) items grid-stride; while it computes item n, the global loads of
+// item n + grid (its Q/K/V(/dC) slices and, in the backward, each wave's P strip) are already in
+// flight in registers, so the staging round trip no longer sits between one item's compute and the
+// next (the one-item-per-workgroup kernels above wait out a full round trip per item: latency-bound,
+// SQ_WAIT_ANY 51% of wave time in the backward).  US = float4 slots per thread and tile.
+template <int NT, int US>
+__device__ __forceinline__ void att_load_regs(f32x4 (&v)[NT][US], const float* const (&src)[NT],
+                                              const int64_t (&ld)[NT], const int (&col0)[NT], int64_t row0, int T,
+                                              int dh, int TP, int DP) {
+  const int q = DP / 4, n = TP * q;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int u = 0; u < US; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int r = i / q, k = 4 * (i - r * q);
+      v[t][u] = (i < n && r < T && k < dh) ? *reinterpret_cast<const f32x4*>(src[t] + (row0 + r) * ld[t] + col0[t] + k)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+template <int NT, int US>
+__device__ __forceinline__ void att_store_regs(float* const (&dst)[NT], const f32x4 (&v)[NT][US], int ldt, int TP,
+                                               int DP) {
+  const int q = DP / 4, n = TP * q;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int u = 0; u < US; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int r = i / q, k = 4 * (i - r * q);
+      if (i < n) *reinterpret_cast<f32x4*>(dst[t] + r * ldt + k) = v[t][u];
+    }
+}
+
+template <int US>
+__global__ __launch_bounds__(256, 2) void bst_attn_train_fwd_pkernel(const float* __restrict__ qkv, int64_t B, int T,
+                                                                  int d, int heads,
+                                                                  const int64_t* __restrict__ seq_len,
+                                                                  float* __restrict__ P, float* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float att_sm[];
+  const int dh = d / heads;
+  const int TP = (T + 15) & ~15, DP = (dh + 15) & ~15, ldt = DP + 4;
+  const int NS = TP / 16, ND = DP / 16;
+  float* const sQ = att_sm;
+  float* const sK = sQ + TP * ldt;
+  float* const sV = sK + TP * ldt;
+  float* const dst[3] = {sQ, sK, sV};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  const int64_t items = B * heads, ld = 3 * (int64_t)d;
+  const float sq = sqrtf((float)dh);  // scores / math.sqrt(q.size(-1)), bst.py:77
+  const int64_t lds3[3] = {ld, ld, ld};
+  const float* const src3[3] = {qkv, qkv, qkv};
+  f32x4 v[3][US];
+  int64_t it = blockIdx.x;
+  if (it < items) {
+    const int64_t b = it / heads;
+    const int h = (int)(it - b * heads);
+    const int c0[3] = {h * dh, d + h * dh, 2 * d + h * dh};
+    att_load_regs<3, US>(v, src3, lds3, c0, b * T, T, dh, TP, DP);
+  }
+  for (; it < items; it += gridDim.x) {
+    const int64_t b = it / heads;
+    const int h = (int)(it - b * heads);
+    const int64_t row0 = b * T;
+    att_store_regs<3, US>(dst, v, ldt, TP, DP);
+    __syncthreads();
+    const int64_t nx = it + gridDim.x;
+    if (nx < items) {
+      const int64_t nb = nx / heads;
+      const int nh = (int)(nx - nb * heads);
+      const int c0[3] = {nh * dh, d + nh * dh, 2 * d + nh * dh};
+      att_load_regs<3, US>(v, src3, lds3, c0, nb * T, T, dh, TP, DP);
+    }
+    if (w < NS) {
+      const int64_t len = seq_len[b];
+      f32x4 s[4];
+      att_rowdot(s, sK, sQ, ldt, w, NS, ND, lane);  // s[jt][r] = S[i = 16w + li][j = 16jt + kq + r]
+      float mx = -INFINITY;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * jt + kq + r;
+          const float x = (jt < NS && j < T) ? ((int64_t)j < len ? s[jt][r] / sq : -INFINITY) : -INFINITY;
+          s[jt][r] = x;  // masked_fill(key_padding_mask, -inf), bst.py:80
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+      float sum = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * jt + kq + r;
+          const float e = (jt < NS && j < T) ? expf(s[jt][r] - mx) : 0.f;
+          s[jt][r] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 16, kWave);
+      sum += __shfl_xor(sum, 32, kWave);
+      const int i = 16 * w + li;
+      float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+        if (jt >= NS) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * jt + kq + r;
+          s[jt][r] = j < T ? s[jt][r] / sum : 0.f;
+        }
+        if (i < T && 16 * jt + kq < T) *reinterpret_cast<f32x4*>(Pi + 16 * jt + kq) = s[jt];
+      }
+      f32x4 c[4];
+      att_regmm(c, s, sV, ldt, NS, ND, lane);
+      att_store(c, ctx, d, row0, h * dh, w, T, dh, ND, lane);
+    }
+    __syncthreads();  // the next item's staging overwrites the tiles
+  }
+}
+
+template <int US>
+__global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float* __restrict__ qkv,
+                                                                  const float* __restrict__ P,
+                                                                  const float* __restrict__ dctx, int64_t B, int T,
+                                                                  int d, int heads, float* __restrict__ dqkv) {
+  extern __shared__ __attribute__((aligned(16))) float att_sm[];
+  const int dh = d / heads;
+  const int TP = (T + 15) & ~15, DP = (dh + 15) & ~15, ldt = DP + 4, ldp = TP + 4;
+  const int NS = TP / 16, ND = DP / 16;
+  float* const sQ = att_sm;
+  float* const sK = sQ + TP * ldt;
+  float* const sV = sK + TP * ldt;
+  float* const sC = sV + TP * ldt;
+  float* const sP = sC + TP * ldt;
+  float* const sS = sP + TP * ldp;
+  float* const dst[4] = {sQ, sK, sV, sC};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  const int64_t items = B * heads, ld = 3 * (int64_t)d;
+  const float sq = sqrtf((float)dh);
+  const int64_t lds4[4] = {ld, ld, ld, (int64_t)d};
+  const float* const src4[4] = {qkv, qkv, qkv, dctx};
+  const int i = 16 * w + li;
+  const bool prow = w < NS && i < T;
+  f32x4 v[4][US], pc[4];
+  // item `x`'s operand slices, and this wave's P strip, into registers
+  auto load_tiles = [&](int64_t x) {
+    const int64_t b = x / heads;
+    const int h = (int)(x - b * heads);
+    const int c0[4] = {h * dh, d + h * dh, 2 * d + h * dh, h * dh};
+    att_load_regs<4, US>(v, src4, lds4, c0, b * T, T, dh, TP, DP);
+  };
+  auto load_p = [&](int64_t x) {
+    const float* Pi = P + (x * (int64_t)T + (prow ? i : 0)) * T;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+      pc[jt] = (prow && jt < NS && 16 * jt + kq < T) ? *reinterpret_cast<const f32x4*>(Pi + 16 * jt + kq)
+                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  int64_t it = blockIdx.x;
+  if (it < items) {
+    load_tiles(it);
+    load_p(it);
+  }
+  for (; it < items; it += gridDim.x) {
+    const int64_t b = it / heads;
+    const int h = (int)(it - b * heads);
+    const int64_t row0 = b * T;
+    const bool more = it + gridDim.x < items;
+    att_store_regs<4, US>(dst, v, ldt, TP, DP);
+    __syncthreads();
+    if (more) load_tiles(it + gridDim.x);
+    if (w < NS) {
+      f32x4 g[4];
+      att_rowdot(g, sV, sC, ldt, w, NS, ND, lane);  // g[jt][r] = dP[i = 16w + li][j = 16jt + kq + r]
+      float D = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D += pc[jt][r] * g[jt][r];
+      D += __shfl_xor(D, 16, kWave);
+      D += __shfl_xor(D, 32, kWave);
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+        if (jt >= NS) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[jt][r] = pc[jt][r] * (g[jt][r] - D) / sq;
+        *reinterpret_cast<f32x4*>(sP + i * ldp + 16 * jt + kq) = pc[jt];
+        *reinterpret_cast<f32x4*>(sS + i * ldp + 16 * jt + kq) = g[jt];
+      }
+      if (more) load_p(it + gridDim.x);  // pc is in LDS now: the next strip's loads overlap the rest
+      f32x4 q[4];
+      att_regmm(q, g, sK, ldt, NS, ND, lane);  // dQ[i] = sum_j dS[i, j] K[j]
+      att_store(q, dqkv, ld, row0, h * dh, w, T, dh, ND, lane);
+    }
+    __syncthreads();
+    if (w < NS) {
+      f32x4 o[4];
+      att_tmm(o, sS, ldp, sQ, ldt, w, NS, ND, lane);  // dK[j] = sum_i dS[i, j] Q[i]
+      att_store(o, dqkv, ld, row0, d + h * dh, w, T, dh, ND, lane);
+      att_tmm(o, sP, ldp, sC, ldt, w, NS, ND, lane);  // dV[j] = sum_i P[i, j] dC[i]
+      att_store(o, dqkv, ld, row0, 2 * d + h * dh, w, T, dh, ND, lane);
+    }
+    __syncthreads();  // the next item's staging overwrites the tiles
   }
 }
 
@@ -682,10 +962,29 @@ __global__ __launch_bounds__(256) void bst_pool_bwd_kernel(const float* __restri
 
 static inline unsigned grid_of(int64_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
 
+// float4 slots per thread and operand tile of the persistent attention kernels (0: dh not a
+// multiple of 4 -> the one-item kernels).
+static int att_slots(int T, int dh) {
+  if (dh % 4) return 0;
+  const int n = att_pad16(T) * att_pad16(dh) / 4;
+  return n <= 256 ? 1 : n <= 512 ? 2 : 4;
+}
+
+// Persistent grid: as many workgroups as fit on the GPU at this LDS size (at most 8 per CU), or
+// one per item when there are fewer items.
+static unsigned att_grid(int64_t items, size_t lds) {
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)(160 * 1024) / (int64_t)std::max<size_t>(lds, 1)));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, per_cu * num_cus()));
+}
+
 // Dynamic LDS above the 64 KiB default: up to 104 KiB (T = 64, dh = 64 backward).
 static void att_set_attrs() {
   static bool done = false;
   if (done) return;
+  for (const void* f : {(const void*)bst_attn_train_fwd_pkernel<1>, (const void*)bst_attn_train_fwd_pkernel<2>,
+                        (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1>,
+                        (const void*)bst_attn_train_bwd_pkernel<2>, (const void*)bst_attn_train_bwd_pkernel<4>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)bst_attn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
   (void)hipFuncSetAttribute((const void*)bst_attn_train_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -744,6 +1043,19 @@ RK_API int rk_bst_add_pos(const float* x, const float* pos, int32_t T, int64_t r
   return check_launch("rk_bst_add_pos");
 }
 
+RK_API int rk_bst_gather_pos(const float* table, int64_t rows, int64_t ld_table, const int64_t* idx, int64_t n,
+                             int32_t T, int32_t d, const float* pos, float* x, float* xp, void* stream) {
+  if (!table || !idx || !pos || !x || !xp || rows <= 0 || n < 0 || T <= 0 || d <= 0 || ld_table < d)
+    return fail(RK_ERR_INVALID, "rk_bst_gather_pos: bad arguments");
+  if (d % 4 || ld_table % 4 || ((reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(pos) |
+                                 reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(xp)) & 15))
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_gather_pos: needs d %% 4 == 0 and 16-B aligned rows");
+  if (n == 0) return RK_OK;
+  bst_gather_pos_kernel<<<grid_of(n * (d / 4)), 256, 0, (hipStream_t)stream>>>(table, rows, ld_table, idx, n, T, d,
+                                                                              pos, x, xp, device_flags());
+  return check_launch("rk_bst_gather_pos");
+}
+
 RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_t d, int32_t heads,
                                      const int64_t* seq_len, float* probs, float* ctx, void* stream) {
   if (!qkv || !seq_len || !probs || !ctx || batch < 0 || T <= 0 || T > kBstTMax || heads <= 0 || d % heads ||
@@ -752,6 +1064,20 @@ RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T,
                 kBstDhMax);
   if (batch == 0) return RK_OK;
   att_set_attrs();
+  const int dh = d / heads;
+  const int US = att_slots(T, dh);
+  if (US && T % 4 == 0 && d % 4 == 0) {
+    const size_t lds = att_lds_bytes(T, dh, false);
+    const unsigned grid = att_grid(batch * heads, lds);
+#define RK_ATT_FWD(U_)                                                                                          \
+  case U_:                                                                                                      \
+    bst_attn_train_fwd_pkernel<U_><<<grid, 256, lds, (hipStream_t)stream>>>(qkv, batch, T, d, heads, seq_len,   \
+                                                                            probs, ctx);                        \
+    break;
+    switch (US) { RK_ATT_FWD(1) RK_ATT_FWD(2) RK_ATT_FWD(4) }
+#undef RK_ATT_FWD
+    return check_launch("rk_bst_attn_train_forward");
+  }
   bst_attn_train_fwd_kernel<<<(unsigned)(batch * heads), 256, att_lds_bytes(T, d / heads, false),
                               (hipStream_t)stream>>>(qkv, batch, T, d, heads,
                                                                                         seq_len, probs, ctx);
@@ -765,6 +1091,20 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_backward: T <= %d, d/heads <= %d", kBstTMax, kBstDhMax);
   if (batch == 0) return RK_OK;
   att_set_attrs();
+  const int dh = d / heads;
+  const int US = att_slots(T, dh);
+  if (US && T % 4 == 0 && d % 4 == 0) {
+    const size_t lds = att_lds_bytes(T, dh, true);
+    const unsigned grid = att_grid(batch * heads, lds);
+#define RK_ATT_BWD(U_)                                                                                          \
+  case U_:                                                                                                      \
+    bst_attn_train_bwd_pkernel<U_><<<grid, 256, lds, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T, d, heads, \
+                                                                            dqkv);                              \
+    break;
+    switch (US) { RK_ATT_BWD(1) RK_ATT_BWD(2) RK_ATT_BWD(4) }
+#undef RK_ATT_BWD
+    return check_launch("rk_bst_attn_train_backward");
+  }
   bst_attn_train_bwd_kernel<<<(unsigned)(batch * heads), 256, att_lds_bytes(T, d / heads, true),
                               (hipStream_t)stream>>>(qkv, probs, dctx, batch, T,
                                                                                         d, heads, dqkv);

@@ -678,6 +678,19 @@ def bst_add_pos(x, pos, T, xp):
           "rk_bst_add_pos")
 
 
+def bst_gather_pos(table, idx, T, pos, x, xp):
+    """x = table[idx], xp = x + pos[m % T] in one pass (rk_bst_gather_pos); False when the layout
+    does not allow it (nothing launched)."""
+    d = table.shape[1]
+    if (d % 4 or table.stride(0) % 4 or idx.stride(0) != 1 or pos.stride(0) != d
+            or any(t.data_ptr() % 16 for t in (table, pos, x, xp))):
+        return False
+    lib = _lib.load()
+    check(lib.rk_bst_gather_pos(ptr(table), table.shape[0], table.stride(0), ptr(idx), idx.shape[0], T, d, ptr(pos),
+                                ptr(x), ptr(xp), _lib.stream_of(x)), "rk_bst_gather_pos")
+    return True
+
+
 def bst_attn_train_forward(qkv, B, T, d, heads, seq_len, probs, ctx):
     lib = _lib.load()
     check(lib.rk_bst_attn_train_forward(ptr(qkv), B, T, d, heads, ptr(seq_len), ptr(probs), ptr(ctx),

@@ -758,14 +758,17 @@ class _BSTTrain(torch.autograd.Function):
         ops.concat_gather(plan["segs"], B, row)
         feed = model.embeddings["feedid"].weight
         x = torch.empty(M, d, **f32)
-        ops.concat_gather([ops.table_segment(feed, seq.view(-1), 0)], M, x)
         seed, slot = model._dropout.next(dev)
         saves = []
         for i, blk in enumerate(model.transformer_blocks):
             p_o, p_f = float(blk.dropout.p) if blk.training else 0.0, float(blk.ffn[2].p) if blk.training else 0.0
             h = blk.nhead
             xp = torch.empty(M, d, **f32)
-            ops.bst_add_pos(x, blk.position_embedding.weight, T, xp)
+            pos = blk.position_embedding.weight
+            if i > 0 or not ops.bst_gather_pos(feed, seq.reshape(-1), T, pos, x, xp):
+                if i == 0:
+                    ops.concat_gather([ops.table_segment(feed, seq.view(-1), 0)], M, x)
+                ops.bst_add_pos(x, pos, T, xp)
             qkv = torch.empty(M, 3 * d, **f32)
             ops.linear(xp, blk.w_q.weight, None, y_ptr=qkv.data_ptr(), ldy=3 * d,
                        epilogue=ops.make_epilogue(bias=blk.w_q.bias))

@@ -55,7 +55,7 @@
  *   rk_row_l2norm_backward  DIN mini-batch-aware l2 term backward           din.py:318-322
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
- *   rk_bst_add_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
+ *   rk_bst_add_pos, rk_bst_gather_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
  *   rk_bst_ln_backward, rk_bst_pool_ln_backward, rk_bst_pos_backward, rk_bst_leaky_dropout,
  *   rk_bst_pool / _backward
  *                      BSTTransformer train forward (activations kept) and backward  bst.py:66-91,238-241
@@ -567,6 +567,12 @@ int rk_afm_pair_fold(const float* d_pairs, const float* emb, int32_t num_fields,
  * Dropout masks: the counter hash of rk_dropout_mask with index m * d + k.                      */
 int rk_bst_add_pos(const float* x, const float* pos, int32_t T, int64_t rows, int32_t d, float* xp,
                    void* stream);
+/* Behaviour-sequence gather + position add of the first block's train forward (bst.py:224,73-75):
+ * x[m] = table[idx[m]] (out-of-range: zeros + RK_FLAG_INDEX_OOB), xp[m] = x[m] + pos[m % T, :].
+ * Needs d % 4 == 0 and 16-B aligned rows (RK_ERR_UNSUPPORTED otherwise).                       */
+int rk_bst_gather_pos(const float* table, int64_t rows, int64_t ld_table, const int64_t* idx,
+                      int64_t n, int32_t T, int32_t d, const float* pos, float* x, float* xp,
+                      void* stream);
 int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_t d, int32_t heads,
                               const int64_t* seq_len, float* probs, float* ctx, void* stream);
 int rk_bst_attn_train_backward(const float* qkv, const float* probs, const float* dctx,
