@@ -46,6 +46,37 @@ __global__ __launch_bounds__(256) void din_att_cross_kernel(const float* __restr
   c[3 * H + h] = q * k;
 }
 
+// float4 form of din_att_cross_kernel (H % 4 == 0, 16-B aligned table rows / x row): a thread per
+// (b, t, 4 columns), 128-bit loads and stores.
+__global__ __launch_bounds__(256) void din_att_cross4_kernel(const float* __restrict__ x, int64_t ldx, int q_col,
+                                                             const float* __restrict__ table, int64_t rows,
+                                                             int64_t ld_tab, const int64_t* __restrict__ seq,
+                                                             int64_t ld_seq, int64_t B, int T, int H,
+                                                             float* __restrict__ keys, float* __restrict__ cross,
+                                                             uint32_t* flags) {
+  const int H4 = H / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T * H4) return;
+  const int h = 4 * (int)(i % H4);
+  const int64_t bt = i / H4;
+  const int64_t b = bt / T;
+  const int t = (int)(bt - b * T);
+  const int64_t r = seq[b * ld_seq + t];
+  f32x4 k = {0.f, 0.f, 0.f, 0.f};
+  if (r >= 0 && r < rows)
+    k = *reinterpret_cast<const f32x4*>(table + r * ld_tab + h);
+  else if (h == 0)
+    flag_oob(flags);
+  const float* qp = x + b * ldx + q_col + h;  // the feature row need not be 16-B aligned
+  const f32x4 q = {qp[0], qp[1], qp[2], qp[3]};
+  *reinterpret_cast<f32x4*>(keys + bt * H + h) = k;
+  float* c = cross + bt * 4 * H;
+  *reinterpret_cast<f32x4*>(c + h) = q;
+  *reinterpret_cast<f32x4*>(c + H + h) = k;
+  *reinterpret_cast<f32x4*>(c + 2 * H + h) = q - k;
+  *reinterpret_cast<f32x4*>(c + 3 * H + h) = q * k;
+}
+
 // One wave per sample: s_t = a2[b, t] . w3 + b3; weights (masked, or masked softmax with the
 // reference's -2^32 + 1 padding scaled by 1/sqrt(H)); out = sum_t w_t k_t written to
 // x[b, att_col : att_col + H].  Saves w (B, T).  T <= kDinMaxT, H <= 64.
@@ -68,10 +99,21 @@ __global__ __launch_bounds__(256) void din_att_pool_forward_kernel(const float* 
   const int64_t len = seq_len[b];
   const float bias3 = b3[0];
   float mx = -INFINITY;
+  const bool vec = (A2 & 3) == 0;  // a2 rows 16-B aligned: float4 row reads, 4x fewer load instructions
   for (int t = lane; t < T; t += 64) {
     const float* row = a2 + (b * T + t) * A2;
     float s = 0.f;
-    for (int j = 0; j < A2; ++j) s = fmaf(row[j], w3[j], s);
+    if (vec) {
+      for (int j = 0; j < A2; j += 4) {
+        const f32x4 r4 = *reinterpret_cast<const f32x4*>(row + j);
+        s = fmaf(r4[0], w3[j], s);
+        s = fmaf(r4[1], w3[j + 1], s);
+        s = fmaf(r4[2], w3[j + 2], s);
+        s = fmaf(r4[3], w3[j + 3], s);
+      }
+    } else {
+      for (int j = 0; j < A2; ++j) s = fmaf(row[j], w3[j], s);
+    }
     s += bias3;
     const bool m = t < len;
     float v;
@@ -131,9 +173,20 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
   const float* kb = keys + b * T * H;
   const float* wb = wts + b * T;
   float g = 0.f;
+  const bool vec = (H & 3) == 0;  // key rows 16-B aligned: float4 reads
   for (int t = lane; t < T; t += 64) {
     float dw = 0.f;
-    for (int h = 0; h < H; ++h) dw = fmaf(so[wv][h], kb[(int64_t)t * H + h], dw);
+    if (vec) {
+      for (int h = 0; h < H; h += 4) {
+        const f32x4 k4 = *reinterpret_cast<const f32x4*>(kb + (int64_t)t * H + h);
+        dw = fmaf(so[wv][h], k4[0], dw);
+        dw = fmaf(so[wv][h + 1], k4[1], dw);
+        dw = fmaf(so[wv][h + 2], k4[2], dw);
+        dw = fmaf(so[wv][h + 3], k4[3], dw);
+      }
+    } else {
+      for (int h = 0; h < H; ++h) dw = fmaf(so[wv][h], kb[(int64_t)t * H + h], dw);
+    }
     DS[t] = dw;
     g += wb[t] * dw;
   }
@@ -145,6 +198,26 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
   }
   __syncthreads();
   if (!live) return;
+  if (vec && (A2 & 3) == 0) {  // float4 stores of dkeys and da2 (rows 16-B aligned)
+    const int H4 = H / 4, A4 = A2 / 4;
+    for (int i = lane; i < T * H4; i += 64) {
+      const int t = i / H4, h = 4 * (i - t * H4);
+      const float wt = wb[t];
+      *reinterpret_cast<f32x4*>(dkeys + b * T * H + (int64_t)t * H + h) =
+          f32x4{wt * so[wv][h], wt * so[wv][h + 1], wt * so[wv][h + 2], wt * so[wv][h + 3]};
+    }
+    for (int i = lane; i < T * A4; i += 64) {
+      const int t = i / A4, j = 4 * (i - t * A4);
+      const int64_t o = (b * T + t) * A2 + j;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(a2 + o);
+      const float dt = DS[t];
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = a[e] > 0.f ? dt * w3[j + e] : 0.f;
+      *reinterpret_cast<f32x4*>(da2 + o) = r;
+    }
+    return;
+  }
   for (int64_t i = lane; i < (int64_t)T * H; i += 64) {
     const int t = (int)(i / H), h = (int)(i - (int64_t)t * H);
     dkeys[b * T * H + i] = wb[t] * so[wv][h];
@@ -153,6 +226,39 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
     const int t = (int)(i / A2), j = (int)(i - (int64_t)t * A2);
     const int64_t o = (b * T + t) * A2 + j;
     da2[o] = a2[o] > 0.f ? DS[t] * w3[j] : 0.f;
+  }
+}
+
+// Workgroup-per-sample form (H <= 64, 256 / H position groups): every (t, h) of the sample is a
+// thread's work (the dkeys update is elementwise), dq is summed per position group in registers
+// and across the groups in LDS in a fixed order.
+__global__ __launch_bounds__(256) void din_cross_fold_wg_kernel(const float* __restrict__ dcross,
+                                                                const float* __restrict__ x, int64_t ldx, int q_col,
+                                                                const float* __restrict__ keys, int64_t B, int T,
+                                                                int H, float* __restrict__ dkeys,
+                                                                float* __restrict__ dx, int64_t lddx) {
+  __shared__ float red[256];
+  const int64_t b = blockIdx.x;
+  const int G = 256 / H;  // position groups
+  const int h = threadIdx.x % H, tg = threadIdx.x / H;
+  float dq = 0.f;
+  if (tg < G) {
+    const float q = x[b * ldx + q_col + h];
+    for (int t = tg; t < T; t += G) {
+      const int64_t bt = b * T + t;
+      const float* dc = dcross + bt * 4 * H;
+      const float k = keys[bt * H + h];
+      const float d0 = dc[h], d1 = dc[H + h], d2 = dc[2 * H + h], d3 = dc[3 * H + h];
+      dq += d0 + d2 + d3 * k;
+      dkeys[bt * H + h] += d1 - d2 + d3 * q;
+    }
+  }
+  red[threadIdx.x] = dq;
+  __syncthreads();
+  if (threadIdx.x < H) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += red[g * H + threadIdx.x];
+    dx[b * lddx + q_col + threadIdx.x] += s;
   }
 }
 
@@ -211,6 +317,13 @@ RK_API int rk_din_att_cross(const float* x, int64_t ldx, int32_t q_col, const fl
     return fail(RK_ERR_INVALID, "rk_din_att_cross: bad arguments");
   const int64_t n = batch * T * H;
   if (n == 0) return RK_OK;
+  if (H % 4 == 0 && ld_key % 4 == 0 &&
+      ((reinterpret_cast<uintptr_t>(key_table) | reinterpret_cast<uintptr_t>(keys) |
+        reinterpret_cast<uintptr_t>(cross)) & 15) == 0) {
+    din_att_cross4_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        x, ldx, q_col, key_table, key_rows, ld_key, seq, ld_seq, batch, T, H, keys, cross, device_flags());
+    return check_launch("rk_din_att_cross");
+  }
   din_att_cross_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
       x, ldx, q_col, key_table, key_rows, ld_key, seq, ld_seq, batch, T, H, keys, cross, device_flags());
   return check_launch("rk_din_att_cross");
@@ -251,6 +364,11 @@ RK_API int rk_din_cross_fold(const float* dcross, const float* x, int64_t ldx, i
     return fail(RK_ERR_INVALID, "rk_din_cross_fold: bad arguments");
   const int64_t n = batch * H;
   if (n == 0) return RK_OK;
+  if (H <= 64) {
+    din_cross_fold_wg_kernel<<<(unsigned)batch, 256, 0, (hipStream_t)stream>>>(dcross, x, ldx, q_col, keys, batch, T,
+                                                                             H, dkeys, dx, lddx);
+    return check_launch("rk_din_cross_fold");
+  }
   din_cross_fold_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(dcross, x, ldx, q_col, keys,
                                                                                        batch, T, H, dkeys, dx, lddx);
   return check_launch("rk_din_cross_fold");
