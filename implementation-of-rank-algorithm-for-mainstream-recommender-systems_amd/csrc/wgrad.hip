@@ -72,6 +72,14 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(int64_t N, int64_t K,
   __shared__ float Bs[kWgR * kWgP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 3, wk = w >> 2;
+#ifdef RK_WGRAD_STAMP  // diagnostic build only (tools/wgrad_clock.cpp): per-workgroup clock stamps
+  uint64_t t0 = 0, r0s = 0;
+  if (tid == 0) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0s = __builtin_amdgcn_s_memrealtime();
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
   const int n0 = blockIdx.y * kWgT, k0 = blockIdx.z * kWgT;
   const int64_t rb = (int64_t)blockIdx.x * rps;
   const int64_t re = min<int64_t>(R, rb + rps);
@@ -140,6 +148,14 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(int64_t N, int64_t K,
       if (k + 32 < K) out[n * K + k + 32] = acc1[r];
     }
   }
+#ifdef RK_WGRAD_STAMP
+  if (tid == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    extern __device__ uint64_t g_wgrad_stamp[];
+    uint64_t* st = g_wgrad_stamp + 4 * (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    st[0] = t0; st[1] = t1; st[2] = r0s; st[3] = r1;
+  }
+#endif
   if (sums) {  // fold the 16 row groups holding the same four columns (threads t, t + 32, ...)
     __syncthreads();
     float* red = As;  // [16][128]
@@ -193,7 +209,8 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_kernel(const float* __restr
 
 static int64_t wgrad_splits(int64_t N, int64_t K, int64_t R) {
   const int64_t tiles = ((N + kWgT - 1) / kWgT) * ((K + kWgT - 1) / kWgT);
-  // one workgroup per CU and output tile (two per CU measured slower: the partial tiles double)
+  // one workgroup per CU and output tile.  Two per CU (4 waves / SIMD) measured no faster
+  // (tools/wgrad_clock.cpp: 40.7 us for half the rows vs 42.9 us), and the partial tiles double.
   const int64_t want = std::max<int64_t>(1, num_cus() / tiles);
   const int64_t steps = (R + kWgR - 1) / kWgR;
   return std::max<int64_t>(1, std::min<int64_t>(want, steps));
