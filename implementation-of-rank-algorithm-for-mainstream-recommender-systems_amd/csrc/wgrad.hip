@@ -8,11 +8,12 @@
 // atomics; here one 512-thread workgroup owns a whole 128 x 128 output tile for a slab of rows, so
 // dZ and X are each read once from HBM, and the slabs' partial tiles go to a workspace summed in a
 // fixed order by a second kernel (deterministic).
-//   * 64-row steps staged row-major in LDS ([64][132] per operand, float4 global loads, the next
-//     step's loads in flight during this step's MFMAs);
+//   * 64-row steps staged into a k-major (transposed) LDS image [128 cols][64 rows + 4] per operand:
+//     float4 global loads, a 4 x 4 register transpose, ds_write_b128; the next step's loads are in
+//     flight during this step's MFMAs;
 //   * wave w owns n rows 32 (w & 3) .. +32 and k columns 64 (w >> 2) .. +64: two
-//     v_mfma_f32_32x32x2_f32 tiles, operands read straight from the row-major LDS tiles
-//     (lane l takes reduction row 2j + (l >> 5));
+//     v_mfma_f32_32x32x2_f32 tiles; each lane reads 4 consecutive reduction rows of its column with
+//     one ds_read_b128 (3 reads per 8 MFMAs; the row-major image needed 8, and measured 51 us);
 //   * the bias sums come from the staged registers (each thread's four columns, all its rows) and
 //     are folded across the workgroup once at the end.
 #include "common.h"
@@ -21,43 +22,49 @@ namespace rk {
 
 constexpr int kWgT = 128;        // output tile edge (n and k)
 constexpr int kWgR = 64;         // rows per step
-constexpr int kWgP = kWgT + 4;   // LDS row pitch (floats)
+constexpr int kWgP = kWgR + 4;   // LDS pitch of the k-major image S[col][row] (floats)
 constexpr int kWgThreads = 512;
-constexpr int kWgLoads = kWgR * kWgT / 4 / kWgThreads;  // float4 loads per thread and operand (4)
+static_assert(kWgR * kWgT == 16 * kWgThreads, "one 4 x 4 staging block per thread and operand");
 
+// Staging: thread t owns the 4 x 4 block (rows 4 (t >> 5) .. +3 of the step, columns 4 (t & 31) .. +3)
+// of each operand: four float4 row loads (a wave covers two rows x 512 B per instruction), then a
+// register transpose and four ds_write_b128 into the k-major LDS image S[col][row] (pitch kWgP), so
+// the MFMA loop reads 4 consecutive reduction rows per lane with one ds_read_b128.
 // Raw loads only (out-of-range rows / columns read a clamped in-range address): the zeroing and
 // masking happen in wg_store, so nothing consumes the loaded registers until the next step's store
 // and the loads stay in flight across this step's MFMAs.
 template <bool MASK>
 __device__ __forceinline__ void wg_load(const float* __restrict__ P, int64_t ld, const float* __restrict__ mask,
-                                        int64_t r0, int64_t re, int c0, int cols, int tid, f32x4 (&v)[kWgLoads],
-                                        f32x4 (&m)[kWgLoads]) {
+                                        int64_t r0, int64_t re, int c0, int cols, int tid, f32x4 (&v)[4],
+                                        f32x4 (&m)[4]) {
   const int c = 4 * (tid & 31);
   const int cc = c0 + c < cols ? c0 + c : c0;
 #pragma unroll
-  for (int i = 0; i < kWgLoads; ++i) {
-    const int64_t r = min<int64_t>(r0 + (tid >> 5) + 16 * i, re - 1);
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = min<int64_t>(r0 + 4 * (tid >> 5) + i, re - 1);
     v[i] = *reinterpret_cast<const f32x4*>(P + r * ld + cc);
     if (MASK) m[i] = *reinterpret_cast<const f32x4*>(mask + r * ld + cc);
   }
 }
 
-// Store a staged step into LDS with rows >= re / columns >= cols zeroed and the mask applied;
-// adds the stored values to bsum when SUMS.
+// Store a staged step (rows >= re / columns >= cols zeroed, mask applied) transposed into the
+// k-major LDS image; adds the stored values to bsum (per column) when SUMS.
 template <bool MASK, bool SUMS>
-__device__ __forceinline__ void wg_store(float* __restrict__ S, int tid, const f32x4 (&v)[kWgLoads],
-                                         const f32x4 (&m)[kWgLoads], int64_t r0, int64_t re, int c0, int cols,
-                                         f32x4& bsum) {
+__device__ __forceinline__ void wg_store(float* __restrict__ S, int tid, const f32x4 (&v)[4], const f32x4 (&m)[4],
+                                         int64_t r0, int64_t re, int c0, int cols, f32x4& bsum) {
   const bool cok = c0 + 4 * (tid & 31) < cols;
+  f32x4 x[4];
 #pragma unroll
-  for (int i = 0; i < kWgLoads; ++i) {
-    const bool ok = cok && r0 + (tid >> 5) + 16 * i < re;
-    f32x4 x = v[i];
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = cok && r0 + 4 * (tid >> 5) + i < re;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] = (ok && (!MASK || m[i][e] > 0.f)) ? x[e] : 0.f;
-    if (SUMS) bsum += x;
-    *reinterpret_cast<f32x4*>(S + ((tid >> 5) + 16 * i) * kWgP + 4 * (tid & 31)) = x;
+    for (int e = 0; e < 4; ++e) x[i][e] = (ok && (!MASK || m[i][e] > 0.f)) ? v[i][e] : 0.f;
+    if (SUMS) bsum += x[i];
   }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    *reinterpret_cast<f32x4*>(S + (4 * (tid & 31) + e) * kWgP + 4 * (tid >> 5)) =
+        f32x4{x[0][e], x[1][e], x[2][e], x[3][e]};
 }
 
 // grid (splits, n tiles, k tiles); partial tile of split s -> ws[s][n][k] (N x K), bias partial ->
@@ -68,8 +75,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(int64_t N, int64_t K,
                                                            const float* __restrict__ A_mask,
                                                            const float* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ ws, float* __restrict__ wsb) {
-  __shared__ float As[kWgR * kWgP];
-  __shared__ float Bs[kWgR * kWgP];
+  __shared__ float As2[2][kWgT * kWgP];  // double-buffered k-major images (139 KB, one workgroup per CU)
+  __shared__ float Bs2[2][kWgT * kWgP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 3, wk = w >> 2;
 #ifdef RK_WGRAD_STAMP  // diagnostic build only (tools/wgrad_clock.cpp): per-workgroup clock stamps
@@ -88,51 +95,58 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(int64_t N, int64_t K,
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   const bool sums = wsb && blockIdx.z == 0;
-  f32x4 va[kWgLoads], vb[kWgLoads], ma[kWgLoads], mb[kWgLoads];
+  f32x4 va[4], vb[4], ma[4], mb[4];
+  // lane half h = lane >> 5 takes reduction rows 8g + 4h + e at MFMA e of row group g (the same rows
+  // for the A and B operands, so the k-permutation cancels in the sum)
+  const int a_off = (32 * wm + (lane & 31)) * kWgP + 4 * (lane >> 5);
+  const int b_off = (64 * wk + (lane & 31)) * kWgP + 4 * (lane >> 5);
+  // prologue: step 0 into buffer 0, step 1's loads in flight
   wg_load<MASK>(A, lda, A_mask, rb, re, n0, (int)N, tid, va, ma);
   wg_load<false>(B, ldb, nullptr, rb, re, k0, (int)K, tid, vb, mb);
-  const float* a_col = As + 32 * wm + (lane & 31) + (lane >> 5) * kWgP;
-  const float* b_col = Bs + 64 * wk + (lane & 31) + (lane >> 5) * kWgP;
-  for (int64_t r0 = rb; r0 < re; r0 += kWgR) {
-    if (sums)
-      wg_store<MASK, true>(As, tid, va, ma, r0, re, n0, (int)N, bsum);
-    else
-      wg_store<MASK, false>(As, tid, va, ma, r0, re, n0, (int)N, bsum);
-    wg_store<false, false>(Bs, tid, vb, mb, r0, re, k0, (int)K, bsum);
-    __syncthreads();
-    if (r0 + kWgR < re) {  // next step's rows in flight during this step's MFMAs
-      wg_load<MASK>(A, lda, A_mask, r0 + kWgR, re, n0, (int)N, tid, va, ma);
-      wg_load<false>(B, ldb, nullptr, r0 + kWgR, re, k0, (int)K, tid, vb, mb);
-    }
-    {
-      // operand registers double-buffered across the four 8-k-step groups: group g + 1's 24 LDS
-      // reads are issued before group g's 16 MFMAs, a whole group ahead of their use
-      float a[2][8], b0[2][8], b1[2][8];
+  if (sums)
+    wg_store<MASK, true>(As2[0], tid, va, ma, rb, re, n0, (int)N, bsum);
+  else
+    wg_store<MASK, false>(As2[0], tid, va, ma, rb, re, n0, (int)N, bsum);
+  wg_store<false, false>(Bs2[0], tid, vb, mb, rb, re, k0, (int)K, bsum);
+  if (rb + kWgR < re) {
+    wg_load<MASK>(A, lda, A_mask, rb + kWgR, re, n0, (int)N, tid, va, ma);
+    wg_load<false>(B, ldb, nullptr, rb + kWgR, re, k0, (int)K, tid, vb, mb);
+  }
+  __syncthreads();
+  int cb = 0;
+  // one barrier per step: step s computes from buffer s & 1 while step s + 1's rows (loaded during
+  // step s - 1) are written into the other buffer between the MFMA groups
+  for (int64_t r0 = rb; r0 < re; r0 += kWgR, cb ^= 1) {
+    const float* a_col = As2[cb] + a_off;
+    const float* b_col = Bs2[cb] + b_off;
+    const bool more = r0 + kWgR < re;
+    f32x4 a[2], b0[2], b1[2];
+    a[0] = *reinterpret_cast<const f32x4*>(a_col);
+    b0[0] = *reinterpret_cast<const f32x4*>(b_col);
+    b1[0] = *reinterpret_cast<const f32x4*>(b_col + 32 * kWgP);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        a[0][j] = a_col[2 * j * kWgP];
-        b0[0][j] = b_col[2 * j * kWgP];
-        b1[0][j] = b_col[2 * j * kWgP + 32];
+    for (int g = 0; g < kWgR / 8; ++g) {
+      const int cur = g & 1, nxt = cur ^ 1;
+      if (g + 1 < kWgR / 8) {
+        a[nxt] = *reinterpret_cast<const f32x4*>(a_col + 8 * (g + 1));
+        b0[nxt] = *reinterpret_cast<const f32x4*>(b_col + 8 * (g + 1));
+        b1[nxt] = *reinterpret_cast<const f32x4*>(b_col + 32 * kWgP + 8 * (g + 1));
       }
 #pragma unroll
-      for (int g = 0; g < kWgR / 16; ++g) {
-        const int cur = g & 1, nxt = cur ^ 1;
-        if (g + 1 < kWgR / 16) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int row = 2 * (8 * (g + 1) + j) * kWgP;
-            a[nxt][j] = a_col[row];
-            b0[nxt][j] = b_col[row];
-            b1[nxt][j] = b_col[row + 32];
-          }
+      for (int e = 0; e < 4; ++e) {
+        acc0 = mfma32(a[cur][e], b0[cur][e], acc0);
+        acc1 = mfma32(a[cur][e], b1[cur][e], acc1);
+      }
+      if (g == 1 && more) {  // the next step's rows have had a whole step to arrive
+        if (sums)
+          wg_store<MASK, true>(As2[cb ^ 1], tid, va, ma, r0 + kWgR, re, n0, (int)N, bsum);
+        else
+          wg_store<MASK, false>(As2[cb ^ 1], tid, va, ma, r0 + kWgR, re, n0, (int)N, bsum);
+        wg_store<false, false>(Bs2[cb ^ 1], tid, vb, mb, r0 + kWgR, re, k0, (int)K, bsum);
+        if (r0 + 2 * kWgR < re) {
+          wg_load<MASK>(A, lda, A_mask, r0 + 2 * kWgR, re, n0, (int)N, tid, va, ma);
+          wg_load<false>(B, ldb, nullptr, r0 + 2 * kWgR, re, k0, (int)K, tid, vb, mb);
         }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          acc0 = mfma32(a[cur][j], b0[cur][j], acc0);
-          acc1 = mfma32(a[cur][j], b1[cur][j], acc1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __syncthreads();
@@ -158,7 +172,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(int64_t N, int64_t K,
 #endif
   if (sums) {  // fold the 16 row groups holding the same four columns (threads t, t + 32, ...)
     __syncthreads();
-    float* red = As;  // [16][128]
+    float* red = As2[0];  // [16][128]
     *reinterpret_cast<f32x4*>(red + (tid >> 5) * kWgT + 4 * (tid & 31)) = bsum;
     __syncthreads();
     if (tid < kWgT && n0 + tid < N) {
