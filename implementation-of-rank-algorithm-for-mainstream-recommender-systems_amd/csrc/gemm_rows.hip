@@ -146,8 +146,27 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   RowsChunk<AM> ring[PD];
 #pragma unroll
   for (int j = 0; j < PD; ++j) ring[j] = rows_fetch<AM>(a, s, j, l32, hk);
+  // Epilogue operands in registers ahead of use: the bias (per column, the same for every slab)
+  // once, and for an accumulating product the slab's C values at the top of the slab, so their
+  // round trips overlap the MFMAs instead of sitting, one float4 at a time, behind them.
+  const bool cvec = a.c_vec && n0 + BN <= a.N;
+  f32x4 epi[NT][4];
+  if (EPI && cvec && a.ep.bias) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) epi[t][q] = *reinterpret_cast<const f32x4*>(a.ep.bias + n0 + 32 * t + 8 * q + hk);
+  }
   for (; s < nslabs; s += stride) {
     const int64_t sn = s + stride < nslabs ? s + stride : s;  // past the end: re-read (unused)
+    if (!EPI && cvec && a.accumulate) {
+      const int64_t mr = s * 32 + l32 < a.M ? s * 32 + l32 : a.M - 1;
+      const float* crow = a.C + mr * a.ldc + n0 + hk;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) epi[t][q] = *reinterpret_cast<const f32x4*>(crow + 32 * t + 8 * q);
+    }
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -183,7 +202,17 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
         for (int q = 0; q < 4; ++q) {
           const int n = n0 + 32 * t + 8 * q + hk;
           f32x4 z = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-          if (a.c_vec && n + 3 < a.N) {
+          if (cvec) {  // epilogue operands already in registers
+            f32x4* c = reinterpret_cast<f32x4*>(crow + n);
+            if (EPI) {
+              if (a.ep.bias) z += epi[t][q];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) z[e] = rows_act(a, z[e]);
+            } else if (a.accumulate) {
+              z += epi[t][q];
+            }
+            *c = z;
+          } else if (a.c_vec && n + 3 < a.N) {
             f32x4* c = reinterpret_cast<f32x4*>(crow + n);
             if (EPI) {
               if (a.ep.bias) z += *reinterpret_cast<const f32x4*>(a.ep.bias + n);
