@@ -696,7 +696,7 @@ __global__ __launch_bounds__(256) void bst_res_dropout_ln_fwd4_kernel(
 // its columns' dgamma = sum dy xhat and dbeta = sum dy in registers, the workgroup combines them
 // in LDS and writes one partial row per workgroup to ws [kLnBlocks][2d], summed in block order by
 // bst_ln_param_kernel (deterministic; per-row atomics on the same 2d addresses serialised).
-constexpr int kLnBlocks = 512;
+constexpr int kLnBlocks = 2048;  // 8 per CU: enough row groups in flight for the HBM stream
 constexpr int kLnRows = 4;  // rows in flight per wave
 
 __global__ __launch_bounds__(256) void bst_ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ r,
@@ -814,7 +814,8 @@ __global__ __launch_bounds__(256) void bst_ln_bwd4_kernel(const float* __restric
       if (on) {
         if (drow) {
           const int64_t b = mm / T;
-          dyv[i] = ld4(drow + b * ld_row + col + k);
+          const float* src = drow + b * ld_row + col + k;  // the DNN row: any alignment (col = 50 in BST)
+          dyv[i] = f32x4{src[0], src[1], src[2], src[3]};
           if (mean_pool) {
             const float inv = 1.0f / (float)seq_len[b];
 #pragma unroll
@@ -932,6 +933,55 @@ __global__ __launch_bounds__(256) void bst_leaky_dropout_kernel(const float* __r
     out[i] = keep ? (fv > 0.f ? fv : fv * slope) * s : 0.f;
 }
 
+// float4 form (n % 4 == 0, 16-B aligned): four elements per thread, same per-element hash index.
+template <bool BWD>
+__global__ __launch_bounds__(256) void bst_leaky_dropout4_kernel(const float* __restrict__ in,
+                                                                 const float* __restrict__ f, int64_t n, float slope,
+                                                                 uint64_t seed, const int64_t* __restrict__ stream_slot,
+                                                                 uint32_t threshold, float scale,
+                                                                 float* __restrict__ out) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * i4 >= n) return;
+  const uint64_t stream = threshold ? (uint64_t)*stream_slot : 0;
+  const float s = threshold ? scale : 1.f;
+  const f32x4 fv = *reinterpret_cast<const f32x4*>(f + 4 * i4);
+  f32x4 iv = {0.f, 0.f, 0.f, 0.f};
+  if (BWD) iv = *reinterpret_cast<const f32x4*>(in + 4 * i4);
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bool keep = threshold ? dropout_keep(seed, stream, (uint64_t)(4 * i4 + e), threshold) : true;
+    if (BWD)
+      o[e] = keep ? iv[e] * s * (fv[e] > 0.f ? 1.f : slope) : 0.f;
+    else
+      o[e] = keep ? (fv[e] > 0.f ? fv[e] : fv[e] * slope) * s : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(out + 4 * i4) = o;
+}
+
+// Pooling, float4 form (d % 4 == 0): workgroup per sample, thread = (4 columns, row group of 256 /
+// (d / 4)); row-group partial sums folded in LDS in a fixed order.
+__global__ __launch_bounds__(256) void bst_pool_fwd4_kernel(const float* __restrict__ out, int T, int d,
+                                                            const int64_t* __restrict__ seq_len, int mean,
+                                                            float* __restrict__ row, int64_t ld_row, int col) {
+  __shared__ f32x4 red[256];
+  const int64_t b = blockIdx.x;
+  const int q = d / 4, G = 256 / q;
+  const int c = threadIdx.x % q, g = threadIdx.x / q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (g < G)
+    for (int t = g; t < T; t += G) acc += *reinterpret_cast<const f32x4*>(out + (b * T + t) * d + 4 * c);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < q) {
+    f32x4 sum = red[threadIdx.x];
+    for (int k = 1; k < G; ++k) sum += red[k * q + threadIdx.x];
+    float* dst = row + b * ld_row + col + 4 * threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[e] = mean ? sum[e] / (float)seq_len[b] : sum[e];
+  }
+}
+
 // Pooling over all T rows of a sample (bst.py:238-241): sum, or sum / len (mean).
 __global__ __launch_bounds__(256) void bst_pool_fwd_kernel(const float* __restrict__ out, int64_t B, int T, int d,
                                                            const int64_t* __restrict__ seq_len, int mean,
@@ -1009,7 +1059,7 @@ static int ln_backward(const float* dy, const float* drow, int64_t ld_row, int c
                        float* d_o, float* dgamma, float* dbeta, float* workspace, hipStream_t st, const char* what) {
   const uint32_t thr = dropout_threshold(dropout_p);
   const float scale = (float)(1.0 / (1.0 - dropout_p));
-  const int L = ln_lanes(d, {dy, drow ? drow + col : nullptr, r, gamma, dr, d_o, workspace});
+  const int L = ln_lanes(d, {dy, r, gamma, dr, d_o, workspace});
   int blocks;
   if (L) {
     const int64_t groups = (rows + 64 / L - 1) / (64 / L);
@@ -1169,7 +1219,7 @@ RK_API int rk_bst_pool_ln_backward(const float* drow, int64_t ld_row, int32_t co
   if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
     return fail(RK_ERR_INVALID, "rk_bst_pool_ln_backward: workspace of %lld floats, needs %lld",
                 (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d));
-  if (ln_lanes(d, {drow + col, r, gamma, dr, d_o}) == 0 || ld_row % 4)
+  if (ln_lanes(d, {r, gamma, dr, d_o}) == 0)
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_pool_ln_backward: needs d %% 4 == 0, 16-B aligned rows");
   return ln_backward(nullptr, drow, ld_row, col, T, seq_len, mean_pool, r, mean, rstd, gamma, rows, d, dropout_p, seed,
                      stream_slot, dr, d_o, dgamma, dbeta, workspace, (hipStream_t)stream, "rk_bst_pool_ln_backward");
@@ -1193,6 +1243,16 @@ RK_API int rk_bst_leaky_dropout(const float* in, const float* f, int64_t n, floa
   const uint32_t thr = dropout_threshold(dropout_p);
   const float scale = (float)(1.0 / (1.0 - dropout_p));
   hipStream_t st = (hipStream_t)stream;
+  if (n % 4 == 0 && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(f) |
+                       reinterpret_cast<uintptr_t>(out)) & 15) == 0) {
+    if (backward)
+      bst_leaky_dropout4_kernel<true><<<grid_of(n / 4), 256, 0, st>>>(in, f, n, slope, seed, stream_slot, thr, scale,
+                                                                      out);
+    else
+      bst_leaky_dropout4_kernel<false><<<grid_of(n / 4), 256, 0, st>>>(in, f, n, slope, seed, stream_slot, thr,
+                                                                       scale, out);
+    return check_launch("rk_bst_leaky_dropout");
+  }
   if (backward)
     bst_leaky_dropout_kernel<true><<<grid_of(n), 256, 0, st>>>(in, f, n, slope, seed, stream_slot, thr, scale, out);
   else
@@ -1205,6 +1265,10 @@ RK_API int rk_bst_pool(const float* out, int64_t batch, int32_t T, int32_t d, co
   if (!out || !seq_len || !row || batch < 0 || T <= 0 || d <= 0 || col < 0 || col + d > ld_row)
     return fail(RK_ERR_INVALID, "rk_bst_pool: bad arguments");
   if (batch == 0) return RK_OK;
+  if (d % 4 == 0 && d <= 1024 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    bst_pool_fwd4_kernel<<<(unsigned)batch, 256, 0, (hipStream_t)stream>>>(out, T, d, seq_len, mean, row, ld_row, col);
+    return check_launch("rk_bst_pool");
+  }
   bst_pool_fwd_kernel<<<grid_of(batch * d), 256, 0, (hipStream_t)stream>>>(out, batch, T, d, seq_len, mean, row,
                                                                           ld_row, col);
   return check_launch("rk_bst_pool");

@@ -726,8 +726,7 @@ def bst_pool_ln_backward(drow, col, T, seq_len, mean_pool, r, mean, rstd, ln, p,
     (rk_bst_pool_ln_backward); returns False (nothing launched) when the layout does not allow it."""
     lib = _lib.load()
     d = r.shape[1]
-    if d % 4 or drow.stride(0) % 4 or col % 4 or any(t is not None and t.data_ptr() % 16
-                                                     for t in (drow, r, ln.weight, dr, d_o)):
+    if d % 4 or any(t is not None and t.data_ptr() % 16 for t in (r, ln.weight, dr, d_o)):
         return False
     nws = lib.rk_bst_ln_backward_workspace_floats(d)
     ws = torch.empty(nws, device=r.device, dtype=torch.float32)

@@ -588,8 +588,9 @@ int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const
                        float* workspace, int64_t workspace_floats, void* stream);
 /* rk_bst_ln_backward of the last block fused with the pooling backward (bst.py:238-241): the
  * incoming gradient of row m is drow[m / T, col:col+d] (/ seq_len[m / T] when mean_pool), so the
- * [rows, d] broadcast is never written.  rows = batch * T; needs d % 4 == 0 and 16-B aligned rows
- * (RK_ERR_UNSUPPORTED otherwise: use rk_bst_pool_backward + rk_bst_ln_backward).               */
+ * [rows, d] broadcast is never written.  rows = batch * T; needs d % 4 == 0 and 16-B aligned r /
+ * dr / d_o rows (drow any alignment; RK_ERR_UNSUPPORTED otherwise: use rk_bst_pool_backward +
+ * rk_bst_ln_backward).                                                                         */
 int rk_bst_pool_ln_backward(const float* drow, int64_t ld_row, int32_t col, int32_t T,
                             const int64_t* seq_len, int32_t mean_pool, const float* r,
                             const float* mean, const float* rstd, const float* gamma, int64_t rows,
