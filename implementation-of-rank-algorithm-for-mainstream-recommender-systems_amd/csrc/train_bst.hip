@@ -878,6 +878,28 @@ __global__ __launch_bounds__(256) void bst_ln_bwd4_kernel(const float* __restric
   }
 }
 
+// First pass over the per-workgroup partials: workgroup (x, y) sums partial rows y*C .. y*C + C - 1
+// of columns 64x .. 64x + 63 (16 waves, every 16th row each, LDS combine in a fixed order) into
+// out[y][2d]; bst_ln_param_kernel then folds the gridDim.y rows.
+constexpr int kLnChunk = 64;
+__global__ __launch_bounds__(1024) void bst_ln_partial_kernel(const float* __restrict__ ws, int nblocks, int d,
+                                                              float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * kLnChunk, r1 = min(nblocks, r0 + kLnChunk);
+  float s = 0.f;
+  if (k < 2 * d)
+    for (int r = r0 + wv; r < r1; r += 16) s += ws[(int64_t)r * 2 * d + k];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && k < 2 * d) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    out[(int64_t)blockIdx.y * 2 * d + k] = t;
+  }
+}
+
 // 16 waves per workgroup, each summing every 16th block partial of 64 columns; LDS combine.
 __global__ __launch_bounds__(1024) void bst_ln_param_kernel(const float* __restrict__ ws, int nblocks, int d,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
@@ -1077,7 +1099,11 @@ static int ln_backward(const float* dy, const float* drow, int64_t ld_row, int c
     bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot, thr, scale, dr,
                                               d_o, workspace);
   }
-  bst_ln_param_kernel<<<grid_of(2 * d, 64), 1024, 0, st>>>(workspace, blocks, d, dgamma, dbeta);
+  // two deterministic passes: chunks of kLnChunk partial rows, then the chunk sums
+  const int chunks = (blocks + kLnChunk - 1) / kLnChunk;
+  float* ws2 = workspace + (int64_t)kLnBlocks * 2 * d;
+  bst_ln_partial_kernel<<<dim3(grid_of(2 * d, 64), chunks), 1024, 0, st>>>(workspace, blocks, d, ws2);
+  bst_ln_param_kernel<<<grid_of(2 * d, 64), 1024, 0, st>>>(ws2, chunks, d, dgamma, dbeta);
   return check_launch(what);
 }
 
@@ -1191,7 +1217,10 @@ RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int6
   return check_launch("rk_bst_res_dropout_ln_forward");
 }
 
-RK_API int64_t rk_bst_ln_backward_workspace_floats(int32_t d) { return (int64_t)kLnBlocks * 2 * (d > 0 ? d : 0); }
+RK_API int64_t rk_bst_ln_backward_workspace_floats(int32_t d) {
+  // per-workgroup partials, then the chunk sums of the first reduction pass
+  return ((int64_t)kLnBlocks + (kLnBlocks + kLnChunk - 1) / kLnChunk) * 2 * (d > 0 ? d : 0);
+}
 
 RK_API int rk_bst_ln_backward(const float* dy, const float* r, const float* mean, const float* rstd,
                               const float* gamma, int64_t rows, int32_t d, double dropout_p, uint64_t seed,
@@ -1201,8 +1230,8 @@ RK_API int rk_bst_ln_backward(const float* dy, const float* r, const float* mean
       d > 256 || !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
     return fail(RK_ERR_INVALID, "rk_bst_ln_backward: bad arguments (d <= 256)");
   if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
-    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: workspace of %lld floats, needs %lld (%d * 2d)",
-                (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d), kLnBlocks);
+    return fail(RK_ERR_INVALID, "rk_bst_ln_backward: workspace of %lld floats, needs %lld",
+                (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d));
   return ln_backward(dy, nullptr, 0, 0, 1, nullptr, 0, r, mean, rstd, gamma, rows, d, dropout_p, seed, stream_slot,
                      dr, d_o, dgamma, dbeta, workspace, (hipStream_t)stream, "rk_bst_ln_backward");
 }
