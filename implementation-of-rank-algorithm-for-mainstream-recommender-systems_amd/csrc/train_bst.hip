@@ -1042,11 +1042,13 @@ static int att_slots(int T, int dh) {
   return n <= 256 ? 1 : n <= 512 ? 2 : 4;
 }
 
-// Persistent grid: as many workgroups as fit on the GPU at this LDS size (at most 8 per CU), or
-// one per item when there are fewer items.
-static unsigned att_grid(int64_t items, size_t lds) {
-  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)(160 * 1024) / (int64_t)std::max<size_t>(lds, 1)));
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, per_cu * num_cus()));
+// Persistent grid: as many workgroups as are resident at once (the runtime's occupancy for this
+// kernel, LDS and registers both), or one per item when there are fewer items.
+static unsigned att_grid(const void* kernel, int64_t items, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0)
+    per_cu = std::max<int>(1, (int)((160 * 1024) / std::max<size_t>(lds, 1)));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, (int64_t)per_cu * num_cus()));
 }
 
 // Dynamic LDS above the 64 KiB default: up to 104 KiB (T = 64, dh = 64 backward).
@@ -1144,10 +1146,10 @@ RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T,
   const int US = att_slots(T, dh);
   if (US && T % 4 == 0 && d % 4 == 0) {
     const size_t lds = att_lds_bytes(T, dh, false);
-    const unsigned grid = att_grid(batch * heads, lds);
 #define RK_ATT_FWD(U_)                                                                                          \
   case U_:                                                                                                      \
-    bst_attn_train_fwd_pkernel<U_><<<grid, 256, lds, (hipStream_t)stream>>>(qkv, batch, T, d, heads, seq_len,   \
+    bst_attn_train_fwd_pkernel<U_><<<att_grid((const void*)bst_attn_train_fwd_pkernel<U_>, batch * heads, lds), \
+                                     256, lds, (hipStream_t)stream>>>(qkv, batch, T, d, heads, seq_len,   \
                                                                             probs, ctx);                        \
     break;
     switch (US) { RK_ATT_FWD(1) RK_ATT_FWD(2) RK_ATT_FWD(4) }
@@ -1171,10 +1173,10 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
   const int US = att_slots(T, dh);
   if (US && T % 4 == 0 && d % 4 == 0) {
     const size_t lds = att_lds_bytes(T, dh, true);
-    const unsigned grid = att_grid(batch * heads, lds);
 #define RK_ATT_BWD(U_)                                                                                          \
   case U_:                                                                                                      \
-    bst_attn_train_bwd_pkernel<U_><<<grid, 256, lds, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T, d, heads, \
+    bst_attn_train_bwd_pkernel<U_><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_>, batch * heads, lds), \
+                                     256, lds, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T, d, heads, \
                                                                             dqkv);                              \
     break;
     switch (US) { RK_ATT_BWD(1) RK_ATT_BWD(2) RK_ATT_BWD(4) }

@@ -53,6 +53,78 @@ __global__ __launch_bounds__(256) void emb_sorted_reduce_kernel(const uint32_t* 
   }
 }
 
+// Behaviour-sequence form without the sort (B x T index matrix, dim even and <= 128): one wave per
+// sample walks its T positions in order (lane = 2 columns), summing each run of equal consecutive
+// ids and flushing one atomic per column per run.  A padded tail (the same id repeated to T, the
+// hot row of the sorted path) is the sample's last run: the kSeqWaves samples of a workgroup merge
+// equal tail ids in LDS first, so a padding row costs one atomic per column per 16 samples.
+constexpr int kSeqWaves = 16;
+__global__ __launch_bounds__(64 * kSeqWaves) void emb_seq_runs_kernel(const int64_t* __restrict__ idx, int64_t ld_idx, int64_t B,
+                                                           int T, int64_t rows, const float* __restrict__ dx,
+                                                           int64_t ld_dx, int out_col, int dim,
+                                                           float* __restrict__ grad, int64_t ld_grad,
+                                                           uint32_t* flags) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  __shared__ f32x2 tail[kSeqWaves][64];
+  __shared__ int64_t tail_key[kSeqWaves];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kSeqWaves + w;
+  const int c = 2 * lane;
+  const bool on = c < dim;
+  int64_t key = -1;
+  f32x2 acc = {0.f, 0.f};
+  if (b < B) {
+    const int64_t* ids = idx + b * ld_idx;
+    const float* rowp = dx + b * T * ld_dx + out_col + c;
+    key = ids[0];
+    for (int t0 = 0; t0 < T; t0 += 8) {
+      int64_t id[9];
+      f32x2 v[8];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) id[j] = t0 + j < T ? ids[t0 + j] : -2;  // -2: past the end
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (on && t0 + j < T) ? *reinterpret_cast<const f32x2*>(rowp + (int64_t)(t0 + j) * ld_dx)
+                                  : f32x2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (t0 + j >= T) break;
+        acc += v[j];
+        if (id[j + 1] != id[j] && id[j + 1] != -2) {  // a run ends before the sample's last position
+          const int64_t r = id[j];
+          if (r >= 0 && r < rows) {
+            if (on) {
+              float* g = grad + r * ld_grad + c;
+              if (acc[0] != 0.f) atomicAdd(g, acc[0]);
+              if (acc[1] != 0.f) atomicAdd(g + 1, acc[1]);
+            }
+          } else if (lane == 0) {
+            flag_oob(flags);
+          }
+          acc = f32x2{0.f, 0.f};
+          key = id[j + 1];
+        }
+      }
+    }
+    if (!(key >= 0 && key < rows)) {
+      if (lane == 0) flag_oob(flags);
+      key = -1;
+    }
+  }
+  tail[w][lane] = acc;
+  if (lane == 0) tail_key[w] = key;
+  __syncthreads();
+  if (key < 0 || !on) return;
+  for (int u = 0; u < w; ++u)
+    if (tail_key[u] == key) return;  // merged by the first wave holding this tail id
+  f32x2 sum = acc;
+  for (int u = w + 1; u < kSeqWaves; ++u)
+    if (tail_key[u] == key) sum += tail[u][lane];
+  float* g = grad + key * ld_grad + c;
+  if (sum[0] != 0.f) atomicAdd(g, sum[0]);
+  if (sum[1] != 0.f) atomicAdd(g + 1, sum[1]);
+}
+
 struct SortPlan {
   size_t sort_bytes = 0, total = 0;
   size_t off_k0 = 0, off_k1 = 0, off_p0 = 0, off_p1 = 0, off_tmp = 0;
@@ -114,4 +186,19 @@ RK_API int rk_embedding_backward_sorted(const rk_segment* grad, int64_t n, const
       k1, p1, n, dx, ld_dx, grad->out_col, grad->dim, (uint32_t)grad->rows, const_cast<float*>(grad->src),
       grad->src_ld);
   return check_launch("rk_embedding_backward_sorted");
+}
+
+RK_API int rk_embedding_backward_seq(const rk_segment* grad, int64_t batch, int32_t T, const float* dx, int64_t ld_dx,
+                                     void* stream) {
+  if (!grad || !grad->src || !grad->idx || grad->dim <= 0 || grad->rows <= 0 || grad->out_col < 0 ||
+      grad->out_col + grad->dim > ld_dx || !dx || batch < 0 || T <= 0 || grad->idx_stride < T)
+    return fail(RK_ERR_INVALID, "rk_embedding_backward_seq: bad arguments");
+  if (grad->dim % 2 || grad->dim > 128 || grad->out_col % 2 || ld_dx % 2 || grad->src_ld % 2 ||
+      ((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(grad->src)) & 7))
+    return fail(RK_ERR_UNSUPPORTED, "rk_embedding_backward_seq: needs an even dim <= 128 and 8-B aligned rows");
+  if (batch == 0) return RK_OK;
+  emb_seq_runs_kernel<<<(unsigned)((batch + kSeqWaves - 1) / kSeqWaves), 64 * kSeqWaves, 0, (hipStream_t)stream>>>(
+      grad->idx, grad->idx_stride, batch, T, grad->rows, dx, ld_dx, grad->out_col, grad->dim,
+      const_cast<float*>(grad->src), grad->src_ld, device_flags());
+  return check_launch("rk_embedding_backward_seq");
 }

@@ -494,6 +494,21 @@ def embedding_backward(grad_segs, batch, dx):
                                     _lib.stream_of(dx)), "rk_embedding_backward")
 
 
+def embedding_backward_seq(grad, seq, dx):
+    """rk_embedding_backward_seq: grad[seq[b, t]] += dx[b*T + t] with runs of equal consecutive ids
+    pre-summed (no sort); False (nothing launched) when the layout does not allow it."""
+    B, T = seq.shape
+    d = grad.shape[1]
+    if (d % 2 or d > 128 or dx.stride(0) % 2 or grad.stride(0) % 2 or seq.stride(1) != 1
+            or dx.data_ptr() % 8 or grad.data_ptr() % 8):
+        return False
+    lib = _lib.load()
+    seg = table_segment(grad, seq, 0, idx_stride=seq.stride(0))
+    check(lib.rk_embedding_backward_seq(ctypes.byref(seg), B, T, ptr(dx), dx.stride(0), _lib.stream_of(dx)),
+          "rk_embedding_backward_seq")
+    return True
+
+
 def embedding_backward_sorted(grad_seg, n, dx):
     """rk_embedding_backward_sorted: one table segment over n index entries (sorted segment-reduce)."""
     lib = _lib.load()

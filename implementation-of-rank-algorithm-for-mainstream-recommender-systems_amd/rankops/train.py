@@ -882,8 +882,10 @@ class _BSTTrain(torch.autograd.Function):
         segs = [ops.table_segment(tgrads[k], idx, c) for k, idx, c in looks]
         if segs:
             ops.embedding_backward(segs, B, d_row)
-        # padded positions all map to row 0 and carry non-zero gradients: sorted segment-reduce
-        ops.embedding_backward_sorted(ops.table_segment(tgrads[plan["feed_slot"]], seq.view(-1), 0), M, dx)
+        # padded positions all map to row 0 and carry non-zero gradients (sum pooling): their runs are
+        # pre-summed per sample (rk_embedding_backward_seq), else the sorted segment-reduce
+        if not ops.embedding_backward_seq(tgrads[plan["feed_slot"]], seq, dx):
+            ops.embedding_backward_sorted(ops.table_segment(tgrads[plan["feed_slot"]], seq.view(-1), 0), M, dx)
         flat_units = [t for g in unit_grads for t in g if t is not None]
         return (None, None, *tgrads, *[t for g in block_grads for t in g], *flat_units, dw_last, db_last)
 

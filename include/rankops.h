@@ -41,6 +41,7 @@
  *   rk_dcn_cross_backward   cross_layer backward w.r.t. x0        dcn.py:46-49
  *   rk_relu_backward   ReLU backward (residual_unit's outer ReLU) deepcrossing.py:41
  *   rk_embedding_backward   nn.Embedding dense weight gradient    dcn.py:131-138,163-166
+ *   rk_embedding_backward_seq  the same for a [batch, T] behaviour sequence (runs pre-summed)
  *   rk_embedding_backward_sorted  the same for long, skewed index lists (behaviour sequences)
  *                      as a sorted segment-reduce                din.py:300-303, bst.py:224
  *   rk_adam_step       torch.optim.Adam step (all tensors, one launch)  dcn.py:275
@@ -402,6 +403,13 @@ int rk_logit_head_backward(const float* dlogit, const float* dprob, const float*
                            int32_t kb, const float* w, float* dxa, int64_t ld_dxa, float* dxb,
                            int64_t ld_dxb, float* dw, float* db, float* g_out, void* stream);
 
+/* nn.Embedding gradient of a behaviour sequence without sorting (bst.py:224): grad[idx[b*stride + t]]
+ * += dx[b*T + t, out_col : out_col + dim] for b < batch, t < T (grad->idx_stride = the row stride
+ * of the [batch, T] index matrix).  Runs of equal consecutive ids in a sample (a padded tail) are
+ * summed before their atomics.  Needs an even dim <= 128 and 8-B aligned rows
+ * (RK_ERR_UNSUPPORTED otherwise: use rk_embedding_backward_sorted).                            */
+int rk_embedding_backward_seq(const rk_segment* grad, int64_t batch, int32_t T, const float* dx,
+                              int64_t ld_dx, void* stream);
 /* Sorted segment-reduce form of rk_embedding_backward for ONE table segment and a long index list
  * with hot rows (padded behaviour sequences): grad[idx[i]] += dx[i, out_col:+dim] for i < n, via a
  * radix sort of the indices and one atomic per (distinct row in a 64-position chunk, column).

@@ -989,3 +989,25 @@ def test_gemm_wgrad_strided_views_match_fp64(N, K, R, col):
     tol = 2e-4 * max(1.0, float(want.abs().max()))
     torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
     torch.testing.assert_close(sums.cpu().double(), rs, rtol=0, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,d", [(37, 64, 128), (5, 9, 6), (130, 50, 32)])
+def test_embedding_backward_seq_matches_index_add(B, T, d):
+    """rk_embedding_backward_seq (BST's sequence gradient without the sort): runs of equal
+    consecutive ids inside a sample, padded tails of one id shared by neighbouring samples, and a
+    whole sample of one id, against torch.index_add_ in float64."""
+    g = torch.Generator().manual_seed(B * T + d)
+    V = 40
+    seq = torch.randint(0, V, (B, T), generator=g)
+    for b in range(B):
+        n = int(torch.randint(1, T + 1, (1,), generator=g))
+        seq[b, n:] = 0  # padded tail
+        if b % 3 == 1 and T > 4:
+            seq[b, 1:4] = seq[b, 1]  # a run in the middle
+    seq[0, :] = 7  # one id for the whole sample
+    dx = torch.randn(B * T, d, generator=g)
+    want = torch.zeros(V, d, dtype=torch.float64).index_add_(0, seq.reshape(-1), dx.double())
+    grad = torch.zeros(V, d, device="cuda")
+    assert ops.embedding_backward_seq(grad, seq.cuda(), dx.cuda())
+    torch.testing.assert_close(grad.cpu().double(), want, rtol=0, atol=1e-4 * max(1.0, float(want.abs().max())))
