@@ -403,6 +403,49 @@ __device__ __forceinline__ void att_store_regs(float* const (&dst)[NT], const f3
     }
 }
 
+// Row softmax of the strip of wave w (bst.py:77-84): s[jt][r] = P[i = 16w + li][j = 16jt + kq + r],
+// from the staged Q and K tiles; the same code for the forward (which may save P) and for the
+// backward that recomputes P instead of reading it (bit-identical values).
+__device__ __forceinline__ void att_softmax_strip(f32x4 (&s)[4], const float* __restrict__ sK,
+                                                  const float* __restrict__ sQ, int ldt, int w, int NS, int ND,
+                                                  int lane, int T, int64_t len, float sq) {
+  const int kq = 4 * (lane >> 4);
+  att_rowdot(s, sK, sQ, ldt, w, NS, ND, lane);  // s[jt][r] = S[i = 16w + li][j = 16jt + kq + r]
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      const float x = (jt < NS && j < T) ? ((int64_t)j < len ? s[jt][r] / sq : -INFINITY) : -INFINITY;
+      s[jt][r] = x;  // masked_fill(key_padding_mask, -inf), bst.py:80
+      mx = fmaxf(mx, x);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  float sum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      const float e = (jt < NS && j < T) ? expf(s[jt][r] - mx) : 0.f;
+      s[jt][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 16, kWave);
+  sum += __shfl_xor(sum, 32, kWave);
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    if (jt >= NS) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + kq + r;
+      s[jt][r] = j < T ? s[jt][r] / sum : 0.f;
+    }
+  }
+}
+
 template <int US>
 __global__ __launch_bounds__(256, 2) void bst_attn_train_fwd_pkernel(const float* __restrict__ qkv, int64_t B, int T,
                                                                   int d, int heads,
@@ -444,44 +487,14 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_fwd_pkernel(const float
       att_load_regs<3, US>(v, src3, lds3, c0, nb * T, T, dh, TP, DP);
     }
     if (w < NS) {
-      const int64_t len = seq_len[b];
       f32x4 s[4];
-      att_rowdot(s, sK, sQ, ldt, w, NS, ND, lane);  // s[jt][r] = S[i = 16w + li][j = 16jt + kq + r]
-      float mx = -INFINITY;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 16 * jt + kq + r;
-          const float x = (jt < NS && j < T) ? ((int64_t)j < len ? s[jt][r] / sq : -INFINITY) : -INFINITY;
-          s[jt][r] = x;  // masked_fill(key_padding_mask, -inf), bst.py:80
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-      float sum = 0.f;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 16 * jt + kq + r;
-          const float e = (jt < NS && j < T) ? expf(s[jt][r] - mx) : 0.f;
-          s[jt][r] = e;
-          sum += e;
-        }
-      sum += __shfl_xor(sum, 16, kWave);
-      sum += __shfl_xor(sum, 32, kWave);
+      att_softmax_strip(s, sK, sQ, ldt, w, NS, ND, lane, T, seq_len[b], sq);
       const int i = 16 * w + li;
-      float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
+      if (P && i < T) {  // P == NULL: the backward recomputes it
+        float* Pi = P + ((b * heads + h) * (int64_t)T + i) * T;
 #pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
-        if (jt >= NS) break;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 16 * jt + kq + r;
-          s[jt][r] = j < T ? s[jt][r] / sum : 0.f;
-        }
-        if (i < T && 16 * jt + kq < T) *reinterpret_cast<f32x4*>(Pi + 16 * jt + kq) = s[jt];
+        for (int jt = 0; jt < 4; ++jt)
+          if (jt < NS && 16 * jt + kq < T) *reinterpret_cast<f32x4*>(Pi + 16 * jt + kq) = s[jt];
       }
       f32x4 c[4];
       att_regmm(c, s, sV, ldt, NS, ND, lane);
@@ -491,8 +504,9 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_fwd_pkernel(const float
   }
 }
 
-template <int US>
+template <int US, bool RECOMP>
 __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float* __restrict__ qkv,
+                                                                  const int64_t* __restrict__ seq_len,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ dctx, int64_t B, int T,
                                                                   int d, int heads, float* __restrict__ dqkv) {
@@ -524,6 +538,7 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float
     att_load_regs<4, US>(v, src4, lds4, c0, b * T, T, dh, TP, DP);
   };
   auto load_p = [&](int64_t x) {
+    if (RECOMP) return;  // recomputed from the staged Q and K instead
     const float* Pi = P + (x * (int64_t)T + (prow ? i : 0)) * T;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
@@ -544,6 +559,7 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float
     __syncthreads();
     if (more) load_tiles(it + gridDim.x);
     if (w < NS) {
+      if (RECOMP) att_softmax_strip(pc, sK, sQ, ldt, w, NS, ND, lane, T, seq_len[b], sq);
       f32x4 g[4];
       att_rowdot(g, sV, sC, ldt, w, NS, ND, lane);  // g[jt][r] = dP[i = 16w + li][j = 16jt + kq + r]
       float D = 0.f;
@@ -1056,8 +1072,10 @@ static void att_set_attrs() {
   static bool done = false;
   if (done) return;
   for (const void* f : {(const void*)bst_attn_train_fwd_pkernel<1>, (const void*)bst_attn_train_fwd_pkernel<2>,
-                        (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1>,
-                        (const void*)bst_attn_train_bwd_pkernel<2>, (const void*)bst_attn_train_bwd_pkernel<4>})
+                        (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1, false>,
+                        (const void*)bst_attn_train_bwd_pkernel<2, false>, (const void*)bst_attn_train_bwd_pkernel<4, false>,
+                        (const void*)bst_attn_train_bwd_pkernel<1, true>, (const void*)bst_attn_train_bwd_pkernel<2, true>,
+                        (const void*)bst_attn_train_bwd_pkernel<4, true>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)bst_attn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
@@ -1136,7 +1154,7 @@ RK_API int rk_bst_gather_pos(const float* table, int64_t rows, int64_t ld_table,
 
 RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_t d, int32_t heads,
                                      const int64_t* seq_len, float* probs, float* ctx, void* stream) {
-  if (!qkv || !seq_len || !probs || !ctx || batch < 0 || T <= 0 || T > kBstTMax || heads <= 0 || d % heads ||
+  if (!qkv || !seq_len || !ctx || batch < 0 || T <= 0 || T > kBstTMax || heads <= 0 || d % heads ||
       d / heads > kBstDhMax)
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_forward: T <= %d, d %% heads == 0, d/heads <= %d", kBstTMax,
                 kBstDhMax);
@@ -1144,6 +1162,8 @@ RK_API int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T,
   att_set_attrs();
   const int dh = d / heads;
   const int US = att_slots(T, dh);
+  if (!probs && !(US && T % 4 == 0 && d % 4 == 0))
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_forward: probs may be NULL only for T %% 4 == 0, dh %% 4 == 0");
   if (US && T % 4 == 0 && d % 4 == 0) {
     const size_t lds = att_lds_bytes(T, dh, false);
 #define RK_ATT_FWD(U_)                                                                                          \
@@ -1175,8 +1195,9 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
     const size_t lds = att_lds_bytes(T, dh, true);
 #define RK_ATT_BWD(U_)                                                                                          \
   case U_:                                                                                                      \
-    bst_attn_train_bwd_pkernel<U_><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_>, batch * heads, lds), \
-                                     256, lds, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T, d, heads, \
+    bst_attn_train_bwd_pkernel<U_, false><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_, false>,       \
+                                                     batch * heads, lds),                                      \
+                                            256, lds, (hipStream_t)stream>>>(qkv, nullptr, probs, dctx, batch, T, d, heads, \
                                                                             dqkv);                              \
     break;
     switch (US) { RK_ATT_BWD(1) RK_ATT_BWD(2) RK_ATT_BWD(4) }
@@ -1187,6 +1208,29 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
                               (hipStream_t)stream>>>(qkv, probs, dctx, batch, T,
                                                                                         d, heads, dqkv);
   return check_launch("rk_bst_attn_train_backward");
+}
+
+RK_API int rk_bst_attn_train_backward_recompute(const float* qkv, const int64_t* seq_len, const float* dctx,
+                                                int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
+                                                void* stream) {
+  if (!qkv || !seq_len || !dctx || !dqkv || batch < 0 || T <= 0 || T > kBstTMax || heads <= 0 || d % heads ||
+      d / heads > kBstDhMax || T % 4 || d % 4 || att_slots(T, d / heads) == 0)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_backward_recompute: T <= %d, T %% 4 == 0, dh %% 4 == 0, "
+                                    "dh <= %d", kBstTMax, kBstDhMax);
+  if (batch == 0) return RK_OK;
+  att_set_attrs();
+  const int dh = d / heads;
+  const size_t lds = att_lds_bytes(T, dh, true);
+#define RK_ATT_BWDR(U_)                                                                                         \
+  case U_:                                                                                                      \
+    bst_attn_train_bwd_pkernel<U_, true><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_, true>,           \
+                                                    batch * heads, lds),                                        \
+                                           256, lds, (hipStream_t)stream>>>(qkv, seq_len, nullptr, dctx, batch, T, d, \
+                                                                            heads, dqkv);                       \
+    break;
+  switch (att_slots(T, dh)) { RK_ATT_BWDR(1) RK_ATT_BWDR(2) RK_ATT_BWDR(4) }
+#undef RK_ATT_BWDR
+  return check_launch("rk_bst_attn_train_backward_recompute");
 }
 
 RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,

@@ -561,7 +561,8 @@ int rk_afm_pair_fold(const float* d_pairs, const float* emb, int32_t num_fields,
 
 /* BST training (bst.py:66-91, 238-241), rows = B*T of width d:
  *   add_pos: xp[m] = x[m] + pos[m % T].
- *   attn_train_forward: per (sample, head) P = softmax(mask(Q K^T / sqrt(dh))) saved to probs
+ *   attn_train_forward: per (sample, head) P = softmax(mask(Q K^T / sqrt(dh))) saved to probs (or not
+ *     saved when probs == NULL; T % 4 == 0, dh % 4 == 0)
  *     [B, heads, T, T] and ctx = P V [rows, d]; qkv is [rows, 3d] = [Q | K | V].  T <= 64,
  *     d / heads <= 64.  attn_train_backward: dqkv [rows, 3d] from dctx (overwritten).
  *   res_dropout_ln_forward: r = base + Dropout_p(o) (saved), y = LayerNorm(r) (gamma, beta, eps),
@@ -586,6 +587,11 @@ int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_
 int rk_bst_attn_train_backward(const float* qkv, const float* probs, const float* dctx,
                                int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
                                void* stream);
+/* The same backward with P recomputed from Q, K and seq_len (no saved probabilities: pair it with
+ * rk_bst_attn_train_forward(probs = NULL)); bit-identical P.  Needs T % 4 == 0 and dh % 4 == 0. */
+int rk_bst_attn_train_backward_recompute(const float* qkv, const int64_t* seq_len, const float* dctx,
+                                         int64_t batch, int32_t T, int32_t d, int32_t heads,
+                                         float* dqkv, void* stream);
 int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,
                                   double dropout_p, uint64_t seed, const int64_t* stream_slot,
                                   const float* gamma, const float* beta, float eps, float* r, float* y,
