@@ -782,9 +782,10 @@ class _BSTTrain(torch.autograd.Function):
             ops.linear(x, blk.w_v.weight, None, y_ptr=ops._lib.fptr(qkv, 2 * d), ldy=3 * d,
                        epilogue=ops.make_epilogue(bias=blk.w_v.bias))
             cx = torch.empty(M, d, **f32)
-            # the backward recomputes P from Q and K (saves its [B, h, T, T] write and read) where
-            # the kernels allow it, else P is kept
-            recompute = T % 4 == 0 and (d // h) % 4 == 0
+            # P is kept for the backward: recomputing it there (rk_bst_attn_train_backward_recompute,
+            # forward with probs=None) measured slower at configs[3] (backward 185 -> 242 us, forward
+            # 114 -> 108 us): the backward is latency-bound and the recompute lengthens its chain
+            recompute = False
             probs = torch.empty(0 if recompute else B * h * T * T, **f32)
             ops.bst_attn_train_forward(qkv, B, T, d, h, seq_len, None if recompute else probs, cx)
             o = torch.empty(M, d, **f32)
