@@ -298,32 +298,7 @@ def bench_sharded(world, rank, steps, warmup):
         # the exchange pipeline of ShardedDeepFM.run_steps with each chunk's local segments
         # (index pack, gather, FM + tail) captured as hipGraphs and the RCCL all-to-alls issued
         # asynchronously between them: chunk c's rows travel while chunk c+1 gathers
-        segs = []
-        for b0, b1 in model.chunk_bounds(B_l):
-            Bc = b1 - b0
-            cc = {f: v[b0:b1] for f, v in cat.items()}
-            out_i, in_i = model.index_splits(Bc)
-            out_r, in_r = model.row_splits(Bc)
-            recv_idx = torch.empty(sum(out_i), dtype=torch.int64, device=dev)
-            recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
-            g1, send = graph_of(lambda cc=cc: model.pack_indices(cc))
-            g2, rows = graph_of(lambda ri=recv_idx, Bc=Bc: model.gather_local(ri, world * Bc))
-            g3, _ = graph_of(lambda rr=recv_rows, Bc=Bc: model.fm_and_tail(rr, Bc))
-            segs.append((g1, send, g2, rows, g3, recv_idx, recv_rows, out_i, in_i, out_r, in_r))
-
-        def step():
-            works = []
-            for g1, send, _, _, _, recv_idx, _, out_i, in_i, _, _ in segs:
-                g1.replay()
-                works.append(model._exchange(recv_idx, send, out_i, in_i, async_op=True)[1])
-            rworks = []
-            for (_, _, g2, rows, _, _, recv_rows, _, _, out_r, in_r), w in zip(segs, works):
-                w.wait()
-                g2.replay()
-                rworks.append(model._exchange(recv_rows, rows.reshape(-1), out_r, in_r, async_op=True)[1])
-            for (_, _, _, _, g3, _, _, _, _, _, _), w in zip(segs, rworks):
-                w.wait()
-                g3.replay()
+        step = model.capture_pipeline(cat).step
 
     t = max_over_ranks(world, time_replays(step, steps, warmup, world))
     wire = B_l * SHARDED_FIELDS * (8 + 4 * row_stride(32)) * (world - 1) / world

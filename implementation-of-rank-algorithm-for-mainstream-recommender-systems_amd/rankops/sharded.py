@@ -62,6 +62,10 @@ class ShardedDeepFM(EngineModule):
         self.local_fields = self.fields_of[rank]
         self.pipeline_chunks = 4  # exchange pipeline depth at P > 1 (chunk_bounds)
         self.min_chunk = 512
+        # all-to-all transport: None = torch.distributed.all_to_all_single on `group` (RCCL);
+        # otherwise a callable (out, inp, out_splits, in_splits, async_op) -> out | (out, work)
+        # with the same semantics (tests drive P shards in one process through an emulator)
+        self.exchange_fn = None
         self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
                                                      for f in self.local_fields})
         self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
@@ -115,6 +119,8 @@ class ShardedDeepFM(EngineModule):
         if self.world == 1:
             out.copy_(inp)
             return (out, None) if async_op else out
+        if self.exchange_fn is not None:
+            return self.exchange_fn(out, inp, out_splits, in_splits, async_op)
         work = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=async_op)
         return (out, work) if async_op else out
 
@@ -252,6 +258,76 @@ class ShardedDeepFM(EngineModule):
             if work is not None:
                 work.wait()
             outs.append(self.fm_and_tail(recv_rows, b1 - b0))
+        if len(outs) == 1:
+            return outs[0]
+        return tuple(torch.cat([o[i] for o in outs], 0) for i in range(len(outs[0])))
+
+    def capture_pipeline(self, cat: dict, chunks: int = None) -> "CapturedPipeline":
+        """run_steps with each chunk's three local segments (index pack, gather, FM + tail)
+        captured as hipGraphs; the all-to-alls stay outside the graphs (RCCL collectives are
+        issued per step with async_op, so chunk c's rows travel while chunk c+1 gathers).
+        Capture is local (no collective), so the ranks may capture in any order."""
+        return CapturedPipeline(self, cat, chunks)
+
+
+def _graph_of(fn):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.no_grad():
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        out = fn()
+    return g, out
+
+
+class CapturedPipeline:
+    """The P > 1 exchange pipeline of ShardedDeepFM.run_steps as replayable segments.  step()
+    issues, per chunk: pack graph -> async index all-to-all; then per chunk: wait -> gather graph
+    -> async row all-to-all; then per chunk: wait -> FM + tail graph.  `outputs` are the five
+    forward outputs of the last step (concatenated over chunks by result())."""
+
+    def __init__(self, model: ShardedDeepFM, cat: dict, chunks: int = None):
+        if model.world == 1:
+            raise ValueError("capture_pipeline: P = 1 has no exchange; capture run_steps as one graph")
+        self.model = model
+        dev = model._device()
+        B_l = cat[model.fields[0]].shape[0]
+        self.segs = []
+        for b0, b1 in model.chunk_bounds(B_l, chunks):
+            Bc = b1 - b0
+            cc = {f: v[b0:b1] for f, v in cat.items()}
+            out_i, in_i = model.index_splits(Bc)
+            out_r, in_r = model.row_splits(Bc)
+            recv_idx = torch.zeros(sum(out_i), dtype=torch.int64, device=dev)  # valid rows for the warm-up gathers
+            recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
+            g1, send = _graph_of(lambda cc=cc: model.pack_indices(cc))
+            g2, rows = _graph_of(lambda ri=recv_idx, Bc=Bc: model.gather_local(ri, model.world * Bc))
+            g3, outs = _graph_of(lambda rr=recv_rows, Bc=Bc: model.fm_and_tail(rr, Bc))
+            self.segs.append(dict(g1=g1, send=send, g2=g2, rows=rows, g3=g3, outs=outs, recv_idx=recv_idx,
+                                  recv_rows=recv_rows, idx_splits=(out_i, in_i), row_splits=(out_r, in_r)))
+
+    def step(self):
+        m = self.model
+        works = []
+        for s in self.segs:
+            s["g1"].replay()
+            works.append(m._exchange(s["recv_idx"], s["send"], *s["idx_splits"], async_op=True)[1])
+        rworks = []
+        for s, w in zip(self.segs, works):
+            if w is not None:
+                w.wait()
+            s["g2"].replay()
+            rworks.append(m._exchange(s["recv_rows"], s["rows"].reshape(-1), *s["row_splits"], async_op=True)[1])
+        for s, w in zip(self.segs, rworks):
+            if w is not None:
+                w.wait()
+            s["g3"].replay()
+
+    def result(self):
+        outs = [s["outs"] for s in self.segs]
         if len(outs) == 1:
             return outs[0]
         return tuple(torch.cat([o[i] for o in outs], 0) for i in range(len(outs[0])))

@@ -1,0 +1,183 @@
+"""The P > 1 table-sharded DeepFM (rankops.sharded, BASELINE configs[4]) with P shards in one
+process on one device: every device step is the real one — pack_indices, gather_local
+(rk_concat_gather over the packed tables), fm_and_tail (rk_fm_gather over the received rows'
+dense segments + the fused tail) and run_steps' chunk pipeline — and only the RCCL transport is
+replaced by the in-process all-to-all emulator (tests/a2a_emulator.py).  Outputs are compared
+with the oracle (oracle.reference_forward.deepfm_forward: deepfm.py:121-151) at configs[4]'s field
+shape: 30 fields, emb_dim 32, 512-256-128, field f on rank f % P (4/4/4/4/4/4/3/3 at P = 8).
+
+The CPU test runs the same emulator under the CPU stand-ins of test_distributed.py, so the
+emulator itself is checked against the gloo all_to_all_single routing there."""
+import pytest
+import torch
+
+import helpers as H
+from a2a_emulator import InProcessAllToAll, run_ranks
+from oracle import reference_forward as ref
+from rankops import sharded
+
+FIELDS30 = {f"field_{i:02d}": 300 + 37 * i for i in range(30)}
+CFG30 = {"dim": 32, "fields": FIELDS30, "hidden": [512, 256, 128]}
+
+
+def _shards(full, world, cls=sharded.ShardedDeepFM, device=None):
+    rows = {f: e.num_embeddings for f, e in full.second_order_embeddings.items()}
+    hidden = [l.out_features for l in full.deep_layers if isinstance(l, torch.nn.Linear)]
+    emu = InProcessAllToAll(world)
+    shards = []
+    for r in range(world):
+        if cls is sharded.ShardedDeepFM:
+            sh = cls.from_deepfm(full, rank=r, world_size=world)
+        else:
+            sh = cls(rows, full.embedding_dim, hidden, rank=r, world_size=world)
+            sd = {k: v for k, v in full.state_dict().items()
+                  if not k.startswith(("first_order", "second_order")) or k.split(".")[1] in sh.local_fields}
+            sh.load_state_dict(sd, strict=True)
+            sh.eval()
+        sh.exchange_fn = emu.bind(r)
+        shards.append(sh)
+    return shards, emu
+
+
+def _oracle(full, cfg, cat):
+    with torch.no_grad():
+        return ref.deepfm_forward(H.cpu_params(full), {f: v.cpu() for f, v in cat.items()}, list(cfg["fields"]),
+                                  len(cfg["hidden"]))
+
+
+def _check(got, expect, lo, hi, tol):
+    names = ("prob", "total_logit", "fm1", "fm2", "deep_logit")
+    for n, g, e in zip(names, got, expect):
+        torch.testing.assert_close(g.cpu(), e[lo:hi], atol=tol, rtol=tol, msg=lambda m: f"{n}: {m}")
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4), (8, 3)])
+def test_emulator_routes_like_gloo_cpu(world, chunks):
+    """CPU: the emulator under the CPU stand-in device steps reproduces the oracle (the gloo
+    routing test's counterpart), so a GPU failure below is a device-step failure."""
+    from test_distributed import CFG, CpuStepsSharded
+    full = H.build("deepfm", CFG, seed=42)
+    B = 24
+    inp = H.make_inputs("deepfm", CFG, B * world, seed=77)
+    expect = _oracle(full, CFG, inp["category"])
+    shards, emu = _shards(full, world, cls=CpuStepsSharded)
+
+    def rank_fn(r):
+        sh = shards[r]
+        sh.min_chunk = 4
+        mine = {f: v[r * B:(r + 1) * B].contiguous() for f, v in inp["category"].items()}
+        with torch.no_grad():
+            return sh.run_steps(mine, chunks=chunks)
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    for r, got in enumerate(outs):
+        _check(got, expect, r * B, (r + 1) * B, 1e-5)
+    assert emu.calls == 2 * chunks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_sharded_pipeline_emulated_on_gpu(world, chunks):
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 520
+    inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=4000 + world), "cuda")
+    expect = _oracle(full, CFG30, inp["category"])
+    shards, emu = _shards(full, world)
+    counts = [len(sh.local_fields) for sh in shards]
+    assert counts == [sum(1 for f in range(30) if f % world == r) for r in range(world)]
+    if world == 8:
+        assert counts == [4, 4, 4, 4, 4, 4, 3, 3]
+
+    def rank_fn(r):
+        sh = shards[r]
+        sh.min_chunk = 64
+        mine = {f: v[r * B_l:(r + 1) * B_l] for f, v in inp["category"].items()}
+        assert len(sh.chunk_bounds(B_l, chunks)) == chunks
+        with torch.no_grad():
+            out = sh(mine) if chunks == sh.pipeline_chunks else sh.run_steps(
+                {f: v.contiguous() for f, v in mine.items()}, chunks=chunks)
+        torch.cuda.synchronize()
+        return tuple(o.cpu() for o in out)
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    torch.cuda.synchronize()
+    for r, got in enumerate(outs):
+        _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
+    import rankops
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_step_functions_emulated_on_gpu(world):
+    """The four steps one by one (index exchange, local gather, row exchange, FM + tail):
+    received indices equal the owner's fields of every source, gathered rows equal the packed
+    table rows (second order, then the first-order weight at column D), and the FM + tail equals
+    the oracle."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 96
+    inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=11), "cuda")
+    expect = _oracle(full, CFG30, inp["category"])
+    shards, emu = _shards(full, world)
+    D, RS = 32, sharded.row_stride(32)
+
+    def rank_fn(r):
+        sh = shards[r]
+        mine = {f: v[r * B_l:(r + 1) * B_l] for f, v in inp["category"].items()}
+        with torch.no_grad():
+            recv_idx = sh.exchange_indices(mine, B_l)
+            rows = sh.gather_local(recv_idx, world * B_l)
+            recv_rows = sh.exchange_rows(rows, B_l)
+            out = sh.fm_and_tail(recv_rows, B_l)
+        torch.cuda.synchronize()
+        return recv_idx.cpu(), rows.cpu(), tuple(o.cpu() for o in out)
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    names = list(FIELDS30)
+    for r, (recv_idx, rows, got) in enumerate(outs):
+        mine = shards[r].local_fields
+        ri = recv_idx.view(world * B_l, len(mine))
+        want_idx = torch.stack([inp["category"][f].cpu() for f in mine], 1)  # sources in order = global rows
+        assert torch.equal(ri, want_idx)
+        rv = rows.view(world * B_l, len(mine), RS)
+        for j, f in enumerate(mine):
+            w2 = full.second_order_embeddings[f].weight.detach().cpu()
+            w1 = full.first_order_embeddings[f].weight.detach().cpu()
+            assert torch.equal(rv[:, j, :D], w2[want_idx[:, j]])
+            assert torch.equal(rv[:, j, D], w1[want_idx[:, j], 0])
+        _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
+        assert names.index(mine[0]) == r
+    import rankops
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_captured_pipeline_emulated_on_gpu(world):
+    """bench.py's world > 1 step (ShardedDeepFM.capture_pipeline: per chunk three hipGraph
+    segments with the exchanges between them) driven through the emulator, replayed twice."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 1024
+    inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=21), "cuda")
+    expect = _oracle(full, CFG30, inp["category"])
+    shards, emu = _shards(full, world)
+    pipes = []
+    for r, sh in enumerate(shards):  # capture is local (no collective): serially, here
+        sh.min_chunk = 256
+        mine = {f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in inp["category"].items()}
+        pipes.append((sh.capture_pipeline(mine), mine))
+    assert len(pipes[0][0].segs) == 4
+
+    def rank_fn(r):
+        for _ in range(2):
+            pipes[r][0].step()
+        torch.cuda.synchronize()
+        return tuple(o.cpu() for o in pipes[r][0].result())
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    for r, got in enumerate(outs):
+        _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
+    assert emu.calls == 2 * 2 * 4
+    import rankops
+    assert rankops.error_flags() == 0  # the capture's warm-up gathers read valid (zeroed) indices
