@@ -105,9 +105,7 @@ static int launch_bst_attention(const float* qkv, int64_t ld_qkv, int64_t batch,
   hipStream_t st = (hipStream_t)stream;
 #define RK_BST_CASE(DD)                                                                                       \
   case DD:                                                                                                    \
-    if (shm > 64 * 1024)                                                                                      \
-      (void)hipFuncSetAttribute((const void*)bst_attention_kernel<DD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          (int)shm);                                                                          \
+    if (shm > 64 * 1024) raise_lds_limit((const void*)bst_attention_kernel<DD>, (int)shm);                   \
     bst_attention_kernel<DD><<<blocks, 64 * wpg, shm, st>>>(qkv, ld_qkv, batch, T, d_model, heads, seq_len,   \
                                                            key_mask, ld_mask, ctx, ld_ctx, wpg);              \
     break;

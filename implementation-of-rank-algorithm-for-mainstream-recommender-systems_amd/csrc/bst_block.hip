@@ -554,11 +554,7 @@ RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t
   a.flags = device_flags();
   if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_bst_forward_blocks: negative batch");
   const size_t shm = (size_t)(4 * kBT * kBLD + 4 * kBD) * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)bst_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  raise_lds_limit((const void*)bst_block_kernel, 160 * 1024);
   // one resident workgroup per CU (LDS-bound); each walks samples blockIdx.x + k * gridDim.x
   const int64_t grid = std::min<int64_t>(batch, num_cus());
   bst_block_kernel<<<(unsigned)grid, 512, shm, (hipStream_t)stream>>>(a);

@@ -17,6 +17,9 @@ constexpr int kWave = 64;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// 16-B alignment of a device pointer (float4 / dwordx4 paths are chosen on the host).
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
 // ---- host-side error plumbing (runtime.cpp) ----
 int fail(int code, const char* fmt, ...);
 int check_launch(const char* what);
@@ -24,6 +27,9 @@ int check_launch(const char* what);
 uint32_t* device_flags();
 // Number of CUs on the current device (cached).
 int num_cus();
+// Raises `kern`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel, device);
+// thread-safe (runtime.hip).
+void raise_lds_limit(const void* kern, int bytes);
 // out[0] = scale * (sum of part[0..n)) / rows, one wave, fixed order (embedding.hip).
 int launch_l2_final(const float* part, int n, int64_t rows, float scale, float* out, hipStream_t st);
 

@@ -353,8 +353,14 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   __syncthreads();
   DIN_TS(2);
   // l2 partials: the last workgroup to publish its partial also finishes the mean, after its own
-  // phase B (hand-off per MI355X_MICROARCH.md: sc1 partial stores, vmcnt(0), one agent atomic
-  // add per workgroup; the adder that returns n-1 reads every partial with sc1 loads)
+  // phase B.  Hand-off = MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1
+  // table (measured valid on gfx950 / ROCm 7.2, not an architectural guarantee): one lane per
+  // workgroup stores its partial sc1 (relaxed agent store), waits vmcnt(0), then adds to ONE
+  // counter (relaxed agent atomic); the workgroup whose add returns n-1 loads every partial with
+  // sc1 loads (relaxed agent loads) in the adding wave, after the add returned.  The memory-model
+  // form (release/acquire at agent scope) lowers to buffer_wbl2 / buffer_inv, ~1.7-3.5 us each on
+  // the critical path of a ~50 us kernel; tests/test_gpu_din_plan.py checks l2 against the
+  // deterministic host-order sum over repeated launches.
   int& l2_last = *reinterpret_cast<int*>(col_seg + 512);
   if (a.l2_part && tid == 0) {
     float t = 0.f;
@@ -541,13 +547,9 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
 
 static int din_launch(const DinPlan& p, hipStream_t st) {
   if (p.blocks == 0) return RK_OK;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)din_forward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)din_forward_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)din_forward_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  raise_lds_limit((const void*)din_forward_kernel<8>, 160 * 1024);
+  raise_lds_limit((const void*)din_forward_kernel<16>, 160 * 1024);
+  raise_lds_limit((const void*)din_forward_kernel<32>, 160 * 1024);
   const unsigned blocks = (unsigned)p.blocks;
   switch (p.H) {
     case 8: din_forward_kernel<8><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;

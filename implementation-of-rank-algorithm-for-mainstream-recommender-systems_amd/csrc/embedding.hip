@@ -319,7 +319,6 @@ __global__ void bn_fold_kernel(const float* __restrict__ mean, const float* __re
   shift[i] = (bias ? bias[i] : 0.f) - mean[i] * a;
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 int launch_l2_final(const float* part, int n, int64_t rows, float scale, float* out, hipStream_t st) {
   row_l2norm_final_kernel<<<1, 64, 0, st>>>(part, n, rows, scale, out);

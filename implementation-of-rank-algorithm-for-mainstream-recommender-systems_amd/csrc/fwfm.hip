@@ -172,7 +172,6 @@ __global__ __launch_bounds__(256) void fwfm_backward_kernel(FwfmTables t, int F,
   for (int i = threadIdx.x; i <= P; i += blockDim.x) atomicAdd(i < P ? d_field_weight + i : d_bias, red[i]);
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace rk
 

@@ -289,14 +289,7 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
   dim3 grid((unsigned)std::max<int64_t>(1, per_tile / ntile), (unsigned)ntile);
   bool done = false;
   auto go = [&](void (*kern)(RowsArgs)) {
-    static const void* raised[64];  // kernels whose dynamic-LDS limit is raised (> 64 KiB at nt 4, K 128)
-    static int nraised = 0;
-    bool seen = false;
-    for (int i = 0; i < nraised; ++i) seen |= raised[i] == (const void*)kern;
-    if (!seen && nraised < 64) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      raised[nraised++] = (const void*)kern;
-    }
+    raise_lds_limit((const void*)kern, 80 * 1024);  // > 64 KiB at nt 4, K 128
     kern<<<grid, 256, shm, st>>>(a);
     done = true;
   };

@@ -245,7 +245,6 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ X
   }
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 template <int TM, int TN, bool ROWEPI>
 static void launch(bool vec, dim3 grid, hipStream_t st, const float* X, int64_t ldx, const float* Xp, int xperiod,

@@ -164,11 +164,7 @@ RK_API int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, co
   a.x_vec = (ldx % 4 == 0) && (((uintptr_t)x & 15u) == 0);
   const dim3 grid((unsigned)((M + kLtRows - 1) / kLtRows), (unsigned)((pad64(L.n) + kLtCols - 1) / kLtCols));
   const size_t shm = 2 * kLtRows * kLtLd * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)linear_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr_set = true;
-  }
+  raise_lds_limit((const void*)linear_tiled_kernel, (int)shm);
   linear_tiled_kernel<<<grid, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   return check_launch("rk_linear_tiled");
 }

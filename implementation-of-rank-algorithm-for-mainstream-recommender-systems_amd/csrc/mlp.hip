@@ -177,7 +177,6 @@ __global__ void mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int n,
   out[i] = (r < n && col < k) ? w[(int64_t)r * ldw + col] : 0.f;
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 int mlp_validate(const rk_mlp_layer* layers, int nlayers, int K0, const rk_epilogue& head, int* need0, int* need1,
                  const char* what) {
@@ -268,12 +267,8 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   if (M == 0) return RK_OK;
   const int64_t blocks = (M + rows_per_wg - 1) / rows_per_wg;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward: M too large");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)mlp_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)mlp_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  raise_lds_limit((const void*)mlp_kernel<1>, 160 * 1024);
+  raise_lds_limit((const void*)mlp_kernel<2>, 160 * 1024);
   if (rt == 2)
     mlp_kernel<2><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   else
@@ -321,11 +316,7 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)dcn_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  raise_lds_limit((const void*)dcn_fused_kernel, 160 * 1024);
   dcn_fused_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   return check_launch("rk_dcn_forward");
 }

@@ -23,6 +23,21 @@ int current_device() {
 }
 }  // namespace
 
+void raise_lds_limit(const void* kern, int bytes) {
+  struct Entry {
+    const void* kern;
+    int dev, bytes;
+  };
+  static Entry done[256];
+  static int n = 0;
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_mu);
+  for (int i = 0; i < n; ++i)
+    if (done[i].kern == kern && done[i].dev == dev && done[i].bytes >= bytes) return;
+  (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (n < 256) done[n++] = Entry{kern, dev, bytes};
+}
+
 int fail(int code, const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -72,7 +87,7 @@ RK_API int rk_init(int32_t device) {
   hipError_t e = hipMalloc(&p, 64);
   if (e == hipSuccess) e = hipMemset(p, 0, 64);
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  hipSetDevice(prev);
+  (void)hipSetDevice(prev);
   if (e != hipSuccess) return rk::fail(RK_ERR_RUNTIME, "rk_init: %s", hipGetErrorString(e));
   rk::g_flags[device] = p;
   return RK_OK;
@@ -83,13 +98,13 @@ RK_API int rk_error_flags(int32_t device, uint32_t* flags, int32_t reset) {
   if (device < 0 || device >= rk::kMaxDevices || !rk::g_flags[device])
     return rk::fail(RK_ERR_INVALID, "rk_error_flags: device %d not initialised", device);
   int prev = 0;
-  hipGetDevice(&prev);
-  hipSetDevice(device);
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(flags, rk::g_flags[device], sizeof(uint32_t), hipMemcpyDeviceToHost);
   if (e == hipSuccess && reset) e = hipMemset(rk::g_flags[device], 0, sizeof(uint32_t));
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  hipSetDevice(prev);
+  (void)hipSetDevice(prev);
   if (e != hipSuccess) return rk::fail(RK_ERR_RUNTIME, "rk_error_flags: %s", hipGetErrorString(e));
   return RK_OK;
 }

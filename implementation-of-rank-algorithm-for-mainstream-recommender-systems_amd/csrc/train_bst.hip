@@ -1069,19 +1069,13 @@ static unsigned att_grid(const void* kernel, int64_t items, size_t lds) {
 
 // Dynamic LDS above the 64 KiB default: up to 104 KiB (T = 64, dh = 64 backward).
 static void att_set_attrs() {
-  static bool done = false;
-  if (done) return;
   for (const void* f : {(const void*)bst_attn_train_fwd_pkernel<1>, (const void*)bst_attn_train_fwd_pkernel<2>,
                         (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1, false>,
                         (const void*)bst_attn_train_bwd_pkernel<2, false>, (const void*)bst_attn_train_bwd_pkernel<4, false>,
                         (const void*)bst_attn_train_bwd_pkernel<1, true>, (const void*)bst_attn_train_bwd_pkernel<2, true>,
-                        (const void*)bst_attn_train_bwd_pkernel<4, true>})
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)bst_attn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-  (void)hipFuncSetAttribute((const void*)bst_attn_train_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-  done = true;
+                        (const void*)bst_attn_train_bwd_pkernel<4, true>, (const void*)bst_attn_train_fwd_kernel,
+                        (const void*)bst_attn_train_bwd_kernel})
+    raise_lds_limit(f, 160 * 1024);
 }
 
 // Lanes per row of the float4 LayerNorm kernels (0: use the scalar kernels): d % 4 == 0 and every
@@ -1115,6 +1109,8 @@ static int ln_backward(const float* dy, const float* drow, int64_t ld_row, int c
     switch (L) { RK_LN_BWD(8) RK_LN_BWD(16) RK_LN_BWD(32) RK_LN_BWD(64) }
 #undef RK_LN_BWD
   } else {
+    // the scalar kernel reads dy only: the pooled-row form (drow) exists in the float4 kernels
+    if (!dy) return fail(RK_ERR_UNSUPPORTED, "%s: the pooled-row backward needs the float4 path", what);
     blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kLnBlocks, (rows + 3) / 4));
     bst_ln_bwd_kernel<<<blocks, 256, 0, st>>>(dy, r, mean, rstd, gamma, rows, d, seed, stream_slot, thr, scale, dr,
                                               d_o, workspace);
@@ -1294,8 +1290,8 @@ RK_API int rk_bst_pool_ln_backward(const float* drow, int64_t ld_row, int32_t co
   if (workspace_floats < rk_bst_ln_backward_workspace_floats(d))
     return fail(RK_ERR_INVALID, "rk_bst_pool_ln_backward: workspace of %lld floats, needs %lld",
                 (long long)workspace_floats, (long long)rk_bst_ln_backward_workspace_floats(d));
-  if (ln_lanes(d, {r, gamma, dr, d_o}) == 0)
-    return fail(RK_ERR_UNSUPPORTED, "rk_bst_pool_ln_backward: needs d %% 4 == 0, 16-B aligned rows");
+  if (ln_lanes(d, {r, gamma, dr, d_o, workspace}) == 0)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_pool_ln_backward: needs d %% 4 == 0, 16-B aligned rows and workspace");
   return ln_backward(nullptr, drow, ld_row, col, T, seq_len, mean_pool, r, mean, rstd, gamma, rows, d, dropout_p, seed,
                      stream_slot, dr, d_o, dgamma, dbeta, workspace, (hipStream_t)stream, "rk_bst_pool_ln_backward");
 }

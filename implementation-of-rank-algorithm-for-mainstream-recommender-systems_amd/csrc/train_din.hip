@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void din_att_pool_forward_kernel(const float* 
                                                                    const int64_t* __restrict__ seq_len, int64_t B,
                                                                    int T, int H, int softmax, float sqrt_h,
                                                                    float* __restrict__ wts, float* __restrict__ x,
-                                                                   int64_t ldx, int att_col) {
+                                                                   int64_t ldx, int att_col, int vec_a2) {
   __shared__ float sw[4][kDinMaxT];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * 4 + wv;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void din_att_pool_forward_kernel(const float* 
   const int64_t len = seq_len[b];
   const float bias3 = b3[0];
   float mx = -INFINITY;
-  const bool vec = (A2 & 3) == 0;  // a2 rows 16-B aligned: float4 row reads, 4x fewer load instructions
+  const bool vec = vec_a2;  // A2 % 4 == 0 and a2 16-B aligned (host): float4 row reads, 4x fewer loads
   for (int t = lane; t < T; t += 64) {
     const float* row = a2 + (b * T + t) * A2;
     float s = 0.f;
@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
                                                                     const int64_t* __restrict__ seq_len, int64_t B,
                                                                     int T, int H, int softmax, float sqrt_h,
                                                                     float* __restrict__ dkeys,
-                                                                    float* __restrict__ da2) {
+                                                                    float* __restrict__ da2, int vec_keys,
+                                                                    int vec_a2) {
   __shared__ float sd[4][kDinMaxT];
   __shared__ float so[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
   const float* kb = keys + b * T * H;
   const float* wb = wts + b * T;
   float g = 0.f;
-  const bool vec = (H & 3) == 0;  // key rows 16-B aligned: float4 reads
+  const bool vec = vec_keys;  // H % 4 == 0, keys and dkeys 16-B aligned (host): float4 reads
   for (int t = lane; t < T; t += 64) {
     float dw = 0.f;
     if (vec) {
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void din_att_pool_backward_kernel(const float*
   }
   __syncthreads();
   if (!live) return;
-  if (vec && (A2 & 3) == 0) {  // float4 stores of dkeys and da2 (rows 16-B aligned)
+  if (vec && vec_a2) {  // float4 stores of dkeys and da2 (rows 16-B aligned)
     const int H4 = H / 4, A4 = A2 / 4;
     for (int i = lane; i < T * H4; i += 64) {
       const int t = i / H4, h = 4 * (i - t * H4);
@@ -339,7 +340,7 @@ RK_API int rk_din_att_pool_forward(const float* a2, int32_t a2_width, const floa
   if (batch == 0) return RK_OK;
   din_att_pool_forward_kernel<<<(unsigned)((batch + 3) / 4), 256, 0, (hipStream_t)stream>>>(
       a2, a2_width, w3, b3, keys, seq_len, batch, T, H, use_softmax, sqrtf((float)H), weights, x, ldx,
-      att_col);
+      att_col, a2_width % 4 == 0 && aligned16(a2));
   return check_launch("rk_din_att_pool_forward");
 }
 
@@ -353,7 +354,8 @@ RK_API int rk_din_att_pool_backward(const float* dx, int64_t lddx, int32_t att_c
   if (batch == 0) return RK_OK;
   din_att_pool_backward_kernel<<<(unsigned)((batch + 3) / 4), 256, 0, (hipStream_t)stream>>>(
       dx, lddx, att_col, weights, keys, a2, a2_width, w3, seq_len, batch, T, H, use_softmax, sqrtf((float)H),
-      dkeys, da2);
+      dkeys, da2, H % 4 == 0 && aligned16(keys) && aligned16(dkeys), a2_width % 4 == 0 && aligned16(a2) &&
+      aligned16(da2));
   return check_launch("rk_din_att_pool_backward");
 }
 

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64 * kSeqWaves) void emb_seq_runs_kernel(const int6
       int64_t id[9];
       f32x2 v[8];
 #pragma unroll
-      for (int j = 0; j < 9; ++j) id[j] = t0 + j < T ? ids[t0 + j] : -2;  // -2: past the end
+      for (int j = 0; j < 9; ++j) id[j] = t0 + j < T ? ids[t0 + j] : 0;  // past the end: never compared
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         v[j] = (on && t0 + j < T) ? *reinterpret_cast<const f32x2*>(rowp + (int64_t)(t0 + j) * ld_dx)
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64 * kSeqWaves) void emb_seq_runs_kernel(const int6
       for (int j = 0; j < 8; ++j) {
         if (t0 + j >= T) break;
         acc += v[j];
-        if (id[j + 1] != id[j] && id[j + 1] != -2) {  // a run ends before the sample's last position
+        if (t0 + j + 1 < T && id[j + 1] != id[j]) {  // a run ends before the sample's last position
           const int64_t r = id[j];
           if (r >= 0 && r < rows) {
             if (on) {

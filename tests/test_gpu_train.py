@@ -739,8 +739,9 @@ def _bst_step_check(cfg, B, seed, steps):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [{"T": 20}, {"T": 20, "dim": 32, "blocks": 2, "pooling": "mean"},
-                                 {"T": 64, "dim": 128, "max_len": 64, "vocab": H.WECHAT_VOCAB}],
-                         ids=["reference", "two_blocks_mean", "bench_shape"])
+                                 {"T": 64, "dim": 128, "max_len": 64, "vocab": H.WECHAT_VOCAB},
+                                 {"T": 50, "dim": 32, "max_len": 50}],
+                         ids=["reference", "two_blocks_mean", "bench_shape", "reference_T50"])
 def test_bst_train_steps_match_autograd(cfg):
     _bst_step_check(cfg, 256, seed=2600, steps=2)
 
@@ -1020,3 +1021,50 @@ def test_embedding_backward_seq_matches_index_add(B, T, d):
     grad = torch.zeros(V, d, device="cuda")
     assert ops.embedding_backward_seq(grad, seq.cuda(), dx.cuda())
     torch.testing.assert_close(grad.cpu().double(), want, rtol=0, atol=1e-4 * max(1.0, float(want.abs().max())))
+
+
+@pytest.mark.gpu
+def test_embedding_backward_seq_out_of_range_ids():
+    """an out-of-range id (-2 included) is skipped and flagged; the gradients of the
+    valid positions around it are still applied."""
+    import rankops
+    rankops.error_flags()
+    V, d = 10, 8
+    seq = torch.tensor([[5, -2, 7, 7], [3, 3, V + 4, 3], [-2, -2, 1, 0]])
+    dx = torch.randn(seq.numel(), d, generator=torch.Generator().manual_seed(3))
+    ok = (seq >= 0) & (seq < V)
+    want = torch.zeros(V, d, dtype=torch.float64).index_add_(0, seq.reshape(-1)[ok.reshape(-1)],
+                                                              dx[ok.reshape(-1)].double())
+    grad = torch.zeros(V, d, device="cuda")
+    assert ops.embedding_backward_seq(grad, seq.cuda(), dx.cuda())
+    torch.testing.assert_close(grad.cpu().double(), want, rtol=0, atol=1e-5)
+    assert rankops.error_flags() == rankops._lib.RK_FLAG_INDEX_OOB
+
+
+@pytest.mark.gpu
+def test_pool_ln_backward_misaligned_workspace_is_unsupported():
+    """a workspace pointer that is not 16-B aligned is refused (RK_ERR_UNSUPPORTED)
+    instead of reaching the scalar kernel, which has no pooled-row form."""
+    lib = rankops_lib()
+    B, T, d = 4, 8, 32
+    r = torch.randn(B * T, d, device="cuda")
+    mean = torch.zeros(B * T, device="cuda")
+    rstd = torch.ones(B * T, device="cuda")
+    gamma = torch.ones(d, device="cuda")
+    drow = torch.randn(B, 16 + d, device="cuda")
+    dr, d_o = torch.empty_like(r), torch.empty_like(r)
+    dg, db = torch.empty(d, device="cuda"), torch.empty(d, device="cuda")
+    nws = lib.rk_bst_ln_backward_workspace_floats(d)
+    ws = torch.empty(nws + 4, device="cuda")
+    seq_len = torch.full((B,), T, dtype=torch.int64, device="cuda")
+    P = ops.ptr
+    args = lambda w: (P(drow), drow.stride(0), 16, T, P(seq_len), 0, P(r), P(mean), P(rstd), P(gamma), B * T, d,  # noqa
+                      0.0, 0, None, P(dr), P(d_o), P(dg), P(db), w, nws, None)
+    assert lib.rk_bst_pool_ln_backward(*args(ws.data_ptr() + 4)) == 4  # RK_ERR_UNSUPPORTED
+    assert lib.rk_bst_pool_ln_backward(*args(ws.data_ptr())) == 0
+    torch.cuda.synchronize()
+
+
+def rankops_lib():
+    import rankops
+    return rankops.load_library()
