@@ -39,6 +39,10 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
                    const rk_epilogue* ep, hipStream_t st);
 
 // ---- device helpers ----
+// Wave index of the calling thread in its workgroup, as a wave-uniform (SGPR) value: branches and
+// addresses that depend only on it compile to scalar code.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

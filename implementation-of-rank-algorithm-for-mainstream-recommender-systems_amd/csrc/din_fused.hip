@@ -66,10 +66,21 @@ struct DinLds {
 constexpr int kDinPhaseWG = 1024;
 __device__ unsigned long long g_din_ts[kDinPhaseWG][4];       // entry, staged, phase A done, phase B done
 __device__ unsigned long long g_din_wave[kDinPhaseWG][16];    // per-wave phase-A cycles (clock64)
-#define DIN_TS(i)                                                                       \
-  do {                                                                                  \
-    if (tid == 0 && blockIdx.x < kDinPhaseWG) g_din_ts[blockIdx.x][i] = wall_clock64(); \
+// marks are kept in LDS while the kernel runs (a global store mid-kernel joins the vmcnt queue
+// every later wait drains) and written out by din_marks_flush() at the end
+__shared__ unsigned long long s_din_ts[4];
+__shared__ unsigned long long s_din_wave[16];
+#define DIN_TS(i)                                \
+  do {                                           \
+    if (tid == 0) s_din_ts[i] = wall_clock64();  \
   } while (0)
+__device__ __forceinline__ void din_marks_flush(int tid) {
+  __syncthreads();
+  if (blockIdx.x < kDinPhaseWG) {
+    if (tid < 4) g_din_ts[blockIdx.x][tid] = s_din_ts[tid];
+    if (tid < 16) g_din_wave[blockIdx.x][tid] = s_din_wave[tid];
+  }
+}
 #else
 #define DIN_TS(i) \
   do {            \
@@ -348,7 +359,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
   if (lane == 0) sm[Ly::NORM + wave] = norm_part;
 #ifdef RK_DIN_PHASES
-  if (lane == 0 && blockIdx.x < kDinPhaseWG) g_din_wave[blockIdx.x][wave] = clock64() - wave_t0;
+  if (lane == 0) s_din_wave[wave] = clock64() - wave_t0;
 #endif
   __syncthreads();
   DIN_TS(2);
@@ -388,6 +399,10 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       __hip_atomic_store(a.l2_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+#ifdef RK_DIN_PHASES
+  din_marks_flush(tid);
+#endif
+  MLP_FLUSH(tid);
 }
 
 // The LDS image of the split attention weights (see the layout above): WK = W1b - W1c,
@@ -606,8 +621,7 @@ RK_API int rk_debug_din_phases(unsigned long long* ts, unsigned long long* waves
   if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_din_ts), sizeof(g_din_ts)) != hipSuccess) return 1;
   if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_din_wave), sizeof(g_din_wave)) != hipSuccess) return 1;
 #ifdef RK_MLP_PHASES
-  if (hipMemcpyFromSymbol(mlp, HIP_SYMBOL(g_mlp_phase), sizeof(g_mlp_phase)) != hipSuccess) return 1;
-  (void)hipMemset(mlp, 0, 0);
+  if (hipMemcpyFromSymbol(mlp, HIP_SYMBOL(g_mlp_marks), sizeof(g_mlp_marks[0]) * kDinPhaseWG) != hipSuccess) return 1;
 #else
   (void)mlp;
 #endif

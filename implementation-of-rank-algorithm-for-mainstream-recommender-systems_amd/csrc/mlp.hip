@@ -26,18 +26,14 @@ struct MlpArgs {
 };
 
 // RT row tiles of 16 rows per workgroup: every weight element streamed from L2 serves 16*RT rows
-template <int RT>
+template <int RT, bool STORE>
 __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ROWS = kMlpRows * RT;
   const int tid = threadIdx.x;
 #ifdef RK_MLP_PHASES
   const unsigned long long k_t0 = clock64();
-  const unsigned long long w0 = wall_clock64();
-  if (tid == 0) {
-    atomicMin(&g_mlp_span[0], w0);
-    atomicMax(&g_mlp_span[2], w0);  // last workgroup start
-  }
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
 #endif
   const int64_t m0 = (int64_t)blockIdx.x * ROWS;
   const int rows = (int)min<int64_t>(ROWS, a.M - m0);
@@ -63,25 +59,11 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
       }
     }
   };
-  mlp_rows<RT>(a.L, a.nl, a.K0, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, a.y, a.ldy, tid, stage);
-  MLP_MARK(3 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. head)
-#ifdef RK_MLP_PHASES
-  if (tid == 0) {
-    const unsigned long long w1 = wall_clock64();
-    atomicMax(&g_mlp_span[1], w1);
-    atomicMax(&g_mlp_span[3], w1 - w0);  // longest workgroup
-    atomicAdd(&g_mlp_span[4], w1 - w0);  // sum of workgroup durations
-    unsigned hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    if (blockIdx.x < 8192) {
-      g_mlp_wg[blockIdx.x][0] = hw;
-      g_mlp_wg[blockIdx.x][1] = xcc;
-      g_mlp_wg[blockIdx.x][2] = (unsigned)(w1 - w0);
-      g_mlp_wg[blockIdx.x][3] = (unsigned)(w0 - g_mlp_span[0]);
-    }
-  }
-#endif
+  mlp_rows<RT, STORE>(a.L, a.nl, a.K0, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, a.y, a.ldy, tid,
+                      finish_only(stage));
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. head)
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
+  MLP_FLUSH(tid);
 }
 
 // Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): per 16-row tile, wave w
@@ -93,10 +75,24 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
 // rk_mlp_forward (two launches and an x0 / partial round trip through HBM).
 constexpr int kDcnSegs = 8;
 constexpr int kDcnPerLane = 4;  // width <= 256
+constexpr int kDcnPreLayers = 3;  // cross layers whose weights are fetched with the row values
+
+// The gather plan of the stage, with every slot loadable unconditionally: a dense segment (and an
+// unused slot) reads its "index" from the device flag word (ignored; the row is the sample), an
+// unused slot has out_col past the width, so no column selects it.
+struct DcnSeg {
+  const float* src;
+  const int64_t* idx;  // never null
+  int64_t idx_stride;  // 0 for dense / unused slots
+  int64_t src_ld;
+  int64_t rows;        // bounds of a table; INT64_MAX for dense / unused slots
+  int32_t out_col;
+  int32_t dense;
+};
 
 struct DcnArgs {
   MlpArgs m;
-  rk_segment segs[kDcnSegs];
+  DcnSeg segs[kDcnSegs];
   int nseg;
   const float* cross_w;
   const float* cross_b;
@@ -105,61 +101,140 @@ struct DcnArgs {
   uint32_t* flags;
 };
 
+// NJ = column groups of 64 per lane (1: width <= 64, the DCN wechat row of 50; 4: width <= 256)
+template <int NJ>
 __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+#ifdef RK_MLP_PHASES
+  const unsigned long long k_t0 = clock64();
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
+#endif
   const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
   const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
   float* const buf0 = sm;
   float* const buf1 = sm + a.m.off1;
   float* const part = buf1 + kMlpRows * a.m.ld1;
   const int width = a.m.K0;
-  auto stage = [&]() {
+  // Two memory round trips per row instead of one dependent index -> row chain per column: (1) the
+  // sample's row index in every segment (wave-uniform loads), (2) the row values of the lane's
+  // columns together with the cross weights, the cross biases and the cross half of output_layer.
+  // Out-of-range indices read row 0 with the value forced to zero and raise RK_FLAG_INDEX_OOB.
+  // stage state carried from issue() (before layer 0's weight prefetch) to the finish
+  const int nl = a.num_layers;
+  float x0[NJ], xl[NJ], cw[kDcnPreLayers][NJ], cb[kDcnPreLayers][NJ], hw[NJ];
+  auto stage_issue = [&]() {
     const int64_t b = m0 + wave;
     const bool live = wave < rows;
-    const int K0p = pad64(width);
-    float x0[kDcnPerLane], xl[kDcnPerLane];
+    const int64_t bb = live ? b : m0;
+    // round trip 1: the sample's row in every segment — lane t loads segment t's index (one vector
+    // load per wave; 8 scalar loads measured ~2.4 us at kernel start), then every lane reads them
+    // back (wave-uniform)
+    int64_t rix[kDcnSegs];
+    {
+      const int64_t* ip = a.segs[0].idx;
+      int64_t st = a.segs[0].idx_stride;
 #pragma unroll
-    for (int j = 0; j < kDcnPerLane; ++j) {
-      const int c = lane + 64 * j;
-      float v = 0.f;
-      if (live && c < width) {
-        int s = 0;
-        for (int t = 1; t < a.nseg; ++t) s = c >= a.segs[t].out_col ? t : s;  // out_col ascending
-        const float* row = segment_row(a.segs[s], b, a.flags);
-        if (row) v = row[c - a.segs[s].out_col];
+      for (int t = 1; t < kDcnSegs; ++t)
+        if (lane == t) ip = a.segs[t].idx, st = a.segs[t].idx_stride;
+      const int64_t mine = ip[bb * st];
+#pragma unroll
+      for (int t = 0; t < kDcnSegs; ++t) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, t);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)mine >> 32), t);
+        rix[t] = (int64_t)(((uint64_t)hi << 32) | lo);
       }
-      x0[j] = xl[j] = v;
-      if (c < K0p) buf0[wave * a.m.ld0 + c] = v;
     }
-    for (int l = 0; l < a.num_layers; ++l) {
-      float d = 0.f;
+    bool bad = false;
 #pragma unroll
-      for (int j = 0; j < kDcnPerLane; ++j) {
+    for (int t = 0; t < kDcnSegs; ++t) {
+      if (a.segs[t].dense) rix[t] = bb;
+      const bool okt = rix[t] >= 0 && rix[t] < a.segs[t].rows;
+      bad = bad || !okt;
+      rix[t] = okt ? rix[t] : -1;  // -1: zero row (read row 0, value dropped)
+    }
+    if (bad && live && lane == 0) flag_oob(a.flags);
+    // round trip 2: the lane's row values, the cross weights / biases of the first layers and the
+    // cross half of output_layer
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      x0[j] = hw[j] = 0.f;
+#pragma unroll
+      for (int l = 0; l < kDcnPreLayers; ++l) cw[l][j] = cb[l][j] = 0.f;
+      {
         const int c = lane + 64 * j;
-        if (c < width) d = fmaf(xl[j], a.cross_w[(int64_t)l * width + c], d);
+        const int cc = min(c, width - 1);
+        const float* src = a.segs[0].src;
+        int64_t r = rix[0], ld = a.segs[0].src_ld;
+        int col = cc;
+#pragma unroll
+        for (int t = 1; t < kDcnSegs; ++t) {
+          const bool sel = cc >= a.segs[t].out_col;  // out_col ascending
+          src = sel ? a.segs[t].src : src;
+          r = sel ? rix[t] : r;
+          ld = sel ? a.segs[t].src_ld : ld;
+          col = sel ? cc - a.segs[t].out_col : col;
+        }
+        const float v = src[(r < 0 ? 0 : r) * ld + col];
+        x0[j] = (live && c < width && r >= 0) ? v : 0.f;
+#pragma unroll
+        for (int l = 0; l < kDcnPreLayers; ++l)
+          if (l < nl) {
+            cw[l][j] = a.cross_w[(int64_t)l * width + cc];
+            cb[l][j] = a.cross_b[(int64_t)l * width + cc];
+          }
+        hw[j] = a.cross_head_w[cc];
       }
-      d = wave_sum(d);
+    }
+  };
+  auto stage_finish = [&]() {
+    const int K0p = pad64(width);
 #pragma unroll
-      for (int j = 0; j < kDcnPerLane; ++j) {
-        const int c = lane + 64 * j;
-        if (c < width) {
-          float t = x0[j] * d;                        // torch.mul(x0, xl_wl)
-          t = t + a.cross_b[(int64_t)l * width + c];  // + bl.t()
-          xl[j] = t + xl[j];                          // + xl
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      xl[j] = x0[j];
+      if (c < K0p) buf0[wave * a.m.ld0 + c] = x0[j];
+    }
+    for (int l = 0; l < nl; ++l) {
+      float w[NJ], bl[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        w[j] = cw[0][j];
+        bl[j] = cb[0][j];
+#pragma unroll
+        for (int q = 1; q < kDcnPreLayers; ++q)
+          if (q == l) w[j] = cw[q][j], bl[j] = cb[q][j];
+        if (l >= kDcnPreLayers) {
+          const int c = min(lane + 64 * j, width - 1);
+          w[j] = a.cross_w[(int64_t)l * width + c];
+          bl[j] = a.cross_b[(int64_t)l * width + c];
         }
       }
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (lane + 64 * j < width) d = fmaf(xl[j], w[j], d);
+      d = wave_sum(d);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (lane + 64 * j < width) {
+          float t = x0[j] * d;   // torch.mul(x0, xl_wl)
+          t = t + bl[j];         // + bl.t()
+          xl[j] = t + xl[j];     // + xl
+        }
     }
     float p = 0.f;
 #pragma unroll
-    for (int j = 0; j < kDcnPerLane; ++j) {
-      const int c = lane + 64 * j;
-      if (c < width) p = fmaf(xl[j], a.cross_head_w[c], p);
-    }
+    for (int j = 0; j < NJ; ++j)
+      if (lane + 64 * j < width) p = fmaf(xl[j], hw[j], p);
     p = wave_sum(p);
     if (lane == 0) part[wave] = p;
   };
-  mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid, stage, part);
+  mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
+           two_phase(stage_issue, stage_finish), part);
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
+  MLP_FLUSH(tid);
 }
 
 // Fragment-major image (mlp_core.h wfrag): element i of the image is lane (i >> 2) & 63, component
@@ -267,14 +342,30 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   if (M == 0) return RK_OK;
   const int64_t blocks = (M + rows_per_wg - 1) / rows_per_wg;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward: M too large");
-  raise_lds_limit((const void*)mlp_kernel<1>, 160 * 1024);
-  raise_lds_limit((const void*)mlp_kernel<2>, 160 * 1024);
+  bool store = false;  // hidden activations written out (training); eval compiles the path out
+  for (int l = 0; l < nlayers; ++l) store = store || layers[l].store != nullptr;
+  auto go = [&](auto kern) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  };
   if (rt == 2)
-    mlp_kernel<2><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+    store ? go(mlp_kernel<2, true>) : go(mlp_kernel<2, false>);
   else
-    mlp_kernel<1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+    store ? go(mlp_kernel<1, true>) : go(mlp_kernel<1, false>);
   return check_launch("rk_mlp_forward");
 }
+
+#ifdef RK_MLP_PHASES
+// Timing build only (tools/dcn_phases.py): copies and clears this module's phase counters.
+RK_API int rk_debug_mlp_phases(unsigned long long* marks, int32_t nwg, unsigned* wave_marks) {
+  if (nwg < 0 || nwg > kMlpMarkWG) return 1;
+  if (hipMemcpyFromSymbol(marks, HIP_SYMBOL(g_mlp_marks), sizeof(g_mlp_marks[0]) * nwg) != hipSuccess) return 1;
+  if (wave_marks &&
+      hipMemcpyFromSymbol(wave_marks, HIP_SYMBOL(g_mlp_wave_marks), sizeof(g_mlp_wave_marks[0]) * nwg) != hipSuccess)
+    return 1;
+  return 0;
+}
+#endif
 
 RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t width, const float* cross_w,
                           const float* cross_b, int32_t num_layers, const float* cross_head_w,
@@ -289,13 +380,34 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
     return fail(RK_ERR_INVALID, "rk_dcn_forward: the cross partial comes from the kernel (no head_partial / fm1)");
   int need0 = 0, need1 = 0;
   if (int e = mlp_validate(layers, nlayers, width, a.m.head, &need0, &need1, "rk_dcn_forward")) return e;
+  uint32_t* flags = device_flags();
+  if (!flags) return fail(RK_ERR_RUNTIME, "rk_dcn_forward: device not initialised (rk_init)");
   int prev = -1;
-  for (int i = 0; i < nseg; ++i) {
+  for (int i = 0; i < kDcnSegs; ++i) {
+    DcnSeg& d = a.segs[i];
+    if (i >= nseg) {  // unused slot: never selected, loads stay inside the flag word
+      d = DcnSeg{reinterpret_cast<const float*>(flags), reinterpret_cast<const int64_t*>(flags), 0, 0, INT64_MAX,
+                 INT32_MAX, 1};
+      continue;
+    }
     const rk_segment& g = segs[i];
     if (!g.src || g.dim <= 0 || g.out_col <= prev || g.out_col + g.dim > width || (g.idx && g.rows <= 0))
       return fail(RK_ERR_INVALID, "rk_dcn_forward: segment %d (out_col ascending, inside width)", i);
     prev = g.out_col;
-    a.segs[i] = g;
+    d.src = g.src;
+    d.src_ld = g.src_ld;
+    d.out_col = g.out_col;
+    if (g.idx) {
+      d.idx = g.idx;
+      d.idx_stride = g.idx_stride;
+      d.rows = g.rows;
+      d.dense = 0;
+    } else {
+      d.idx = reinterpret_cast<const int64_t*>(flags);
+      d.idx_stride = 0;
+      d.rows = INT64_MAX;
+      d.dense = 1;
+    }
   }
   if (segs[0].out_col != 0) return fail(RK_ERR_INVALID, "rk_dcn_forward: segments must start at column 0");
   for (int l = 0; l < nlayers; ++l) a.m.L[l] = layers[l];
@@ -306,17 +418,22 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   a.m.M = batch;
   a.m.K0 = width;
   a.nseg = nseg;
-  a.cross_w = cross_w;
-  a.cross_b = cross_b;
+  // the stage loads cross weights unconditionally (layer index clamped): any valid pointer will do
+  // when there are no cross layers
+  a.cross_w = num_layers > 0 ? cross_w : cross_head_w;
+  a.cross_b = num_layers > 0 ? cross_b : cross_head_w;
   a.num_layers = num_layers;
   a.cross_head_w = cross_head_w;
-  a.flags = device_flags();
+  a.flags = flags;
   const size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
-  raise_lds_limit((const void*)dcn_fused_kernel, 160 * 1024);
-  dcn_fused_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  auto go = [&](auto kern) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  };
+  width <= 64 ? go(dcn_fused_kernel<1>) : go(dcn_fused_kernel<kDcnPerLane>);
   return check_launch("rk_dcn_forward");
 }

@@ -14,14 +14,32 @@
 // 38k -> 8k cycles; DIN 48.8 -> 51.4 M samples/s).
 #pragma once
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace rk {
+
+#ifndef RK_MLP_EPI_PRIO
+#define RK_MLP_EPI_PRIO 1
+#endif
+// Lockstep within a layer: every kMlpSyncChunks K-chunks all waves meet at a barrier.  Without it
+// the SIMD's matrix pipe serves its 4 waves oldest-first: in DCN's 512 -> 256 layer wave w
+// finished its MFMAs at 10.2k / 13.5k / 17.6k / 21.5k cycles for w = 0..3 / 4..7 / 8..11 /
+// 12..15 (tools/dcn_phases.py), and the last wave of each SIMD, running alone, could not cover
+// the L2 latency of its weight ring with its own 8 chunks of MFMAs.
+#ifndef RK_MLP_SYNC
+#define RK_MLP_SYNC 1
+#endif
 
 constexpr int kMlpRows = 16;
 constexpr int kMlpWaves = 16;
 constexpr int kMlpThreads = 64 * kMlpWaves;
 constexpr int kMlpPD = 4;    // prefetch depth (chunks)
+constexpr int kMlpSyncChunks = 8;  // RK_MLP_SYNC barrier interval (K-chunks of 16)
+
+// A bare s_barrier: no wait on this wave's memory counters (the weight ring stays in flight).
+__device__ __forceinline__ void mlp_sync_barrier() { asm volatile("s_barrier"); }
 
 constexpr int kMlpPad = 64;  // K and N padding of packed weights
 constexpr int kMlpMaxN = 512;
@@ -85,20 +103,46 @@ __device__ __forceinline__ float col_apply(const ColEpi& e, bool dice, float z, 
   return z * e.post_s + e.post_b;
 }
 
-// Optional per-layer shader-clock counters (tools/mlp_phases.hip builds with RK_MLP_PHASES):
-// g_mlp_phase[3*l + {0,1,2}] += cycles from the layer's start to (MFMA loop done, epilogue
-// stored, barrier passed), wave 0 of each workgroup.
+// Optional per-workgroup phase marks (timing builds with RK_MLP_PHASES: tools/dcn_phases.py,
+// tools/din_phases.py).  Wave 0 keeps clock64() deltas in LDS (no memory traffic while the kernel
+// runs: global atomics here used to stall every later vmcnt wait of the wave); the kernel's last
+// step copies them to g_mlp_marks[workgroup]:
+//   [4l + {0,1,2,3}]  cycles from layer l's start to: MFMA loop issued, epilogue stored, the next
+//                     layer's prepare issued, barrier passed
+//   [4L]              mlp_rows prologue (input staged, layer 0 weights in flight)
+//   [4L + 1]          whole workgroup (kernel entry to end), [4L + 2 / 3] wall clock at entry / end
 #ifdef RK_MLP_PHASES
-__device__ unsigned long long g_mlp_phase[3 * RK_MLP_MAX_LAYERS + 2];
-__device__ unsigned long long g_mlp_span[5];  // wall_clock64 (100 MHz): first start, last end, last start, max, sum
-__device__ unsigned g_mlp_wg[8192][4];  // per workgroup: HW_ID, XCC_ID, wall duration, start offset (10 ns)
-#define MLP_MARK(i, t0) \
-  do {                  \
-    if (tid == 0) atomicAdd(&g_mlp_phase[i], clock64() - (t0)); \
+constexpr int kMlpMarks = 4 * RK_MLP_MAX_LAYERS + 4;
+constexpr int kMlpMarkWG = 8192;
+__device__ unsigned long long g_mlp_marks[kMlpMarkWG][kMlpMarks];
+__shared__ unsigned long long s_mlp_marks[kMlpMarks];
+// per wave, layers 0..3: cycles from the layer's start to its MFMA loop issued / epilogue stored
+__device__ unsigned g_mlp_wave_marks[kMlpMarkWG][4][16][2];
+__shared__ unsigned s_mlp_wave_marks[4][16][2];
+#define MLP_MARK(i, t0)                                   \
+  do {                                                    \
+    if (tid == 0) s_mlp_marks[i] = clock64() - (t0);      \
   } while (0)
+#define MLP_WALL(i)                                       \
+  do {                                                    \
+    if (tid == 0) s_mlp_marks[i] = wall_clock64();        \
+  } while (0)
+__device__ __forceinline__ void mlp_marks_flush(int tid) {
+  __syncthreads();
+  if (tid < kMlpMarks && blockIdx.x < kMlpMarkWG) g_mlp_marks[blockIdx.x][tid] = s_mlp_marks[tid];
+  if (tid < 4 * 16 * 2 && blockIdx.x < kMlpMarkWG)
+    (&g_mlp_wave_marks[blockIdx.x][0][0][0])[tid] = (&s_mlp_wave_marks[0][0][0])[tid];
+}
+#define MLP_FLUSH(tid) mlp_marks_flush(tid)
 #else
 #define MLP_MARK(i, t0) \
   do {                  \
+  } while (0)
+#define MLP_WALL(i) \
+  do {              \
+  } while (0)
+#define MLP_FLUSH(tid) \
+  do {                 \
   } while (0)
 #endif
 
@@ -116,25 +160,34 @@ struct LayerPipe {
   f32x4_t ring[kMlpRing];
   ColEpi ep[2];
   template <int TPW, int PD>
-  __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int wave, int lane) {
+  __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int kchunks, int wave, int lane) {
     static_assert(TPW * PD <= kMlpRing, "ring overflow");
     const int li = lane & 15;
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      const int n = 16 * (wave + kMlpWaves * j) + li;
-      wrow[j] = wfrag(L, wave + kMlpWaves * j, lane);
-      ep[j] = col_epi(L, n < L.n ? n : 0);
-    }
+    for (int j = 0; j < TPW; ++j) wrow[j] = wfrag(L, wave + kMlpWaves * j, lane);
+    // issue the ring in consumption order (slot-major): the MFMA loop's vmcnt waits assume that
+    // ring register k is the k-th outstanding load; a reordered prepare (the scheduler groups
+    // loads by base address) makes every wait of the loop that follows it conservative.  The ring
+    // goes first: nothing is outstanding in front of it, so reloading the ring registers costs no
+    // wait; the epilogue parameters behind it are consumed only after the whole loop.
 #pragma unroll
     for (int s = 0; s < PD; ++s)
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * s);
+      for (int j = 0; j < TPW; ++j) {
+        ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * min(s, kchunks - 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int n = 16 * (wave + kMlpWaves * j) + li;
+      ep[j] = col_epi(L, n < L.n ? n : 0);
+    }
   }
 };
 
 // One layer (weights already in flight in P) over RT row tiles of 16 rows: each weight float4
-// feeds RT x 4 MFMAs.  kchunks = Kp / 16 must be a multiple of PD.
-template <int TPW, int RT, int PD>
+// feeds RT x 4 MFMAs.  kchunks = Kp / 16 (a multiple of 4).
+template <int TPW, int RT, int PD, bool STORE>
 __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, const float* __restrict__ in,
                                           int ldin, float* __restrict__ out, int ldout, int Kp, int wave, int lane,
                                           int64_t m0, int rows, int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
@@ -147,44 +200,76 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
     for (int t = 0; t < RT; ++t) acc[j][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const float* arow = in + li * ldin + kq;
-  // A float4s run one chunk ahead of their MFMAs (the sched_barrier below keeps the compiler
-  // from hoisting the next chunk's reads itself)
-  f32x4_t an[RT];
+  // A float4s run one chunk ahead of their MFMAs in two explicit register sets (slot s reads set
+  // s & 1 and loads chunk c + 1 into the other; PD is even, so the parity of a chunk is the parity
+  // of its slot).  With one set the copy av = an was coalesced away and the next chunk's
+  // ds_read_b128 had to wait for this chunk's MFMAs to read their operands: every slot then
+  // opened with the full LDS latency exposed.
+  f32x4_t ab[2][RT];
 #pragma unroll
-  for (int t = 0; t < RT; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin);
-  for (int c0 = 0; c0 < kchunks; c0 += PD) {
+  for (int t = 0; t < RT; ++t) ab[0][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin);
+  // One ring cycle (PD chunks starting at c0); REFILL loads chunk c + PD into the slot just used.
+  // The last cycle issues no refill: a load past the end would still be in flight at the
+  // epilogue, and the next layer's prepare() (which reloads the same ring registers) would have
+  // to drain it with a full vmcnt(0) — the 4-7k-cycle "epilogue" of the round-2 phase counters.
+  auto cycle = [&](int c0, int nslots, auto refill) {
 #pragma unroll
     for (int s = 0; s < PD; ++s) {
-      const int c = c0 + s;
-      f32x4_t av[RT];
+      if (s < nslots) {  // nslots == PD except the last cycle of a reduction that is not a multiple of PD
+        const int c = c0 + s;
+        const int cA = min(c + 1, kchunks - 1);
 #pragma unroll
-      for (int t = 0; t < RT; ++t) av[t] = an[t];
-      const int cA = min(c + 1, kchunks - 1);
+        for (int t = 0; t < RT; ++t)
+          ab[(s + 1) & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin + 16 * cA);
+        __builtin_amdgcn_sched_barrier(0);  // the read goes out before this slot's MFMAs
 #pragma unroll
-      for (int t = 0; t < RT; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin + 16 * cA);
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+          for (int j = 0; j < TPW; ++j)
 #pragma unroll
-        for (int j = 0; j < TPW; ++j)
+            for (int t = 0; t < RT; ++t) acc[j][t] = mfma16(ab[s & 1][t][e], P.ring[s * TPW + j][e], acc[j][t]);
+        if constexpr (decltype(refill)::value) {
+          const int cn = min(c + PD, kchunks - 1);  // clamped only when kchunks % PD != 0
 #pragma unroll
-          for (int t = 0; t < RT; ++t) acc[j][t] = mfma16(av[t][e], P.ring[s * TPW + j][e], acc[j][t]);
-      // refill this slot with chunk c + PD (clamped: the tail re-reads the last chunk, unused)
-      const int cn = min(c + PD, kchunks - 1);
-#pragma unroll
-      for (int j = 0; j < TPW; ++j)
-        P.ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + kFragStep * cn);
+          for (int j = 0; j < TPW; ++j)
+            P.ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(P.wrow[j] + kFragStep * cn);
+        }
+      }
       // keep the refill here: sinking it to the end of the unrolled body would leave each
       // slot's latency uncovered by the other slots' MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  int c0 = 0;
+  for (; c0 + PD < kchunks; c0 += PD) {
+    cycle(c0, PD, std::true_type{});
+#if RK_MLP_SYNC
+    if ((c0 + PD) % kMlpSyncChunks == 0) mlp_sync_barrier();
+#endif
+  }
+  if (kchunks - c0 == PD) {
+    cycle(c0, PD, std::false_type{});
+  } else {
+    cycle(c0, kchunks - c0, std::false_type{});
+    // the slots this short cycle left unused still hold clamped loads: drain them here, so the
+    // state after this layer is the same on both paths (no pending ring load for the next
+    // prepare() to wait behind)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only (lgkmcnt / expcnt at their maximum)
   }
 
 #ifdef RK_MLP_PHASES
-  if (wave == 0 && lane == 0) atomicAdd(&g_mlp_phase[dbg_mark], clock64() - dbg_t0);
+  if (wave == 0 && lane == 0) s_mlp_marks[dbg_mark] = clock64() - dbg_t0;
+  if (lane == 0 && dbg_mark / 4 < 4) s_mlp_wave_marks[dbg_mark / 4][wave][0] = (unsigned)(clock64() - dbg_t0);
+#endif
+#if RK_MLP_EPI_PRIO
+  // this wave's MFMAs are all issued: its epilogue and the next layer's prepare are on the
+  // layer boundary's critical path, so let them win issue arbitration against the waves of the
+  // SIMD still in their MFMA loops (reset to 0 after the barrier)
+  __builtin_amdgcn_s_setprio(2);
 #endif
   const bool dice = L.act == RK_ACT_DICE;
   const bool has_res = L.residual != 0;
-  float* const store = L.store;
+  float* const store = STORE ? L.store : nullptr;  // eval kernels compile the store path out
   const int64_t ld_store = L.ld_store;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
@@ -204,9 +289,13 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
         const float z =
             real ? col_apply(P.ep[j], dice, acc[j][t][r], has_res, res[t][r]) : 0.f;
         out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
-        if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
+        if constexpr (STORE)
+          if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
       }
   }
+#ifdef RK_MLP_PHASES
+  if (lane == 0 && dbg_mark / 4 < 4) s_mlp_wave_marks[dbg_mark / 4][wave][1] = (unsigned)(clock64() - dbg_t0);
+#endif
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its global
@@ -216,33 +305,50 @@ __device__ __forceinline__ void mlp_lds_barrier() { asm volatile("s_waitcnt lgkm
 // Runs layers[0..nl) on the 16*RT rows staged (zero-padded to pad64(K0) columns) in buf0, then
 // the head (one wave per row) or a plain copy of the last activation to y.  Must be called by
 // all kMlpThreads threads of the workgroup.
-// `stage()` (default: nothing) fills buf0 after layer 0's weights are already in flight, so the
-// two memory round trips that open the workgroup overlap; a barrier follows it.
+// The stage fills buf0 in two calls around layer 0's weight prefetch: stage.issue() runs first
+// (the gather's own loads go out ahead of the 8 ring loads per wave, which would otherwise queue
+// in front of them in the CU's memory pipeline), stage() after it (the rest, then a barrier).
 struct NoStage {
+  __device__ void issue() const {}
   __device__ void operator()() const {}
 };
+template <class I, class F>
+struct TwoPhaseStage {
+  I i;
+  F f;
+  __device__ void issue() { i(); }
+  __device__ void operator()() { f(); }
+};
+template <class I, class F>
+__device__ __forceinline__ TwoPhaseStage<I, F> two_phase(I i, F f) {
+  return TwoPhaseStage<I, F>{i, f};
+}
+template <class F>
+__device__ __forceinline__ auto finish_only(F f) {
+  return two_phase([] {}, f);
+}
 
 // `lds_partial` (optional): per-row head partials the stage left in LDS (DCN's cross half of
 // output_layer), used instead of h.head_partial.
-template <int RT = 1, class Stage = NoStage>
+template <int RT = 1, bool STORE = false, class Stage = NoStage>
 __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers, int nl, int K0, float* buf0,
                                          int ld0, float* buf1, int ld1, int64_t m0, int rows,
                                          const rk_epilogue& h, float* y, int64_t ldy, int tid,
                                          Stage stage = Stage(), const float* lds_partial = nullptr) {
-  const int lane = tid & 63, wave = tid >> 6;
+  // wave index as an SGPR: the per-wave tile / variant choices become scalar branches
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   LayerPipe pipe;
-  // one-tile layers with a reduction of a multiple of 128 run the 8-deep ring
-  auto deep = [&](int l) { return (pad64(l ? layers[l - 1].n : K0) / 16) % 8 == 0; };
+  // Ring discipline shared by every layer variant: 8 loads in flight, ring register k is always the
+  // k-th outstanding load (two-tile layers: 4 chunks x 2 tiles, one-tile layers: 8 chunks), so
+  // the loop after any prepare() gets the same vmcnt waits.  (A 4-deep one-tile variant used to
+  // merge into the 8-deep loop's entry and cut every one of its waits from vmcnt(7) to vmcnt(3).)
   auto prepare = [&](int l) {
     const int nt = pad64(layers[l].n) / 16;  // multiple of 4
+    const int kch = pad64(l ? layers[l - 1].n : K0) / 16;
     if (wave + kMlpWaves < nt)
-      pipe.prepare<2, 4>(layers[l], wave, lane);
-    else if (wave < nt) {
-      if (deep(l))
-        pipe.prepare<1, 8>(layers[l], wave, lane);
-      else
-        pipe.prepare<1, 4>(layers[l], wave, lane);
-    }
+      pipe.prepare<2, 4>(layers[l], kch, wave, lane);
+    else if (wave < nt)
+      pipe.prepare<1, 8>(layers[l], kch, wave, lane);
   };
   // The head's operands (head_w for this lane's columns, this wave's row scalars) are loaded while
   // the last layer runs: fetched after the final barrier they put two dependent L2 round trips
@@ -261,11 +367,13 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
 #ifdef RK_MLP_PHASES
   const unsigned long long t_start = clock64();
 #endif
+  stage.issue();
   if (nl > 0) prepare(0);
   if (nl <= 1) head_prefetch();
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS - 4, t_start);  // (timing builds: the last layer's slots, unused here)
   stage();
   mlp_lds_barrier();
-  MLP_MARK(3 * RK_MLP_MAX_LAYERS, t_start);  // prologue: input staged, layer 0 weights in flight
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS, t_start);  // prologue: input staged, layer 0 weights in flight
   int Kp = pad64(K0);
   for (int l = 0; l < nl; ++l) {
     const unsigned long long t0 =
@@ -280,18 +388,22 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
     if (wave + kMlpWaves < ntiles)
-      mlp_layer<2, RT, 4>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
-    else if (wave < ntiles) {
-      if (deep(l))
-        mlp_layer<1, RT, 8>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
-      else
-        mlp_layer<1, RT, 4>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 3 * l, t0);
-    }
+      mlp_layer<2, RT, 4, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 4 * l, t0);
+    else if (wave < ntiles)
+      mlp_layer<1, RT, 8, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 4 * l, t0);
+#if RK_MLP_SYNC
+    else  // no tile in this layer: take part in the active waves' lockstep barriers
+      for (int i = 0; i < (Kp / 16 - 1) / kMlpSyncChunks; ++i) mlp_sync_barrier();
+#endif
+    MLP_MARK(4 * l + 1, t0);
     if (l + 1 < nl) prepare(l + 1);
     if (l + 2 == nl) head_prefetch();
-    MLP_MARK(3 * l + 1, t0);
+    MLP_MARK(4 * l + 2, t0);
     mlp_lds_barrier();
-    MLP_MARK(3 * l + 2, t0);
+#if RK_MLP_EPI_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    MLP_MARK(4 * l + 3, t0);
     Kp = pad64(L.n);
   }
   const float* fin = (nl & 1) ? buf1 : buf0;

@@ -34,7 +34,11 @@ void raise_lds_limit(const void* kern, int bytes) {
   std::lock_guard<std::mutex> lock(g_mu);
   for (int i = 0; i < n; ++i)
     if (done[i].kern == kern && done[i].dev == dev && done[i].bytes >= bytes) return;
-  (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  // static LDS (timing builds add some) counts against the same 160 KiB
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, kern) == hipSuccess) bytes = std::min<int>(bytes, 160 * 1024 - (int)fa.sharedSizeBytes);
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+    (void)hipGetLastError();  // leave no sticky error for the launch check that follows
   if (n < 256) done[n++] = Entry{kern, dev, bytes};
 }
 

@@ -24,7 +24,7 @@ from rankops import _lib  # noqa: E402
 lib = _lib.load()
 ts = (ctypes.c_ulonglong * (1024 * 4))()
 wv = (ctypes.c_ulonglong * (1024 * 16))()
-ml = (ctypes.c_ulonglong * (3 * 8 + 2))()
+ml = (ctypes.c_ulonglong * (1024 * (4 * 8 + 4)))()
 lib.rk_debug_din_phases.argtypes = [ctypes.c_void_p] * 3
 assert lib.rk_debug_din_phases(ts, wv, ml) == 0
 nwg = min(1024, (batch + 15) // 16)
@@ -48,8 +48,8 @@ print("end          ", q(rel[:, 3]))
 print("wave A cycles", q(w.reshape(-1) / 1e3), "(k cycles)")
 print("wave A max/mean per WG", q(w.max(1) / np.maximum(w.mean(1), 1)))
 print("lengths: mean", lens.mean(), "frac <= 32:", (lens <= 32).mean())
-mlp = np.array(ml, dtype=np.float64)
+mlp = np.array(ml, dtype=np.float64).reshape(1024, 4 * 8 + 4)[:nwg] / 1e3
 if mlp.any():
-    per = mlp / (n_launch * nwg) / 1e3
+    print(f"phase B prologue {np.median(mlp[:, 32]):6.2f}k cycles (median over workgroups, wave 0)")
     for l in range(3):
-        print(f"layer {l}: mfma done {per[3*l]:6.2f}  epilogue stored {per[3*l+1]:6.2f}  barrier {per[3*l+2]:6.2f} (k cycles, wave 0)")
+        print(f"layer {l}: mfma issued {q(mlp[:, 4*l])} | epilogue {q(mlp[:, 4*l+1])} | prepare {q(mlp[:, 4*l+2])} | barrier {q(mlp[:, 4*l+3])}")
