@@ -51,6 +51,7 @@ DEEPFM_GATHER_BYTES = 30 * (8 + 128 + 4) + 30 * 128 + 8  # 8,048 B: gather+FM ke
 BST_BLOCK_FLOP = 14_680_064
 FWFM_BYTES_PER_SAMPLE = 6 * (8 + 32 + 4) + 4
 DCN_FLOP = 379_236
+ZIPF_A = 1.1  # Zipf(1.1) index variant for cache sensitivity
 
 
 def parse():
@@ -63,7 +64,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call")
+    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call,din_zipf,"
+                                        "dcn_eager,din_eager,deepfm_eager,bst_eager")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step legs")
     return ap.parse_args()
@@ -99,10 +101,12 @@ def max_over_ranks(world, value: float) -> float:
 
 # ------------------------------------------------------------------ workloads
 
-def workload(name: str, batch: int, seed: int):
-    """(model, inputs, call, cfg) for a benchmark workload, built directly on the GPU."""
+def workload(name: str, batch: int, seed: int, zipf: float = None):
+    """(model, inputs, call, cfg) for a benchmark workload, built directly on the GPU.  `zipf`:
+    table indices drawn from Zipf(zipf) popularity instead of uniformly."""
     import helpers as H
     dev = torch.device("cuda", torch.cuda.current_device())
+    name = name[:-len("_eager")] if name.endswith("_eager") else name
     if name in ("din", "din_per_call"):
         cfg = {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 32,
                "interaction_weights": "frozen" if name == "din" else "per_call"}
@@ -124,6 +128,8 @@ def workload(name: str, batch: int, seed: int):
     with torch.device(dev):
         model = H.build(model_name, cfg, seed=42)
     model = model.to(dev).eval()
+    if zipf is not None:
+        cfg = dict(cfg, zipf=zipf)
     inp = H.to_device(H.make_inputs(model_name, cfg, batch, seed=1000 + seed), dev)
     return model, inp, (lambda: H.call_model(model, model_name, inp)), cfg, model_name
 
@@ -209,13 +215,14 @@ def _frozen_interaction(name, cfg):
     return None
 
 
-def cpu_baseline(name, model, cfg, batch, budget_s, frozen):
+def cpu_baseline(name, model, cfg, batch, budget_s, frozen, threads=None):
     """The oracle (CPU restatement of the reference forward) on this host, on a bounded sample:
     repeated forwards of batch `batch` until ~budget_s.  `frozen` times the same H2 mode as the
     GPU headline (interaction MLP drawn once); otherwise every call redraws it from the CPU
     generator as the reference does."""
     import helpers as H
-    n = min(16, len(os.sched_getaffinity(0)))
+    n = threads or min(16, len(os.sched_getaffinity(0)))
+    prev_threads = torch.get_num_threads()
     torch.set_num_threads(n)
     p = H.cpu_params(model)
     cfg_cpu = dict(cfg)
@@ -231,6 +238,7 @@ def cpu_baseline(name, model, cfg, batch, budget_s, frozen):
             el = time.perf_counter() - t0
             if el >= budget_s or iters >= 2000:
                 break
+    torch.set_num_threads(prev_threads)
     mode = "H2 weights frozen (drawn once)" if frozen else "per-call H2 draws included"
     return {"value": round(iters * batch / el, 1), "unit": "samples/s", "cores": n, "kind": "port",
             "sample": f"{iters} oracle {name.upper()} forwards of batch {batch} ({el:.1f} s, {mode}, fp32, "
@@ -263,6 +271,15 @@ def cpu_baselines(model, cfg, head_value, extras, batch, budget_s):
             leg["gpu_over_cpu"] = round(leg["gpu_samples_per_s"] / leg["value"], 1)
         legs[key] = leg
     legs["dcn_4096"]["target"] = ">= 10x (BASELINE.json north star, DCN batch 4096, 1 MI355X)"
+    # single-threaded ("It is also reported single-threaded")
+    for key, nm, mdl, c, b, gpu_v in (("din_1thread", "din", model, cfg, batch, head_value),
+                                      ("dcn_4096_1thread", "dcn", dcn, dcn_cfg, 4096,
+                                       extras.get("dcn", {}).get("samples_per_s"))):
+        leg = cpu_baseline(nm, mdl, c, b, budget_s / 3, True, threads=1)
+        if gpu_v:
+            leg["gpu_samples_per_s"] = gpu_v
+            leg["gpu_over_cpu"] = round(gpu_v / leg["value"], 1)
+        legs[key] = leg
     out["legs"] = legs
     return out
 
@@ -509,34 +526,51 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
     out = {"kernel": "fm_gather_kernel<8>", "bound": "hbm", "peak": PEAK_HBM / 1e9, "unit": "GB/s",
            "bytes_per_sample": DEEPFM_GATHER_BYTES,
            "tables": "30 fields x 1,000,000 rows x 32 fp32 (3.84 GB) + 30 x 1e6 x 1 (beyond the 256 MiB MALL)"}
-    for b, cat in ((batch, inp["category"]),
-                   (big_batch, H.to_device(H.make_inputs("deepfm", cfg, big_batch, seed=1234),
-                                           torch.device("cuda", torch.cuda.current_device()))["category"])):
+    dev = torch.device("cuda", torch.cuda.current_device())
+    legs = [(f"batch_{batch}", batch, inp["category"]),
+            (f"batch_{big_batch}", big_batch, H.to_device(H.make_inputs("deepfm", cfg, big_batch, seed=1234),
+                                                          dev)["category"])]
+    for b in (batch, big_batch):  # SURVEY §8d cache-sensitivity variant: Zipf(1.1) row popularity
+        legs.append((f"zipf_{ZIPF_A}_batch_{b}", b,
+                     H.to_device(H.make_inputs("deepfm", dict(cfg, zipf=ZIPF_A), b, seed=4321 + b), dev)["category"]))
+    for key, b, cat in legs:
         ms = graph_kernel_avg_ms(model.gather_launcher(cat))
         achieved = DEEPFM_GATHER_BYTES * b / (ms * 1e-3)
-        tr = load_traffic("fm_gather_kernel", "deepfm" if b == batch else f"deepfm@{b}")
-        out[f"batch_{b}"] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
-                             "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
+        tr = load_traffic("fm_gather_kernel", "deepfm" if key == f"batch_{batch}" else f"deepfm@{b}") \
+            if not key.startswith("zipf") else None
+        out[key] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
+                    "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
         if tr:  # PMC-measured HBM bytes at the same launch time
-            out[f"batch_{b}"]["hbm_gb_per_s"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
-            out[f"batch_{b}"]["hbm_frac"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / PEAK_HBM, 4)
+            out[key]["hbm_gb_per_s"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
+            out[key]["hbm_frac"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / PEAK_HBM, 4)
+    # the calibrated physical ceiling: a 144-B packed row spans two 128-B lines, so
+    # the gather moves ~30 x 256 B + indices + the 3,848-B write = 11.8 KB per 8,048 algorithmic
+    # bytes; at the guide's ~6.3 TB/s achievable HBM rate the algorithmic fraction tops out at
+    # 6.3 / 8.0 x 8,048 / 11,848 = 0.54
+    out["physical_ceiling_frac"] = round(6.3 / 8.0 * DEEPFM_GATHER_BYTES / (30 * (256 + 8) + 3848 + 8), 3)
+    out["physical_ceiling_basis"] = ("2 x 128-B lines per 144-B packed row + 8-B index per field + 3,848-B "
+                                     "write per sample, at 6.3 TB/s achievable (MI355X_MICROARCH.md)")
     return out
 
 
 # ------------------------------------------------------------------ main
 
-def bench_one(name, batch, steps, warmup, world, rank):
-    model, inp, fn, cfg, model_name = workload(name, batch, rank)
-    if name.endswith("per_call"):  # eager: per-call CPU draws + H2D are part of every forward
+def bench_one(name, batch, steps, warmup, world, rank, zipf=None):
+    model, inp, fn, cfg, model_name = workload(name, batch, rank, zipf)
+    if name.endswith("per_call") or name.endswith("_eager"):
+        # eager: one Python forward per step, as the reference's evaluate() / predict loops call
+        # the model (dcn.py:214-239); per-call H2 draws + H2D included in the per_call legs
         def run():
             with torch.no_grad():
                 fn()
-        t = time_replays(run, max(5, steps // 5), 2, 1)
-        return {"samples_per_s": round(batch * max(5, steps // 5) / t, 1), "mode": "eager, per-call H2 draws",
-                "ms_per_step": round(1e3 * t / max(5, steps // 5), 4)}, model, inp, cfg, model_name
+        n = max(5, steps // 5) if name.endswith("per_call") else steps
+        t = time_replays(run, n, 2 if name.endswith("per_call") else warmup, 1)
+        mode = "eager, per-call H2 draws" if name.endswith("per_call") else "eager (no graph), frozen H2"
+        return {"samples_per_s": round(batch * n / t, 1), "mode": mode,
+                "ms_per_step": round(1e3 * t / n, 4)}, model, inp, cfg, model_name
     g, _ = graph_of(fn)
     res = {}
-    if name == "din":
+    if model_name == "din":
         # the whole DIN forward is one kernel: a prepared launch (DIN.prepare ->
         # rk_din_forward_plan) replays it without a graph's per-replay gap; the graph replay of the
         # same forward is timed too and reported beside it
@@ -549,6 +583,8 @@ def bench_one(name, batch, steps, warmup, world, rank):
     t = time_replays(run, steps, warmup, world)
     t = max_over_ranks(world, t)
     res.update({"samples_per_s": round(world * batch * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4)})
+    if zipf is not None:
+        res["index_distribution"] = f"Zipf({zipf}) over table rows (hot rows scattered)"
     return res, model, inp, cfg, model_name
 
 
@@ -595,8 +631,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         extras = {}
         for name in [m for m in args.models.split(",") if m]:
-            batch = {"bst": 2048, "dcn_256_per_call": 256}.get(name, args.batch)
-            r, m2, inp2, cfg2, mn2 = bench_one(name, batch, args.steps, args.warmup, 1, 0)
+            batch = {"bst": 2048, "bst_eager": 2048, "dcn_256_per_call": 256}.get(name, args.batch)
+            zipf = ZIPF_A if name.endswith("_zipf") else None
+            r, m2, inp2, cfg2, mn2 = bench_one(name[:-5] if zipf else name, batch, args.steps, args.warmup, 1, 0,
+                                               zipf=zipf)
+            if name.endswith("_eager") and name[:-6] in extras:
+                r["eager_over_graph"] = round(r["ms_per_step"] / extras[name[:-6]]["ms_per_step"], 3)
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
             if name == "deepfm":

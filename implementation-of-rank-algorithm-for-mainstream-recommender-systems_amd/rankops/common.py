@@ -138,6 +138,13 @@ class EngineModule(nn.Module):
         _GENERATION[0] += 1
         return super()._apply(fn, *args, **kwargs)
 
+    def __getstate__(self):
+        # the EagerCalls cache holds ctypes argument blocks (raw device pointers): never pickled
+        # or deep-copied with the module; a copy builds its own
+        state = self.__dict__.copy()
+        state.pop("_eager", None)
+        return state
+
     def train(self, mode: bool = True):
         # A mode switch also invalidates every derived cache: replays of a captured train step
         # (hipGraph) update weights and BatchNorm running statistics without bumping tensor
@@ -149,6 +156,51 @@ class EngineModule(nn.Module):
 
 def _key(tensors):
     return (_GENERATION[0],) + tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)
+
+
+# ---------------------------------------------------------------- eager eval forwards
+
+def tensor_sig(t: torch.Tensor):
+    """What a marshalled launch binds of an input tensor: its storage address, dtype, shape and
+    strides (not its contents — the kernels read those at launch time)."""
+    return (t.data_ptr(), t.dtype, t.shape, t.stride())
+
+
+class EagerCalls:
+    """Marshalled C-ABI calls of one model's eval forward, reused across eager forwards.
+
+    The reference's evaluate() / predict loops call the model eagerly once per batch
+    (dcn.py:214-239); rebuilding every ctypes segment, layer and epilogue struct per call cost more
+    host time than the forward's kernels.  An entry is keyed on the input tensors' addresses,
+    dtypes, shapes and strides, on every parameter / buffer (address, version), on the module
+    generation (bumped by .to() / .train() / .eval()) and on the stream, so any change of what a
+    launch binds builds a new entry; the output tensors are allocated fresh on every call and
+    patched into the cached argument blocks (callers may keep the previous outputs).  Steady-state
+    loops alternate between a few input buffers of the caching allocator: a handful of entries."""
+
+    def __init__(self, size: int = 4):
+        self._d = {}
+        self._size = size
+        self._watch = None  # (generation, [parameters and buffers])
+
+    def watched(self, module: nn.Module):
+        if self._watch is None or self._watch[0] != _GENERATION[0]:
+            self._watch = (_GENERATION[0], [t for t in module.parameters()] + [t for t in module.buffers()])
+        return self._watch[1]
+
+    def key(self, module: nn.Module, inputs, stream: int, extra=()):
+        ws = self.watched(module)
+        return ((_GENERATION[0], stream) + tuple(map(tensor_sig, inputs))
+                + tuple((t.data_ptr(), t._version) for t in ws) + tuple(extra))
+
+    def get(self, key):
+        return self._d.get(key)
+
+    def put(self, key, entry):
+        if len(self._d) >= self._size:
+            self._d.pop(next(iter(self._d)))
+        self._d[key] = entry
+        return entry
 
 
 class FoldedBN:
@@ -245,6 +297,7 @@ class Layer:
         return kw
 
 
+EAGER_CACHE = True  # eval forwards reuse their marshalled launches (EagerCalls); False: rebuild per call
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
 FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
 FUSED_BST = True  # BST: all transformer blocks + pooling in one rk_bst_forward_blocks launch
@@ -340,6 +393,42 @@ def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit:
     ep = ops.make_epilogue(bias=head.bias, head_w=const(dev, 1.0), head_b=const(dev, 0.0), head_logit=logit,
                            head_prob=prob, **head_kwargs)
     ops.linear(h, head_w, None, epilogue=ep)
+
+
+def tail_launches(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict):
+    """run_tail's fused path as a reusable launch list for EagerCalls: [(C function name, argument
+    list)] with the stream slot last (None), the head epilogue (its output pointers — head_logit,
+    head_prob, head_aux, fm1 / fm2 — are patched per call) and the objects the argument blocks
+    point into.  None when run_tail would not take the fused path."""
+    B, dev = x.shape[0], x.device
+    if not (FUSED_MLP and fused_mlp_fits(x.shape[1], [l.linear.out_features for l in layers])):
+        return None
+    packed = [PACKED(l.linear.weight) for l in layers]
+    mls = [ops.make_mlp_layer(l.linear.weight, pk, **l.epilogue_kwargs()) for l, pk in zip(layers, packed)]
+    ep = ops.make_epilogue(head_w=head.weight, head_b=head.bias, **head_kwargs)
+    launches, keep = [], [packed, mls]
+    h, i = x, 0
+    cus = _num_cus(dev)
+    while (TILED_FIRST_MIN_K and i < len(mls) - 1 and h.shape[1] >= TILED_FIRST_MIN_K
+           and B >= TILED_FIRST_MIN_ROWS and mls[i].residual == 0
+           and ((B + 63) // 64) * ((_pad64(mls[i].n) + 127) // 128) >= cus):
+        y = torch.empty(B, layers[i].linear.out_features, device=dev, dtype=torch.float32)
+        launches.append(("rk_linear_tiled", [h.data_ptr(), h.stride(0), B, h.shape[1], ops.ctypes.byref(mls[i]),
+                                             y.data_ptr(), y.stride(0), None]))
+        keep.append(y)
+        h, i = y, i + 1
+    arr = (ops._lib.MlpLayer * max(1, len(mls) - i))(*mls[i:])
+    keep.append(arr)
+    launches.append(("rk_mlp_forward", [h.data_ptr(), h.stride(0), B, h.shape[1], arr, len(mls) - i,
+                                        ops.ctypes.byref(ep), None, 0, None]))
+    return launches, ep, keep
+
+
+def run_launches(launches, stream: int):
+    lib = ops._lib.load()
+    for name, args in launches:
+        args[-1] = stream
+        ops.check(getattr(lib, name)(*args), name)
 
 
 def check_eval(module: nn.Module):

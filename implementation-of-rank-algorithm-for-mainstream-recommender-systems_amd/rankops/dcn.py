@@ -71,25 +71,82 @@ class DCNModel(EngineModule):
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
 
+    def _eager_eval(self, dense, category):
+        """The fused eval forward through the EagerCalls cache: on a hit one ctypes call with fresh
+        output pointers (and the per-call H2 weights, if any) patched in; None when the fused
+        path does not apply."""
+        if not common.EAGER_CACHE:
+            return None
+        try:
+            idx = [category[n] for n in self.embeddings]
+        except (KeyError, TypeError):
+            return None
+        if not isinstance(dense, torch.Tensor) or dense.device.type != "cuda":
+            return None
+        dev = dense.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        calls = self.__dict__.setdefault("_eager", common.EagerCalls())
+        key = calls.key(self, [dense] + idx, stream, (self.cross_weights.mode,))
+        hit = calls.get(key)
+        if hit is None and self._eager_build(dense, category, key, calls) is None:
+            return None
+        cw, cb = self.cross_weights.get(dev)  # per-call mode: the reference's draws, once per forward
+        args, head, B, _keep = calls.get(key)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head.head_logit = logit.data_ptr()
+        head.head_prob = prob.data_ptr()
+        args[4], args[5], args[-1] = cw.data_ptr(), cb.data_ptr(), stream
+        ops.check(ops._lib.load().rk_dcn_forward(*args), "rk_dcn_forward")
+        return prob, logit
+
+    def _eager_build(self, dense, category, key, calls):
+        dense = ops.as_f32(dense, "dense")
+        B, dev = dense.shape[0], dense.device
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col = self.num_dense_features
+        for name, emb in self.embeddings.items():
+            idx = category[name]
+            if not isinstance(idx, torch.Tensor) or idx.dtype != torch.int64 or idx.device != dev:
+                return None  # conversions make new tensors per call: the uncached path
+            segs.append(ops.table_segment(emb.weight, ops.as_index(idx, f"category[{name!r}]"), col))
+            col += emb.embedding_dim
+        if not (common.FUSED_MLP and len(segs) <= 8 and self.input_dim <= 256
+                and common.fused_mlp_fits(self.input_dim, [l.linear.out_features for l in self._tail])):
+            return None
+        packed = [common.PACKED(l.linear.weight) for l in self._tail]
+        mls = [ops.make_mlp_layer(l.linear.weight, pk, **l.epilogue_kwargs()) for l, pk in zip(self._tail, packed)]
+        head = _HeadView(self.output_layer, self.input_dim)
+        ep = ops.make_epilogue(head_w=head.weight, head_b=head.bias)
+        args = ops.dcn_forward_args(segs, B, self.input_dim, None, None, self.num_cross_layer,
+                                    self.output_layer.weight, mls, ep, dev)
+        # the packed images and the head view stay referenced by the entry: the argument block
+        # holds their raw pointers (cross weights and outputs are patched in per call)
+        return calls.put(key, (args, ep, B, (packed, head, segs)))
+
     def forward(self, dense, category):
+        if not self.training:
+            out = self._eager_eval(dense, category)
+            if out is not None:
+                return out
         # no BatchNorm / Dropout: the train-mode forward computes what the eval forward does; with
         # autograd recording it also keeps the activations for the HIP backward (rankops.train)
         dense = ops.as_f32(dense, "dense")
         B = dense.shape[0]
         dev = dense.device
-        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
-        col = self.num_dense_features
         idx_keep = []
-        for name, emb in self.embeddings.items():
+        for name in self.embeddings:
             if name not in category:
                 raise KeyError(f"DCNModel.forward: category feature {name!r} missing")
-            idx = ops.as_index(category[name], f"category[{name!r}]")
-            idx_keep.append(idx)
-            segs.append(ops.table_segment(emb.weight, idx, col))
-            col += emb.embedding_dim
+            idx_keep.append(ops.as_index(category[name], f"category[{name!r}]"))
         cw, cb = self.cross_weights.get(dev)
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            return train.dcn_train_forward(self, dense, idx_keep, cw, cb)
+            return train.dcn_train_forward(self, dense, idx_keep, cw, cb)  # marshals its own segments
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col = self.num_dense_features
+        for (name, emb), idx in zip(self.embeddings.items(), idx_keep):
+            segs.append(ops.table_segment(emb.weight, idx, col))
+            col += emb.embedding_dim
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
         if (common.FUSED_MLP and len(segs) <= 8 and self.input_dim <= 256

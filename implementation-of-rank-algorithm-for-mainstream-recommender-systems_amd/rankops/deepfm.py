@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import ops, train
+from . import common
 from .common import EngineModule, Layer, PackedFMTable, check_eval, load_vocabulary, run_tail, table_rows
 
 WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
@@ -119,7 +120,61 @@ class DeepFM(EngineModule):
         plan = self._gather_plan(names, category)
         return lambda: self._launch(plan)
 
+    def _eager_eval(self, category):
+        """The eval forward through the EagerCalls cache (common.EagerCalls): the packed FM gather
+        and the tail's launches reused with fresh outputs patched in; None off that path."""
+        if not common.EAGER_CACHE:
+            return None
+        try:
+            idx = [category[n] for n in self.second_order_embeddings]
+        except (KeyError, TypeError):
+            return None
+        if not all(isinstance(t, torch.Tensor) and t.dtype == torch.int64 for t in idx) or idx[0].device.type != "cuda":
+            return None
+        dev = idx[0].device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        calls = self.__dict__.setdefault("_eager", common.EagerCalls())
+        key = calls.key(self, idx, stream)
+        hit = calls.get(key)
+        if hit is None:
+            hit = self._eager_build(category, key, calls)
+            if hit is None:
+                return None
+        launches, ep, B, _keep = hit
+        fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        deep = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        total = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        gather = launches[0][1]
+        gather[6], gather[7] = fm1.data_ptr(), fm2.data_ptr()
+        ep.fm1, ep.fm2, ep.head_aux = fm1.data_ptr(), fm2.data_ptr(), deep.data_ptr()
+        ep.head_logit, ep.head_prob = total.data_ptr(), prob.data_ptr()
+        common.run_launches(launches, stream)
+        return prob, total, fm1, fm2, deep
+
+    def _eager_build(self, category, key, calls):
+        names = list(self.second_order_embeddings)
+        plan = self._gather_plan(names, category)
+        packed, second, first, D, B, deep_in, fm1, fm2 = plan
+        if not packed or any(t.data_ptr() != category[n].data_ptr() for t, n in zip(first, names)):
+            return None  # unpacked tables, or contiguous copies of the indices: the uncached path
+        tail = common.tail_launches(deep_in, self._tail, self.deep_output_layer,
+                                    dict(final_w=self.final_layer.weight, final_b=self.final_layer.bias))
+        if tail is None:
+            return None
+        tl, ep, keep = tail
+        ops._lib.ensure_device(deep_in.device)
+        arr = ops._seg_array(second)
+        gather = ["rk_fm_gather_packed", [arr, len(second), D, B, deep_in.data_ptr(), deep_in.stride(0), None, None,
+                                          None]]
+        return calls.put(key, ([gather] + tl, ep, B, (keep, arr, plan)))
+
     def forward(self, category):
+        if not self.training:
+            out = self._eager_eval(category)
+            if out is not None:
+                return out
         if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
             check_eval(self)  # a train-mode forward without autograd is not implemented
         names = [c for c in self.second_order_embeddings if c in category]

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops, train
+from . import common, ops, train
 from .common import EngineModule, check_eval
 
 FWFM_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id")
@@ -40,9 +40,46 @@ class FwFM(EngineModule):
         self.field_weight = nn.Parameter(torch.randn(self.num_pairs), requires_grad=True)
         self.bias = nn.Parameter(torch.zeros(1))
 
+    def _eager_eval(self, x, return_logit):
+        """The eval forward through the EagerCalls cache (common.EagerCalls): one rk_fwfm_forward
+        call with fresh outputs patched in; None off that path."""
+        if not common.EAGER_CACHE:
+            return None
+        try:
+            idx = [x[n] for n in self.field_names]
+        except (KeyError, TypeError):
+            return None
+        if not all(isinstance(t, torch.Tensor) and t.dtype == torch.int64 and t.dim() == 1 for t in idx) \
+                or idx[0].device.type != "cuda" or any(t.shape != idx[0].shape for t in idx):
+            return None
+        dev = idx[0].device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        calls = self.__dict__.setdefault("_eager", common.EagerCalls())
+        key = calls.key(self, idx, stream)
+        hit = calls.get(key)
+        if hit is None:
+            emb = [ops.table_segment(self.embedding[f].weight, t, 0) for f, t in enumerate(idx)]
+            lin = [ops.table_segment(self.linear[f].weight, t, 0) for f, t in enumerate(idx)]
+            ops._lib.ensure_device(dev)
+            ea, la = ops._seg_array(emb), ops._seg_array(lin)
+            args = [ea, la, len(emb), self.embed_dim, idx[0].shape[0], ops.as_f32(self.field_weight, "field_weight")
+                    .data_ptr(), ops.as_f32(self.bias, "bias").data_ptr(), None, None, None]
+            hit = calls.put(key, (args, idx[0].shape[0], (ea, la)))
+        args, B, _keep = hit
+        prob = torch.empty(B, device=dev, dtype=torch.float32)
+        logit = torch.empty(B, device=dev, dtype=torch.float32) if return_logit else None
+        args[7] = logit.data_ptr() if return_logit else None
+        args[8], args[9] = prob.data_ptr(), stream
+        ops.check(ops._lib.load().rk_fwfm_forward(*args), "rk_fwfm_forward")
+        return (prob, logit) if return_logit else prob
+
     def forward(self, x, *, return_logit=False):
         """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit).
         Under .train() with autograd on, the probabilities carry the HIP backward (rankops.train)."""
+        if not self.training:
+            out = self._eager_eval(x, return_logit)
+            if out is not None:
+                return out
         if self.training and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
             check_eval(self)  # a train-mode forward without autograd is not implemented
         idx0 = ops.as_index(x[self.field_names[0]], f"x[{self.field_names[0]!r}]")
@@ -52,11 +89,12 @@ class FwFM(EngineModule):
             idx = ops.as_index(x[name], f"x[{name!r}]")
             if idx.shape != (B,):
                 raise ValueError(f"FwFM.forward: x[{name!r}] has shape {tuple(idx.shape)}, expected ({B},)")
+            idxs.append(idx)
+        if self.training:  # the train Function marshals its own segments
+            return train.fwfm_train_forward(self, idxs, return_logit)
+        for f, idx in enumerate(idxs):
             emb.append(ops.table_segment(self.embedding[f].weight, idx, 0))
             lin.append(ops.table_segment(self.linear[f].weight, idx, 0))
-            idxs.append(idx)
-        if self.training:
-            return train.fwfm_train_forward(self, idxs, return_logit)
         prob = torch.empty(B, device=idx0.device, dtype=torch.float32)
         logit = torch.empty(B, device=idx0.device, dtype=torch.float32) if return_logit else None
         ops.fwfm_forward(emb, lin, self.embed_dim, B, ops.as_f32(self.field_weight, "field_weight"),

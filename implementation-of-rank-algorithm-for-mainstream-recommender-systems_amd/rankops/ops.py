@@ -103,16 +103,23 @@ def dcn_cross(segs, batch, width, cross_w, cross_b, num_layers, head_w_ptr, x0, 
                            ptr(partial), torch.cuda.current_stream(device).cuda_stream), "rk_dcn_cross")
 
 
-def dcn_forward(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head: Epilogue,
-                device):
-    """rk_dcn_forward: gather + cross stack + MLP tail + head in one launch (DCNModel eval forward)."""
-    lib = _lib.load()
+def dcn_forward_args(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head: Epilogue,
+                     device):
+    """The rk_dcn_forward argument list (the stream last, None) — cross_w / cross_b at [4] / [5] and
+    the stream at [-1] are the per-call slots of a cached eager forward (DCNModel)."""
     _lib.ensure_device(device)
     arr = _seg_array(segs)
     mls = (_lib.MlpLayer * max(1, len(layers)))(*layers)
-    check(lib.rk_dcn_forward(arr, len(segs), batch, width, ptr(cross_w), ptr(cross_b), num_layers,
-                             cross_head_w.data_ptr(), mls, len(layers), ctypes.byref(head),
-                             torch.cuda.current_stream(device).cuda_stream), "rk_dcn_forward")
+    return [arr, len(segs), batch, width, ptr(cross_w), ptr(cross_b), num_layers, cross_head_w.data_ptr(), mls,
+            len(layers), ctypes.byref(head), None]
+
+
+def dcn_forward(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head: Epilogue,
+                device):
+    """rk_dcn_forward: gather + cross stack + MLP tail + head in one launch (DCNModel eval forward)."""
+    args = dcn_forward_args(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head, device)
+    args[-1] = torch.cuda.current_stream(device).cuda_stream
+    check(_lib.load().rk_dcn_forward(*args), "rk_dcn_forward")
 
 
 def fm_gather(second, first, dim, batch, deep_in, fm1, fm2):

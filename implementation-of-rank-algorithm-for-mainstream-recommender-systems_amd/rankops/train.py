@@ -1008,7 +1008,10 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
+            if not group["capturable"] and self._fast_step(gi, group):
+                continue
+            self.__dict__.get("_fast", {}).pop(gi, None)  # the general path moves step counts
             beta1, beta2 = group["betas"]
             capturable = group["capturable"]
             by_step = {}
@@ -1046,3 +1049,50 @@ class Adam(torch.optim.Optimizer):
                 # in-place ops would, so weight-derived caches (packed MLP images) are rebuilt
                 torch.autograd.graph.increment_version([t for e in entries for t in (e[0], e[2], e[3])])
         return loss
+
+    def _fast_step(self, gi, group) -> bool:
+        """The eager step with the marshalled rk_adam_step argument block reused: valid while the
+        group's parameters, their states and their gradients' storages stay the same and every
+        parameter is at the same step count (the reference's loop: every parameter gets a gradient
+        every step).  Per step: one foreach increment of the CPU step tensors, one launch, one
+        version bump.  Anything else (first step, a missing gradient, new gradient storage, mixed
+        step counts) takes the general path, which rebuilds the block next time."""
+        params = group["params"]
+        grads = [p.grad for p in params]
+        if not params or any(g is None for g in grads):
+            return False
+        cache = self.__dict__.setdefault("_fast", {})
+        key = tuple(g.data_ptr() for g in grads) + tuple(p.data_ptr() for p in params)
+        hit = cache.get(gi)
+        if hit is None or hit[0] != key:
+            states = [self.state.get(p) for p in params]
+            if any(not st for st in states) or any(st["step"].device.type != "cpu" for st in states):
+                cache.pop(gi, None)
+                return False
+            if any(g.dtype != torch.float32 or not g.is_contiguous() or g.is_sparse for g in grads) or \
+                    any(p.device.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous() for p in params):
+                return False
+            counts = {float(st["step"]) for st in states}
+            if len(counts) != 1:
+                return False
+            entries = [(p, g, st["exp_avg"], st["exp_avg_sq"]) for p, g, st in zip(params, grads, states)]
+            arr = (ops._lib.AdamTensor * len(entries))(*[
+                ops._lib.AdamTensor(e[0].data_ptr(), e[1].data_ptr(), e[2].data_ptr(), e[3].data_ptr(), e[0].numel(),
+                                    None) for e in entries])
+            bumped = [t for e in entries for t in (e[0], e[2], e[3])]
+            hit = [key, arr, len(entries), [st["step"] for st in states], int(counts.pop()), bumped, entries,
+                   params[0].device]
+            cache[gi] = hit
+        _key, arr, n, steps, count, bumped, _entries, dev = hit
+        torch._foreach_add_(steps, 1.0)
+        hit[4] = count = count + 1
+        beta1, beta2 = group["betas"]
+        ops.check(ops._lib.load().rk_adam_step(arr, n, float(group["lr"]), beta1, beta2, group["eps"],
+                                               group["weight_decay"], count,
+                                               torch.cuda.current_stream(dev).cuda_stream), "rk_adam_step")
+        torch.autograd.graph.increment_version(bumped)
+        return True
+
+    def load_state_dict(self, state_dict):
+        self.__dict__.pop("_fast", None)  # new state tensors: rebuild the argument blocks
+        return super().load_state_dict(state_dict)

@@ -48,9 +48,23 @@ def randomize_eval_stats(model: torch.nn.Module, seed: int = 7):
     return model
 
 
-def _idx(rng, n, size):
+def _idx(rng, n, size, zipf=None):
     # uniform over [0, len(vocab)-1]: the last table row (len(vocab)) is never addressed (H1)
-    return torch.from_numpy(rng.integers(0, n, size=size, dtype=np.int64))
+    if zipf is None:
+        return torch.from_numpy(rng.integers(0, n, size=size, dtype=np.int64))
+    return torch.from_numpy(zipf_rows(rng, n, size, zipf))
+
+
+def zipf_rows(rng, n, size, a=1.1):
+    """Zipf(a) popularity over the rows of an n-row table (SURVEY.md §8d cache-sensitivity
+    variant): rank r ~ Zipf(a) (ranks past n wrap), row = (r * 2654435761 + 12345) mod n — a
+    bijection on [0, n) for n coprime to the multiplier — so the hot rows are scattered over the
+    table instead of packed at its start."""
+    r = (rng.zipf(a, size=size).astype(np.uint64) - np.uint64(1)) % np.uint64(n)
+    m = 2654435761 % n if n > 1 else 0
+    while n > 1 and np.gcd(m, n) != 1:
+        m += 1
+    return ((r * np.uint64(m) + np.uint64(12345)) % np.uint64(n)).astype(np.int64)
 
 
 def _dense(rng, size):
@@ -62,20 +76,20 @@ def dcn_inputs(B, vocab, seed=1000):
     return {"dense": _dense(rng, (B, 16)), "category": {f: _idx(rng, vocab[f], B) for f in DCN_FIELDS}}
 
 
-def deepfm_inputs(B, vocab_sizes, seed=1001):
+def deepfm_inputs(B, vocab_sizes, seed=1001, zipf=None):
     rng = np.random.default_rng(seed)
-    return {"category": {f: _idx(rng, n, B) for f, n in vocab_sizes.items()}}
+    return {"category": {f: _idx(rng, n, B, zipf) for f, n in vocab_sizes.items()}}
 
 
-def din_inputs(B, T, vocab, seed=1002, min_len=1):
+def din_inputs(B, T, vocab, seed=1002, min_len=1, zipf=None):
     rng = np.random.default_rng(seed)
     dense = {name: _dense(rng, (B,)) for name in rankops.common.DENSE_FEATURES}
     lengths = torch.from_numpy(rng.integers(min_len, T + 1, size=B, dtype=np.int64))
-    seq = _idx(rng, vocab["feedid"], (B, T))
+    seq = _idx(rng, vocab["feedid"], (B, T), zipf)
     seq = seq * (torch.arange(T).unsqueeze(0) < lengths.unsqueeze(1))  # zero padding (din.py:207-212)
     return {"dense": dense, "category": {f: _idx(rng, vocab[f], B) for f in DCN_FIELDS},
             "sequence": {"his_read_comment_7d_seq": seq, "his_read_comment_7d_seq_length": lengths},
-            "target": {"feedid": _idx(rng, vocab["feedid"], B)}}
+            "target": {"feedid": _idx(rng, vocab["feedid"], B, zipf)}}
 
 
 def afm_inputs(B, feature_columns, seed=1003):
@@ -159,9 +173,10 @@ def make_inputs(name: str, cfg: dict, B: int, seed: int = 1000):
     if name in ("dcn", "deepcrossing"):
         return dcn_inputs(B, vocab, seed)
     if name == "deepfm":
-        return deepfm_inputs(B, cfg.get("fields", {f: vocab[f] for f in rankops.deepfm.WECHAT_FIELDS}), seed)
+        return deepfm_inputs(B, cfg.get("fields", {f: vocab[f] for f in rankops.deepfm.WECHAT_FIELDS}), seed,
+                             cfg.get("zipf"))
     if name == "din":
-        return din_inputs(B, cfg.get("T", 50), vocab, seed, cfg.get("min_len", 1))
+        return din_inputs(B, cfg.get("T", 50), vocab, seed, cfg.get("min_len", 1), cfg.get("zipf"))
     if name == "afm":
         return afm_inputs(B, afm_feature_columns(vocab), seed)
     if name == "bst":

@@ -1068,3 +1068,48 @@ def test_pool_ln_backward_misaligned_workspace_is_unsupported():
 def rankops_lib():
     import rankops
     return rankops.load_library()
+
+
+@pytest.mark.gpu
+def test_adam_fast_step_matches_torch_over_storage_changes():
+    """rankops.Adam's cached eager step (same gradient storages every step) against torch.optim.Adam,
+    through gradient storages that change, a skipped parameter, an lr change and a state_dict
+    round trip."""
+    g = torch.Generator().manual_seed(21)
+    shapes = [(300, 16), (7,), (4096,)]
+    pa = [torch.nn.Parameter(torch.randn(s, generator=g).cuda()) for s in shapes]
+    qa = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+    ours = rankops.Adam(pa, lr=1e-3)
+    theirs = torch.optim.Adam(qa, lr=1e-3)
+    bufs = [torch.empty(s, device="cuda") for s in shapes]  # the same gradient storages each step
+    for step in range(12):
+        for a, b, buf in zip(pa, qa, bufs):
+            gr = torch.randn(a.shape, generator=g).cuda()
+            if step in (5, 6):  # new storages for two steps
+                a.grad = gr.clone()
+            else:
+                buf.copy_(gr)
+                a.grad = buf
+            b.grad = gr.clone()
+        if step == 8:
+            pa[1].grad = None
+            qa[1].grad = None
+        if step == 10:
+            for grp in (ours.param_groups[0], theirs.param_groups[0]):
+                grp["lr"] = 5e-4
+        ours.step()
+        theirs.step()
+        for a, b in zip(pa, qa):
+            torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-6, msg=lambda m: f"step {step}: {m}")
+    assert [float(ours.state[p]["step"]) for p in pa] == [12.0, 11.0, 12.0]
+    # (a deep copy: Optimizer.load_state_dict keeps same-device tensors as they are, so the two
+    # optimizers would otherwise share their moment buffers)
+    import copy
+    ours.load_state_dict(copy.deepcopy(theirs.state_dict()))
+    for a, b, buf in zip(pa, qa, bufs):
+        buf.copy_(torch.ones_like(buf))
+        a.grad, b.grad = buf, buf.clone()
+    ours.step()
+    theirs.step()
+    for a, b in zip(pa, qa):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-6)
