@@ -542,8 +542,8 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   a.l2_out = l2_out;
   a.l2_scale = l2_scale;
   a.flags = device_flags();
-  a.ld0 = need0 + 4;
-  a.ld1 = need1 + 4;
+  a.ld0 = need0 + kMlpLdPad;
+  a.ld1 = need1 + kMlpLdPad;
   static_assert(sizeof(DinArgs) <= 4096, "kernel arguments beyond 4 KiB");
   if (batch < 0) return fail(RK_ERR_INVALID, "rk_din_forward: negative batch");
   plan->blocks = (batch + kMlpRows - 1) / kMlpRows;

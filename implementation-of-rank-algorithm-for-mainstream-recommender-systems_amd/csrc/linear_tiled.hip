@@ -17,7 +17,15 @@ namespace rk {
 constexpr int kLtRows = 64;   // rows per workgroup
 constexpr int kLtCols = 128;  // output columns per workgroup (8 tiles of 16)
 constexpr int kLtKB = 256;    // K-block staged in LDS
-constexpr int kLtLd = kLtKB + 4;
+constexpr int kLtLd = kLtKB + kMlpLdPad;
+constexpr int kLtMaxFields = 32;
+// Lockstep inside a K-block: all waves meet at a bare s_barrier every RK_LT_SYNC chunks (0: only at
+// the block ends).  Without it the matrix pipe serves a SIMD's 4 waves oldest-first and each
+// block closes on one lone wave per SIMD (tools/lt_phases.py: block 0's MFMAs issued at 14.7k /
+// 17.4k / 21.8k / 24.3k cycles for the SIMD's waves 0 / 4 / 8 / 12).
+#ifndef RK_LT_SYNC
+#define RK_LT_SYNC 4
+#endif
 
 struct LtArgs {
   const float* x;
@@ -27,14 +35,41 @@ struct LtArgs {
   float* y;
   int64_t ldy;
   int x_vec;
+  int nrt, nct;  // row tiles, column tiles
 };
 
-__global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lt_sm[];  // [2][kLtRows * kLtLd]
+// The fused DeepFM front end's A source (rk_fm_linear_packed): row b of A is the concatenation of
+// the num_fields packed-table rows idx[f][b] (rk_fm_pack_table layout: dim floats, then the
+// first-order weight), and the same pass produces fm1 / fm2 (deepfm.py:122-140) for the rows it
+// stages.
+struct LtFm {
+  const float* src[kLtMaxFields];
+  const int64_t* idx[kLtMaxFields];
+  int64_t ld[kLtMaxFields], rows[kLtMaxFields];
+  int F, dim_shift;
+  float* fm1;
+  float* fm2;
+  uint32_t* flags;
+};
+
+// Tile order: block l works on row tile 8 (l / 8 nct) + l % 8 and column tile (l / 8) % nct, so the
+// nct workgroups that stage the same 64 rows are dealt to one XCD (blocks b and b + 8 share one,
+// MI355X_MICROARCH.md) and read those rows through one L2.
+template <bool FM>
+__global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtFm fm) {
+  // [2][kLtRows * kLtLd] A blocks, then (FM) [F][kLtRows] row pointers
+  extern __shared__ __attribute__((aligned(16))) float lt_sm[];
+  const int l = blockIdx.x, within = l % (8 * a.nct);
+  const int rt = 8 * (l / (8 * a.nct)) + within % 8, ctile = within / 8;
+  if (rt >= a.nrt) return;  // the whole workgroup, before any barrier
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef RK_MLP_PHASES
+  const unsigned long long t0 = clock64();
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
+#endif
   const int li = lane & 15, kq = 4 * (lane >> 4);
-  const int64_t m0 = (int64_t)blockIdx.x * kLtRows;
-  const int n0 = blockIdx.y * kLtCols;
+  const int64_t m0 = (int64_t)rt * kLtRows;
+  const int n0 = ctile * kLtCols;
   const int ct = wave & 7, rh = wave >> 3;
   const int n = n0 + 16 * ct + li;  // this lane's weight row / output column
   const rk_mlp_layer& L = a.L;
@@ -48,19 +83,65 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
   for (int s = 0; s < kMlpPD; ++s) ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * s);
   const ColEpi ep = col_epi(L, n < L.n ? n : 0);
 
+  // FM: the staged rows' row pointers (null past M or out of range: a zero row, as rk_fm_gather)
+  const float** s_ptr = reinterpret_cast<const float**>(lt_sm + 2 * kLtRows * kLtLd);
+  if constexpr (FM) {
+    bool oob = false;
+    for (int e = tid; e < fm.F * kLtRows; e += kMlpThreads) {
+      const int f = e / kLtRows, r = e % kLtRows;  // f is wave-uniform
+      const int64_t m = m0 + r;
+      const float* p = nullptr;
+      if (m < a.M) {
+        const int64_t i = fm.idx[f][m];
+        if ((uint64_t)i < (uint64_t)fm.rows[f])
+          p = fm.src[f] + i * fm.ld[f];
+        else
+          oob = true;
+      }
+      s_ptr[e] = p;
+    }
+    if (oob) flag_oob(fm.flags);
+    mlp_lds_barrier();
+  }
+  MLP_MARK(0, t0);
+  // FM sums: this workgroup owns the rows wave + 16 j with j % min(nct, 4) == ctile; lane holds quad
+  // (lane % G) of field (k / dim) for every block, so the field sum is a shuffle over lane / G
+  const int G = FM ? (1 << fm.dim_shift) / 4 : 1;
+  f32x4_t fs[4], fq[4];
+  float fo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    fs[j] = fq[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    fo[j] = 0.f;
+  }
+  const int fm_groups = a.nct < 4 ? a.nct : 4;
+  auto fm_mine = [&](int j) { return FM && ctile < fm_groups && j % fm_groups == ctile; };
+
   // A staging: block b covers columns [256 b, min(256 b + 256, Kp)); thread tid moves float4s
-  // i = tid + 1024 j of the 64 x 256 block (4 per thread)
+  // i = tid + 1024 j of the 64 x 256 block (4 per thread): row wave + 16 j, columns 4 lane ..
   f32x4_t stage[4];
   auto load_block = [&](int b) {
     const int kb = b * kLtKB, w = min(kLtKB, a.Kp - kb);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int i = tid + kMlpThreads * j;
-      const int r = i / (kLtKB / 4), c = (i % (kLtKB / 4)) * 4;
+      const int r = wave + 16 * j, c = 4 * lane;
       f32x4_t v = {0.f, 0.f, 0.f, 0.f};
       const int64_t m = m0 + r;
-      if (c < w && m < a.M) {
-        const int k = kb + c;
+      const int k = kb + c;
+      if constexpr (FM) {
+        if (c < w && k < a.K) {
+          const float* p = s_ptr[(k >> fm.dim_shift) * kLtRows + r];
+          if (p) {
+            const int d = k & ((1 << fm.dim_shift) - 1);
+            v = *reinterpret_cast<const f32x4_t*>(p + d);
+            if (fm_mine(j) && d + 4 == (1 << fm.dim_shift)) fo[j] += p[d + 4];
+          }
+        }
+        if (fm_mine(j)) {
+          fs[j] += v;
+          fq[j] += v * v;
+        }
+      } else if (c < w && m < a.M) {
         if (a.x_vec) {
           if (k < a.K) v = *reinterpret_cast<const f32x4_t*>(a.x + m * a.ldx + k);
         } else {
@@ -73,17 +154,15 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
   };
   auto store_block = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + kMlpThreads * j;
-      const int r = i / (kLtKB / 4), c = (i % (kLtKB / 4)) * 4;
-      *reinterpret_cast<f32x4_t*>(lt_sm + buf * kLtRows * kLtLd + r * kLtLd + c) = stage[j];
-    }
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<f32x4_t*>(lt_sm + buf * kLtRows * kLtLd + (wave + 16 * j) * kLtLd + 4 * lane) = stage[j];
   };
 
   const int nblocks = (a.Kp + kLtKB - 1) / kLtKB;
   load_block(0);
   store_block(0);
   mlp_lds_barrier();
+  MLP_MARK(1, t0);
 
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   int c = 0;  // global chunk index of the weight stream
@@ -92,32 +171,42 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
     if (b + 1 < nblocks) load_block(b + 1);
     const int bchunks = min(kLtKB, a.Kp - b * kLtKB) / 16;
     const float* arow = lt_sm + buf * kLtRows * kLtLd + (32 * rh + li) * kLtLd + kq;
-    f32x4_t an[2];
+    // A float4s one chunk ahead in two explicit register sets (slot s reads set s & 1; kMlpPD is
+    // even), the read issued before the slot's MFMAs (see mlp_core.h mlp_layer)
+    f32x4_t ab[2][2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd);
+    for (int t = 0; t < 2; ++t) ab[0][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd);
     for (int q0 = 0; q0 < bchunks; q0 += kMlpPD) {
 #pragma unroll
       for (int s = 0; s < kMlpPD; ++s) {
         const int q = q0 + s;
-        f32x4_t av[2] = {an[0], an[1]};
         const int qa = min(q + 1, bchunks - 1);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) an[t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd + 16 * qa);
+        for (int t = 0; t < 2; ++t)
+          ab[(s + 1) & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd + 16 * qa);
+        __builtin_amdgcn_sched_barrier(0);
         const f32x4_t bv = ring[s];  // c is a multiple of kMlpPD
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int t = 0; t < 2; ++t) acc[t] = mfma16(av[t][e], bv[e], acc[t]);
+          for (int t = 0; t < 2; ++t) acc[t] = mfma16(ab[s & 1][t][e], bv[e], acc[t]);
         const int cn = min(c + s + kMlpPD, kchunks - 1);
         ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * cn);
         __builtin_amdgcn_sched_barrier(0);
       }
       c += kMlpPD;
+      if (RK_LT_SYNC && (q0 + kMlpPD) % RK_LT_SYNC == 0 && q0 + kMlpPD < bchunks) mlp_sync_barrier();
     }
+    if (b < 4) MLP_MARK(2 + 2 * b, t0);
+#ifdef RK_MLP_PHASES
+    if (lane == 0 && b == 0) s_mlp_wave_marks[1][wave][0] = (unsigned)(clock64() - t0);
+    if (lane == 0 && b + 1 == nblocks) s_mlp_wave_marks[0][wave][0] = (unsigned)(clock64() - t0);
+#endif
     if (b + 1 < nblocks) {
       store_block(buf ^ 1);
       mlp_lds_barrier();
     }
+    if (b < 4) MLP_MARK(3 + 2 * b, t0);
   }
 
   // epilogue: bias, BatchNorm affine, activation; rows < M, columns < n
@@ -130,6 +219,82 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a) {
         if (m < a.M) a.y[m * a.ldy + n] = col_apply(ep, L.act == RK_ACT_DICE, acc[t][r], false, 0.f);
       }
   }
+  MLP_MARK(10, t0);
+#ifdef RK_MLP_PHASES
+  if (lane == 0) s_mlp_wave_marks[0][wave][1] = (unsigned)(clock64() - t0);
+#endif
+
+  // FM outputs: sums over the fields (lanes of equal lane % G), then fm2 = 0.5 sum_d (S_d^2 - Q_d)
+  // over the quads (deepfm.py:128-140)
+  if constexpr (FM) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!fm_mine(j)) continue;
+      f32x4_t s = fs[j], q = fq[j];
+      float o = fo[j];
+      for (int x = G; x < 64; x <<= 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[e] += __shfl_xor(s[e], x, kWave);
+          q[e] += __shfl_xor(q[e], x, kWave);
+        }
+        o += __shfl_xor(o, x, kWave);
+      }
+      float part = (s[0] * s[0] - q[0]) + (s[1] * s[1] - q[1]) + (s[2] * s[2] - q[2]) + (s[3] * s[3] - q[3]);
+      for (int x = G / 2; x > 0; x >>= 1) {  // the first-order weights sit in the lanes of quad G - 1
+        part += __shfl_xor(part, x, kWave);
+        o += __shfl_xor(o, x, kWave);
+      }
+      const int64_t m = m0 + wave + 16 * j;
+      if (lane == 0 && m < a.M) {
+        fm.fm2[m] = 0.5f * part;
+        fm.fm1[m] = o;
+      }
+    }
+  }
+  MLP_MARK(11, t0);
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
+  MLP_FLUSH(tid);
+}
+
+static int check_layer(const rk_mlp_layer& L, int K, int64_t ldy, const char* what) {
+  if (!L.w || L.n <= 0 || L.ldw != pad64(K) || ((uintptr_t)L.w & 15u))
+    return fail(RK_ERR_UNSUPPORTED, "%s: the weight must be packed by rk_mlp_pack_weight (ldw %lld, K %d)", what,
+                (long long)L.ldw, K);
+  if (L.residual) return fail(RK_ERR_UNSUPPORTED, "%s: residual layers are not supported", what);
+  if (L.act == RK_ACT_DICE && (!L.act_scale || !L.act_shift || !L.act_alpha))
+    return fail(RK_ERR_INVALID, "%s: Dice layer incomplete", what);
+  if (L.act == RK_ACT_PRELU && !L.act_alpha) return fail(RK_ERR_INVALID, "%s: PReLU needs alpha", what);
+  if ((L.pre_scale != nullptr) != (L.pre_shift != nullptr) || (L.post_scale != nullptr) != (L.post_shift != nullptr))
+    return fail(RK_ERR_INVALID, "%s: affine scale/shift must come in pairs", what);
+  if (ldy < L.n) return fail(RK_ERR_INVALID, "%s: ldy %lld < n %d", what, (long long)ldy, L.n);
+  return RK_OK;
+}
+
+#ifdef RK_MLP_PHASES
+// Timing build only (tools/lt_phases.py): this module's phase counters (marks: 0 prologue, 1 block 0
+// staged, 2 + 2b / 3 + 2b block b MFMAs issued / barrier passed, 10 epilogue, 11 end; wave marks
+// [0][w] last block issued / epilogue, [1][w][0] block 0 issued).
+RK_API int rk_debug_lt_phases(unsigned long long* marks, int32_t nwg, unsigned* wave_marks) {
+  if (nwg < 0 || nwg > kMlpMarkWG) return 1;
+  if (hipMemcpyFromSymbol(marks, HIP_SYMBOL(g_mlp_marks), sizeof(g_mlp_marks[0]) * nwg) != hipSuccess) return 1;
+  if (wave_marks &&
+      hipMemcpyFromSymbol(wave_marks, HIP_SYMBOL(g_mlp_wave_marks), sizeof(g_mlp_wave_marks[0]) * nwg) != hipSuccess)
+    return 1;
+  return 0;
+}
+#endif
+
+template <bool FM>
+static int launch_linear_tiled(LtArgs& a, const LtFm& fm, hipStream_t st, const char* what) {
+  a.nrt = (int)((a.M + kLtRows - 1) / kLtRows);
+  a.nct = (pad64(a.L.n) + kLtCols - 1) / kLtCols;
+  const int64_t blocks = (int64_t)((a.nrt + 7) / 8) * 8 * a.nct;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "%s: batch too large", what);
+  const size_t shm = 2 * kLtRows * kLtLd * sizeof(float) + (FM ? (size_t)fm.F * kLtRows * sizeof(void*) : 0);
+  raise_lds_limit((const void*)linear_tiled_kernel<FM>, (int)shm);
+  linear_tiled_kernel<FM><<<(unsigned)blocks, kMlpThreads, shm, st>>>(a, fm);
+  return check_launch(what);
 }
 
 }  // namespace rk
@@ -140,17 +305,7 @@ RK_API int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, co
                            int64_t ldy, void* stream) {
   if (!x || !layer || !y || M < 0 || K <= 0 || ldx < K)
     return fail(RK_ERR_INVALID, "rk_linear_tiled: bad arguments (M=%lld K=%d)", (long long)M, K);
-  const rk_mlp_layer& L = *layer;
-  if (!L.w || L.n <= 0 || L.ldw != pad64(K) || ((uintptr_t)L.w & 15u))
-    return fail(RK_ERR_UNSUPPORTED, "rk_linear_tiled: the weight must be packed by rk_mlp_pack_weight (ldw %lld, K %d)",
-                (long long)L.ldw, K);
-  if (L.residual) return fail(RK_ERR_UNSUPPORTED, "rk_linear_tiled: residual layers are not supported");
-  if (L.act == RK_ACT_DICE && (!L.act_scale || !L.act_shift || !L.act_alpha))
-    return fail(RK_ERR_INVALID, "rk_linear_tiled: Dice layer incomplete");
-  if (L.act == RK_ACT_PRELU && !L.act_alpha) return fail(RK_ERR_INVALID, "rk_linear_tiled: PReLU needs alpha");
-  if ((L.pre_scale != nullptr) != (L.pre_shift != nullptr) || (L.post_scale != nullptr) != (L.post_shift != nullptr))
-    return fail(RK_ERR_INVALID, "rk_linear_tiled: affine scale/shift must come in pairs");
-  if (ldy < L.n) return fail(RK_ERR_INVALID, "rk_linear_tiled: ldy %lld < n %d", (long long)ldy, L.n);
+  if (int e = check_layer(*layer, K, ldy, "rk_linear_tiled")) return e;
   if (M == 0) return RK_OK;
   LtArgs a = {};
   a.x = x;
@@ -158,13 +313,50 @@ RK_API int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, co
   a.M = M;
   a.K = K;
   a.Kp = pad64(K);
-  a.L = L;
+  a.L = *layer;
   a.y = y;
   a.ldy = ldy;
   a.x_vec = (ldx % 4 == 0) && (((uintptr_t)x & 15u) == 0);
-  const dim3 grid((unsigned)((M + kLtRows - 1) / kLtRows), (unsigned)((pad64(L.n) + kLtCols - 1) / kLtCols));
-  const size_t shm = 2 * kLtRows * kLtLd * sizeof(float);
-  raise_lds_limit((const void*)linear_tiled_kernel, (int)shm);
-  linear_tiled_kernel<<<grid, kMlpThreads, shm, (hipStream_t)stream>>>(a);
-  return check_launch("rk_linear_tiled");
+  LtFm fm = {};
+  return launch_linear_tiled<false>(a, fm, (hipStream_t)stream, "rk_linear_tiled");
+}
+
+RK_API int rk_fm_linear_packed(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                               const rk_mlp_layer* layer, float* y, int64_t ldy, float* fm1, float* fm2,
+                               void* stream) {
+  if (!fields || num_fields <= 0 || num_fields > kLtMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_linear_packed: %d fields (max %d)", num_fields, kLtMaxFields);
+  if (dim < 4 || dim > 256 || (dim & (dim - 1)))
+    return fail(RK_ERR_UNSUPPORTED, "rk_fm_linear_packed: dim %d must be a power of two in [4, 256]", dim);
+  if (!layer || !y || !fm1 || !fm2 || batch < 0)
+    return fail(RK_ERR_INVALID, "rk_fm_linear_packed: bad arguments (batch %lld)", (long long)batch);
+  const int K = num_fields * dim;
+  if (int e = check_layer(*layer, K, ldy, "rk_fm_linear_packed")) return e;
+  LtFm fm = {};
+  for (int f = 0; f < num_fields; ++f) {
+    const rk_segment& s = fields[f];
+    if (!s.src || !s.idx || s.rows <= 0 || s.idx_stride != 1 || s.dim != dim || s.src_ld < dim + 1 || s.src_ld % 4 ||
+        !aligned16(s.src) || s.out_col != f * dim)
+      return fail(RK_ERR_INVALID,
+                  "rk_fm_linear_packed: field %d is not a unit-stride packed [rows, >= dim+1] table at column f*dim", f);
+    fm.src[f] = s.src;
+    fm.idx[f] = s.idx;
+    fm.ld[f] = s.src_ld;
+    fm.rows[f] = s.rows;
+  }
+  fm.F = num_fields;
+  fm.dim_shift = __builtin_ctz((unsigned)dim);
+  fm.fm1 = fm1;
+  fm.fm2 = fm2;
+  fm.flags = device_flags();
+  if (!fm.flags) return fail(RK_ERR_RUNTIME, "rk_fm_linear_packed: no device flag word");
+  if (batch == 0) return RK_OK;
+  LtArgs a = {};
+  a.M = batch;
+  a.K = K;
+  a.Kp = pad64(K);
+  a.L = *layer;
+  a.y = y;
+  a.ldy = ldy;
+  return launch_linear_tiled<true>(a, fm, (hipStream_t)stream, "rk_fm_linear_packed");
 }

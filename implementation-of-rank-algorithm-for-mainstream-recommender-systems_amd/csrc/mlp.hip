@@ -319,9 +319,9 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   if (int e = mlp_validate(layers, nlayers, K0, a.head, &need0, &need1, "rk_mlp_forward")) return e;
   for (int l = 0; l < nlayers; ++l) a.L[l] = layers[l];
   a.nl = nlayers;
-  // row stride = width + 4 (width is a multiple of 64): conflict-free float4 row reads
-  a.ld0 = need0 + 4;
-  a.ld1 = need1 + 4;
+  // row stride = width + kMlpLdPad (width is a multiple of 64): conflict-free float4 row reads
+  a.ld0 = need0 + kMlpLdPad;
+  a.ld1 = need1 + kMlpLdPad;
   // rows per workgroup: 16.  32 (two row tiles per wave: half the L2 weight traffic per row)
   // measured slower at batch 4096 — DCN 46.6 vs 52.6 us: half the workgroups, same per-workgroup
   // latency — and is kept as an option (RANKOPS_MLP_ROWS=32) where the buffers fit in LDS.
@@ -412,8 +412,8 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   if (segs[0].out_col != 0) return fail(RK_ERR_INVALID, "rk_dcn_forward: segments must start at column 0");
   for (int l = 0; l < nlayers; ++l) a.m.L[l] = layers[l];
   a.m.nl = nlayers;
-  a.m.ld0 = need0 + 4;
-  a.m.ld1 = need1 + 4;
+  a.m.ld0 = need0 + kMlpLdPad;
+  a.m.ld1 = need1 + kMlpLdPad;
   a.m.off1 = kMlpRows * a.m.ld0;
   a.m.M = batch;
   a.m.K0 = width;

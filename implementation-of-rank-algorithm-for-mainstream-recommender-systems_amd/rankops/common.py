@@ -326,7 +326,7 @@ def fused_mlp_fits(k0: int, widths) -> bool:
         return False
     need0 = max([_pad64(k0)] + [_pad64(n) for i, n in enumerate(widths) if i % 2 == 1])
     need1 = max([64] + [_pad64(n) for i, n in enumerate(widths) if i % 2 == 0])
-    return 16 * (need0 + 4 + need1 + 4) * 4 <= 160 * 1024
+    return 16 * (need0 + 8 + need1 + 8) * 4 <= 160 * 1024  # rows padded by kMlpLdPad (mlp_core.h)
 
 
 class PackedWeights:
@@ -352,6 +352,14 @@ class PackedWeights:
 PACKED = PackedWeights()
 
 
+def tiled_layer(K: int, B: int, device, ml) -> bool:
+    """Whether a K-wide layer of the fused path runs as its own 2D-tiled GEMM (rk_linear_tiled,
+    64 x 128 tiles): wide enough, and that grid still fills the GPU (DeepFM: 960 -> 512 yes,
+    512 -> 256 no: 128 tiles measured slower than the fused kernel)."""
+    return bool(TILED_FIRST_MIN_K and K >= TILED_FIRST_MIN_K and B >= TILED_FIRST_MIN_ROWS and ml.residual == 0
+                and ((B + 63) // 64) * ((_pad64(ml.n) + 127) // 128) >= _num_cus(device))
+
+
 def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit: torch.Tensor,
              prob: torch.Tensor):
     """Runs the hidden layers and the final Linear(N, 1) + sigmoid.  Normally one fused
@@ -364,14 +372,9 @@ def run_tail(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict, logit:
     if FUSED_MLP and fused_mlp_fits(x.shape[1], [l.linear.out_features for l in layers]):
         mls = [ops.make_mlp_layer(l.linear.weight, PACKED(l.linear.weight), **l.epilogue_kwargs()) for l in layers]
         ep = ops.make_epilogue(head_w=head_w, head_b=head.bias, head_logit=logit, head_prob=prob, **head_kwargs)
-        # leading layers at least TILED_FIRST_MIN_K wide run as 2D-tiled GEMMs (64 x 128 tiles)
-        # while that grid still fills the GPU (DeepFM: 960 -> 512 yes, 512 -> 256 no: 128 tiles
-        # measured slower than the fused kernel), the rest fused
+        # leading wide layers as 2D-tiled GEMMs (tiled_layer), the rest fused
         i = 0
-        cus = _num_cus(dev)
-        while (TILED_FIRST_MIN_K and i < len(mls) - 1 and h.shape[1] >= TILED_FIRST_MIN_K
-               and B >= TILED_FIRST_MIN_ROWS and mls[i].residual == 0
-               and ((B + 63) // 64) * ((_pad64(mls[i].n) + 127) // 128) >= cus):
+        while i < len(mls) - 1 and tiled_layer(h.shape[1], B, dev, mls[i]):
             y = torch.empty(B, layers[i].linear.out_features, device=dev, dtype=torch.float32)
             ops.linear_tiled(h, mls[i], y)
             h, i = y, i + 1
@@ -408,10 +411,7 @@ def tail_launches(x: torch.Tensor, layers, head: nn.Linear, head_kwargs: dict):
     ep = ops.make_epilogue(head_w=head.weight, head_b=head.bias, **head_kwargs)
     launches, keep = [], [packed, mls]
     h, i = x, 0
-    cus = _num_cus(dev)
-    while (TILED_FIRST_MIN_K and i < len(mls) - 1 and h.shape[1] >= TILED_FIRST_MIN_K
-           and B >= TILED_FIRST_MIN_ROWS and mls[i].residual == 0
-           and ((B + 63) // 64) * ((_pad64(mls[i].n) + 127) // 128) >= cus):
+    while i < len(mls) - 1 and tiled_layer(h.shape[1], B, dev, mls[i]):
         y = torch.empty(B, layers[i].linear.out_features, device=dev, dtype=torch.float32)
         launches.append(("rk_linear_tiled", [h.data_ptr(), h.stride(0), B, h.shape[1], ops.ctypes.byref(mls[i]),
                                              y.data_ptr(), y.stride(0), None]))

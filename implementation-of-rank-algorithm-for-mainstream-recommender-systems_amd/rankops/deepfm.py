@@ -14,7 +14,10 @@ Launches: rk_fm_gather_packed (both embedding orders, fm1, fm2 and the deep inpu
 one packed [V, pad4(D+1)] table per field, built once per weight version by rk_fm_pack_table;
 PACKED_TABLES = False gathers from the two nn.Embedding weights with rk_fm_gather), then
 the deep layers on rk_linear with BatchNorm folded into the epilogue; the last one also
-evaluates deep_output_layer, final_layer(3->1) and the sigmoid.
+evaluates deep_output_layer, final_layer(3->1) and the sigmoid.  When the first deep layer runs as a
+2D-tiled GEMM (common.tiled_layer: the 30-field benchmark configuration), the gather, fm1, fm2 and
+that layer are one rk_fm_linear_packed launch (FUSED_FRONT): the deep input is staged in LDS and
+never written to HBM, and the eval forward is two launches.
 """
 from __future__ import annotations
 
@@ -29,6 +32,8 @@ WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_s
 # Eval gather from packed [V, pad4(D+1)] tables (one line pair per row instead of a row line plus
 # a separate line for the 4-B first-order weight; costs one extra table copy in HBM).
 PACKED_TABLES = True
+# Gather + FM + first deep layer in one rk_fm_linear_packed launch when that layer is tiled.
+FUSED_FRONT = True
 
 
 class DeepFM(EngineModule):
@@ -77,7 +82,7 @@ class DeepFM(EngineModule):
             pk = self._fm_packs[name] = PackedFMTable()
         return pk(self.second_order_embeddings[name].weight, self.first_order_embeddings[name].weight)
 
-    def _gather_plan(self, names, category):
+    def _gather_plan(self, names, category, deep=True):
         D = self.embedding_dim
         first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
         B, dev = first.shape[0], first.device
@@ -93,7 +98,7 @@ class DeepFM(EngineModule):
             else:
                 second_segs.append(ops.table_segment(self.second_order_embeddings[name].weight, idx, f * D))
                 first_segs.append(ops.table_segment(self.first_order_embeddings[name].weight, idx, f))
-        deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32)
+        deep_in = torch.empty(B, len(names) * D, device=dev, dtype=torch.float32) if deep else None
         fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         return (packed, second_segs, first_segs, D, B, deep_in, fm1, fm2)
@@ -121,10 +126,9 @@ class DeepFM(EngineModule):
         return lambda: self._launch(plan)
 
     def _eager_eval(self, category):
-        """The eval forward through the EagerCalls cache (common.EagerCalls): the packed FM gather
-        and the tail's launches reused with fresh outputs patched in; None off that path."""
-        if not common.EAGER_CACHE:
-            return None
+        """The eval forward through the EagerCalls cache (common.EagerCalls): the marshalled
+        launches (rk_fm_linear_packed + rk_mlp_forward, or rk_fm_gather_packed + the tail) reused
+        with fresh outputs patched in; rebuilt per call with EAGER_CACHE off.  None off that path."""
         try:
             idx = [category[n] for n in self.second_order_embeddings]
         except (KeyError, TypeError):
@@ -133,42 +137,65 @@ class DeepFM(EngineModule):
             return None
         dev = idx[0].device
         stream = torch.cuda.current_stream(dev).cuda_stream
-        calls = self.__dict__.setdefault("_eager", common.EagerCalls())
-        key = calls.key(self, idx, stream)
-        hit = calls.get(key)
-        if hit is None:
-            hit = self._eager_build(category, key, calls)
+        if common.EAGER_CACHE:
+            calls = self.__dict__.setdefault("_eager", common.EagerCalls())
+            key = calls.key(self, idx, stream)
+            hit = calls.get(key)
+            if hit is None:
+                hit = self._eager_build(category)
+                if hit is None:
+                    return None
+                calls.put(key, hit)
+        else:
+            hit = self._eager_build(category)
             if hit is None:
                 return None
-        launches, ep, B, _keep = hit
+        launches, fm_slots, ep, B, _keep = hit
         fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         deep = torch.empty(B, 1, device=dev, dtype=torch.float32)
         total = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
-        gather = launches[0][1]
-        gather[6], gather[7] = fm1.data_ptr(), fm2.data_ptr()
+        front = launches[0][1]
+        front[fm_slots[0]], front[fm_slots[1]] = fm1.data_ptr(), fm2.data_ptr()
         ep.fm1, ep.fm2, ep.head_aux = fm1.data_ptr(), fm2.data_ptr(), deep.data_ptr()
         ep.head_logit, ep.head_prob = total.data_ptr(), prob.data_ptr()
         common.run_launches(launches, stream)
         return prob, total, fm1, fm2, deep
 
-    def _eager_build(self, category, key, calls):
+    def _eager_build(self, category):
+        """(launches, fm1/fm2 argument slots of launches[0], head epilogue, B, keep-alive objects)."""
         names = list(self.second_order_embeddings)
-        plan = self._gather_plan(names, category)
+        first = category[names[0]]
+        B, dev, D = first.shape[0], first.device, self.embedding_dim
+        head_kwargs = dict(final_w=self.final_layer.weight, final_b=self.final_layer.bias)
+        l0, fused = self._tail[0], None
+        if FUSED_FRONT and len(self._tail) >= 2 and len(names) <= 32 and first.dim() == 1:
+            w0 = common.PACKED(l0.linear.weight)
+            ml0 = ops.make_mlp_layer(l0.linear.weight, w0, **l0.epilogue_kwargs())
+            fused = common.tiled_layer(len(names) * D, B, dev, ml0)
+        plan = self._gather_plan(names, category, deep=not fused)
         packed, second, first, D, B, deep_in, fm1, fm2 = plan
         if not packed or any(t.data_ptr() != category[n].data_ptr() for t, n in zip(first, names)):
             return None  # unpacked tables, or contiguous copies of the indices: the uncached path
-        tail = common.tail_launches(deep_in, self._tail, self.deep_output_layer,
-                                    dict(final_w=self.final_layer.weight, final_b=self.final_layer.bias))
+        ops._lib.ensure_device(dev)
+        arr = ops._seg_array(second)
+        if fused:  # rk_fm_linear_packed (gather, fm1, fm2, deep layer 0) + the rest of the tail
+            y = torch.empty(B, l0.linear.out_features, device=dev, dtype=torch.float32)
+            tail = common.tail_launches(y, self._tail[1:], self.deep_output_layer, head_kwargs)
+            if tail is None:
+                return None
+            tl, ep, keep = tail
+            front = ["rk_fm_linear_packed", [arr, len(second), D, B, ops.ctypes.byref(ml0), y.data_ptr(), y.stride(0),
+                                             None, None, None]]
+            return [front] + tl, (7, 8), ep, B, (keep, arr, plan, w0, ml0, y)
+        tail = common.tail_launches(deep_in, self._tail, self.deep_output_layer, head_kwargs)
         if tail is None:
             return None
         tl, ep, keep = tail
-        ops._lib.ensure_device(deep_in.device)
-        arr = ops._seg_array(second)
         gather = ["rk_fm_gather_packed", [arr, len(second), D, B, deep_in.data_ptr(), deep_in.stride(0), None, None,
                                           None]]
-        return calls.put(key, ([gather] + tl, ep, B, (keep, arr, plan)))
+        return [gather] + tl, (6, 7), ep, B, (keep, arr, plan)
 
     def forward(self, category):
         if not self.training:

@@ -152,6 +152,16 @@ def fm_gather_packed(fields, dim, batch, deep_in, fm1, fm2):
                                   ptr(fm2), _lib.stream_of(deep_in)), "rk_fm_gather_packed")
 
 
+def fm_linear_packed(fields, dim, batch, layer: "_lib.MlpLayer", y, fm1, fm2):
+    """rk_fm_linear_packed: the packed FM gather, fm1, fm2 and the first deep layer into y [batch, n]
+    in one launch; fields = packed_segment(table, idx, dim, f * dim) per field."""
+    lib = _lib.load()
+    _lib.ensure_device(y.device)
+    arr = _seg_array(fields)
+    check(lib.rk_fm_linear_packed(arr, len(fields), dim, batch, ctypes.byref(layer), ptr(y), y.stride(0), ptr(fm1),
+                                  ptr(fm2), _lib.stream_of(y)), "rk_fm_linear_packed")
+
+
 def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, use_softmax, out_ptr, ld_out,
                   batch, device):
     lib = _lib.load()

@@ -32,6 +32,8 @@
  *   rk_bst_attention_masked  the same with BSTTransformer.forward's key_padding_mask  bst.py:66-84
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
+ *   rk_fm_linear_packed  the DeepFM front end in one launch: packed-table gather, fm1, fm2 and the
+ *                      first deep layer (the deep input never reaches HBM)  deepfm.py:100-112,122-142
  *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
  *   rk_fwfm_forward    FwFM.forward()                        fwfm.py:114-139
  *   training (loss.backward() + optimizer.step() of the train() loops, dcn.py:196-201):
@@ -353,6 +355,18 @@ int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, int32_t 
  * (deepfm.py:100-112, 960 -> 512) it reads every weight 64 times per 4096 rows instead of 256. */
 int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_mlp_layer* layer,
                     float* y, int64_t ldy, void* stream);
+
+/* The DeepFM eval front end as one 2D-tiled launch (deepfm.py:122-142 then deepfm.py:100-112 for the
+ * first deep layer): for every sample b, fm1[b] = sum_f first-order weight, fm2[b] = 0.5 sum_d
+ * ((sum_f e_f)^2 - sum_f e_f^2)[d], and y[b, :] = epilogue(concat_f(e_f) . W^T) with
+ * e_f = row idx_f[b] of field f's packed table (rk_fm_pack_table layout, as rk_fm_gather_packed:
+ * segment f = {packed table, unit-stride index, rows, dim, src_ld >= dim + 1, out_col = f * dim}).
+ * The layer is packed by rk_mlp_pack_weight for K = num_fields * dim (no residual).  dim a power of
+ * two in [4, 256], num_fields <= 32.  The concatenated deep input is staged in LDS only.
+ * Out-of-range indices read zero rows and raise RK_FLAG_INDEX_OOB.                               */
+int rk_fm_linear_packed(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                        const rk_mlp_layer* layer, float* y, int64_t ldy, float* fm1, float* fm2,
+                        void* stream);
 
 /* FwFM.forward (fwfm.py:114-139): per sample, logit = sum_f linear[f] row + sum_{i<j} field_weight[p]
  * <embeddings[i] row, embeddings[j] row> + bias[0] (p runs i-major over i < j, fwfm.py:129-136),

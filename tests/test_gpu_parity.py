@@ -305,8 +305,11 @@ def test_bst_fused_blocks_oob_sequence_index_is_flagged():
 @pytest.mark.parametrize("tiled", [True, False])
 def test_deepfm_wide_first_layer_tiled(tiled, monkeypatch):
     """DeepFM configs[1] shape (30 fields x 32: a 960-wide first layer) at batch >= 2048 runs its
-    first layer through rk_linear_tiled; both paths match the oracle and each other."""
+    first layer tiled (the fused rk_fm_linear_packed front end) or in the fused tail; both match
+    the oracle."""
     monkeypatch.setattr(rankops.common, "TILED_FIRST_MIN_K", 512 if tiled else 0)
+    if tiled:  # 33 x 4 tiles at batch 2100: let them count as filling the GPU
+        monkeypatch.setattr(rankops.common, "_num_cus", lambda device: 64)
     cfg = {"dim": 32, "fields": FIELDS30}
     out, ref = run_pair("deepfm", cfg, B=2100)
     _compare(out, ref, f"deepfm-wide-tiled{tiled}")
