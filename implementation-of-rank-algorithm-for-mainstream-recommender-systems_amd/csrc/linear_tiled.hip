@@ -19,13 +19,12 @@ constexpr int kLtCols = 128;  // output columns per workgroup (8 tiles of 16)
 constexpr int kLtKB = 256;    // K-block staged in LDS
 constexpr int kLtLd = kLtKB + kMlpLdPad;
 constexpr int kLtMaxFields = 32;
-// Lockstep inside a K-block: all waves meet at a bare s_barrier every RK_LT_SYNC chunks (0: only at
-// the block ends).  Without it the matrix pipe serves a SIMD's 4 waves oldest-first and each
-// block closes on one lone wave per SIMD (tools/lt_phases.py: block 0's MFMAs issued at 14.7k /
-// 17.4k / 21.8k / 24.3k cycles for the SIMD's waves 0 / 4 / 8 / 12).
-#ifndef RK_LT_SYNC
-#define RK_LT_SYNC 4
-#endif
+// Weight ring depth (chunks of 16 k).  Loads retire in order and the compiler's wait for ring slot
+// s in the block loop is vmcnt(kLtPD - 1): at a block's start the next block's A loads (issued
+// ahead of the refills) must land within kLtPD - 5 chunks.  With 4 the first chunk of every block
+// waited for the gather (tools/lt_phases.py: ~22.4k cycles per 16-chunk block against 16.4k of
+// MFMA).
+constexpr int kLtPD = 8;
 
 struct LtArgs {
   const float* x;
@@ -36,6 +35,7 @@ struct LtArgs {
   int64_t ldy;
   int x_vec;
   int nrt, nct;  // row tiles, column tiles
+  int nctg;      // column tiles in the grid: nct, or (FM) at least 4 so that every row has an FM owner
 };
 
 // The fused DeepFM front end's A source (rk_fm_linear_packed): row b of A is the concatenation of
@@ -59,8 +59,8 @@ template <bool FM>
 __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtFm fm) {
   // [2][kLtRows * kLtLd] A blocks, then (FM) [F][kLtRows] row pointers
   extern __shared__ __attribute__((aligned(16))) float lt_sm[];
-  const int l = blockIdx.x, within = l % (8 * a.nct);
-  const int rt = 8 * (l / (8 * a.nct)) + within % 8, ctile = within / 8;
+  const int l = blockIdx.x, within = l % (8 * a.nctg);
+  const int rt = 8 * (l / (8 * a.nctg)) + within % 8, ctile = within / 8;
   if (rt >= a.nrt) return;  // the whole workgroup, before any barrier
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef RK_MLP_PHASES
@@ -75,87 +75,131 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
   const rk_mlp_layer& L = a.L;
   const bool col_live = n < pad64(L.n);
 
-  // weight stream of this lane's row over the whole K (ring of 4 chunks)
-  const float* wrow = wfrag(L, col_live ? (n >> 4) : 0, lane);
-  const int kchunks = a.Kp / 16;
-  f32x4_t ring[kMlpPD];
+  // FM: the staged rows' indices, issued first (F * 64 <= 2048 entries: at most 2 per thread;
+  // entry e = field e / 64, row e % 64, so a wave's loads are one field's 64 contiguous indices)
+  constexpr int kIdxPer = kLtMaxFields * kLtRows / kMlpThreads;
+  int64_t iv[kIdxPer];
+  if constexpr (FM) {
 #pragma unroll
-  for (int s = 0; s < kMlpPD; ++s) ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * s);
+    for (int u = 0; u < kIdxPer; ++u) {
+      const int e = tid + kMlpThreads * u;
+      const int f = __builtin_amdgcn_readfirstlane(e / kLtRows);  // wave-uniform: scalar descriptor loads
+      const int64_t m = m0 + e % kLtRows;
+      iv[u] = (f < fm.F && m < a.M) ? fm.idx[f][m] : -1;
+    }
+  }
+
+  // weight stream of this wave's column tile over the whole K (ring of kLtPD chunks), as buffer
+  // loads: the tile's fragment slab is one wave-uniform descriptor, a lane's address one 32-bit
+  // offset (16 lane), the chunk a scalar offset; chunks past the slab read as zeros (bounds check)
+  const int kchunks = a.Kp / 16;
+  const int wtile = __builtin_amdgcn_readfirstlane(col_live ? (n >> 4) : 0);  // n >> 4 = n0 / 16 + ct
+  const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(L.w + (int64_t)wtile * (L.ldw / 16) * kFragStep), 0, kchunks * kFragStep * (int)sizeof(float),
+      0x00020000);
+  auto wload = [&](int chunk) {
+    return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(wsrd, 16 * lane,
+                                                                              chunk * kFragStep * 4, 0));
+  };
+  f32x4_t ring[kLtPD];
+#pragma unroll
+  for (int s = 0; s < kLtPD; ++s) ring[s] = wload(s);
   const ColEpi ep = col_epi(L, n < L.n ? n : 0);
 
   // FM: the staged rows' row pointers (null past M or out of range: a zero row, as rk_fm_gather)
   const float** s_ptr = reinterpret_cast<const float**>(lt_sm + 2 * kLtRows * kLtLd);
   if constexpr (FM) {
     bool oob = false;
-    for (int e = tid; e < fm.F * kLtRows; e += kMlpThreads) {
-      const int f = e / kLtRows, r = e % kLtRows;  // f is wave-uniform
-      const int64_t m = m0 + r;
-      const float* p = nullptr;
-      if (m < a.M) {
-        const int64_t i = fm.idx[f][m];
-        if ((uint64_t)i < (uint64_t)fm.rows[f])
-          p = fm.src[f] + i * fm.ld[f];
-        else
+#pragma unroll
+    for (int u = 0; u < kIdxPer; ++u) {
+      const int e = tid + kMlpThreads * u;
+      const int f = __builtin_amdgcn_readfirstlane(e / kLtRows);
+      if (f < fm.F) {
+        const float* p = nullptr;
+        if ((uint64_t)iv[u] < (uint64_t)fm.rows[f])
+          p = fm.src[f] + iv[u] * fm.ld[f];
+        else if (m0 + e % kLtRows < a.M)
           oob = true;
+        s_ptr[e] = p;
       }
-      s_ptr[e] = p;
     }
     if (oob) flag_oob(fm.flags);
     mlp_lds_barrier();
   }
   MLP_MARK(0, t0);
-  // FM sums: this workgroup owns the rows wave + 16 j with j % min(nct, 4) == ctile; lane holds quad
-  // (lane % G) of field (k / dim) for every block, so the field sum is a shuffle over lane / G
+  // FM sums: workgroup ctile < 4 owns the rows wave + 16 ctile (the grid has >= 4 column tiles);
+  // lane holds quad (lane % G) of field (k / dim) for every block, so the field sum is a shuffle
+  // over lane / G
   const int G = FM ? (1 << fm.dim_shift) / 4 : 1;
-  f32x4_t fs[4], fq[4];
-  float fo[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    fs[j] = fq[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    fo[j] = 0.f;
-  }
-  const int fm_groups = a.nct < 4 ? a.nct : 4;
-  auto fm_mine = [&](int j) { return FM && ctile < fm_groups && j % fm_groups == ctile; };
+  const bool fm_owner = FM && ctile < 4;
+  f32x4_t fs = {0.f, 0.f, 0.f, 0.f}, fq = {0.f, 0.f, 0.f, 0.f};
+  float fo = 0.f;
 
   // A staging: block b covers columns [256 b, min(256 b + 256, Kp)); thread tid moves float4s
   // i = tid + 1024 j of the 64 x 256 block (4 per thread): row wave + 16 j, columns 4 lane ..
+  // The loads are unconditional global loads from a valid address (dead ones from a safe row) and
+  // the zero masks are applied in store_block: a load under a branch, or a select on its value,
+  // made the compiler wait for the gather right after issuing it, and a generic (flat) pointer
+  // read from LDS made every later LDS wait of the MFMA loop wait for the gather too.
+  typedef const f32x4_t __attribute__((address_space(1)))* g4ptr;
+  typedef const float __attribute__((address_space(1)))* gptr;
   f32x4_t stage[4];
+  float fw = 0.f;     // (FM) the owned row's first-order weight of this lane's field
+  unsigned live = 0;  // bit j: stage[j] is real data
+  bool fw_live = false;
   auto load_block = [&](int b) {
     const int kb = b * kLtKB, w = min(kLtKB, a.Kp - kb);
+    const int c = 4 * lane, k = kb + c;
+    const bool kin = c < w && k < a.K;
+    live = 0;
+    if constexpr (FM) {
+      const int dmask = (1 << fm.dim_shift) - 1, d = k & dmask;
+      const float* p[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = wave + 16 * j, c = 4 * lane;
-      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-      const int64_t m = m0 + r;
-      const int k = kb + c;
-      if constexpr (FM) {
-        if (c < w && k < a.K) {
-          const float* p = s_ptr[(k >> fm.dim_shift) * kLtRows + r];
-          if (p) {
-            const int d = k & ((1 << fm.dim_shift) - 1);
-            v = *reinterpret_cast<const f32x4_t*>(p + d);
-            if (fm_mine(j) && d + 4 == (1 << fm.dim_shift)) fo[j] += p[d + 4];
-          }
-        }
-        if (fm_mine(j)) {
-          fs[j] += v;
-          fq[j] += v * v;
-        }
-      } else if (c < w && m < a.M) {
+      for (int j = 0; j < 4; ++j) p[j] = s_ptr[(kin ? (k >> fm.dim_shift) : 0) * kLtRows + wave + 16 * j];
+      const float* safe = fm.src[0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = kin && p[j] != nullptr;
+        live |= (unsigned)ok << j;
+        stage[j] = *(g4ptr)(ok ? p[j] + d : safe);
+      }
+      const float* pm = ctile == 0 ? p[0] : ctile == 1 ? p[1] : ctile == 2 ? p[2] : p[3];
+      fw_live = fm_owner && kin && pm != nullptr && d + 4 == dmask + 1;
+      fw = *(gptr)(fw_live ? pm + dmask + 1 : safe);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t m = m0 + wave + 16 * j;
+        const bool ok = kin && m < a.M;
         if (a.x_vec) {
-          if (k < a.K) v = *reinterpret_cast<const f32x4_t*>(a.x + m * a.ldx + k);
-        } else {
+          live |= (unsigned)ok << j;
+          stage[j] = *(g4ptr)(ok ? a.x + m * a.ldx + k : a.x);
+        } else {  // unaligned rows: scalar loads, zeros written here
+          live |= 1u << j;
+          f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+          if (c < w && m < a.M) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = k + e < a.K ? a.x[m * a.ldx + k + e] : 0.f;
+            for (int e = 0; e < 4; ++e) v[e] = k + e < a.K ? a.x[m * a.ldx + k + e] : 0.f;
+          }
+          stage[j] = v;
         }
       }
-      stage[j] = v;
     }
   };
+  // (the FM sums are taken here, after the block's MFMAs, not at the loads: summing at the loads
+  // made every block wait for its gather before its first MFMA)
   auto store_block = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      *reinterpret_cast<f32x4_t*>(lt_sm + buf * kLtRows * kLtLd + (wave + 16 * j) * kLtLd + 4 * lane) = stage[j];
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_t v = (live >> j) & 1 ? stage[j] : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4_t*>(lt_sm + buf * kLtRows * kLtLd + (wave + 16 * j) * kLtLd + 4 * lane) = v;
+      if (fm_owner && j == ctile) {
+        fs += v;
+        fq += v * v;
+      }
+    }
+    if (fm_owner) fo += fw_live ? fw : 0.f;
   };
 
   const int nblocks = (a.Kp + kLtKB - 1) / kLtKB;
@@ -165,38 +209,54 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
   MLP_MARK(1, t0);
 
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  int c = 0;  // global chunk index of the weight stream
+  int c = 0;  // global chunk index of the weight stream (a multiple of kLtPD at every block start)
+  // One K-block of nc chunks (4, 8, 12 or 16: Kp % 64 == 0) in groups of kLtPD plus a 4-chunk tail.
+  auto slot = [&](const float* arow, f32x4_t (&ab)[2][2], int q, int nc, auto SS, auto REFILL) {
+    constexpr int S = decltype(SS)::value;  // ring slot = q % kLtPD (c is a multiple of kLtPD)
+    const int qa = min(q + 1, nc - 1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) ab[(S + 1) & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd + 16 * qa);
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4_t bv = ring[S];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = mfma16(ab[S & 1][t][e], bv[e], acc[t]);
+    if constexpr (decltype(REFILL)::value) ring[S] = wload(c + q + kLtPD);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto run_block = [&](const float* arow, int nc) {
+    // A float4s one chunk ahead in two explicit register sets, the read issued before the chunk's
+    // MFMAs (see mlp_core.h mlp_layer)
+    f32x4_t ab[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) ab[0][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd);
+    int q0 = 0;
+    for (; q0 + kLtPD <= nc; q0 += kLtPD) {
+      slot(arow, ab, q0 + 0, nc, std::integral_constant<int, 0>(), std::true_type());
+      slot(arow, ab, q0 + 1, nc, std::integral_constant<int, 1>(), std::true_type());
+      slot(arow, ab, q0 + 2, nc, std::integral_constant<int, 2>(), std::true_type());
+      slot(arow, ab, q0 + 3, nc, std::integral_constant<int, 3>(), std::true_type());
+      slot(arow, ab, q0 + 4, nc, std::integral_constant<int, 4>(), std::true_type());
+      slot(arow, ab, q0 + 5, nc, std::integral_constant<int, 5>(), std::true_type());
+      slot(arow, ab, q0 + 6, nc, std::integral_constant<int, 6>(), std::true_type());
+      slot(arow, ab, q0 + 7, nc, std::integral_constant<int, 7>(), std::true_type());
+    }
+    // nc % 8 == 4: the last block only, so no refills (the ring's load order then stays the same on
+    // every path into the group loop, whose waits the compiler derives from the merged paths)
+    if (q0 < nc) {
+      slot(arow, ab, q0 + 0, nc, std::integral_constant<int, 0>(), std::false_type());
+      slot(arow, ab, q0 + 1, nc, std::integral_constant<int, 1>(), std::false_type());
+      slot(arow, ab, q0 + 2, nc, std::integral_constant<int, 2>(), std::false_type());
+      slot(arow, ab, q0 + 3, nc, std::integral_constant<int, 3>(), std::false_type());
+    }
+    c += nc;
+  };
   for (int b = 0; b < nblocks; ++b) {
     const int buf = b & 1;
     if (b + 1 < nblocks) load_block(b + 1);
     const int bchunks = min(kLtKB, a.Kp - b * kLtKB) / 16;
-    const float* arow = lt_sm + buf * kLtRows * kLtLd + (32 * rh + li) * kLtLd + kq;
-    // A float4s one chunk ahead in two explicit register sets (slot s reads set s & 1; kMlpPD is
-    // even), the read issued before the slot's MFMAs (see mlp_core.h mlp_layer)
-    f32x4_t ab[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) ab[0][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd);
-    for (int q0 = 0; q0 < bchunks; q0 += kMlpPD) {
-#pragma unroll
-      for (int s = 0; s < kMlpPD; ++s) {
-        const int q = q0 + s;
-        const int qa = min(q + 1, bchunks - 1);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          ab[(s + 1) & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * kLtLd + 16 * qa);
-        __builtin_amdgcn_sched_barrier(0);
-        const f32x4_t bv = ring[s];  // c is a multiple of kMlpPD
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) acc[t] = mfma16(ab[s & 1][t][e], bv[e], acc[t]);
-        const int cn = min(c + s + kMlpPD, kchunks - 1);
-        ring[s] = *reinterpret_cast<const f32x4_t*>(wrow + kFragStep * cn);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      c += kMlpPD;
-      if (RK_LT_SYNC && (q0 + kMlpPD) % RK_LT_SYNC == 0 && q0 + kMlpPD < bchunks) mlp_sync_barrier();
-    }
+    run_block(lt_sm + buf * kLtRows * kLtLd + (32 * rh + li) * kLtLd + kq, bchunks);
     if (b < 4) MLP_MARK(2 + 2 * b, t0);
 #ifdef RK_MLP_PHASES
     if (lane == 0 && b == 0) s_mlp_wave_marks[1][wave][0] = (unsigned)(clock64() - t0);
@@ -227,11 +287,9 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
   // FM outputs: sums over the fields (lanes of equal lane % G), then fm2 = 0.5 sum_d (S_d^2 - Q_d)
   // over the quads (deepfm.py:128-140)
   if constexpr (FM) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!fm_mine(j)) continue;
-      f32x4_t s = fs[j], q = fq[j];
-      float o = fo[j];
+    if (fm_owner) {
+      f32x4_t s = fs, q = fq;
+      float o = fo;
       for (int x = G; x < 64; x <<= 1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -245,7 +303,7 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
         part += __shfl_xor(part, x, kWave);
         o += __shfl_xor(o, x, kWave);
       }
-      const int64_t m = m0 + wave + 16 * j;
+      const int64_t m = m0 + wave + 16 * ctile;
       if (lane == 0 && m < a.M) {
         fm.fm2[m] = 0.5f * part;
         fm.fm1[m] = o;
@@ -289,7 +347,8 @@ template <bool FM>
 static int launch_linear_tiled(LtArgs& a, const LtFm& fm, hipStream_t st, const char* what) {
   a.nrt = (int)((a.M + kLtRows - 1) / kLtRows);
   a.nct = (pad64(a.L.n) + kLtCols - 1) / kLtCols;
-  const int64_t blocks = (int64_t)((a.nrt + 7) / 8) * 8 * a.nct;
+  a.nctg = FM ? std::max(a.nct, 4) : a.nct;  // column tiles >= nct only stage rows for their FM sums
+  const int64_t blocks = (int64_t)((a.nrt + 7) / 8) * 8 * a.nctg;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "%s: batch too large", what);
   const size_t shm = 2 * kLtRows * kLtLd * sizeof(float) + (FM ? (size_t)fm.F * kLtRows * sizeof(void*) : 0);
   raise_lds_limit((const void*)linear_tiled_kernel<FM>, (int)shm);

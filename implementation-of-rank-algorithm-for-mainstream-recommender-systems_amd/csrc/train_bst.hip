@@ -504,9 +504,8 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_fwd_pkernel(const float
   }
 }
 
-template <int US, bool RECOMP>
+template <int US>
 __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float* __restrict__ qkv,
-                                                                  const int64_t* __restrict__ seq_len,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ dctx, int64_t B, int T,
                                                                   int d, int heads, float* __restrict__ dqkv) {
@@ -538,7 +537,6 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float
     att_load_regs<4, US>(v, src4, lds4, c0, b * T, T, dh, TP, DP);
   };
   auto load_p = [&](int64_t x) {
-    if (RECOMP) return;  // recomputed from the staged Q and K instead
     const float* Pi = P + (x * (int64_t)T + (prow ? i : 0)) * T;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
@@ -559,7 +557,6 @@ __global__ __launch_bounds__(256, 2) void bst_attn_train_bwd_pkernel(const float
     __syncthreads();
     if (more) load_tiles(it + gridDim.x);
     if (w < NS) {
-      if (RECOMP) att_softmax_strip(pc, sK, sQ, ldt, w, NS, ND, lane, T, seq_len[b], sq);
       f32x4 g[4];
       att_rowdot(g, sV, sC, ldt, w, NS, ND, lane);  // g[jt][r] = dP[i = 16w + li][j = 16jt + kq + r]
       float D = 0.f;
@@ -1070,10 +1067,9 @@ static unsigned att_grid(const void* kernel, int64_t items, size_t lds) {
 // Dynamic LDS above the 64 KiB default: up to 104 KiB (T = 64, dh = 64 backward).
 static void att_set_attrs() {
   for (const void* f : {(const void*)bst_attn_train_fwd_pkernel<1>, (const void*)bst_attn_train_fwd_pkernel<2>,
-                        (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1, false>,
-                        (const void*)bst_attn_train_bwd_pkernel<2, false>, (const void*)bst_attn_train_bwd_pkernel<4, false>,
-                        (const void*)bst_attn_train_bwd_pkernel<1, true>, (const void*)bst_attn_train_bwd_pkernel<2, true>,
-                        (const void*)bst_attn_train_bwd_pkernel<4, true>, (const void*)bst_attn_train_fwd_kernel,
+                        (const void*)bst_attn_train_fwd_pkernel<4>, (const void*)bst_attn_train_bwd_pkernel<1>,
+                        (const void*)bst_attn_train_bwd_pkernel<2>, (const void*)bst_attn_train_bwd_pkernel<4>,
+                        (const void*)bst_attn_train_fwd_kernel,
                         (const void*)bst_attn_train_bwd_kernel})
     raise_lds_limit(f, 160 * 1024);
 }
@@ -1191,10 +1187,8 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
     const size_t lds = att_lds_bytes(T, dh, true);
 #define RK_ATT_BWD(U_)                                                                                          \
   case U_:                                                                                                      \
-    bst_attn_train_bwd_pkernel<U_, false><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_, false>,       \
-                                                     batch * heads, lds),                                      \
-                                            256, lds, (hipStream_t)stream>>>(qkv, nullptr, probs, dctx, batch, T, d, heads, \
-                                                                            dqkv);                              \
+    bst_attn_train_bwd_pkernel<U_><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_>, batch * heads, lds), \
+                                     256, lds, (hipStream_t)stream>>>(qkv, probs, dctx, batch, T, d, heads, dqkv);     \
     break;
     switch (US) { RK_ATT_BWD(1) RK_ATT_BWD(2) RK_ATT_BWD(4) }
 #undef RK_ATT_BWD
@@ -1204,29 +1198,6 @@ RK_API int rk_bst_attn_train_backward(const float* qkv, const float* probs, cons
                               (hipStream_t)stream>>>(qkv, probs, dctx, batch, T,
                                                                                         d, heads, dqkv);
   return check_launch("rk_bst_attn_train_backward");
-}
-
-RK_API int rk_bst_attn_train_backward_recompute(const float* qkv, const int64_t* seq_len, const float* dctx,
-                                                int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
-                                                void* stream) {
-  if (!qkv || !seq_len || !dctx || !dqkv || batch < 0 || T <= 0 || T > kBstTMax || heads <= 0 || d % heads ||
-      d / heads > kBstDhMax || T % 4 || d % 4 || att_slots(T, d / heads) == 0)
-    return fail(RK_ERR_UNSUPPORTED, "rk_bst_attn_train_backward_recompute: T <= %d, T %% 4 == 0, dh %% 4 == 0, "
-                                    "dh <= %d", kBstTMax, kBstDhMax);
-  if (batch == 0) return RK_OK;
-  att_set_attrs();
-  const int dh = d / heads;
-  const size_t lds = att_lds_bytes(T, dh, true);
-#define RK_ATT_BWDR(U_)                                                                                         \
-  case U_:                                                                                                      \
-    bst_attn_train_bwd_pkernel<U_, true><<<att_grid((const void*)bst_attn_train_bwd_pkernel<U_, true>,           \
-                                                    batch * heads, lds),                                        \
-                                           256, lds, (hipStream_t)stream>>>(qkv, seq_len, nullptr, dctx, batch, T, d, \
-                                                                            heads, dqkv);                       \
-    break;
-  switch (att_slots(T, dh)) { RK_ATT_BWDR(1) RK_ATT_BWDR(2) RK_ATT_BWDR(4) }
-#undef RK_ATT_BWDR
-  return check_launch("rk_bst_attn_train_backward_recompute");
 }
 
 RK_API int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,

@@ -256,8 +256,6 @@ SIGNATURES = {
     "rk_bst_gather_pos": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_int32, c_void_p,
                                          c_void_p, c_void_p, c_void_p]),
     "rk_embedding_backward_seq": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p]),
-    "rk_bst_attn_train_backward_recompute": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
-                                                            c_int32, c_void_p, c_void_p]),
     "rk_gemm_wgrad": (ctypes.c_int, [c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                      c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "rk_gemm_wgrad_workspace_floats": (c_int64, [c_int64, c_int64, c_int64]),

@@ -735,14 +735,6 @@ def bst_attn_train_backward(qkv, probs, dctx, B, T, d, heads, dqkv):
                                          _lib.stream_of(qkv)), "rk_bst_attn_train_backward")
 
 
-def bst_attn_train_backward_recompute(qkv, seq_len, dctx, B, T, d, heads, dqkv):
-    """rk_bst_attn_train_backward_recompute: P recomputed from Q, K and seq_len (forward run with
-    probs=None)."""
-    lib = _lib.load()
-    check(lib.rk_bst_attn_train_backward_recompute(ptr(qkv), ptr(seq_len), ptr(dctx), B, T, d, heads, ptr(dqkv),
-                                                   _lib.stream_of(qkv)), "rk_bst_attn_train_backward_recompute")
-
-
 def bst_res_dropout_ln_forward(base, o, p, seed, slot, ln, r, y, mean, rstd):
     lib = _lib.load()
     check(lib.rk_bst_res_dropout_ln_forward(ptr(base), ptr(o), base.shape[0], base.shape[1], float(p), seed,

@@ -782,12 +782,10 @@ class _BSTTrain(torch.autograd.Function):
             ops.linear(x, blk.w_v.weight, None, y_ptr=ops._lib.fptr(qkv, 2 * d), ldy=3 * d,
                        epilogue=ops.make_epilogue(bias=blk.w_v.bias))
             cx = torch.empty(M, d, **f32)
-            # P is kept for the backward: recomputing it there (rk_bst_attn_train_backward_recompute,
-            # forward with probs=None) measured slower at configs[3] (backward 185 -> 242 us, forward
-            # 114 -> 108 us): the backward is latency-bound and the recompute lengthens its chain
-            recompute = False
-            probs = torch.empty(0 if recompute else B * h * T * T, **f32)
-            ops.bst_attn_train_forward(qkv, B, T, d, h, seq_len, None if recompute else probs, cx)
+            # P is kept for the backward (recomputing it there measured slower at configs[3]: backward
+            # 185 -> 242 us against forward 114 -> 108 us)
+            probs = torch.empty(B * h * T * T, **f32)
+            ops.bst_attn_train_forward(qkv, B, T, d, h, seq_len, probs, cx)
             o = torch.empty(M, d, **f32)
             ops.linear(cx, blk.w_o.weight, o, epilogue=ops.make_epilogue(bias=blk.w_o.bias))
             r1, out1 = torch.empty(M, d, **f32), torch.empty(M, d, **f32)
@@ -871,10 +869,7 @@ class _BSTTrain(torch.autograd.Function):
                                 dbe1)
             dWo, dbo, dcx = _lin_grads(do, cx, blk.w_o.weight)
             dqkv = torch.empty(M, 3 * d, **f32)
-            if probs.numel() == 0:
-                ops.bst_attn_train_backward_recompute(qkv, seq_len, dcx, B, T, d, blk.nhead, dqkv)
-            else:
-                ops.bst_attn_train_backward(qkv, probs, dcx, B, T, d, blk.nhead, dqkv)
+            ops.bst_attn_train_backward(qkv, probs, dcx, B, T, d, blk.nhead, dqkv)
             dQ, dK, dV = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
             dWq, dbq, _ = _lin_grads(dQ, xp, blk.w_q.weight, dx=dxp, accumulate=True)
             dWk, dbk, _ = _lin_grads(dK, xp, blk.w_k.weight, dx=dxp, accumulate=True)

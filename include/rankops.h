@@ -601,11 +601,6 @@ int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_
 int rk_bst_attn_train_backward(const float* qkv, const float* probs, const float* dctx,
                                int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
                                void* stream);
-/* The same backward with P recomputed from Q, K and seq_len (no saved probabilities: pair it with
- * rk_bst_attn_train_forward(probs = NULL)); bit-identical P.  Needs T % 4 == 0 and dh % 4 == 0. */
-int rk_bst_attn_train_backward_recompute(const float* qkv, const int64_t* seq_len, const float* dctx,
-                                         int64_t batch, int32_t T, int32_t d, int32_t heads,
-                                         float* dqkv, void* stream);
 int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,
                                   double dropout_p, uint64_t seed, const int64_t* stream_slot,
                                   const float* gamma, const float* beta, float eps, float* r, float* y,

@@ -879,14 +879,11 @@ def test_bst_attention_train_kernels_match_autograd(T, d, heads):
     torch.testing.assert_close(ctx.cpu().double(), c_ref.detach(), atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(dqkv.cpu().double(), dx_ref, atol=1e-4, rtol=1e-4)
     if T % 4 == 0 and (d // heads) % 4 == 0:
-        # no saved P: the forward skips the store, the backward recomputes it (bit-identical values)
+        # no P output (probs = NULL): the same context, bit for bit
         ctx2 = torch.full((B * T, d), float("nan"), device=dev)
-        dqkv2 = torch.full((B * T, 3 * d), float("nan"), device=dev)
         ops.bst_attn_train_forward(qkv_d, B, T, d, heads, len_d, None, ctx2)
-        ops.bst_attn_train_backward_recompute(qkv_d, len_d, dctx_d, B, T, d, heads, dqkv2)
         torch.cuda.synchronize()
         assert torch.equal(ctx2, ctx)
-        assert torch.equal(dqkv2, dqkv)
 
 
 @pytest.mark.gpu
