@@ -509,6 +509,7 @@ def bench_train(batch, steps, warmup, name="dcn"):
         res[mode] = {"samples_per_s": round(batch / t, 1), "ms_per_step": round(1e3 * t, 4)}
         res["params"] = sum(p.numel() for p in model.parameters())
         del model, opt
+    res["eager_over_graph"] = round(res["eager"]["ms_per_step"] / res["graph"]["ms_per_step"], 2)
     res["mode"] = ("forward + loss.backward() + Adam over all params (dense embedding gradients, as "
                    "nn.Embedding(sparse=False) + torch.optim.Adam do)")
     return res

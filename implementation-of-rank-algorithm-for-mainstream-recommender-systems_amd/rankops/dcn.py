@@ -84,7 +84,7 @@ class DCNModel(EngineModule):
         if not isinstance(dense, torch.Tensor) or dense.device.type != "cuda":
             return None
         dev = dense.device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = ops._lib.raw_stream(dev)
         calls = self.__dict__.setdefault("_eager", common.EagerCalls())
         key = calls.key(self, [dense] + idx, stream, (self.cross_weights.mode,))
         hit = calls.get(key)

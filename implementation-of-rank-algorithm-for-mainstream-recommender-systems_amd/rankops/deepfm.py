@@ -136,7 +136,7 @@ class DeepFM(EngineModule):
         if not all(isinstance(t, torch.Tensor) and t.dtype == torch.int64 for t in idx) or idx[0].device.type != "cuda":
             return None
         dev = idx[0].device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = ops._lib.raw_stream(dev)
         if common.EAGER_CACHE:
             calls = self.__dict__.setdefault("_eager", common.EagerCalls())
             key = calls.key(self, idx, stream)

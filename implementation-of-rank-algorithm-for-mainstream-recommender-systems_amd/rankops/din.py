@@ -304,7 +304,7 @@ class DIN(EngineModule):
         if not all(isinstance(t, torch.Tensor) for t in ins) or ins[0].device.type != "cuda":
             return None
         dev = ins[0].device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = ops._lib.raw_stream(dev)
         calls = self.__dict__.setdefault("_eager", common.EagerCalls())
         key = calls.key(self, ins, stream, (self.att_weights.mode, tuple(dense), tuple(category)))
         if calls.get(key) is None and self._eager_build(dense, category, sequence, target, key, calls) is None:

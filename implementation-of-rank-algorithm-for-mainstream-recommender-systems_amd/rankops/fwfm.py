@@ -53,7 +53,7 @@ class FwFM(EngineModule):
                 or idx[0].device.type != "cuda" or any(t.shape != idx[0].shape for t in idx):
             return None
         dev = idx[0].device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = ops._lib.raw_stream(dev)
         calls = self.__dict__.setdefault("_eager", common.EagerCalls())
         key = calls.key(self, idx, stream)
         hit = calls.get(key)

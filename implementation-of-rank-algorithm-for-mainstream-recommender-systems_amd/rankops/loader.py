@@ -300,7 +300,7 @@ def _device_lookup(vocab, chunks, dev, T, sep):
         out = torch.zeros(n, T, dtype=torch.int64, device=dev)
         lens = torch.zeros(n, dtype=torch.int64, device=dev)
     slots, arena, mask = vocab.to_device(dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = _lib.raw_stream(dev)
     keep = []
     r0 = 0
     for c in chunks:
@@ -520,7 +520,7 @@ class BatchAssembler:
         B = _num_rows(table)
         dev = self.device
         lib = _lib.load()
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _lib.raw_stream(dev)
         jobs = self._string_jobs(table, B)
         seq_T = 0
         for kind, _, _, chunks in jobs:

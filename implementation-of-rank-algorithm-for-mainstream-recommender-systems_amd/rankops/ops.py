@@ -82,6 +82,45 @@ def _seg_array(segs):
     return arr
 
 
+_SEG_ARRAYS = {}
+
+
+def table_seg_array(weights, idxs, cols):
+    """The rk_segment array of table segments weights[k][idxs[k]] -> column cols[k], memoized on
+    every field of the structs (pointers, strides, shapes): a repeated training step, whose tables,
+    index tensors and (recycled) gradient buffers come back at the same addresses, reuses the
+    marshalled array instead of building a ctypes struct per field.  The library copies the array
+    into the kernel arguments at launch, so sharing it is safe."""
+    key = tuple((w.data_ptr(), w.stride(0), w.shape[0], w.shape[1], w.stride(1), i.data_ptr(), i.stride(0), i.dim(), c)
+                for w, i, c in zip(weights, idxs, cols))
+    arr = _SEG_ARRAYS.get(key)
+    if arr is None:
+        arr = _seg_array([table_segment(w, i, c) for w, i, c in zip(weights, idxs, cols)])
+        if len(_SEG_ARRAYS) >= 512:
+            _SEG_ARRAYS.clear()
+        _SEG_ARRAYS[key] = arr
+    return arr
+
+
+def dense_table_seg_array(dense, ndense, weights, idxs):
+    """[dense columns 0..ndense) + table segments side by side] as a memoized rk_segment array
+    (DCN / DeepCrossing feature rows; table_seg_array's rules)."""
+    key = (dense.data_ptr(), dense.stride(0), dense.dim(), ndense) + tuple(
+        (w.data_ptr(), w.stride(0), w.shape[0], w.shape[1], w.stride(1), i.data_ptr(), i.stride(0), i.dim())
+        for w, i in zip(weights, idxs))
+    arr = _SEG_ARRAYS.get(key)
+    if arr is None:
+        segs, col = [dense_segment(dense, ndense, 0)], ndense
+        for w, i in zip(weights, idxs):
+            segs.append(table_segment(w, i, col))
+            col += w.shape[1]
+        arr = _seg_array(segs)
+        if len(_SEG_ARRAYS) >= 512:
+            _SEG_ARRAYS.clear()
+        _SEG_ARRAYS[key] = arr
+    return arr
+
+
 def concat_gather(segs, batch: int, out: torch.Tensor):
     lib = _lib.load()
     _lib.ensure_device(out.device)
@@ -95,12 +134,12 @@ def dcn_cross(segs, batch, width, cross_w, cross_b, num_layers, head_w_ptr, x0, 
               xl_in=None, xl_out=None):
     lib = _lib.load()
     _lib.ensure_device(device)
-    arr = _seg_array(segs)
+    arr = _as_seg_array(segs)
     check(lib.rk_dcn_cross(arr, len(segs), batch, width, ptr(cross_w), ptr(cross_b), num_layers, head_w_ptr,
                            ptr(x0), x0.stride(0) if x0 is not None else 0,
                            ptr(xl_in), xl_in.stride(0) if xl_in is not None else 0,
                            ptr(xl_out), xl_out.stride(0) if xl_out is not None else 0,
-                           ptr(partial), torch.cuda.current_stream(device).cuda_stream), "rk_dcn_cross")
+                           ptr(partial), _lib.raw_stream(device)), "rk_dcn_cross")
 
 
 def dcn_forward_args(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head: Epilogue,
@@ -118,14 +157,14 @@ def dcn_forward(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, 
                 device):
     """rk_dcn_forward: gather + cross stack + MLP tail + head in one launch (DCNModel eval forward)."""
     args = dcn_forward_args(segs, batch, width, cross_w, cross_b, num_layers, cross_head_w, layers, head, device)
-    args[-1] = torch.cuda.current_stream(device).cuda_stream
+    args[-1] = _lib.raw_stream(device)
     check(_lib.load().rk_dcn_forward(*args), "rk_dcn_forward")
 
 
 def fm_gather(second, first, dim, batch, deep_in, fm1, fm2):
     lib = _lib.load()
     _lib.ensure_device(deep_in.device)
-    a2, a1 = _seg_array(second), _seg_array(first)
+    a2, a1 = _as_seg_array(second), _as_seg_array(first)
     check(lib.rk_fm_gather(a2, a1, len(second), dim, batch, ptr(deep_in), deep_in.stride(0), ptr(fm1), ptr(fm2),
                            _lib.stream_of(deep_in)), "rk_fm_gather")
 
@@ -170,7 +209,7 @@ def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, u
     check(lib.rk_din_attention(query_ptr, ld_query, ptr(key_table), key_table.shape[0], key_table.stride(0),
                                ptr(seq), seq.stride(0), T, ptr(seq_len), batch, H, ptr(w1), ptr(b1), ptr(w2),
                                ptr(b2), ptr(w3), ptr(b3), 1 if use_softmax else 0, out_ptr, ld_out,
-                               torch.cuda.current_stream(device).cuda_stream), "rk_din_attention")
+                               _lib.raw_stream(device)), "rk_din_attention")
 
 
 def din_attention_dense(query, keys, keys_length, weights, use_softmax, out):
@@ -213,11 +252,16 @@ def afm_forward(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h
           "rk_afm_forward")
 
 
+def _as_seg_array(segs):
+    return segs if isinstance(segs, ctypes.Array) else _seg_array(segs)
+
+
 def fwfm_forward(emb, lin, dim, batch, field_weight, bias, logit, prob):
+    """emb / lin: lists of Segments or ready rk_segment arrays (table_seg_array)."""
     lib = _lib.load()
     _lib.ensure_device(prob.device)
-    check(lib.rk_fwfm_forward(_seg_array(emb), _seg_array(lin), len(emb), dim, batch, ptr(field_weight), ptr(bias),
-                              ptr(logit), ptr(prob), _lib.stream_of(prob)), "rk_fwfm_forward")
+    check(lib.rk_fwfm_forward(_as_seg_array(emb), _as_seg_array(lin), len(emb), dim, batch, ptr(field_weight),
+                              ptr(bias), ptr(logit), ptr(prob), _lib.stream_of(prob)), "rk_fwfm_forward")
 
 
 def bst_attention(qkv, batch, T, d_model, heads, seq_len, ctx):
@@ -383,7 +427,7 @@ def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_wei
     _lib.ensure_device(device)
     args, _keep = _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights,
                                     use_softmax, layers, head, batch, device, l2_col0, l2_scale, l2_out, att_image)
-    check(lib.rk_din_forward(*args, torch.cuda.current_stream(device).cuda_stream), "rk_din_forward")
+    check(lib.rk_din_forward(*args, _lib.raw_stream(device)), "rk_din_forward")
 
 
 class DinPlan:
@@ -400,7 +444,7 @@ class DinPlan:
         self._keep = keep
 
     def launch(self):
-        check(self._lib.rk_din_plan_launch(self._handle, torch.cuda.current_stream(self._device).cuda_stream),
+        check(self._lib.rk_din_plan_launch(self._handle, _lib.raw_stream(self._device)),
               "rk_din_plan_launch")
 
     def __del__(self):
@@ -440,6 +484,31 @@ def linear(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None, *, M
 
 # ---------------------------------------------------------------- training (§8(f) #2)
 
+_WS_FLOATS = {}
+_WS = {}
+
+
+def _wgrad_ws_floats(lib, M, N, R):
+    key = (M, N, R)
+    n = _WS_FLOATS.get(key)
+    if n is None:
+        n = _WS_FLOATS[key] = lib.rk_gemm_wgrad_workspace_floats(M, N, R)
+    return n
+
+
+def _wgrad_workspace(nws: int, device, stream: int) -> torch.Tensor:
+    """rk_gemm_wgrad scratch: one buffer per (device, stream) reused by every eager call (calls on
+    one stream are ordered, and a launch reads only what it wrote); under stream capture a fresh
+    allocation from the graph's pool, so a replay never shares scratch with eager work."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(nws, device=device, dtype=torch.float32)
+    key = (device, stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nws:
+        ws = _WS[key] = torch.empty(max(nws, 1 << 16), device=device, dtype=torch.float32)
+    return ws
+
+
 def gemm(trans_a: bool, trans_b: bool, M: int, N: int, R: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
          C: torch.Tensor, ldc: int = None, *, A_mask: torch.Tensor = None, row_sums: torch.Tensor = None,
          accumulate: bool = False, split: int = 0):
@@ -450,10 +519,11 @@ def gemm(trans_a: bool, trans_b: bool, M: int, N: int, R: int, A: torch.Tensor, 
     ldc_ = C.stride(0) if ldc is None else ldc
     if (trans_a and trans_b and split <= 0 and R >= 512 and (M | N | lda | ldb | ldc_) % 4 == 0
             and all(t is None or t.data_ptr() % 16 == 0 for t in (A, B, A_mask, C, row_sums))):
-        nws = lib.rk_gemm_wgrad_workspace_floats(M, N, R)
-        ws = torch.empty(nws, device=C.device, dtype=torch.float32)
+        nws = _wgrad_ws_floats(lib, M, N, R)
+        st = _lib.stream_of(C)
+        ws = _wgrad_workspace(nws, C.device, st)
         check(lib.rk_gemm_wgrad(M, N, R, ptr(A), lda, ptr(A_mask), ptr(B), ldb, ptr(C), ldc_, ptr(row_sums),
-                                int(accumulate), ptr(ws), nws, _lib.stream_of(C)), "rk_gemm_wgrad")
+                                int(accumulate), ptr(ws), nws, st), "rk_gemm_wgrad")
         return C
     check(lib.rk_gemm(int(trans_a), int(trans_b), M, N, R, ptr(A), lda, ptr(A_mask), ptr(B), ldb, ptr(C),
                       C.stride(0) if ldc is None else ldc, ptr(row_sums), int(accumulate), split,
@@ -507,7 +577,7 @@ def dcn_cross_backward(x0, cross_w, cross_b, num_layers, dxl, dx0, accumulate=Tr
 
 def embedding_backward(grad_segs, batch, dx):
     lib = _lib.load()
-    check(lib.rk_embedding_backward(_seg_array(grad_segs), len(grad_segs), batch, ptr(dx), dx.stride(0),
+    check(lib.rk_embedding_backward(_as_seg_array(grad_segs), len(grad_segs), batch, ptr(dx), dx.stride(0),
                                     _lib.stream_of(dx)), "rk_embedding_backward")
 
 
@@ -671,7 +741,7 @@ def row_l2norm_backward(x, col0, ncols, scale, grad_out, dx):
 
 def fwfm_backward(emb_segs, dim, batch, field_weight, prob, dprob, d_emb, dz, d_field_weight, d_bias):
     lib = _lib.load()
-    check(lib.rk_fwfm_backward(_seg_array(emb_segs), len(emb_segs), dim, batch, ptr(field_weight), ptr(prob),
+    check(lib.rk_fwfm_backward(_as_seg_array(emb_segs), len(emb_segs), dim, batch, ptr(field_weight), ptr(prob),
                                ptr(dprob), ptr(d_emb), d_emb.stride(0), ptr(dz), ptr(d_field_weight), ptr(d_bias),
                                _lib.stream_of(prob)), "rk_fwfm_backward")
 

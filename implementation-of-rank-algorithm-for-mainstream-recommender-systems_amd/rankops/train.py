@@ -24,6 +24,7 @@ masks, so parity tests hand the engine's masks to the oracle.
 from __future__ import annotations
 
 import torch
+import torch.optim.optimizer as _optim_mod
 
 from . import common, ops
 from .common import PACKED, const, fused_mlp_fits
@@ -96,12 +97,12 @@ def embedding_grads(weights, idx, col0, dx, cols=None):
     col0 on (or at the given `cols`): one zero-filled flat buffer for all tables (one fill),
     then rk_embedding_backward."""
     grads = zero_grads(weights, dx.device)
-    segs = []
-    col = col0
-    for k, (g, i) in enumerate(zip(grads, idx)):
-        segs.append(ops.table_segment(g, i, col if cols is None else cols[k]))
-        col += g.shape[1]
-    ops.embedding_backward(segs, dx.shape[0], dx)
+    if cols is None:
+        cols, col = [], col0
+        for g in grads:
+            cols.append(col)
+            col += g.shape[1]
+    ops.embedding_backward(ops.table_seg_array(grads, idx, cols), dx.shape[0], dx)
     return grads
 
 
@@ -121,11 +122,8 @@ class _DCNTrain(torch.autograd.Function):
     def forward(ctx, model, dense, idx, cw, cb, *params):
         B, dev = dense.shape[0], dense.device
         d = model.input_dim
-        segs = [ops.dense_segment(dense, model.num_dense_features, 0)]
-        col = model.num_dense_features
-        for (name, emb), i in zip(model.embeddings.items(), idx):
-            segs.append(ops.table_segment(emb.weight, i, col))
-            col += emb.embedding_dim
+        segs = ops.dense_table_seg_array(dense, model.num_dense_features, [e.weight for e in model.embeddings.values()],
+                                         idx)
         x0 = torch.empty(B, d, device=dev, dtype=torch.float32)
         xl = torch.empty(B, d, device=dev, dtype=torch.float32)
         partial = torch.empty(B, device=dev, dtype=torch.float32)
@@ -371,10 +369,9 @@ class _DeepFMTrain(torch.autograd.Function):
         D = model.embedding_dim
         F = len(names)
         B, dev = idx[0].shape[0], idx[0].device
-        second, first = [], []
-        for f, (name, i) in enumerate(zip(names, idx)):
-            second.append(ops.table_segment(model.second_order_embeddings[name].weight, i, f * D))
-            first.append(ops.table_segment(model.first_order_embeddings[name].weight, i, f))
+        second = ops.table_seg_array([model.second_order_embeddings[n].weight for n in names], idx,
+                                     [f * D for f in range(F)])
+        first = ops.table_seg_array([model.first_order_embeddings[n].weight for n in names], idx, list(range(F)))
         deep_in = torch.empty(B, F * D, device=dev, dtype=torch.float32)
         fm1 = torch.empty(B, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B, 1, device=dev, dtype=torch.float32)
@@ -938,8 +935,9 @@ class _FwFMTrain(torch.autograd.Function):
         lin_w, emb_w = params[:F], params[F:2 * F]
         field_weight, bias = params[2 * F], params[2 * F + 1]
         B, dev = idx[0].shape[0], idx[0].device
-        emb = [ops.table_segment(w, i, 0) for w, i in zip(emb_w, idx)]
-        lin = [ops.table_segment(w, i, 0) for w, i in zip(lin_w, idx)]
+        zeros = [0] * F
+        emb = ops.table_seg_array(emb_w, idx, zeros)
+        lin = ops.table_seg_array(lin_w, idx, zeros)
         prob = torch.empty(B, device=dev, dtype=torch.float32)
         logit = torch.empty(B, device=dev, dtype=torch.float32) if want_logit else None
         ops.fwfm_forward(emb, lin, model.embed_dim, B, field_weight, bias, logit, prob)
@@ -962,7 +960,7 @@ class _FwFMTrain(torch.autograd.Function):
         dz = torch.empty(B, 1, **f32)
         d_r = torch.empty_like(field_weight)
         d_b = torch.empty(1, **f32)
-        ops.fwfm_backward([ops.table_segment(w, i, 0) for w, i in zip(emb_w, idx)], D, B, field_weight, prob,
+        ops.fwfm_backward(ops.table_seg_array(emb_w, idx, [0] * F), D, B, field_weight, prob,
                           _grad_out(dprob, prob), d_emb, dz, d_r, d_b)
         g_emb = embedding_grads(list(emb_w), idx, 0, d_emb)
         g_lin = embedding_grads(list(lin_w), idx, 0, dz, cols=[0] * F)
@@ -997,8 +995,29 @@ class Adam(torch.optim.Optimizer):
                         foreach=foreach, capturable=capturable, differentiable=differentiable, fused=fused)
         super().__init__(params, defaults)
 
-    @torch.no_grad()
     def step(self, closure=None):
+        """torch.optim's step wrapper (a record_function scope and the step hooks) is taken only when
+        a profiler or a hook is there to see it: on the eager loop its cost is of the order of the
+        fused update itself."""
+        if (torch.autograd.profiler._is_profiler_enabled or _optim_mod._global_optimizer_pre_hooks
+                or _optim_mod._global_optimizer_post_hooks or self._optimizer_step_pre_hooks
+                or self._optimizer_step_post_hooks):
+            return _hooked_step(self, closure)
+        return self._step(closure)
+
+    step.hooked = True  # torch.optim.Optimizer._patch_step_function: do not wrap again
+
+    def zero_grad(self, set_to_none: bool = True):
+        """Optimizer.zero_grad; with set_to_none (the default, the reference's loop) a plain reset of
+        every .grad outside a profiler."""
+        if not set_to_none or torch.autograd.profiler._is_profiler_enabled:
+            return super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                p.grad = None
+
+    @torch.no_grad()
+    def _step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -1039,7 +1058,7 @@ class Adam(torch.optim.Optimizer):
             for step, entries in by_step.items():
                 dev = entries[0][0].device
                 ops.adam_step(entries, float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"], step,
-                              torch.cuda.current_stream(dev).cuda_stream)
+                              ops._lib.raw_stream(dev))
                 # the kernel wrote through raw pointers: bump the version counters as torch's
                 # in-place ops would, so weight-derived caches (packed MLP images) are rebuilt
                 torch.autograd.graph.increment_version([t for e in entries for t in (e[0], e[2], e[3])])
@@ -1084,10 +1103,13 @@ class Adam(torch.optim.Optimizer):
         beta1, beta2 = group["betas"]
         ops.check(ops._lib.load().rk_adam_step(arr, n, float(group["lr"]), beta1, beta2, group["eps"],
                                                group["weight_decay"], count,
-                                               torch.cuda.current_stream(dev).cuda_stream), "rk_adam_step")
+                                               ops._lib.raw_stream(dev)), "rk_adam_step")
         torch.autograd.graph.increment_version(bumped)
         return True
 
     def load_state_dict(self, state_dict):
         self.__dict__.pop("_fast", None)  # new state tensors: rebuild the argument blocks
         return super().load_state_dict(state_dict)
+
+
+_hooked_step = torch.optim.Optimizer.profile_hook_step(Adam._step)

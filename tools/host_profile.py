@@ -52,6 +52,8 @@ def train_step(name):
 
 
 kinds = os.environ.get("KINDS", "eval,train").split(",")
+# run the autograd backward on this thread, so that cProfile sees the HIP backward's host side
+torch.autograd.set_multithreading_enabled(False)
 for name in models:
     for kind, mk in (("eval", eval_step), ("train", train_step)):
         if kind not in kinds:
