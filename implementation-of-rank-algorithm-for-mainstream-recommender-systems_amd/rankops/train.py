@@ -1025,7 +1025,13 @@ class Adam(torch.optim.Optimizer):
         for gi, group in enumerate(self.param_groups):
             if not group["capturable"] and self._fast_step(gi, group):
                 continue
-            self.__dict__.get("_fast", {}).pop(gi, None)  # the general path moves step counts
+            if self.__dict__.get("_fast", {}).pop(gi, None) is not None:
+                # the general path moves step counts one parameter at a time: give every parameter
+                # its own step tensor again (the fast path shares one per group)
+                for p in group["params"]:
+                    st = self.state.get(p)
+                    if st and "step" in st:
+                        st["step"] = st["step"].clone()
             beta1, beta2 = group["betas"]
             capturable = group["capturable"]
             by_step = {}
@@ -1089,16 +1095,20 @@ class Adam(torch.optim.Optimizer):
             counts = {float(st["step"]) for st in states}
             if len(counts) != 1:
                 return False
+            # one step tensor object for the group (all counts are equal here): a step is then one
+            # in-place add instead of a foreach over every parameter's CPU scalar
+            shared = states[0]["step"]
+            for st in states:
+                st["step"] = shared
             entries = [(p, g, st["exp_avg"], st["exp_avg_sq"]) for p, g, st in zip(params, grads, states)]
             arr = (ops._lib.AdamTensor * len(entries))(*[
                 ops._lib.AdamTensor(e[0].data_ptr(), e[1].data_ptr(), e[2].data_ptr(), e[3].data_ptr(), e[0].numel(),
                                     None) for e in entries])
             bumped = [t for e in entries for t in (e[0], e[2], e[3])]
-            hit = [key, arr, len(entries), [st["step"] for st in states], int(counts.pop()), bumped, entries,
-                   params[0].device]
+            hit = [key, arr, len(entries), shared, int(counts.pop()), bumped, entries, params[0].device]
             cache[gi] = hit
-        _key, arr, n, steps, count, bumped, _entries, dev = hit
-        torch._foreach_add_(steps, 1.0)
+        _key, arr, n, step_t, count, bumped, _entries, dev = hit
+        step_t.add_(1.0)
         hit[4] = count = count + 1
         beta1, beta2 = group["betas"]
         ops.check(ops._lib.load().rk_adam_step(arr, n, float(group["lr"]), beta1, beta2, group["eps"],
@@ -1110,6 +1120,15 @@ class Adam(torch.optim.Optimizer):
     def load_state_dict(self, state_dict):
         self.__dict__.pop("_fast", None)  # new state tensors: rebuild the argument blocks
         return super().load_state_dict(state_dict)
+
+    def state_dict(self):
+        """Optimizer.state_dict with a step tensor of its own per parameter (the fast path shares
+        one per group; another optimizer loading the dict must not see them aliased)."""
+        sd = super().state_dict()
+        for st in sd["state"].values():
+            if "step" in st:
+                st["step"] = st["step"].clone()
+        return sd
 
 
 _hooked_step = torch.optim.Optimizer.profile_hook_step(Adam._step)
