@@ -501,12 +501,18 @@ def bench_train(batch, steps, warmup, name="dcn"):
         for _ in range(warmup):
             run()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            run()
-        torch.cuda.synchronize()
-        t = (time.perf_counter() - t0) / steps
-        res[mode] = {"samples_per_s": round(batch / t, 1), "ms_per_step": round(1e3 * t, 4)}
+        # best of 3 windows: the eager step is host-bound, and the host is shared with other work
+        # on the box (the spread between windows is reported)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                run()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) / steps)
+        t = min(ts)
+        res[mode] = {"samples_per_s": round(batch / t, 1), "ms_per_step": round(1e3 * t, 4),
+                     "windows_ms": [round(1e3 * x, 4) for x in ts]}
         res["params"] = sum(p.numel() for p in model.parameters())
         del model, opt
     res["eager_over_graph"] = round(res["eager"]["ms_per_step"] / res["graph"]["ms_per_step"], 2)
@@ -660,7 +666,7 @@ def main():
             result["loader"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     if rank == 0 and world == 1 and not args.no_extras and not args.no_train:
         try:
-            result["train"] = {m: bench_train(2048 if m == "bst" else args.batch, max(10, args.steps // 2), 3, m)
+            result["train"] = {m: bench_train(2048 if m == "bst" else args.batch, max(10, args.steps // 2), 10, m)
                                for m in ("dcn", "deepcrossing", "deepfm", "din", "afm", "bst", "fwfm")}
         except Exception as exc:  # reported, never fatal for the headline line
             result["train"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
