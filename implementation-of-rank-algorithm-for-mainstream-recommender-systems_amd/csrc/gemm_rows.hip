@@ -84,7 +84,12 @@ __device__ __forceinline__ f32x4 rows_operand(const RowsChunk<AM>& c) {
   return v;
 }
 
-template <int NK8, int NT, bool EPI, int AM>
+// FAST: every tile's columns lie inside N and C rows are 16-B aligned (the host checks N % (32 NT)),
+// so the epilogue is straight-line float4 stores; ACC (plain products only): C += the product, the
+// slab's C values prefetched at its top.  Both as template flags, the slab loop has no branches on
+// them, and the compiler's vmcnt waits in it stay partial (a branch around the C prefetch made it
+// wait for every outstanding load and store at the first MFMA of each slab).
+template <int NK8, int NT, bool EPI, int AM, bool FAST = false, bool ACC = false>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sB[];
   constexpr int K8 = 8 * NK8, ldb = K8 + 4, BN = 32 * NT;
@@ -149,17 +154,28 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   // Epilogue operands in registers ahead of use: the bias (per column, the same for every slab)
   // once, and for an accumulating product the slab's C values at the top of the slab, so their
   // round trips overlap the MFMAs instead of sitting, one float4 at a time, behind them.
-  const bool cvec = a.c_vec && n0 + BN <= a.N;
+  const bool cvec = FAST || (a.c_vec && n0 + BN <= a.N);
   f32x4 epi[NT][4];
+  if (FAST && EPI) {  // absent bias: zeros, so the epilogue adds unconditionally
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) epi[t][q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  // the activation as one negative-side slope (ReLU 0, LeakyReLU slope, none 1): z > 0 ? z : z ns
+  // keeps NaN like torch.relu and gives -0 for a negative ReLU input (+0 in torch: equal in use)
+  const float neg_slope = a.ep.act == RK_ACT_RELU ? 0.f : a.ep.act == RK_ACT_LEAKY ? a.ep.slope : 1.f;
   if (EPI && cvec && a.ep.bias) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int q = 0; q < 4; ++q) epi[t][q] = *reinterpret_cast<const f32x4*>(a.ep.bias + n0 + 32 * t + 8 * q + hk);
   }
-  for (; s < nslabs; s += stride) {
+  // one 32-row slab (the first one peeled off the loop below, so that the loop is entered in the
+  // state its back edge leaves: the waitcnt pass then derives its waits from one state)
+  auto slab = [&](const int64_t s) {
     const int64_t sn = s + stride < nslabs ? s + stride : s;  // past the end: re-read (unused)
-    if (!EPI && cvec && a.accumulate) {
+    if (!EPI && (FAST ? ACC : (cvec && a.accumulate))) {
       const int64_t mr = s * 32 + l32 < a.M ? s * 32 + l32 : a.M - 1;
       const float* crow = a.C + mr * a.ldc + n0 + hk;
 #pragma unroll
@@ -202,7 +218,17 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
         for (int q = 0; q < 4; ++q) {
           const int n = n0 + 32 * t + 8 * q + hk;
           f32x4 z = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-          if (cvec) {  // epilogue operands already in registers
+          if (FAST) {
+            f32x4* c = reinterpret_cast<f32x4*>(crow + n);
+            if (EPI) {
+              z += epi[t][q];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : z[e] * neg_slope;
+            } else if (ACC) {
+              z += epi[t][q];
+            }
+            *c = z;
+          } else if (cvec) {  // epilogue operands already in registers
             f32x4* c = reinterpret_cast<f32x4*>(crow + n);
             if (EPI) {
               if (a.ep.bias) z += epi[t][q];
@@ -238,7 +264,9 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
           __builtin_amdgcn_sched_barrier(0);  // one float4 of epilogue loads live at a time
         }
     }
-  }
+  };
+  slab(s);
+  for (s += stride; s < nslabs; s += stride) slab(s);
 }
 
 static bool rows_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -293,11 +321,15 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
     kern<<<grid, 256, shm, st>>>(a);
     done = true;
   };
+  // FAST (straight-line float4 epilogue) when every tile is whole and C rows are 16-B aligned
+  const bool fast = a.c_vec && N % (32 * nt) == 0;
 #define RK_ROWS_NT(NK, NT)                                                      \
   if (nk8 == NK && nt == NT) {                                                  \
     if (ep) {                                                                   \
       if (am == kRowsPeriodic)                                                  \
         go(gemm_rows_kernel<NK, NT, true, kRowsPeriodic>);                      \
+      else if (fast)                                                            \
+        go(gemm_rows_kernel<NK, NT, true, kRowsPlain, true>);                   \
       else                                                                      \
         go(gemm_rows_kernel<NK, NT, true, kRowsPlain>);                         \
     } else {                                                                    \
@@ -305,6 +337,10 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
         go(gemm_rows_kernel<NK, NT, false, kRowsMask>);                         \
       else if (am == kRowsPeriodic)                                             \
         go(gemm_rows_kernel<NK, NT, false, kRowsPeriodic>);                     \
+      else if (fast && accumulate)                                              \
+        go(gemm_rows_kernel<NK, NT, false, kRowsPlain, true, true>);            \
+      else if (fast)                                                            \
+        go(gemm_rows_kernel<NK, NT, false, kRowsPlain, true, false>);           \
       else                                                                      \
         go(gemm_rows_kernel<NK, NT, false, kRowsPlain>);                        \
     }                                                                           \
