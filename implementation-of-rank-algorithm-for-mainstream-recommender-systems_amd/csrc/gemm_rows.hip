@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "train_common.h"
 
 namespace rk {
 
@@ -39,6 +40,18 @@ struct RowsArgs {
   int c_vec;  // C rows 16-B aligned (float4 stores)
   int b_vec;  // B rows 16-B aligned (float4 staging loads)
   rk_epilogue ep;
+  // LN epilogue (rk_linear_res_dropout_ln): C = LayerNorm(base + dropout(A B^T + bias)), N = 128
+  const float* ln_bias;
+  const float* ln_base;
+  const float* ln_gamma;
+  const float* ln_beta;
+  float ln_eps, ln_scale;
+  uint32_t ln_thr;
+  uint64_t ln_seed;
+  const int64_t* ln_slot;
+  float* ln_r;
+  float* ln_mean;
+  float* ln_rstd;
 };
 
 // Linear epilogue handled here: bias and ReLU / LeakyReLU (the training layers); anything else
@@ -89,8 +102,12 @@ __device__ __forceinline__ f32x4 rows_operand(const RowsChunk<AM>& c) {
 // slab's C values prefetched at its top.  Both as template flags, the slab loop has no branches on
 // them, and the compiler's vmcnt waits in it stay partial (a branch around the C prefetch made it
 // wait for every outstanding load and store at the first MFMA of each slab).
-template <int NK8, int NT, bool EPI, int AM, bool FAST = false, bool ACC = false>
+// LN (with EPI, FAST, NT = 4, N = 128: a wave's slab holds whole rows, lane l and l + 32 one half
+// each): the BST block's residual LayerNorm (bst.py:84-90, rk_bst_res_dropout_ln_forward) fused into
+// the projection's epilogue, so the projection output never goes to HBM and back.
+template <int NK8, int NT, bool EPI, int AM, bool FAST = false, bool ACC = false, bool LN = false>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
+  static_assert(!LN || (EPI && FAST && NT == 4), "LN epilogue: whole 128-column rows");
   extern __shared__ __attribute__((aligned(16))) float sB[];
   constexpr int K8 = 8 * NK8, ldb = K8 + 4, BN = 32 * NT;
   constexpr int PD = NK8 < 8 ? NK8 : 8;  // ring depth in chunks (divides NK8)
@@ -139,6 +156,12 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
       *reinterpret_cast<f32x4*>(sB + n * ldb + k) = bvals[i];
     }
   }
+  float* const sLN = sB + BN * ldb;  // LN: bias, gamma, beta [3][128]
+  if (LN && tid < 128) {
+    sLN[tid] = a.ln_bias ? a.ln_bias[tid] : 0.f;
+    sLN[128 + tid] = a.ln_gamma[tid];
+    sLN[256 + tid] = a.ln_beta[tid];
+  }
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6;
@@ -165,7 +188,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   // the activation as one negative-side slope (ReLU 0, LeakyReLU slope, none 1): z > 0 ? z : z ns
   // keeps NaN like torch.relu and gives -0 for a negative ReLU input (+0 in torch: equal in use)
   const float neg_slope = a.ep.act == RK_ACT_RELU ? 0.f : a.ep.act == RK_ACT_LEAKY ? a.ep.slope : 1.f;
-  if (EPI && cvec && a.ep.bias) {
+  const uint64_t ln_stream = LN && a.ln_thr ? (uint64_t)*a.ln_slot : 0;
+  if (EPI && !LN && cvec && a.ep.bias) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -190,6 +214,16 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 #pragma unroll
     for (int j = 0; j < NK8; ++j) {
+      if (LN && j == (NK8 > 4 ? NK8 - 4 : 0)) {
+        // the residual rows, 4 chunks before the epilogue (prefetched at the slab top they would be
+        // live through the whole reduction and push the kernel past its register budget)
+        const int64_t mr = s * 32 + l32 < a.M ? s * 32 + l32 : a.M - 1;
+        const float* brow = a.ln_base + mr * a.ldc + hk;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) epi[t][q] = *reinterpret_cast<const f32x4*>(brow + 32 * t + 8 * q);
+      }
       const f32x4 av = rows_operand<AM>(ring[j % PD]);
       // refill the slot with the chunk PD ahead (this slab's j + PD, else the next slab's)
       ring[j % PD] = j + PD < NK8 ? rows_fetch<AM>(a, s, j + PD, l32, hk)
@@ -210,7 +244,57 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
     // n = 32 t + 8 q + 4 (l >> 5) + 0..3: one float4 store each, 4 NT stores per slab (the waitcnt
     // pass can still count the ring loads across them; 64 scalar stores overflowed its counter).
     const int64_t m = s * 32 + l32;
-    if (m < a.M) {
+    if (LN) {
+      // lanes l and l + 32 hold row m (64 columns each) and take the branch together
+      if (m < a.M) {
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int n = 32 * t + 8 * q + hk;
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(sLN + n);
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float o = acc[t][4 * q + e] + b4[e];
+              if (a.ln_thr)
+                o = dropout_keep(a.ln_seed, ln_stream, (uint64_t)m * 128 + n + e, a.ln_thr) ? o * a.ln_scale : 0.f;
+              r[e] = epi[t][q][e] + o;
+              acc[t][4 * q + e] = r[e];
+            }
+            sum += (r[0] + r[1]) + (r[2] + r[3]);
+            *reinterpret_cast<f32x4*>(a.ln_r + m * a.ldc + n) = r;
+            __builtin_amdgcn_sched_barrier(0);  // one float4's hashes at a time (register budget)
+          }
+        sum += __shfl_xor(sum, 32, kWave);
+        const float mean = sum * (1.0f / 128.0f);
+        float var = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) var += (acc[t][r] - mean) * (acc[t][r] - mean);
+        var += __shfl_xor(var, 32, kWave);
+        const float rstd = 1.0f / sqrtf(var * (1.0f / 128.0f) + a.ln_eps);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int n = 32 * t + 8 * q + hk;
+            const f32x4 g4 = *reinterpret_cast<const f32x4*>(sLN + 128 + n);
+            const f32x4 be4 = *reinterpret_cast<const f32x4*>(sLN + 256 + n);
+            f32x4 yv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[e] = (acc[t][4 * q + e] - mean) * rstd * g4[e] + be4[e];
+            *reinterpret_cast<f32x4*>(a.C + m * a.ldc + n) = yv;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        if (hk == 0) {
+          a.ln_mean[m] = mean;
+          a.ln_rstd[m] = rstd;
+        }
+      }
+    } else if (m < a.M) {
       float* crow = a.C + m * a.ldc;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -354,4 +438,73 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
 }
 
 
+// C = LayerNorm(base + dropout(A W^T + bias)) for whole 128-wide rows (the BST residual LayerNorm
+// after the O projection and after FFN2): false when the shape is not the kernel's.
+bool gemm_rows_ln_try(const float* A, int64_t lda, const float* W, int64_t ldw, int64_t M, int K, const float* bias,
+                      const float* base, uint32_t thr, float scale, uint64_t seed, const int64_t* slot,
+                      const float* gamma, const float* beta, float eps, float* r, float* y, float* mean,
+                      float* rstd, hipStream_t st) {
+  if ((K != 32 && K != 64 && K != 128) || (lda & 3) || (ldw & 3) || M <= 0) return false;
+  for (const void* p : {(const void*)A, (const void*)W, (const void*)base, (const void*)r, (const void*)y})
+    if (!rows_aligned16(p)) return false;
+  const int64_t nslabs = (M + 31) / 32;  // (any M: one launch instead of two pays at every size)
+  RowsArgs a = {};
+  a.A = A;
+  a.lda = lda;
+  a.B = W;
+  a.ldb = ldw;
+  a.M = M;
+  a.N = 128;
+  a.K = K;
+  a.C = y;
+  a.ldc = 128;
+  a.c_vec = 1;
+  a.b_vec = 1;
+  a.ln_bias = bias;
+  a.ln_base = base;
+  a.ln_gamma = gamma;
+  a.ln_beta = beta;
+  a.ln_eps = eps;
+  a.ln_scale = scale;
+  a.ln_thr = thr;
+  a.ln_seed = seed;
+  a.ln_slot = slot;
+  a.ln_r = r;
+  a.ln_mean = mean;
+  a.ln_rstd = rstd;
+  const size_t shm = sizeof(float) * ((size_t)128 * (K + 4) + 3 * 128);
+  const int64_t per_tile = std::min<int64_t>((nslabs + kRowsWaves - 1) / kRowsWaves, (int64_t)2 * num_cus());
+  dim3 grid((unsigned)std::max<int64_t>(1, per_tile), 1);
+  auto go = [&](void (*kern)(RowsArgs)) {
+    raise_lds_limit((const void*)kern, 80 * 1024);
+    kern<<<grid, 256, shm, st>>>(a);
+  };
+  if (K == 32)
+    go(gemm_rows_kernel<4, 4, true, kRowsPlain, true, false, true>);
+  else if (K == 64)
+    go(gemm_rows_kernel<8, 4, true, kRowsPlain, true, false, true>);
+  else
+    go(gemm_rows_kernel<16, 4, true, kRowsPlain, true, false, true>);
+  return true;
+}
+
 }  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_linear_res_dropout_ln(const float* x, int64_t ldx, int64_t M, int32_t K, const float* w, int64_t ldw,
+                                    const float* bias, const float* base, double dropout_p, uint64_t seed,
+                                    const int64_t* stream_slot, const float* gamma, const float* beta, float eps,
+                                    float* r, float* y, float* mean, float* rstd, void* stream) {
+  if (!x || !w || !base || !gamma || !beta || !r || !y || !mean || !rstd || M < 0 || K <= 0 ||
+      !(dropout_p >= 0.0 && dropout_p < 1.0) || (dropout_p > 0.0 && !stream_slot))
+    return fail(RK_ERR_INVALID, "rk_linear_res_dropout_ln: bad arguments");
+  if (M == 0) return RK_OK;
+  const uint32_t thr = dropout_threshold(dropout_p);
+  const float scale = (float)(1.0 / (1.0 - dropout_p));
+  if (!gemm_rows_ln_try(x, ldx, w, ldw, M, K, bias, base, thr, scale, seed, stream_slot, gamma, beta, eps, r, y,
+                        mean, rstd, (hipStream_t)stream))
+    return fail(RK_ERR_UNSUPPORTED,
+                "rk_linear_res_dropout_ln: needs K in {32, 64, 128} and 16-B aligned rows");
+  return check_launch("rk_linear_res_dropout_ln");
+}

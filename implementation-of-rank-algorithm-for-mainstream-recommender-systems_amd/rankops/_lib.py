@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RANKOPS_LIB", os.path.join(_HERE, "librankops.so"))
 
 RK_OK = 0
+RK_ERR_UNSUPPORTED = 4  # include/rankops.h
 RK_FLAG_INDEX_OOB = 1
 RK_ACT_NONE, RK_ACT_RELU, RK_ACT_LEAKY, RK_ACT_DICE, RK_ACT_PRELU = 0, 1, 2, 3, 4
 RK_MAX_SEGMENTS = 64
@@ -242,6 +243,9 @@ SIGNATURES = {
                                                  c_void_p, c_void_p]),
     "rk_bst_attn_train_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,
                                                   c_void_p, c_void_p]),
+    "rk_linear_res_dropout_ln": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p,
+                                                c_void_p, ctypes.c_double, ctypes.c_uint64, c_void_p, c_void_p,
+                                                c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_bst_res_dropout_ln_forward": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, ctypes.c_double,
                                                      ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                                                      c_void_p, c_void_p, c_void_p, c_void_p]),

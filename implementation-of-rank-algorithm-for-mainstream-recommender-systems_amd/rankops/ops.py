@@ -805,6 +805,23 @@ def bst_attn_train_backward(qkv, probs, dctx, B, T, d, heads, dqkv):
                                          _lib.stream_of(qkv)), "rk_bst_attn_train_backward")
 
 
+def linear_res_dropout_ln(x, weight, bias, base, p, seed, slot, ln, r, y, mean, rstd) -> bool:
+    """rk_linear_res_dropout_ln: y = LayerNorm(base + dropout(x W^T + bias)) in one launch; False
+    (nothing launched) when the shape is not the fused kernel's (d_model != 128, K, alignment, M)."""
+    d = weight.shape[0]
+    if (d != 128 or weight.shape[1] != x.shape[1] or weight.stride(1) != 1 or x.stride(1) != 1
+            or not all(t.is_contiguous() for t in (base, r, y)) or ln.weight is None or ln.bias is None):
+        return False
+    lib = _lib.load()
+    rc = lib.rk_linear_res_dropout_ln(ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(weight), weight.stride(0),
+                                      ptr(bias), ptr(base), float(p), seed, ptr(slot), ptr(ln.weight), ptr(ln.bias),
+                                      float(ln.eps), ptr(r), ptr(y), ptr(mean), ptr(rstd), _lib.stream_of(x))
+    if rc == _lib.RK_ERR_UNSUPPORTED:
+        return False
+    check(rc, "rk_linear_res_dropout_ln")
+    return True
+
+
 def bst_res_dropout_ln_forward(base, o, p, seed, slot, ln, r, y, mean, rstd):
     lib = _lib.load()
     check(lib.rk_bst_res_dropout_ln_forward(ptr(base), ptr(o), base.shape[0], base.shape[1], float(p), seed,

@@ -23,11 +23,18 @@ masks, so parity tests hand the engine's masks to the oracle.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.optim.optimizer as _optim_mod
 
 from . import common, ops
 from .common import PACKED, const, fused_mlp_fits
+
+
+# BST blocks: the O / FFN2 projections and the residual LayerNorms after them as one launch each
+# (rk_linear_res_dropout_ln) where the shape allows (d_model 128); False: two launches each.
+FUSED_LN = os.environ.get("RANKOPS_FUSED_LN", "1") != "0"
 
 
 # ---------------------------------------------------------------- shared pieces
@@ -783,21 +790,30 @@ class _BSTTrain(torch.autograd.Function):
             # 185 -> 242 us against forward 114 -> 108 us)
             probs = torch.empty(B * h * T * T, **f32)
             ops.bst_attn_train_forward(qkv, B, T, d, h, seq_len, probs, cx)
-            o = torch.empty(M, d, **f32)
-            ops.linear(cx, blk.w_o.weight, o, epilogue=ops.make_epilogue(bias=blk.w_o.bias))
             r1, out1 = torch.empty(M, d, **f32), torch.empty(M, d, **f32)
             m1, s1 = torch.empty(M, **f32), torch.empty(M, **f32)
-            ops.bst_res_dropout_ln_forward(xp, o, p_o, bst_dropout_seed(seed, i, 0), slot, blk.norm1, r1, out1, m1, s1)
-            del o
+            # out1 = LN1(xp + dropout(w_o(cx))): one launch when the shape allows
+            if not (FUSED_LN and ops.linear_res_dropout_ln(cx, blk.w_o.weight, blk.w_o.bias, xp, p_o,
+                                                           bst_dropout_seed(seed, i, 0), slot, blk.norm1, r1, out1,
+                                                           m1, s1)):
+                o = torch.empty(M, d, **f32)
+                ops.linear(cx, blk.w_o.weight, o, epilogue=ops.make_epilogue(bias=blk.w_o.bias))
+                ops.bst_res_dropout_ln_forward(xp, o, p_o, bst_dropout_seed(seed, i, 0), slot, blk.norm1, r1, out1, m1,
+                                               s1)
+                del o
             f1 = torch.empty(M, d, **f32)
             ops.linear(out1, blk.ffn[0].weight, f1, epilogue=ops.make_epilogue(bias=blk.ffn[0].bias))
             a = torch.empty(M, d, **f32)
             ops.bst_leaky_dropout(None, f1, blk.ffn[1].negative_slope, p_f, bst_dropout_seed(seed, i, 1), slot, False, a)
-            f2 = torch.empty(M, d, **f32)
-            ops.linear(a, blk.ffn[3].weight, f2, epilogue=ops.make_epilogue(bias=blk.ffn[3].bias))
             r2, out = torch.empty(M, d, **f32), torch.empty(M, d, **f32)
             m2, s2 = torch.empty(M, **f32), torch.empty(M, **f32)
-            ops.bst_res_dropout_ln_forward(out1, f2, p_o, bst_dropout_seed(seed, i, 2), slot, blk.norm2, r2, out, m2, s2)
+            if not (FUSED_LN and ops.linear_res_dropout_ln(a, blk.ffn[3].weight, blk.ffn[3].bias, out1, p_o,
+                                                           bst_dropout_seed(seed, i, 2), slot, blk.norm2, r2, out,
+                                                           m2, s2)):
+                f2 = torch.empty(M, d, **f32)
+                ops.linear(a, blk.ffn[3].weight, f2, epilogue=ops.make_epilogue(bias=blk.ffn[3].bias))
+                ops.bst_res_dropout_ln_forward(out1, f2, p_o, bst_dropout_seed(seed, i, 2), slot, blk.norm2, r2, out,
+                                               m2, s2)
             saves.append((x, xp, qkv, probs, cx, r1, out1, m1, s1, f1, a, r2, m2, s2))
             x = out
         mean_pool = model.pooling_method != "sum"

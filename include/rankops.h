@@ -59,6 +59,7 @@
  *   rk_fwfm_backward   FwFM backward (embedding rows, pair weights, bias)  fwfm.py:114-139,150-156
  *   rk_afm_pairs, rk_afm_pool_forward, rk_afm_pool_backward, rk_afm_pair_fold
  *   rk_bst_add_pos, rk_bst_gather_pos, rk_bst_attn_train_forward / _backward, rk_bst_res_dropout_ln_forward,
+ *   rk_linear_res_dropout_ln (projection + residual LayerNorm fused),
  *   rk_bst_ln_backward, rk_bst_pool_ln_backward, rk_bst_pos_backward, rk_bst_leaky_dropout,
  *   rk_bst_pool / _backward
  *                      BSTTransformer train forward (activations kept) and backward  bst.py:66-91,238-241
@@ -601,6 +602,16 @@ int rk_bst_attn_train_forward(const float* qkv, int64_t batch, int32_t T, int32_
 int rk_bst_attn_train_backward(const float* qkv, const float* probs, const float* dctx,
                                int64_t batch, int32_t T, int32_t d, int32_t heads, float* dqkv,
                                void* stream);
+/* The O / FFN2 projection and the residual LayerNorm after it in one launch (bst.py:84-90):
+ * r = base + dropout(x W^T + bias), y = LayerNorm(r) (gamma, beta, eps), mean / rstd per row, for
+ * d_model = N = 128: the projection output never reaches HBM.  x [M, K] (ld ldx), W [128, K] (ld
+ * ldw), base / r / y [M, 128] contiguous; K in {32, 64, 128}, 16-B aligned rows
+ * (RK_ERR_UNSUPPORTED otherwise: use rk_linear + rk_bst_res_dropout_ln_forward).
+ * Same dropout mask as rk_bst_res_dropout_ln_forward for the same (seed, stream slot).          */
+int rk_linear_res_dropout_ln(const float* x, int64_t ldx, int64_t M, int32_t K, const float* w, int64_t ldw,
+                             const float* bias, const float* base, double dropout_p, uint64_t seed,
+                             const int64_t* stream_slot, const float* gamma, const float* beta, float eps,
+                             float* r, float* y, float* mean, float* rstd, void* stream);
 int rk_bst_res_dropout_ln_forward(const float* base, const float* o, int64_t rows, int32_t d,
                                   double dropout_p, uint64_t seed, const int64_t* stream_slot,
                                   const float* gamma, const float* beta, float eps, float* r, float* y,

@@ -1110,3 +1110,47 @@ def test_adam_fast_step_matches_torch_over_storage_changes():
     theirs.step()
     for a, b in zip(pa, qa):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,p", [(131072 + 37, 128, 0.1), (4096, 64, 0.0), (333, 32, 0.25)])
+def test_linear_res_dropout_ln_matches_two_launch_path(M, K, p):
+    """rk_linear_res_dropout_ln (the BST O / FFN2 projection with the residual LayerNorm in its
+    epilogue) against rk_linear + rk_bst_res_dropout_ln_forward on the same inputs and dropout
+    stream: the same projection and mask (r bit-identical), LayerNorm statistics summed in another
+    order (1e-5)."""
+    g = torch.Generator().manual_seed(M + K)
+    d = 128
+    x = torch.randn(M, K, generator=g).cuda()
+    w = (0.1 * torch.randn(d, K, generator=g)).cuda()
+    b = torch.randn(d, generator=g).cuda()
+    base = torch.randn(M, d, generator=g).cuda()
+    ln = torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.1 * torch.randn(d, generator=g))
+        ln.bias.copy_(0.1 * torch.randn(d, generator=g))
+    slot = torch.full((1,), 5, dtype=torch.int64, device="cuda")
+    outs = []
+    for fused in (True, False):
+        r, y = torch.empty(M, d, device="cuda"), torch.empty(M, d, device="cuda")
+        mean, rstd = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+        if fused:
+            assert ops.linear_res_dropout_ln(x, w, b, base, p, 1234, slot, ln, r, y, mean, rstd)
+        else:
+            o = torch.empty(M, d, device="cuda")
+            ops.linear(x, w, o, epilogue=ops.make_epilogue(bias=b))
+            ops.bst_res_dropout_ln_forward(base, o, p, 1234, slot, ln, r, y, mean, rstd)
+        torch.cuda.synchronize()
+        outs.append((r, y, mean, rstd))
+    (r1, y1, m1, s1), (r2, y2, m2, s2) = outs
+    if M >= 131072:  # both projections on gemm_rows: the same products, the same mask
+        assert torch.equal(r1, r2)
+    else:  # rk_linear takes its generic kernel at this M (another k order)
+        torch.testing.assert_close(r1, r2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(m1, m2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s1, s2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y1, y2, rtol=1e-5, atol=1e-5)
+    # and against float64 torch on the fused path's own r
+    rr = r1.double()
+    want = torch.nn.functional.layer_norm(rr, (d,), ln.weight.double(), ln.bias.double(), ln.eps)
+    torch.testing.assert_close(y1.double(), want, rtol=1e-4, atol=1e-4)
