@@ -343,8 +343,14 @@ class PackedWeights:
         hit = self._d.get(id(w))
         if hit is None or hit[0]() is not w or hit[1] != key:
             d, i = self._d, id(w)
-            ref = weakref.ref(w, lambda _r, d=d, i=i: d.pop(i, None) if d.get(i, (None,))[0] is _r else None)
-            hit = (ref, key, ops.pack_mlp_weight(w))
+            if hit is not None and hit[0]() is w and hit[1][:2] == key[:2] and hit[1][3:] == key[3:] \
+                    and not torch.cuda.is_current_stream_capturing():
+                # only the version moved (an optimizer step): rewrite the image in place, on the
+                # stream, behind every launch already reading it
+                hit = (hit[0], key, ops.pack_mlp_weight(w, out=hit[2]))
+            else:
+                ref = weakref.ref(w, lambda _r, d=d, i=i: d.pop(i, None) if d.get(i, (None,))[0] is _r else None)
+                hit = (ref, key, ops.pack_mlp_weight(w))
             self._d[i] = hit
         return hit[2]
 

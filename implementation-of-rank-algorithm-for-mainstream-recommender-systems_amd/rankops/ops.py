@@ -324,13 +324,14 @@ def make_epilogue(**kw) -> Epilogue:
 _MLP_PTR_FIELDS = {f for f, t in _lib.MlpLayer._fields_ if t is ctypes.c_void_p}
 
 
-def pack_mlp_weight(weight: torch.Tensor) -> torch.Tensor:
-    """[n, k] nn.Linear weight -> the zero-padded [pad64(n), pad64(k)] layout rk_mlp_forward reads."""
+def pack_mlp_weight(weight: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """[n, k] nn.Linear weight -> the zero-padded [pad64(n), pad64(k)] layout rk_mlp_forward reads
+    (into `out` when given: a previous image of the same weight shape, rewritten in place)."""
     lib = _lib.load()
     n, k = weight.shape
-    rows, cols = ctypes.c_int64(), ctypes.c_int64()
-    check(lib.rk_mlp_packed_size(n, k, ctypes.byref(rows), ctypes.byref(cols)), "rk_mlp_packed_size")
-    out = torch.empty(rows.value, cols.value, device=weight.device, dtype=torch.float32)
+    rows, cols = (n + 63) // 64 * 64, (k + 63) // 64 * 64  # rk_mlp_packed_size
+    if out is None or tuple(out.shape) != (rows, cols) or out.device != weight.device:
+        out = torch.empty(rows, cols, device=weight.device, dtype=torch.float32)
     w = weight.detach()
     if w.stride(1) != 1:
         w = w.contiguous()
