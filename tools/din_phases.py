@@ -53,3 +53,12 @@ if mlp.any():
     print(f"phase B prologue {np.median(mlp[:, 32]):6.2f}k cycles (median over workgroups, wave 0)")
     for l in range(3):
         print(f"layer {l}: mfma issued {q(mlp[:, 4*l])} | epilogue {q(mlp[:, 4*l+1])} | prepare {q(mlp[:, 4*l+2])} | barrier {q(mlp[:, 4*l+3])}")
+# workgroup imbalance: the number of 2-tile samples per workgroup against its phase-A and end times
+tiles = np.minimum((np.minimum(lens, 50) + 31) // 32, 2)[: nwg * 16].reshape(nwg, 16)
+k2 = (tiles == 2).sum(1)
+pa = (t[:, 2] - t[:, 1]) / 1e3
+print("2-tile samples per WG:", q(k2), "| corr(k2, phase A) =", f"{np.corrcoef(k2, pa)[0, 1]:.3f}",
+      "| corr(k2, end) =", f"{np.corrcoef(k2, rel[:, 3])[0, 1]:.3f}")
+for kk in sorted(set(k2.tolist())):
+    sel = k2 == kk
+    print(f"  k2={kk:2d}: {sel.sum():3d} WGs, phase A med {np.median(pa[sel]):6.2f} us, end med {np.median(rel[sel, 3]):6.2f}")
