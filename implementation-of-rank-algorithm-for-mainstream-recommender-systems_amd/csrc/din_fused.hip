@@ -15,6 +15,7 @@
 //   * the attention output goes into the LDS row; the row's l2 norm (din.py:318-322) is taken.
 //  Phase B: the fcn tail + output layer + sigmoid over the 16 LDS rows (mlp_core.h).
 // The l2 term is finished by a one-wave reduction over the per-workgroup partial sums.
+#include <cstdlib>
 #include <new>
 
 #include "mlp_core.h"
@@ -41,6 +42,7 @@ struct DinArgs {
   int64_t batch;
   const float *w1, *b1, *w2, *b2, *w3, *b3;
   int use_softmax;
+  int bal_nb;         // balanced assignment: tile-count classes (0 .. ceil(T/32))
   float* l2_part;
   unsigned* l2_count;  // zero between launches: the last workgroup to finish phase A resets it
   float* l2_out;
@@ -53,7 +55,8 @@ struct DinArgs {
 };
 
 // LDS carve (floats): [Wk | Wqk | Wq] 3 x 64 x (H+4), W2 32 x 68, b1 64, b2 32, w3 32,
-// u 16 x 64, norms 16, then buf0 16 x ld0, buf1 16 x ld1; column map after that (bytes).
+// u 16 x 64, norms 16, then buf0 16 x ld0, buf1 16 x ld1; column map after that (bytes), then the
+// segment descriptors, the per-wave prefetch slots and (balanced launches) the assignment area.
 template <int H>
 struct DinLds {
   static constexpr int LDH = H + 4;
@@ -64,11 +67,12 @@ struct DinLds {
 
 #ifdef RK_DIN_PHASES  // timing build only (tools/din_phases.py): per-workgroup wall-clock marks
 constexpr int kDinPhaseWG = 1024;
-__device__ unsigned long long g_din_ts[kDinPhaseWG][4];       // entry, staged, phase A done, phase B done
+// entry, staged, phase A done, phase B done, wave 0 assigned, image copied, classes counted (tid 0)
+__device__ unsigned long long g_din_ts[kDinPhaseWG][8];
 __device__ unsigned long long g_din_wave[kDinPhaseWG][16];    // per-wave phase-A cycles (clock64)
 // marks are kept in LDS while the kernel runs (a global store mid-kernel joins the vmcnt queue
 // every later wait drains) and written out by din_marks_flush() at the end
-__shared__ unsigned long long s_din_ts[4];
+__shared__ unsigned long long s_din_ts[8];
 __shared__ unsigned long long s_din_wave[16];
 #define DIN_TS(i)                                \
   do {                                           \
@@ -77,7 +81,7 @@ __shared__ unsigned long long s_din_wave[16];
 __device__ __forceinline__ void din_marks_flush(int tid) {
   __syncthreads();
   if (blockIdx.x < kDinPhaseWG) {
-    if (tid < 4) g_din_ts[blockIdx.x][tid] = s_din_ts[tid];
+    if (tid < 8) g_din_ts[blockIdx.x][tid] = s_din_ts[tid];
     if (tid < 16) g_din_wave[blockIdx.x][tid] = s_din_wave[tid];
   }
 }
@@ -87,7 +91,30 @@ __device__ __forceinline__ void din_marks_flush(int tid) {
   } while (0)
 #endif
 
-template <int H>
+// Balanced assignment (NIT > 0: batch <= NIT * 1024).  The attention cost of a sample is its tile
+// count, and with one workgroup per CU the kernel ends with the workgroup whose SIMDs carry the
+// most tiles (tools/din_phases.py: phase-A time tracks the 2-tile samples per workgroup, corr 0.91).
+// Every workgroup ranks the whole batch by descending tile count (stable in the batch order) and
+// takes ranks blockIdx.x + G * j, j = 0..15 (G workgroups): each workgroup gets the same mix of
+// long and short samples, within one, and wave j gets the j-th longest of its 16.  The ranking is
+// a counting sort over the ceil(T/32) + 1 tile classes: per 64-sample block a ballot mask per
+// class in LDS, then each wave finds its rank's sample by a prefix over the blocks' popcounts.
+constexpr int kDinBalMax = 8;  // NIT <= 8: batch <= 8192
+constexpr int kDinBalClasses = 9;  // T <= 256
+
+// Inclusive prefix sum over the 64 lanes on the DPP network (no LDS round trips): row_shr 1/2/4/8
+// within each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals forward.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
+template <int H, int NIT>
 __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   using Ly = DinLds<H>;
   constexpr int NQ = H / 8;
@@ -109,13 +136,28 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   // (plain: masked weight 0; softmax: exp(pad / sqrt(H) - max) underflows to 0) — except with
   // softmax and len <= 0, where every position carries the same pad score and all T count.
   const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
   const int ntiles_all = (a.T + 31) / 32;
-  int my_tiles = -1;  // lanes 0..15: tiles of sample m0 + lane (-1: past the batch)
+  auto clamp_len = [&](int64_t len) { return len <= 0 ? 0 : (len >= a.T ? a.T : (int)len); };  // 32-bit math
+  auto tiles_of = [&](int lc) { return lc ? (lc + 31) >> 5 : (a.use_softmax ? ntiles_all : 0); };
+  int64_t* const kpre0 = reinterpret_cast<int64_t*>(col_seg + kDinSegLdsOff + sizeof(rk_segment) * kDinSegs);
+  int64_t* const s_rows = kpre0 + 32 * kMlpWaves;                       // NIT > 0: batch row of LDS row j
+  unsigned long long* const s_mask = reinterpret_cast<unsigned long long*>(s_rows + kMlpRows);  // NIT > 0
+  int rows;
+  int my_tiles = -1;  // NIT == 0, lanes 0..15: tiles of sample m0 + lane (-1: past the batch)
   int64_t my_len = 0;
-  if (lane < rows) {
-    my_len = a.seq_len[m0 + lane];
-    my_tiles = my_len <= 0 ? (a.use_softmax ? ntiles_all : 0) : (int)((min<int64_t>(my_len, a.T) + 31) / 32);
+  int64_t lv[NIT > 0 ? NIT : 1];  // NIT > 0: lengths of samples tid + 1024 r (clamped index)
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int r = 0; r < NIT; ++r) {
+      const int i = tid + kMlpThreads * r;
+      lv[r] = a.seq_len[i < a.batch ? i : a.batch - 1];
+    }
+  } else {
+    rows = (int)min<int64_t>(kMlpRows, a.batch - m0);
+    if (lane < rows) {
+      my_len = a.seq_len[m0 + lane];
+      my_tiles = tiles_of(clamp_len(my_len));
+    }
   }
 
   // ---- stage the split attention weights and the column map: with a packed image
@@ -156,6 +198,24 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   static_assert(sizeof(rk_segment) % 4 == 0, "segment descriptor of whole words");
   if (tid < a.nseg * (int)(sizeof(rk_segment) / 4))
     reinterpret_cast<int*>(lsegs)[tid] = reinterpret_cast<const int*>(&a.segs)[tid];
+  DIN_TS(5);
+  if constexpr (NIT > 0) {  // class masks of the 64-sample blocks (block 16 r + wave holds sample tid + 1024 r)
+    const int nblk = (int)((a.batch + 63) / 64);
+#pragma unroll
+    for (int r = 0; r < NIT; ++r) {
+      const int cls = tid + kMlpThreads * r < a.batch ? tiles_of(clamp_len(lv[r])) : -1;
+      // class c's mask lands in lane c; lanes 0 .. nb-1 store them
+      unsigned long long mk = 0;
+#pragma unroll 1
+      for (int c = 0; c < a.bal_nb; ++c) {
+        const unsigned long long m = __ballot(cls == c);
+        mk = lane == c ? m : mk;
+      }
+      const int blk = 16 * r + wave;
+      if (blk < nblk && lane < a.bal_nb) s_mask[blk * a.bal_nb + lane] = mk;
+    }
+  }
+  DIN_TS(6);
   __syncthreads();
   DIN_TS(1);
 #ifdef RK_DIN_PHASES
@@ -165,23 +225,80 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   // ---- balance the attention work over the SIMDs: waves w, w+4, w+8, w+12 share one SIMD, so
   // wave w takes the sample of rank w in descending tile count (the longest four samples land on
   // four different SIMDs, and so on).  Every wave computes the same ranking in registers.
-  int rank = 0;
+  // (Balanced launches: the ranks are already in descending tile order, wave j takes rank j.)
+  int loc, ntiles;
+  int64_t len, b;
+  bool live;
+  if constexpr (NIT > 0) {
+    const int G = gridDim.x, B = (int)a.batch;  // batch <= 8192 here: 32-bit index math
+    const int p = blockIdx.x + G * wave;  // this wave's rank
+    rows = min(kMlpRows, (B - (int)blockIdx.x + G - 1) / G);
+    loc = wave;
+    live = p < B;
+    int cls = 0;
+    b = 0;
+    if (live) {
+      const int nblk = (B + 63) / 64, bpl = nblk > 64 ? 2 : 1;  // 64-sample blocks per lane (nblk <= 128)
+      // lane l's count of each class over its blocks l * bpl .. l * bpl + bpl - 1, prefix-summed
+      // over the lanes; the rank's class is found walking the classes in descending order
+      const int k0 = p;
+      int start = 0, incl = 0, own = 0;
+      cls = 0;
+      for (int c = a.bal_nb - 1; c >= 0; --c) {
+        const int blk = lane * bpl;
+        int n = blk < nblk ? __builtin_popcountll(s_mask[blk * a.bal_nb + c]) : 0;
+        if (bpl > 1 && blk + 1 < nblk) n += __builtin_popcountll(s_mask[(blk + 1) * a.bal_nb + c]);
+        const int sc = wave_incl_scan(n);
+        const int tot = __builtin_amdgcn_readlane(sc, 63);
+        if (k0 < start + tot || c == 0) {
+          cls = c;
+          incl = sc;
+          own = n;
+          break;
+        }
+        start += tot;
+      }
+      // the (k0 - start)-th sample of that class in block order: the lane whose prefix passes it ...
+      const int k = k0 - start;
+      const int L = __builtin_ctzll(__ballot(incl > k));
+      int kk = k - __builtin_amdgcn_readlane(incl - own, L);
+      // ... then the block within the lane's share, then the bit within the block
+      int blk = L * bpl;
+      unsigned long long m = s_mask[blk * a.bal_nb + cls];
+      if (bpl > 1 && kk >= __builtin_popcountll(m)) {
+        kk -= __builtin_popcountll(m);
+        m = s_mask[++blk * a.bal_nb + cls];
+      }
+      const int below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      const int pos = __builtin_ctzll(__ballot(((m >> lane) & 1ull) && below == kk));
+      b = __builtin_amdgcn_readfirstlane(64 * blk + pos);
+    }
+    ntiles = __builtin_amdgcn_readfirstlane(cls);
+    // the length rides with phase A.1's loads (only the tile masks need it) — as a vector load: a
+    // scalar one would hold up the lgkmcnt(0) waits of phase A.1's LDS reads
+    int bv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(bv) : "s"((int)b));
+    len = live ? a.seq_len[bv] : 0;
+    if (lane == 0) s_rows[wave] = b;
+  } else {
+    int rank = 0;
 #pragma unroll
-  for (int j = 0; j < kMlpRows; ++j) {
-    const int tj = __shfl(my_tiles, j, kWave);
-    rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
+    for (int j = 0; j < kMlpRows; ++j) {
+      const int tj = __shfl(my_tiles, j, kWave);
+      rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
+    }
+    const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
+    // wave-uniform values in scalar registers (readfirstlane): the sample's addresses stay scalar
+    loc = __builtin_amdgcn_readfirstlane(pick ? __builtin_ctzll(pick) : wave);  // sample in the WG
+    ntiles = __builtin_amdgcn_readfirstlane(max(0, __shfl(my_tiles, loc, kWave)));
+    len = __shfl(my_len, loc, kWave);
+    b = m0 + loc;
+    live = loc < rows;
   }
-  const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
-  // wave-uniform values in scalar registers (readfirstlane): the sample's addresses stay scalar
-  const int loc = __builtin_amdgcn_readfirstlane(pick ? __builtin_ctzll(pick) : wave);  // sample in the WG
-  const int ntiles = __builtin_amdgcn_readfirstlane(max(0, __shfl(my_tiles, loc, kWave)));
-  const int64_t len = __shfl(my_len, loc, kWave);
-  const int64_t b = m0 + loc;
 #ifdef RK_DIN_SKIP_A  // timing experiment only (tools/din_phase_time.py): phase B on zero rows
-  const bool live = false;
-#else
-  const bool live = loc < rows;
+  live = false;
 #endif
+  DIN_TS(4);
   float* row = buf0 + loc * a.ld0;
   uint32_t* flags = a.flags;
 
@@ -198,7 +315,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     if (live && tt < ntiles && t < a.T) kidx[tt] = a.seq[b * a.ld_seq + t];
   }
   // tile 1's index waits in LDS (a register across tile 0 spills at the 128-VGPR budget)
-  int64_t* const kpre = reinterpret_cast<int64_t*>(col_seg + kDinSegLdsOff + sizeof(rk_segment) * kDinSegs) + 32 * wave;
+  int64_t* const kpre = kpre0 + 32 * wave;
   constexpr int kColIt = 4;  // width <= 255: at most four 64-column passes
   int64_t cidx[kColIt];
   int cseg[kColIt];
@@ -386,7 +503,8 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
   return;
 #endif
-  mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid);
+  mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
+           NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
   // (mlp_rows' barriers order tid 0's l2_last store before these reads)
   if (a.l2_part && tid < 64 && l2_last) {
@@ -470,6 +588,7 @@ struct DinPlan {
   int64_t blocks;
   size_t shm;
   int H;
+  int nit;  // balanced assignment: seq_len loads per thread (0: contiguous 16-sample blocks)
 };
 }  // namespace rk
 
@@ -553,8 +672,20 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
     case 16: base = DinLds<16>::BUF0; break;
     default: base = DinLds<32>::BUF0; break;
   }
-  const size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
-                     sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 32 * kMlpWaves;
+  size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
+               sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 32 * kMlpWaves;
+  // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
+  // by default when the histories span three or more tile counts (T > 64).  Measured (graph
+  // replays, batch 4096, lengths uniform in 1..T): T = 128 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us;
+  // at T = 50 (two tile counts) the ranking costs ~1% more than it recovers.
+  // RANKOPS_DIN_BALANCE=1 / 0 forces it on / off (tests, A/B timing).
+  const char* env = getenv("RANKOPS_DIN_BALANCE");
+  a.bal_nb = (T + 31) / 32 + 1;
+  const bool want_bal = env && env[0] ? env[0] != '0' : a.bal_nb >= 4;
+  if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
+    plan->nit = batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
+    shm += sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
+  }
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
   plan->shm = shm;
   return RK_OK;
@@ -562,14 +693,21 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
 
 static int din_launch(const DinPlan& p, hipStream_t st) {
   if (p.blocks == 0) return RK_OK;
-  raise_lds_limit((const void*)din_forward_kernel<8>, 160 * 1024);
-  raise_lds_limit((const void*)din_forward_kernel<16>, 160 * 1024);
-  raise_lds_limit((const void*)din_forward_kernel<32>, 160 * 1024);
   const unsigned blocks = (unsigned)p.blocks;
-  switch (p.H) {
-    case 8: din_forward_kernel<8><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
-    case 16: din_forward_kernel<16><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
-    default: din_forward_kernel<32><<<blocks, kMlpThreads, p.shm, st>>>(p.a); break;
+  auto go = [&](auto kern) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<blocks, kMlpThreads, p.shm, st>>>(p.a);
+  };
+  switch (p.H * 16 + p.nit) {
+    case 8 * 16: go(din_forward_kernel<8, 0>); break;
+    case 8 * 16 + 4: go(din_forward_kernel<8, 4>); break;
+    case 8 * 16 + 8: go(din_forward_kernel<8, 8>); break;
+    case 16 * 16: go(din_forward_kernel<16, 0>); break;
+    case 16 * 16 + 4: go(din_forward_kernel<16, 4>); break;
+    case 16 * 16 + 8: go(din_forward_kernel<16, 8>); break;
+    case 32 * 16: go(din_forward_kernel<32, 0>); break;
+    case 32 * 16 + 4: go(din_forward_kernel<32, 4>); break;
+    default: go(din_forward_kernel<32, 8>); break;
   }
   return check_launch("rk_din_forward");
 }

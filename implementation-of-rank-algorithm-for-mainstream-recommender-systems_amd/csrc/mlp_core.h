@@ -334,12 +334,14 @@ __device__ __forceinline__ auto finish_only(F f) {
 }
 
 // `lds_partial` (optional): per-row head partials the stage left in LDS (DCN's cross half of
-// output_layer), used instead of h.head_partial.
+// output_layer), used instead of h.head_partial.  `row_ids` (optional, LDS): the batch row of each
+// of the `rows` LDS rows for the head outputs, instead of m0 + r (DIN's balanced assignment).
 template <int RT = 1, bool STORE = false, class Stage = NoStage>
 __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers, int nl, int K0, float* buf0,
                                          int ld0, float* buf1, int ld1, int64_t m0, int rows,
                                          const rk_epilogue& h, float* y, int64_t ldy, int tid,
-                                         Stage stage = Stage(), const float* lds_partial = nullptr) {
+                                         Stage stage = Stage(), const float* lds_partial = nullptr,
+                                         const int64_t* row_ids = nullptr) {
   // wave index as an SGPR: the per-wave tile / variant choices become scalar branches
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   LayerPipe pipe;
@@ -367,7 +369,7 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       if (lane + 64 * c < Kh) hw[c] = h.head_w[lane + 64 * c];
-    if (wave < rows && h.head_partial && !lds_partial) hp = h.head_partial[m0 + wave];
+    if (wave < rows && h.head_partial && !lds_partial) hp = h.head_partial[row_ids ? row_ids[wave] : m0 + wave];
   };
 #ifdef RK_MLP_PHASES
   const unsigned long long t_start = clock64();
@@ -427,7 +429,7 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
       }
       p = wave_sum(p);
       if (lane == 0) {
-        const int64_t m = m0 + r;
+        const int64_t m = row_ids ? row_ids[r] : m0 + r;
         float logit = p + h.head_b[0];
         if (lds_partial)
           logit = lds_partial[r] + logit;
@@ -444,7 +446,7 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
   } else if (y) {
     for (int i = tid; i < rows * K; i += kMlpThreads) {
       const int r = i / K, n = i % K;
-      y[(m0 + r) * ldy + n] = fin[r * ldf + n];
+      y[(row_ids ? row_ids[r] : m0 + r) * ldy + n] = fin[r * ldf + n];
     }
   }
 }

@@ -22,13 +22,13 @@ launch()
 torch.cuda.synchronize()
 from rankops import _lib  # noqa: E402
 lib = _lib.load()
-ts = (ctypes.c_ulonglong * (1024 * 4))()
+ts = (ctypes.c_ulonglong * (1024 * 8))()
 wv = (ctypes.c_ulonglong * (1024 * 16))()
 ml = (ctypes.c_ulonglong * (1024 * (4 * 8 + 4)))()
 lib.rk_debug_din_phases.argtypes = [ctypes.c_void_p] * 3
 assert lib.rk_debug_din_phases(ts, wv, ml) == 0
 nwg = min(1024, (batch + 15) // 16)
-t = np.array(ts, dtype=np.int64).reshape(1024, 4)[:nwg] * 10  # ns
+t = np.array(ts, dtype=np.int64).reshape(1024, 8)[:nwg] * 10  # ns
 w = np.array(wv, dtype=np.int64).reshape(1024, 16)[:nwg]
 t0 = t[:, 0].min()
 rel = (t - t0) / 1e3  # us from the first workgroup's entry
@@ -42,6 +42,9 @@ def q(x):
 print(f"kernel avg {us:.2f} us (events), {nwg} workgroups")
 print("entry        ", q(rel[:, 0]))
 print("staging      ", q((t[:, 1] - t[:, 0]) / 1e3))
+print("  image copied", q((t[:, 5] - t[:, 0]) / 1e3), "(tid 0, from entry)")
+print("  counted     ", q((t[:, 6] - t[:, 0]) / 1e3), "(tid 0, from entry)")
+print("assignment   ", q((t[:, 4] - t[:, 1]) / 1e3), "(wave 0)")
 print("phase A      ", q((t[:, 2] - t[:, 1]) / 1e3))
 print("phase B      ", q((t[:, 3] - t[:, 2]) / 1e3))
 print("end          ", q(rel[:, 3]))
@@ -54,6 +57,9 @@ if mlp.any():
     for l in range(3):
         print(f"layer {l}: mfma issued {q(mlp[:, 4*l])} | epilogue {q(mlp[:, 4*l+1])} | prepare {q(mlp[:, 4*l+2])} | barrier {q(mlp[:, 4*l+3])}")
 # workgroup imbalance: the number of 2-tile samples per workgroup against its phase-A and end times
+# (contiguous 16-sample blocks only: RANKOPS_DIN_BALANCE=0)
+if os.environ.get("RANKOPS_DIN_BALANCE", "1") != "0":
+    sys.exit(0)
 tiles = np.minimum((np.minimum(lens, 50) + 31) // 32, 2)[: nwg * 16].reshape(nwg, 16)
 k2 = (tiles == 2).sum(1)
 pa = (t[:, 2] - t[:, 1]) / 1e3
