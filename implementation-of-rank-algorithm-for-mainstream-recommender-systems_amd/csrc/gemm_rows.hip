@@ -114,6 +114,18 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   const int n0 = blockIdx.y * BN;
   const int bn = min(BN, a.N - n0);
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hk = 4 * (lane >> 5);
+  const int64_t nslabs = (a.M + 31) / 32;
+  const int64_t stride = (int64_t)gridDim.x * kRowsWaves;
+  int64_t s = (int64_t)blockIdx.x * kRowsWaves + wave;
+  RowsChunk<AM> ring[PD];
+  // the wave's first PD A chunks, issued right behind the opB staging loads so that their HBM
+  // round trip overlaps the staging (rows past M read row M - 1: safe for a wave with no slab)
+  auto prefill = [&]() {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) ring[j] = rows_fetch<AM>(a, s, j, l32, hk);
+  };
   // opB slice [bn][K] -> LDS [BN][K8 + 4], zero-padded.  Every thread issues all of its float4
   // loads (coalesced along the contiguous dim) before the first LDS write: a loop of dependent
   // 4-B load -> store pairs put one L2 round trip per element in front of the first MFMA.
@@ -131,6 +143,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
         for (int e = 0; e < 4; ++e) bvals[i][e] = n + e < bn ? src[e] : 0.f;
       }
     }
+    prefill();
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int idx = tid + 256 * i, k = idx / (BN / 4), n = 4 * (idx % (BN / 4));
@@ -150,6 +163,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
       }
       if (n >= bn) bvals[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
+    prefill();
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int idx = tid + 256 * i, n = idx / (K8 / 4), k = 4 * (idx % (K8 / 4));
@@ -164,16 +178,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
   }
   __syncthreads();
 
-  const int lane = tid & 63, wave = tid >> 6;
-  const int l32 = lane & 31, hk = 4 * (lane >> 5);
-  const int64_t nslabs = (a.M + 31) / 32;
-  const int64_t stride = (int64_t)gridDim.x * kRowsWaves;
-  int64_t s = (int64_t)blockIdx.x * kRowsWaves + wave;
   if (s >= nslabs) return;
   const float* bbase = sB + l32 * ldb + hk;
-  RowsChunk<AM> ring[PD];
-#pragma unroll
-  for (int j = 0; j < PD; ++j) ring[j] = rows_fetch<AM>(a, s, j, l32, hk);
   // Epilogue operands in registers ahead of use: the bias (per column, the same for every slab)
   // once, and for an accumulating product the slab's C values at the top of the slab, so their
   // round trips overlap the MFMAs instead of sitting, one float4 at a time, behind them.
@@ -195,6 +201,16 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) epi[t][q] = *reinterpret_cast<const f32x4*>(a.ep.bias + n0 + 32 * t + 8 * q + hk);
   }
+  // opB fragments one chunk ahead (PIPE): chunk j + 1's LDS reads are issued before chunk j's MFMAs,
+  // so their latency hides under the matrix work instead of opening every chunk; the last chunk
+  // reads chunk 0's (the same for every slab) for the next slab.  +4 NT registers: not with LN.
+  constexpr bool PIPE = !LN;
+  f32x4 bnext[NT];
+  auto bload = [&](f32x4* dst, int j) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dst[t] = *reinterpret_cast<const f32x4*>(bbase + 32 * t * ldb + 8 * j);
+  };
+  if (PIPE) bload(bnext, 0);
   // one 32-row slab (the first one peeled off the loop below, so that the loop is entered in the
   // state its back edge leaves: the waitcnt pass then derives its waits from one state)
   auto slab = [&](const int64_t s) {
@@ -229,8 +245,13 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
       ring[j % PD] = j + PD < NK8 ? rows_fetch<AM>(a, s, j + PD, l32, hk)
                                   : rows_fetch<AM>(a, sn, j + PD - NK8, l32, hk);
       f32x4 bv[NT];
+      if (PIPE) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const f32x4*>(bbase + 32 * t * ldb + 8 * j);
+        for (int t = 0; t < NT; ++t) bv[t] = bnext[t];
+        bload(bnext, (j + 1) % NK8);
+      } else {
+        bload(bv, j);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -365,8 +386,10 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
   if (A_mask && !rows_aligned16(A_mask)) return false;
   if (Ap && (!rows_aligned16(Ap) || aperiod <= 0)) return false;
   const int64_t nslabs = (M + 31) / 32;
-  // enough 32-row slabs for every resident wave to get a few (prefetch overlap)
-  if (nslabs < (int64_t)16 * num_cus()) return false;
+  // at least 4 32-row slabs per CU (M >= 32768 on 256 CUs).  N = K = 128, bias+ReLU / accumulate,
+  // against the generic kernels: M = 32768 16.6 / 16.3 us vs 21.9 / 30.1, M = 65536 29.3 / 28.0 us
+  // vs 59.4 / 59.5; at M = 16384 the two are even, below that the generic path wins.
+  if (nslabs < (int64_t)4 * num_cus()) return false;
   RowsArgs a = {};
   a.A = A;
   a.lda = lda;

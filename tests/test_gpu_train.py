@@ -900,7 +900,7 @@ def test_bst_attention_train_length_zero_is_nan():
     assert torch.isfinite(probs[0]).all() and torch.isfinite(ctx[:T]).all() and torch.isfinite(ctx[2 * T:]).all()
 
 
-# Tall-skinny shapes (gemm_rows.hip: M >= 32 x 16 x CUs rows, reduction <= 128) — the BST / DIN training
+# Tall-skinny shapes (gemm_rows.hip: M >= 32 x 4 x CUs rows, reduction <= 128) — the BST / DIN training
 # GEMMs.  M is deliberately not a multiple of 32.
 ROWS_M = 131072 + 77
 
@@ -919,6 +919,22 @@ def test_gemm_rows_tall_skinny_matches_fp64(TB, N, R, masked):
     tol = 1e-4 * max(1.0, float(want.abs().max()))
     torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
     ops.gemm(0, TB, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, A_mask=md, accumulate=True)
+    torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [32768 + 5, 65536 + 77])
+@pytest.mark.parametrize("N,R", [(128, 128), (384, 64), (7, 32)])
+def test_gemm_rows_mid_size_matches_fp64(M, N, R):
+    """The gemm_rows path from 4 slabs per CU (one or two slabs per resident wave): plain and
+    accumulating products against float64."""
+    A, B, mask, want, _ = _gemm_case(0, 1, M, N, R, False, seed=M + N)
+    C = torch.full((M, N), 7.0, device="cuda")
+    Ad, Bd = A.cuda(), B.cuda()
+    ops.gemm(0, 1, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C)
+    tol = 1e-4 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(C.cpu().double(), want, rtol=0, atol=tol)
+    ops.gemm(0, 1, M, N, R, Ad, Ad.stride(0), Bd, Bd.stride(0), C, accumulate=True)
     torch.testing.assert_close(C.cpu().double(), 2 * want, rtol=0, atol=2 * tol)
 
 
@@ -1143,7 +1159,7 @@ def test_linear_res_dropout_ln_matches_two_launch_path(M, K, p):
         torch.cuda.synchronize()
         outs.append((r, y, mean, rstd))
     (r1, y1, m1, s1), (r2, y2, m2, s2) = outs
-    if M >= 131072:  # both projections on gemm_rows: the same products, the same mask
+    if M >= 32768:  # both projections on gemm_rows: the same products, the same mask
         assert torch.equal(r1, r2)
     else:  # rk_linear takes its generic kernel at this M (another k order)
         torch.testing.assert_close(r1, r2, rtol=1e-5, atol=1e-5)
