@@ -105,8 +105,27 @@ __device__ __forceinline__ f32x4 rows_operand(const RowsChunk<AM>& c) {
 // LN (with EPI, FAST, NT = 4, N = 128: a wave's slab holds whole rows, lane l and l + 32 one half
 // each): the BST block's residual LayerNorm (bst.py:84-90, rk_bst_res_dropout_ln_forward) fused into
 // the projection's epilogue, so the projection output never goes to HBM and back.
+#ifdef RK_ROWS_CLOCK  // timing build only (tools/rows_clock.py): shader vs wall clock per workgroup
+constexpr int kRowsClkWG = 4096;
+__device__ unsigned long long g_rows_clk[kRowsClkWG][4];  // clock64 start/end, wall start/end
+#endif
+
 template <int NK8, int NT, bool EPI, int AM, bool FAST = false, bool ACC = false, bool LN = false>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(RowsArgs a) {
+#ifdef RK_ROWS_CLOCK
+  struct ClkMark {
+    unsigned long long c0, w0;
+    __device__ ~ClkMark() {
+      const unsigned wg = blockIdx.x + gridDim.x * blockIdx.y;
+      if (threadIdx.x == 0 && wg < kRowsClkWG) {
+        g_rows_clk[wg][0] = c0;
+        g_rows_clk[wg][1] = clock64();
+        g_rows_clk[wg][2] = w0;
+        g_rows_clk[wg][3] = wall_clock64();
+      }
+    }
+  } clk_mark{(unsigned long long)clock64(), (unsigned long long)wall_clock64()};
+#endif
   static_assert(!LN || (EPI && FAST && NT == 4), "LN epilogue: whole 128-column rows");
   extern __shared__ __attribute__((aligned(16))) float sB[];
   constexpr int K8 = 8 * NK8, ldb = K8 + 4, BN = 32 * NT;
@@ -531,3 +550,9 @@ RK_API int rk_linear_res_dropout_ln(const float* x, int64_t ldx, int64_t M, int3
                 "rk_linear_res_dropout_ln: needs K in {32, 64, 128} and 16-B aligned rows");
   return check_launch("rk_linear_res_dropout_ln");
 }
+
+#ifdef RK_ROWS_CLOCK
+RK_API int rk_debug_rows_clock(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rk::g_rows_clk), sizeof(rk::g_rows_clk)) == hipSuccess ? 0 : 1;
+}
+#endif
