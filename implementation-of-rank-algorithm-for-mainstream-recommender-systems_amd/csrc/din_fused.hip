@@ -67,7 +67,8 @@ struct DinLds {
 
 #ifdef RK_DIN_PHASES  // timing build only (tools/din_phases.py): per-workgroup wall-clock marks
 constexpr int kDinPhaseWG = 1024;
-// entry, staged, phase A done, phase B done, wave 0 assigned, image copied, classes counted (tid 0)
+// entry, staged, phase A done, phase B done, wave 0 assigned, image copied, classes counted,
+// wave 0's row and first keys loaded (tid 0)
 __device__ unsigned long long g_din_ts[kDinPhaseWG][8];
 __device__ unsigned long long g_din_wave[kDinPhaseWG][16];    // per-wave phase-A cycles (clock64)
 // marks are kept in LDS while the kernel runs (a global store mid-kernel joins the vmcnt queue
@@ -131,16 +132,31 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   const int l32 = lane & 31, half = lane >> 5, hk = 4 * half;
   DIN_TS(0);
 
-  // ---- per-sample tile counts, issued first (their latency overlaps the staging below): a sample
-  // needs ceil(min(len, T) / 32) attention tiles — positions past its length contribute exactly 0
-  // (plain: masked weight 0; softmax: exp(pad / sqrt(H) - max) underflows to 0) — except with
-  // softmax and len <= 0, where every position carries the same pad score and all T count.
+  // ---- the column map and the row segments' descriptors, issued first: with contiguous samples
+  // (NIT == 0) they are in LDS one bare barrier later, and the feature-row gather starts while the
+  // attention weights are still in flight
+  static_assert(sizeof(rk_segment) % 4 == 0, "segment descriptor of whole words");
+  const int seg_words = a.nseg * (int)(sizeof(rk_segment) / 4);
+  uint8_t cs_v = 255, co_v = 0;
+  int sw_v = 0;
+  if (tid < 256) {
+    cs_v = a.col_seg[tid];
+    co_v = a.col_off[tid];
+  }
+  if (tid < seg_words) sw_v = reinterpret_cast<const int*>(&a.segs)[tid];
+
+  // ---- per-sample tile counts: a sample needs ceil(min(len, T) / 32) attention tiles — positions
+  // past its length contribute exactly 0 (plain: masked weight 0; softmax: exp(pad / sqrt(H) - max)
+  // underflows to 0) — except with softmax and len <= 0, where every position carries the same pad
+  // score and all T count.
   const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
   const int ntiles_all = (a.T + 31) / 32;
   auto clamp_len = [&](int64_t len) { return len <= 0 ? 0 : (len >= a.T ? a.T : (int)len); };  // 32-bit math
   auto tiles_of = [&](int lc) { return lc ? (lc + 31) >> 5 : (a.use_softmax ? ntiles_all : 0); };
+  // LDS after the descriptors: the history indices of tiles 0 and 1 per LDS row ([16][64]), then
+  // (NIT > 0) the batch row of each LDS row and the class masks
   int64_t* const kpre0 = reinterpret_cast<int64_t*>(col_seg + kDinSegLdsOff + sizeof(rk_segment) * kDinSegs);
-  int64_t* const s_rows = kpre0 + 32 * kMlpWaves;                       // NIT > 0: batch row of LDS row j
+  int64_t* const s_rows = kpre0 + 64 * kMlpRows;
   unsigned long long* const s_mask = reinterpret_cast<unsigned long long*>(s_rows + kMlpRows);  // NIT > 0
   int rows;
   int my_tiles = -1;  // NIT == 0, lanes 0..15: tiles of sample m0 + lane (-1: past the batch)
@@ -160,44 +176,107 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     }
   }
 
-  // ---- stage the split attention weights and the column map: with a packed image
-  // (rk_din_pack_attention) one round of coalesced float4 copies, all loads in flight at once
+  // ---- the split attention weights: with a packed image (rk_din_pack_attention) one round of
+  // coalesced float4 loads, all in flight at once, stored to LDS after the row gather is issued
+  static_assert(Ly::U % 4 == 0, "image of whole float4s");
+  constexpr int kImg4 = Ly::U / 4, kPer = (kImg4 + kMlpThreads - 1) / kMlpThreads;
+  f32x4_t v[kPer];
   if (a.att_image) {
-    static_assert(Ly::U % 4 == 0, "image of whole float4s");
-    constexpr int kImg4 = Ly::U / 4, kPer = (kImg4 + kMlpThreads - 1) / kMlpThreads;
-    f32x4_t v[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const int i = tid + r * kMlpThreads;
       if (i < kImg4) v[r] = reinterpret_cast<const f32x4_t*>(a.att_image)[i];
     }
+  }
+  auto image_to_lds = [&]() {
+    if (a.att_image) {
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const int i = tid + r * kMlpThreads;
-      if (i < kImg4) reinterpret_cast<f32x4_t*>(sm)[i] = v[r];
+      for (int r = 0; r < kPer; ++r) {
+        const int i = tid + r * kMlpThreads;
+        if (i < kImg4) reinterpret_cast<f32x4_t*>(sm)[i] = v[r];
+      }
+    } else {
+      for (int i = tid; i < 64 * H; i += kMlpThreads) {
+        const int j = i / H, h = i % H;
+        const float* r = a.w1 + (int64_t)j * 4 * H;
+        sm[Ly::WQ + j * Ly::LDH + h] = r[h] + r[2 * H + h];
+        sm[Ly::WK + j * Ly::LDH + h] = r[H + h] - r[2 * H + h];
+        sm[Ly::WQK + j * Ly::LDH + h] = r[3 * H + h];
+      }
+      for (int i = tid; i < 32 * 64; i += kMlpThreads) sm[Ly::W2 + (i / 64) * 68 + (i % 64)] = a.w2[i];
+      if (tid < 64) sm[Ly::B1 + tid] = a.b1[tid];
+      if (tid < 32) {
+        sm[Ly::B2 + tid] = a.b2[tid];
+        sm[Ly::W3 + tid] = a.w3[tid];
+      }
     }
-  } else {
-    for (int i = tid; i < 64 * H; i += kMlpThreads) {
-      const int j = i / H, h = i % H;
-      const float* r = a.w1 + (int64_t)j * 4 * H;
-      sm[Ly::WQ + j * Ly::LDH + h] = r[h] + r[2 * H + h];
-      sm[Ly::WK + j * Ly::LDH + h] = r[H + h] - r[2 * H + h];
-      sm[Ly::WQK + j * Ly::LDH + h] = r[3 * H + h];
-    }
-    for (int i = tid; i < 32 * 64; i += kMlpThreads) sm[Ly::W2 + (i / 64) * 68 + (i % 64)] = a.w2[i];
-    if (tid < 64) sm[Ly::B1 + tid] = a.b1[tid];
-    if (tid < 32) {
-      sm[Ly::B2 + tid] = a.b2[tid];
-      sm[Ly::W3 + tid] = a.w3[tid];
-    }
-  }
+  };
   if (tid < 256) {
-    col_seg[tid] = a.col_seg[tid];
-    col_off[tid] = a.col_off[tid];
+    col_seg[tid] = cs_v;
+    col_off[tid] = co_v;
   }
-  static_assert(sizeof(rk_segment) % 4 == 0, "segment descriptor of whole words");
-  if (tid < a.nseg * (int)(sizeof(rk_segment) / 4))
-    reinterpret_cast<int*>(lsegs)[tid] = reinterpret_cast<const int*>(&a.segs)[tid];
+  if (tid < seg_words) reinterpret_cast<int*>(lsegs)[tid] = sw_v;
+  uint32_t* flags = a.flags;
+
+  // ---- the feature row of one sample (zero padded to pad64(width)) and its history indices of
+  // tiles 0 and 1: the indices, the row's segment indices, then the row values (two dependent
+  // rounds); rowp / kslot: its LDS row and index slot
+  const int wp = pad64(a.width);
+  constexpr int kColIt = 4;  // width <= 255: at most four 64-column passes
+  int64_t kidx[2] = {0, 0};  // history index of position tt * 32 + l32, tiles 0 and 1
+  float cval[kColIt];
+  auto gather_issue = [&](int64_t bs, bool lv_, int nt_) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = tt * 32 + l32;
+      kidx[tt] = 0;
+      if (lv_ && tt < nt_ && t < a.T) kidx[tt] = a.seq[bs * a.ld_seq + t];
+    }
+    int64_t cidx[kColIt];
+    int cseg[kColIt];
+#pragma unroll
+    for (int i = 0; i < kColIt; ++i) {
+      const int c = lane + 64 * i;
+      cseg[i] = (lv_ && c < a.width) ? col_seg[c] : 255;
+      cidx[i] = bs;
+      if (cseg[i] != 255 && lsegs[cseg[i]].idx) cidx[i] = lsegs[cseg[i]].idx[bs * lsegs[cseg[i]].idx_stride];
+    }
+#pragma unroll
+    for (int i = 0; i < kColIt; ++i) {
+      const int c = lane + 64 * i;
+      cval[i] = 0.f;
+      if (cseg[i] != 255) {
+        const rk_segment& g = lsegs[cseg[i]];
+        if (g.idx && (cidx[i] < 0 || cidx[i] >= g.rows))
+          flag_oob(flags);
+        else
+          cval[i] = g.src[cidx[i] * g.src_ld + col_off[c]];
+      }
+    }
+  };
+  auto gather_store = [&](float* rowp, int64_t* kslot) {
+    if (half == 0) {
+      kslot[l32] = kidx[0];
+      kslot[32 + l32] = kidx[1];
+    }
+#pragma unroll
+    for (int i = 0; i < kColIt; ++i) {
+      const int c = lane + 64 * i;
+      if (c < wp) rowp[c] = cval[i];
+    }
+  };
+
+  if constexpr (NIT == 0) {
+    // wave w gathers sample m0 + w (LDS row w) while the weights stream in: the column map is in
+    // LDS after a bare barrier (no wait on the weight loads), the tile counts are in lanes 0..15
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int tiles_w = __builtin_amdgcn_readlane(my_tiles, wave);
+    gather_issue(m0 + wave, wave < rows, tiles_w);
+    image_to_lds();
+    gather_store(buf0 + wave * a.ld0, kpre0 + 64 * wave);
+  } else {
+    image_to_lds();
+  }
   DIN_TS(5);
   if constexpr (NIT > 0) {  // class masks of the 64-sample blocks (block 16 r + wave holds sample tid + 1024 r)
     const int nblk = (int)((a.batch + 63) / 64);
@@ -224,8 +303,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 
   // ---- balance the attention work over the SIMDs: waves w, w+4, w+8, w+12 share one SIMD, so
   // wave w takes the sample of rank w in descending tile count (the longest four samples land on
-  // four different SIMDs, and so on).  Every wave computes the same ranking in registers.
-  // (Balanced launches: the ranks are already in descending tile order, wave j takes rank j.)
+  // four different SIMDs, and so on).  Every wave computes the same ranking, from scalar reads of
+  // lanes 0..15.  (Balanced launches: the ranks are already in descending tile order, wave j takes
+  // rank j.)
   int loc, ntiles;
   int64_t len, b;
   bool live;
@@ -284,13 +364,13 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     int rank = 0;
 #pragma unroll
     for (int j = 0; j < kMlpRows; ++j) {
-      const int tj = __shfl(my_tiles, j, kWave);
+      const int tj = __builtin_amdgcn_readlane(my_tiles, j);
       rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
     }
     const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
     // wave-uniform values in scalar registers (readfirstlane): the sample's addresses stay scalar
     loc = __builtin_amdgcn_readfirstlane(pick ? __builtin_ctzll(pick) : wave);  // sample in the WG
-    ntiles = __builtin_amdgcn_readfirstlane(max(0, __shfl(my_tiles, loc, kWave)));
+    ntiles = __builtin_amdgcn_readfirstlane(max(0, __builtin_amdgcn_readlane(my_tiles, loc)));
     len = __shfl(my_len, loc, kWave);
     b = m0 + loc;
     live = loc < rows;
@@ -300,45 +380,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #endif
   DIN_TS(4);
   float* row = buf0 + loc * a.ld0;
-  uint32_t* flags = a.flags;
-
-  // ---- Phase A.1: the feature row (zero padded to pad64(width)) and the first attention tile's
-  // keys, with the loads ordered so that the two dependent rounds (indices, then rows) of the
-  // row and of the keys overlap: history indices of the first two tiles, the row's segment
-  // indices, the row values, the first tile's key rows — then the row goes to LDS while the
-  // key rows are still in flight.
-  const int wp = pad64(a.width);
-  int64_t kidx[2] = {0, 0};  // history index of position tt * 32 + l32, tiles 0 and 1
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    const int t = tt * 32 + l32;
-    if (live && tt < ntiles && t < a.T) kidx[tt] = a.seq[b * a.ld_seq + t];
-  }
   // tile 1's index waits in LDS (a register across tile 0 spills at the 128-VGPR budget)
-  int64_t* const kpre = kpre0 + 32 * wave;
-  constexpr int kColIt = 4;  // width <= 255: at most four 64-column passes
-  int64_t cidx[kColIt];
-  int cseg[kColIt];
-#pragma unroll
-  for (int i = 0; i < kColIt; ++i) {
-    const int c = lane + 64 * i;
-    cseg[i] = (live && c < a.width) ? col_seg[c] : 255;
-    cidx[i] = b;
-    if (cseg[i] != 255 && lsegs[cseg[i]].idx) cidx[i] = lsegs[cseg[i]].idx[b * lsegs[cseg[i]].idx_stride];
-  }
-  float cval[kColIt];
-#pragma unroll
-  for (int i = 0; i < kColIt; ++i) {
-    const int c = lane + 64 * i;
-    cval[i] = 0.f;
-    if (cseg[i] != 255) {
-      const rk_segment& g = lsegs[cseg[i]];
-      if (g.idx && (cidx[i] < 0 || cidx[i] >= g.rows))
-        flag_oob(flags);
-      else
-        cval[i] = g.src[cidx[i] * g.src_ld + col_off[c]];
-    }
-  }
+  int64_t* const kpre = kpre0 + 64 * loc + 32;
+
   f32x4_t k[NQ];
   // key rows of position t (index r) into k; positions past T read as zeros
   auto load_keys = [&](int64_t r, int t) {
@@ -356,15 +400,24 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     for (int c = 0; c < NQ; ++c)
       k[c] = krow ? *reinterpret_cast<const f32x4_t*>(krow + 8 * c + hk) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
   };
-  if (live && ntiles > 0) load_keys(kidx[0], l32);
-  if (half == 0) kpre[l32] = kidx[1];
-#pragma unroll
-  for (int i = 0; i < kColIt; ++i) {
-    const int c = lane + 64 * i;
-    if (c < wp) row[c] = cval[i];
+  // ---- Phase A.1: the first attention tile's keys.  NIT == 0: the row and the indices are in LDS
+  // already (gathered before the barrier above).  NIT > 0: the row, the indices and then the keys
+  // for the assigned sample, the row going to LDS while the key rows are still in flight.
+  if constexpr (NIT == 0) {
+    if (live && ntiles > 0) load_keys(kpre0[64 * loc + l32], l32);
+  } else {
+    gather_issue(b, live, ntiles);
+    if (live && ntiles > 0) load_keys(kidx[0], l32);
+    gather_store(row, kpre0 + 64 * loc);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+#ifdef RK_DIN_PHASES
+  if (tid == 0) {  // wave 0: its row in LDS and its first tile's keys landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_din_ts[7] = wall_clock64();
+  }
+#endif
 
   float norm_part = 0.f;
   if (live) {
@@ -673,7 +726,7 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
     default: base = DinLds<32>::BUF0; break;
   }
   size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
-               sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 32 * kMlpWaves;
+               sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 64 * kMlpRows;
   // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
   // by default when the histories span three or more tile counts (T > 64).  Measured (graph
   // replays, batch 4096, lengths uniform in 1..T): T = 128 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us;

@@ -45,6 +45,7 @@ print("staging      ", q((t[:, 1] - t[:, 0]) / 1e3))
 print("  image copied", q((t[:, 5] - t[:, 0]) / 1e3), "(tid 0, from entry)")
 print("  counted     ", q((t[:, 6] - t[:, 0]) / 1e3), "(tid 0, from entry)")
 print("assignment   ", q((t[:, 4] - t[:, 1]) / 1e3), "(wave 0)")
+print("  A.1 (wave 0)", q((t[:, 7] - t[:, 4]) / 1e3), "(row + first keys loaded, from assignment)")
 print("phase A      ", q((t[:, 2] - t[:, 1]) / 1e3))
 print("phase B      ", q((t[:, 3] - t[:, 2]) / 1e3))
 print("end          ", q(rel[:, 3]))
