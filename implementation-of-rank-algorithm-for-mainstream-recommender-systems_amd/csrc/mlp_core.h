@@ -31,6 +31,12 @@ namespace rk {
 #ifndef RK_MLP_SYNC
 #define RK_MLP_SYNC 1
 #endif
+// RK_MLP_EARLY_RING=1: the next layer's weight ring goes out right after a wave's last MFMA of the
+// current layer, ahead of its epilogue (the epilogue parameters after it).  Measured no gain (DIN
+// kernel 51.1 -> 51.9-53.0 us, DCN / DeepFM within noise: profiles/r03/NOTES.md), so off.
+#ifndef RK_MLP_EARLY_RING
+#define RK_MLP_EARLY_RING 0
+#endif
 
 constexpr int kMlpRows = 16;
 constexpr int kMlpWaves = 16;
@@ -166,8 +172,15 @@ struct LayerPipe {
   ColEpi ep[2];
   template <int TPW, int PD>
   __device__ __forceinline__ void prepare(const rk_mlp_layer& L, int kchunks, int wave, int lane) {
+    prepare_ring<TPW, PD>(L, kchunks, wave, lane);
+    prepare_ep<TPW>(L, wave, lane);
+  }
+  // The two halves of prepare(): the weight ring may go out as soon as the previous layer's last
+  // MFMA is issued (its last ring cycle issues no refill, so the registers and wrow are free); the
+  // epilogue parameters only after that layer's epilogue has consumed ep.
+  template <int TPW, int PD>
+  __device__ __forceinline__ void prepare_ring(const rk_mlp_layer& L, int kchunks, int wave, int lane) {
     static_assert(TPW * PD <= kMlpRing, "ring overflow");
-    const int li = lane & 15;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) wrow[j] = wfrag(L, wave + kMlpWaves * j, lane);
     // issue the ring in consumption order (slot-major): the MFMA loop's vmcnt waits assume that
@@ -182,6 +195,10 @@ struct LayerPipe {
         ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * min(s, kchunks - 1));
         __builtin_amdgcn_sched_barrier(0);
       }
+  }
+  template <int TPW>
+  __device__ __forceinline__ void prepare_ep(const rk_mlp_layer& L, int wave, int lane) {
+    const int li = lane & 15;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int n = 16 * (wave + kMlpWaves * j) + li;
@@ -192,10 +209,12 @@ struct LayerPipe {
 
 // One layer (weights already in flight in P) over RT row tiles of 16 rows: each weight float4
 // feeds RT x 4 MFMAs.  kchunks = Kp / 16 (a multiple of 4).
-template <int TPW, int RT, int PD, bool STORE>
+// `next` runs right after the last MFMA is issued (mlp_rows: the next layer's weight ring).
+template <int TPW, int RT, int PD, bool STORE, class Next>
 __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, const float* __restrict__ in,
                                           int ldin, float* __restrict__ out, int ldout, int Kp, int wave, int lane,
-                                          int64_t m0, int rows, int dbg_mark = 0, unsigned long long dbg_t0 = 0) {
+                                          int64_t m0, int rows, Next next, int dbg_mark = 0,
+                                          unsigned long long dbg_t0 = 0) {
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const int kchunks = Kp / 16;
   f32x4_t acc[TPW][RT];
@@ -261,6 +280,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
     // prepare() to wait behind)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only (lgkmcnt / expcnt at their maximum)
   }
+  next();
 
 #ifdef RK_MLP_PHASES
   if (wave == 0 && lane == 0) s_mlp_marks[dbg_mark] = clock64() - dbg_t0;
@@ -357,6 +377,23 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
     else if (wave < nt)
       pipe.prepare<1, 8>(layers[l], kch, wave, lane);
   };
+#if RK_MLP_EARLY_RING
+  auto prepare_ring = [&](int l) {
+    const int nt = pad64(layers[l].n) / 16;
+    const int kch = pad64(layers[l - 1].n) / 16;
+    if (wave + kMlpWaves < nt)
+      pipe.prepare_ring<2, 4>(layers[l], kch, wave, lane);
+    else if (wave < nt)
+      pipe.prepare_ring<1, 8>(layers[l], kch, wave, lane);
+  };
+  auto prepare_ep = [&](int l) {
+    const int nt = pad64(layers[l].n) / 16;
+    if (wave + kMlpWaves < nt)
+      pipe.prepare_ep<2>(layers[l], wave, lane);
+    else if (wave < nt)
+      pipe.prepare_ep<1>(layers[l], wave, lane);
+  };
+#endif
   // The head's operands (head_w for this lane's columns, this wave's row scalars) are loaded while
   // the last layer runs: fetched after the final barrier they put two dependent L2 round trips
   // (~10k cycles at 256 busy CUs, tools/mlp_phases.hip) between the last MFMA and the logits.
@@ -394,16 +431,30 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
     const float* in = (l & 1) ? buf1 : buf0;
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
-    if (wave + kMlpWaves < ntiles)
-      mlp_layer<2, RT, 4, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 4 * l, t0);
-    else if (wave < ntiles)
-      mlp_layer<1, RT, 8, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, 4 * l, t0);
+#if RK_MLP_EARLY_RING
+    auto next = [&] {
+      if (l + 1 < nl) prepare_ring(l + 1);
+    };
+#else
+    auto next = [] {};
+#endif
+    if (wave + kMlpWaves < ntiles) {
+      mlp_layer<2, RT, 4, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, next, 4 * l, t0);
+    } else if (wave < ntiles) {
+      mlp_layer<1, RT, 8, STORE>(pipe, L, in, ldin, out, ldout, Kp, wave, lane, m0, rows, next, 4 * l, t0);
+    } else {
 #if RK_MLP_SYNC
-    else  // no tile in this layer: take part in the active waves' lockstep barriers
+      // no tile in this layer: take part in the active waves' lockstep barriers
       for (int i = 0; i < (Kp / 16 - 1) / kMlpSyncChunks; ++i) mlp_sync_barrier();
 #endif
+      next();
+    }
     MLP_MARK(4 * l + 1, t0);
+#if RK_MLP_EARLY_RING
+    if (l + 1 < nl) prepare_ep(l + 1);
+#else
     if (l + 1 < nl) prepare(l + 1);
+#endif
     if (l + 2 == nl) head_prefetch();
     MLP_MARK(4 * l + 2, t0);
     mlp_lds_barrier();
