@@ -531,43 +531,46 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #ifdef RK_DIN_PHASES
   if (lane == 0) s_din_wave[wave] = clock64() - wave_t0;
 #endif
-  __syncthreads();
-  DIN_TS(2);
-  // l2 partials: the last workgroup to publish its partial also finishes the mean, after its own
-  // phase B.  Hand-off = MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1
-  // table (measured valid on gfx950 / ROCm 7.2, not an architectural guarantee): one lane per
-  // workgroup stores its partial sc1 (relaxed agent store), waits vmcnt(0), then adds to ONE
-  // counter (relaxed agent atomic); the workgroup whose add returns n-1 loads every partial with
-  // sc1 loads (relaxed agent loads) in the adding wave, after the add returned.  The memory-model
-  // form (release/acquire at agent scope) lowers to buffer_wbl2 / buffer_inv, ~1.7-3.5 us each on
-  // the critical path of a ~50 us kernel; tests/test_gpu_din_plan.py checks l2 against the
-  // deterministic host-order sum over repeated launches.
-  int& l2_last = *reinterpret_cast<int*>(col_seg + 512);
-  if (a.l2_part && tid == 0) {
-    float t = 0.f;
-    for (int w = 0; w < kMlpRows; ++w) t += sm[Ly::NORM + w];
-    __hip_atomic_store(a.l2_part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(a.l2_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    l2_last = prev == gridDim.x - 1;
-  }
+  DIN_TS(2);  // (tid 0's own phase A: no workgroup barrier here any more)
 
-  // ---- Phase B: fcn tail + head over the 16 rows
+  // ---- Phase B: fcn tail + head over the 16 rows.  No barrier in front of it: each wave issues
+  // its layer-0 weight ring (mlp_rows' prepare) as soon as its own phase A is done, and mlp_rows'
+  // barrier after that prepare closes phase A, so the ring's latency overlaps the wait for the
+  // slowest sample instead of opening phase B.
 #ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
   return;
 #endif
   mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
            NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
-  // (mlp_rows' barriers order tid 0's l2_last store before these reads)
-  if (a.l2_part && tid < 64 && l2_last) {
-    float t = 0.f;
-    for (int i = tid; i < (int)gridDim.x; i += 64)
-      t += __hip_atomic_load(a.l2_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = wave_sum(t);  // the order of row_l2norm_final_kernel (embedding.hip)
+  // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =
+  // MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1 table (measured valid on
+  // gfx950 / ROCm 7.2, not an architectural guarantee): one lane per workgroup stores its partial
+  // sc1 (relaxed agent store), waits vmcnt(0), then adds to ONE counter (relaxed agent atomic);
+  // the workgroup whose add returns n-1 loads every partial with sc1 loads (relaxed agent loads)
+  // in the adding wave, after the add returned.  The memory-model form (release/acquire at agent
+  // scope) lowers to buffer_wbl2 / buffer_inv, ~1.7-3.5 us each on the critical path of a ~50 us
+  // kernel; tests/test_gpu_din_plan.py checks l2 against the deterministic host-order sum over
+  // repeated launches.  (The norms in LDS were ordered before this by mlp_rows' barriers.)
+  if (a.l2_part && tid < 64) {
+    unsigned prev = 0;
     if (tid == 0) {
-      a.l2_out[0] = a.l2_scale * (t / (float)a.batch);
-      __hip_atomic_store(a.l2_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float t = 0.f;
+      for (int w = 0; w < kMlpRows; ++w) t += sm[Ly::NORM + w];
+      __hip_atomic_store(a.l2_part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      prev = __hip_atomic_fetch_add(a.l2_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == gridDim.x - 1) {
+      float t = 0.f;
+      for (int i = tid; i < (int)gridDim.x; i += 64)
+        t += __hip_atomic_load(a.l2_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = wave_sum(t);  // the order of row_l2norm_final_kernel (embedding.hip)
+      if (tid == 0) {
+        a.l2_out[0] = a.l2_scale * (t / (float)a.batch);
+        __hip_atomic_store(a.l2_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 #ifdef RK_DIN_PHASES

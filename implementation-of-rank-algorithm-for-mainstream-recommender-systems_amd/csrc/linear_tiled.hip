@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + 32 * rh + 16 * t + 4 * (lane >> 4) + r;
-        if (m < a.M) a.y[m * a.ldy + n] = col_apply(ep, L.act == RK_ACT_DICE, acc[t][r], false, 0.f);
+        if (m < a.M) a.y[m * a.ldy + n] = col_apply(L, ep, L.act == RK_ACT_DICE, acc[t][r], false, 0.f);
       }
   }
   MLP_MARK(10, t0);

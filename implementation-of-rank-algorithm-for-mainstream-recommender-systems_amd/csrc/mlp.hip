@@ -177,12 +177,16 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
         }
         const float v = src[(r < 0 ? 0 : r) * ld + col];
         x0[j] = (live && c < width && r >= 0) ? v : 0.f;
+        // unconditional loads (a clamped layer; with no cross layer, any valid vector): loads under
+        // `if (l < nl)` were placed after layer 0's weight ring, and waiting for them drained it
+        const float* cwp = nl > 0 ? a.cross_w : a.cross_head_w;
+        const float* cbp = nl > 0 ? a.cross_b : a.cross_head_w;
 #pragma unroll
-        for (int l = 0; l < kDcnPreLayers; ++l)
-          if (l < nl) {
-            cw[l][j] = a.cross_w[(int64_t)l * width + cc];
-            cb[l][j] = a.cross_b[(int64_t)l * width + cc];
-          }
+        for (int l = 0; l < kDcnPreLayers; ++l) {
+          const int64_t o = (int64_t)min(l, max(nl - 1, 0)) * width + cc;
+          cw[l][j] = cwp[o];
+          cb[l][j] = cbp[o];
+        }
         hw[j] = a.cross_head_w[cc];
       }
     }
@@ -195,21 +199,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
       xl[j] = x0[j];
       if (c < K0p) buf0[wave * a.m.ld0 + c] = x0[j];
     }
-    for (int l = 0; l < nl; ++l) {
-      float w[NJ], bl[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        w[j] = cw[0][j];
-        bl[j] = cb[0][j];
-#pragma unroll
-        for (int q = 1; q < kDcnPreLayers; ++q)
-          if (q == l) w[j] = cw[q][j], bl[j] = cb[q][j];
-        if (l >= kDcnPreLayers) {
-          const int c = min(lane + 64 * j, width - 1);
-          w[j] = a.cross_w[(int64_t)l * width + c];
-          bl[j] = a.cross_b[(int64_t)l * width + c];
-        }
-      }
+    auto cross = [&](const float* w, const float* bl) {
       float d = 0.f;
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
@@ -222,6 +212,21 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
           t = t + bl[j];         // + bl.t()
           xl[j] = t + xl[j];     // + xl
         }
+    };
+    // the first kDcnPreLayers layers straight-line from registers (a runtime loop with loads in it
+    // made the compiler close its header with vmcnt(0), draining layer 0's weight ring here)
+#pragma unroll
+    for (int l = 0; l < kDcnPreLayers; ++l)
+      if (l < nl) cross(cw[l], cb[l]);
+    for (int l = kDcnPreLayers; l < nl; ++l) {
+      float w[NJ], bl[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = min(lane + 64 * j, width - 1);
+        w[j] = a.cross_w[(int64_t)l * width + c];
+        bl[j] = a.cross_b[(int64_t)l * width + c];
+      }
+      cross(w, bl);
     }
     float p = 0.f;
 #pragma unroll

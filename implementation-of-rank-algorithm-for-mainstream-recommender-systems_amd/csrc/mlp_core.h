@@ -37,6 +37,11 @@ namespace rk {
 #ifndef RK_MLP_EARLY_RING
 #define RK_MLP_EARLY_RING 0
 #endif
+// RK_MLP_UNIFORM_PREP=1: one prepare() code path for both layer shapes (LayerPipe::prepare_any).
+// Measured DCN 130.2 -> 128.4 M, DIN / DeepFM within noise (profiles/r03/NOTES.md), so off.
+#ifndef RK_MLP_UNIFORM_PREP
+#define RK_MLP_UNIFORM_PREP 0
+#endif
 
 constexpr int kMlpRows = 16;
 constexpr int kMlpWaves = 16;
@@ -75,43 +80,49 @@ __device__ __forceinline__ f32x4_t mfma16(float a, float b, f32x4_t c) {
 // Per-column epilogue parameters of one output column, loaded into registers before the MFMA
 // loop: read in the epilogue they would be re-fetched after every LDS store (the compiler cannot
 // prove the generic output pointer does not alias them), each fetch waiting on the whole vmcnt
-// queue of weight loads.
+// queue of weight loads.  The loads are unconditional (an absent vector reads the always-valid
+// weight image instead) and the raw values are resolved against the layer's flags only in the
+// epilogue: loads under `p ? p[n] : default` became scalar branches whose join the compiler
+// closed with a full vmcnt(0), draining the next layer's whole weight ring inside prepare().
 struct ColEpi {
-  float bias, pre_s, pre_b, act_s, act_b, alpha, neg, post_s, post_b;
+  float bias, pre_s, pre_b, act_s, act_b, alpha, post_s, post_b;
 };
 
-// Absent affine parts default to the identity (z * 1 + 0 is exact), and the piecewise-linear
-// activations to one negative-side slope `neg` (ReLU 0, LeakyReLU slope, PReLU alpha, none 1), so
-// the epilogue runs as straight-line code with one wave-uniform branch (Dice).
 __device__ __forceinline__ ColEpi col_epi(const rk_mlp_layer& L, int n) {
+  // L.w holds at least 64 x 64 floats and n < 512: any index read from it is in bounds
+  auto ld = [&](const float* p, int i) { return (p ? p : L.w)[i]; };
   ColEpi e;
-  e.bias = L.bias ? L.bias[n] : 0.f;
-  e.pre_s = L.pre_scale ? L.pre_scale[n] : 1.f;
-  e.pre_b = L.pre_scale ? L.pre_shift[n] : 0.f;
-  e.post_s = L.post_scale ? L.post_scale[n] : 1.f;
-  e.post_b = L.post_scale ? L.post_shift[n] : 0.f;
-  e.act_s = L.act == RK_ACT_DICE ? L.act_scale[n] : 0.f;
-  e.act_b = L.act == RK_ACT_DICE ? L.act_shift[n] : 0.f;
-  e.alpha = L.act == RK_ACT_DICE ? L.act_alpha[n]
-          : L.act == RK_ACT_PRELU ? L.act_alpha[L.act_alpha_len == 1 ? 0 : n] : 0.f;
-  e.neg = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? e.alpha : 1.f;
+  e.bias = ld(L.bias, n);
+  e.pre_s = ld(L.pre_scale, n);
+  e.pre_b = ld(L.pre_scale ? L.pre_shift : nullptr, n);
+  e.post_s = ld(L.post_scale, n);
+  e.post_b = ld(L.post_scale ? L.post_shift : nullptr, n);
+  const bool dice = L.act == RK_ACT_DICE;
+  e.act_s = ld(dice ? L.act_scale : nullptr, n);
+  e.act_b = ld(dice ? L.act_shift : nullptr, n);
+  e.alpha = ld(dice || L.act == RK_ACT_PRELU ? L.act_alpha : nullptr, dice || L.act_alpha_len != 1 ? n : 0);
   return e;
 }
 
 // The element-wise epilogue in the reference's order (bias, residual, pre-BN, activation,
-// post-BN); `dice` and `has_res` are wave-uniform.  ReLU of a negative value gives -0 here
-// (z * 0), equal to torch.relu's +0 in every later use; NaN stays NaN as in torch.relu.
-__device__ __forceinline__ float col_apply(const ColEpi& e, bool dice, float z, bool has_res, float res) {
-  z += e.bias;
+// post-BN); `dice` and `has_res` are wave-uniform.  Absent affine parts are the identity (z * 1 + 0
+// is exact), and the piecewise-linear activations one negative-side slope `neg` (ReLU 0,
+// LeakyReLU slope, PReLU alpha, none 1), so the code is straight-line apart from Dice.  ReLU of a
+// negative value gives -0 here (z * 0), equal to torch.relu's +0 in every later use; NaN stays NaN
+// as in torch.relu.
+__device__ __forceinline__ float col_apply(const rk_mlp_layer& L, const ColEpi& e, bool dice, float z, bool has_res,
+                                           float res) {
+  z += L.bias ? e.bias : 0.f;
   if (has_res) z = res + z;
-  z = z * e.pre_s + e.pre_b;
+  z = z * (L.pre_scale ? e.pre_s : 1.f) + (L.pre_scale ? e.pre_b : 0.f);
   if (dice) {
     const float p = sigmoid_fast(z * e.act_s + e.act_b);
     z = e.alpha * (1.0f - p) * z + p * z;
   } else {
-    z = z > 0.f ? z : z * e.neg;
+    const float neg = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? e.alpha : 1.f;
+    z = z > 0.f ? z : z * neg;
   }
-  return z * e.post_s + e.post_b;
+  return z * (L.post_scale ? e.post_s : 1.f) + (L.post_scale ? e.post_b : 0.f);
 }
 
 // Optional per-workgroup phase marks (timing builds with RK_MLP_PHASES: tools/dcn_phases.py,
@@ -195,6 +206,27 @@ struct LayerPipe {
         ring[s * TPW + j] = *reinterpret_cast<const f32x4_t*>(wrow[j] + kFragStep * min(s, kchunks - 1));
         __builtin_amdgcn_sched_barrier(0);
       }
+  }
+  // Both layer shapes in one code path (`two`: the wave owns two column tiles): slot k holds chunk
+  // k >> 1 of tile k & 1 (two tiles) or chunk k (one tile), the order the two mlp_layer variants
+  // consume.  With a prepare per variant the ring values met at a join after it, and the compiler
+  // copied them into one register set there — copies that wait for each load to land, i.e. a full
+  // vmcnt(0) drain of the ring right after issuing it, before the layer barrier.
+  __device__ __forceinline__ void prepare_any(const rk_mlp_layer& L, int kchunks, bool two, int wave, int lane) {
+    wrow[0] = wfrag(L, wave, lane);
+    wrow[1] = wfrag(L, wave + kMlpWaves, lane);  // dereferenced only when two
+#pragma unroll
+    for (int k = 0; k < kMlpRing; ++k) {
+      const float* p = two ? wrow[k & 1] + kFragStep * min(k >> 1, kchunks - 1) : wrow[0] + kFragStep * min(k, kchunks - 1);
+      ring[k] = *reinterpret_cast<const f32x4_t*>(p);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int li = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * (wave + kMlpWaves * j) + li;
+      ep[j] = col_epi(L, n < L.n ? n : 0);
+    }
   }
   template <int TPW>
   __device__ __forceinline__ void prepare_ep(const rk_mlp_layer& L, int wave, int lane) {
@@ -292,31 +324,47 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
   // SIMD still in their MFMA loops (reset to 0 after the barrier)
   __builtin_amdgcn_s_setprio(2);
 #endif
-  const bool dice = L.act == RK_ACT_DICE;
-  const bool has_res = L.residual != 0;
   float* const store = STORE ? L.store : nullptr;  // eval kernels compile the store path out
   const int64_t ld_store = L.ld_store;
+  // The two wave-uniform switches (Dice, residual) are taken once for the whole epilogue: inside
+  // the unrolled element loop the compiler kept them as per-element scalar branches around exec-
+  // masked blocks (~25 instructions per element); specialised, each element is straight-line VALU
+  // and the pad columns a select.
+  auto epilogue = [&](auto DICE, auto RES) {
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    const int n = 16 * (wave + kMlpWaves * j) + li;
-    const bool real = n < L.n;
-    // x + f(x): the previous layer's input still sits in `out` (read all, then write: same lane)
-    float res[RT][4];
+    for (int j = 0; j < TPW; ++j) {
+      const int n = 16 * (wave + kMlpWaves * j) + li;
+      const bool real = n < L.n;
+      // x + f(x): the previous layer's input still sits in `out` (read all, then write: same lane)
+      float res[RT][4];
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) res[t][r] = has_res ? out[(16 * t + (lane >> 4) * 4 + r) * ldout + n] : 0.f;
+        for (int r = 0; r < 4; ++r) res[t][r] = RES ? out[(16 * t + (lane >> 4) * 4 + r) * ldout + n] : 0.f;
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * t + (lane >> 4) * 4 + r;
-        const float z =
-            real ? col_apply(P.ep[j], dice, acc[j][t][r], has_res, res[t][r]) : 0.f;
-        out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
-        if constexpr (STORE)
-          if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * t + (lane >> 4) * 4 + r;
+          const float v = col_apply(L, P.ep[j], DICE, acc[j][t][r], RES, res[t][r]);
+          const float z = real ? v : 0.f;
+          out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
+          if constexpr (STORE)
+            if (store && real && row < rows) store[(m0 + row) * ld_store + n] = z;
+        }
+    }
+  };
+  const bool dice = L.act == RK_ACT_DICE;
+  if (L.residual != 0) {
+    if (dice)
+      epilogue(std::true_type{}, std::true_type{});
+    else
+      epilogue(std::false_type{}, std::true_type{});
+  } else {
+    if (dice)
+      epilogue(std::true_type{}, std::false_type{});
+    else
+      epilogue(std::false_type{}, std::false_type{});
   }
 #ifdef RK_MLP_PHASES
   if (lane == 0 && dbg_mark / 4 < 4) s_mlp_wave_marks[dbg_mark / 4][wave][1] = (unsigned)(clock64() - dbg_t0);
@@ -372,10 +420,14 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
   auto prepare = [&](int l) {
     const int nt = pad64(layers[l].n) / 16;  // multiple of 4
     const int kch = pad64(l ? layers[l - 1].n : K0) / 16;
+#if RK_MLP_UNIFORM_PREP
+    if (wave < nt) pipe.prepare_any(layers[l], kch, wave + kMlpWaves < nt, wave, lane);
+#else
     if (wave + kMlpWaves < nt)
       pipe.prepare<2, 4>(layers[l], kch, wave, lane);
     else if (wave < nt)
       pipe.prepare<1, 8>(layers[l], kch, wave, lane);
+#endif
   };
 #if RK_MLP_EARLY_RING
   auto prepare_ring = [&](int l) {
@@ -412,6 +464,7 @@ __device__ __forceinline__ void mlp_rows(const rk_mlp_layer* __restrict__ layers
   const unsigned long long t_start = clock64();
 #endif
   stage.issue();
+  __builtin_amdgcn_sched_barrier(0);  // the stage's loads stay ahead of the weight ring
   if (nl > 0) prepare(0);
   if (nl <= 1) head_prefetch();
   MLP_MARK(4 * RK_MLP_MAX_LAYERS - 4, t_start);  // (timing builds: the last layer's slots, unused here)
