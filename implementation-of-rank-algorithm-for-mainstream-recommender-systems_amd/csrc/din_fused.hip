@@ -22,6 +22,13 @@
 
 namespace rk {
 
+// tile 1's history keys prefetched into LDS by LDS-DMA during tile 0 (phase A below)
+#ifndef RK_DIN_PF1
+#define RK_DIN_PF1 1
+#endif
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
 constexpr int kDinSegs = 32;
 constexpr int kDinSegLdsOff = 528;  // bytes past the column map: 256 + 256 map bytes, l2_last int, pad to 16
 struct DinSegs {
@@ -383,6 +390,15 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   // tile 1's index waits in LDS (a register across tile 0 spills at the 128-VGPR budget)
   int64_t* const kpre = kpre0 + 64 * loc + 32;
 
+  // tile-1 key prefetch slots (see phase A below): NQ KiB per wave in buf1
+  const int pf_slots = min(kMlpRows, (kMlpRows * a.ld1) / (256 * NQ));
+#if RK_DIN_PF1
+  const bool pf1 = live && ntiles > 1 && wave < pf_slots;
+#else
+  const bool pf1 = false;
+#endif
+  float* const pf_slot = buf1 + 256 * NQ * wave;
+
   f32x4_t k[NQ];
   // key rows of position t (index r) into k; positions past T read as zeros
   auto load_keys = [&](int64_t r, int t) {
@@ -433,6 +449,22 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
 
+    // ---- tile 1's key rows straight into LDS (LDS-DMA: no VGPRs, the kernel is at its 128-register
+    // budget) while tile 0 computes: loaded at tile 1's start they cost the wave a full gather
+    // latency, uncovered once the SIMD's shorter samples are done.  Slots (NQ KiB per wave) live in
+    // buf1, which phase B first writes after the barrier that closes phase A; the ranking puts the
+    // longest samples on the lowest waves, so the slots go to waves 0 .. pf_slots - 1.
+    if (pf1) {
+      const int t1 = 32 + l32;
+      const int64_t r1 = NIT == 0 ? kpre[l32] : kidx[1];
+      const bool ok = t1 < a.T && r1 >= 0 && r1 < a.key_rows;
+      if (t1 < a.T && !ok) flag_oob(flags);
+      const float* src = a.key_table + (ok ? r1 * a.ld_key : 0) + hk;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c)
+        __builtin_amdgcn_global_load_lds((glb_void*)(src + 8 * c), (lds_void*)(pf_slot + 256 * c), 16, 0, 0);
+    }
+
     const float sqrt_h = (float)__builtin_sqrt((double)H);
     const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
     float m_run = -INFINITY, l_run = 0.f;
@@ -445,8 +477,18 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       asm volatile("" ::: "memory");
       const int t = tt * 32 + l32;
       const bool in_seq = t < a.T;
-      if (tt > 0)  // tile 0's keys were loaded with the row; tile 1's index was prefetched
+      if (tt == 1 && pf1) {  // tile 1's keys from the LDS-DMA slot (zeros past T / out of range)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only: the DMA went out a tile ago
+        const int64_t r1 = NIT == 0 ? kpre[l32] : kidx[1];
+        const bool ok = in_seq && r1 >= 0 && r1 < a.key_rows;
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(pf_slot + 256 * c + 4 * lane);
+          k[c] = ok ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        }
+      } else if (tt > 0) {  // tile 0's keys were loaded with the row; tile 1's index was prefetched
         load_keys(tt == 1 ? kpre[l32] : (in_seq ? a.seq[b * a.ld_seq + t] : 0), t);
+      }
 
       // layer 1 (transposed) one 32-row block jt at a time, each folded straight into layer 2
       // (acc2 = W2 . h1^T with the layer-1 accumulator as the B operand): one layer-1
