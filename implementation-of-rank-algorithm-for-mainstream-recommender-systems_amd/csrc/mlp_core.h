@@ -39,6 +39,11 @@ namespace rk {
 #endif
 // RK_MLP_UNIFORM_PREP=1: one prepare() code path for both layer shapes (LayerPipe::prepare_any).
 // Measured DCN 130.2 -> 128.4 M, DIN / DeepFM within noise (profiles/r03/NOTES.md), so off.
+// RK_MLP_EP_LANES16=1: epilogue parameters fetched by lanes 0..15 only and broadcast in the
+// epilogue (ep_bcast).  Measured DCN 130.4 -> 127.8 M, DIN / DeepFM -1 % (profiles/r03/NOTES.md): off.
+#ifndef RK_MLP_EP_LANES16
+#define RK_MLP_EP_LANES16 0
+#endif
 #ifndef RK_MLP_UNIFORM_PREP
 #define RK_MLP_UNIFORM_PREP 0
 #endif
@@ -231,13 +236,40 @@ struct LayerPipe {
   template <int TPW>
   __device__ __forceinline__ void prepare_ep(const rk_mlp_layer& L, int wave, int lane) {
     const int li = lane & 15;
+#if RK_MLP_EP_LANES16
+    // the 4 lane groups of a column tile need the same 16 columns: only lanes 0..15 fetch them
+    // (a quarter of the address/data work in the shared TA path, which every wave's prepare
+    // otherwise saturates at the layer boundary), the epilogue broadcasts them (ep_bcast)
+    if (lane < 16)
+#endif
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      const int n = 16 * (wave + kMlpWaves * j) + li;
-      ep[j] = col_epi(L, n < L.n ? n : 0);
-    }
+      for (int j = 0; j < TPW; ++j) {
+        const int n = 16 * (wave + kMlpWaves * j) + li;
+        ep[j] = col_epi(L, n < L.n ? n : 0);
+      }
   }
 };
+
+// Lanes 0..15's epilogue parameters to every lane of the column tile (ds_bpermute; in the
+// epilogue, where waiting for the loads is free).
+__device__ __forceinline__ ColEpi ep_bcast(const ColEpi& e, int lane) {
+#if RK_MLP_EP_LANES16
+  const int src = lane & 15;
+  ColEpi o;
+  o.bias = __shfl(e.bias, src, 64);
+  o.pre_s = __shfl(e.pre_s, src, 64);
+  o.pre_b = __shfl(e.pre_b, src, 64);
+  o.act_s = __shfl(e.act_s, src, 64);
+  o.act_b = __shfl(e.act_b, src, 64);
+  o.alpha = __shfl(e.alpha, src, 64);
+  o.post_s = __shfl(e.post_s, src, 64);
+  o.post_b = __shfl(e.post_b, src, 64);
+  return o;
+#else
+  (void)lane;
+  return e;
+#endif
+}
 
 // One layer (weights already in flight in P) over RT row tiles of 16 rows: each weight float4
 // feeds RT x 4 MFMAs.  kchunks = Kp / 16 (a multiple of 4).
@@ -335,6 +367,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
     for (int j = 0; j < TPW; ++j) {
       const int n = 16 * (wave + kMlpWaves * j) + li;
       const bool real = n < L.n;
+      const ColEpi ep = ep_bcast(P.ep[j], lane);
       // x + f(x): the previous layer's input still sits in `out` (read all, then write: same lane)
       float res[RT][4];
 #pragma unroll
@@ -346,7 +379,7 @@ __device__ __forceinline__ void mlp_layer(LayerPipe& P, const rk_mlp_layer& L, c
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * t + (lane >> 4) * 4 + r;
-          const float v = col_apply(L, P.ep[j], DICE, acc[j][t][r], RES, res[t][r]);
+          const float v = col_apply(L, ep, DICE, acc[j][t][r], RES, res[t][r]);
           const float z = real ? v : 0.f;
           out[row * ldout + n] = z;  // padded columns [n, Np) become the next layer's zero K pad
           if constexpr (STORE)
