@@ -58,6 +58,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--din-streams", type=int, default=1,
+                    help="DIN headline: batches in flight on as many HIP streams (default 1; "
+                         "tools/din_streams.py measures 2-4)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-extras", action="store_true", help="skip the per-model extras")
@@ -562,7 +565,7 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
 
 # ------------------------------------------------------------------ main
 
-def bench_one(name, batch, steps, warmup, world, rank, zipf=None):
+def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
     model, inp, fn, cfg, model_name = workload(name, batch, rank, zipf)
     if name.endswith("per_call") or name.endswith("_eager"):
         # eager: one Python forward per step, as the reference's evaluate() / predict loops call
@@ -585,6 +588,34 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None):
         tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
         res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
         res["step"] = "prepared single-kernel launch (rk_din_plan_launch)"
+        if streams > 1:
+            # S batches in flight: S prepared launches, each with its own inputs (seeded apart),
+            # outputs and l2 workspace, issued round-robin on S HIP streams, so the next batch's
+            # workgroups take the CUs the previous batch's tail frees (tools/din_streams.py:
+            # outputs bit-identical to single-stream launches).  Every step is still one whole
+            # batch forward, all of them inside the timed window.
+            import helpers as H
+            t1 = max_over_ranks(world, time_replays(run, steps, warmup, world))
+            res["single_stream_samples_per_s"] = round(world * batch * steps / t1, 1)
+            res["single_stream_ms_per_step"] = round(1e3 * t1 / steps, 4)
+            dev = torch.device("cuda", torch.cuda.current_device())
+            runs = [run]
+            for i in range(1, streams):
+                x = H.to_device(H.make_inputs(model_name, cfg, batch, seed=1000 + rank + 7919 * i), dev)
+                runs.append(model.prepare(x["dense"], x["category"], x["sequence"], x["target"]))
+            strs = [torch.cuda.Stream() for _ in range(streams)]
+            for st in strs:
+                st.wait_stream(torch.cuda.current_stream())
+            plans = [r.plan for r in runs]
+            handles = [st.cuda_stream for st in strs]
+            cnt = [0]
+
+            def run():
+                i = cnt[0] % streams
+                cnt[0] += 1
+                plans[i].launch_on(handles[i])
+            res["step"] = (f"prepared single-kernel launches (rk_din_plan_launch), {streams} batches in flight "
+                           f"on {streams} HIP streams (round-robin, own inputs/outputs/workspaces)")
     else:
         run = g.replay
     t = time_replays(run, steps, warmup, world)
@@ -602,7 +633,8 @@ def main():
     rankops.load_library()
     torch.backends.cuda.matmul.allow_tf32 = False
 
-    head, model, inp, cfg, model_name = bench_one("din", args.batch, args.steps, args.warmup, world, rank)
+    head, model, inp, cfg, model_name = bench_one("din", args.batch, args.steps, args.warmup, world, rank,
+                                                  streams=args.din_streams)
     result = {
         "metric": METRIC,
         "value": head["samples_per_s"],
@@ -620,7 +652,9 @@ def main():
                    "model": "DIN", "global_batch": world * args.batch, "seq_len": 50, "emb_dim": 32,
                    "tables": "wechat_algo_data1 sizes (feedid 106445 rows)", "mode": "eval, inputs resident in HBM",
                    "interaction_weights": "frozen", "parallelism": f"replicas x{world}",
-                   "step": head.get("step"), "graph_replay_ms_per_step": head.get("graph_replay_ms_per_step")},
+                   "step": head.get("step"), "graph_replay_ms_per_step": head.get("graph_replay_ms_per_step"),
+                   "single_stream_samples_per_s": head.get("single_stream_samples_per_s"),
+                   "single_stream_ms_per_step": head.get("single_stream_ms_per_step")},
     }
     if rank == 0:
         launch = model.fused_kernel_launcher(inp["dense"], inp["category"], inp["sequence"], inp["target"])

@@ -448,6 +448,11 @@ class DinPlan:
         check(self._lib.rk_din_plan_launch(self._handle, _lib.raw_stream(self._device)),
               "rk_din_plan_launch")
 
+    def launch_on(self, stream: int):
+        """Launch on an explicit HIP stream (a raw handle, e.g. `torch.cuda.Stream().cuda_stream`),
+        without making it the current stream."""
+        check(self._lib.rk_din_plan_launch(self._handle, ctypes.c_void_p(stream)), "rk_din_plan_launch")
+
     def __del__(self):
         h = getattr(self, "_handle", None)
         if h is not None and h.value:

@@ -22,6 +22,19 @@ for r in runs:
     torch.cuda.synchronize()
     ref.append((p.clone(), lg.clone(), l2.clone() if torch.is_tensor(l2) else l2))
 streams = [torch.cuda.Stream() for _ in range(4)]
+plans = [r.plan for r in runs]
+handles = [st.cuda_stream for st in streams]
+# one stream, the default one (as bench.py's single-stream leg)
+for n in (50, steps):
+    best = 0.0
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            runs[0]()
+        torch.cuda.synchronize()
+        best = max(best, batch * n / (time.perf_counter() - t0))
+    print(f"default stream, {n} steps: {best / 1e6:.2f} M samples/s", flush=True)
 for S in (1, 2, 3, 4):
     best = 0.0
     for _ in range(3):
@@ -31,8 +44,7 @@ for S in (1, 2, 3, 4):
         t0 = time.perf_counter()
         for k in range(steps):
             i = k % S
-            with torch.cuda.stream(streams[i]):
-                runs[i]()
+            plans[i].launch_on(handles[i])
         for i in range(S):
             torch.cuda.current_stream().wait_stream(streams[i])
         torch.cuda.synchronize()
