@@ -17,6 +17,38 @@ def _cfg(**kw):
 
 
 @pytest.mark.gpu
+def test_batches_in_flight_on_streams_equal_single_stream():
+    """DinPlan.launch_on: several prepared forwards (own inputs, outputs and l2 workspaces) issued
+    round-robin on their own HIP streams, as bench.py --din-streams N runs them, give each batch's
+    single-stream outputs bit for bit (l2 included: each plan has its own hand-off counter)."""
+    cfg = _cfg()
+    model = H.build("din", cfg).cuda().eval()
+    inps = [H.to_device(H.make_inputs("din", cfg, 1000, seed=500 + i), "cuda") for i in range(3)]
+    with torch.no_grad():
+        runs = [model.prepare(x["dense"], x["category"], x["sequence"], x["target"]) for x in inps]
+        live = [r() for r in runs]  # the plan's own output tensors, rewritten by every launch
+        ref = [tuple(x.clone() if isinstance(x, torch.Tensor) else x for x in o) for o in live]
+        for o in live:  # poison them: the stream launches below must rewrite every element
+            for x in o:
+                if isinstance(x, torch.Tensor):
+                    x.fill_(float("nan"))
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream() for _ in runs]
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
+        for k in range(12):
+            i = k % len(runs)
+            runs[i].plan.launch_on(streams[i].cuda_stream)
+        for st in streams:
+            torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        for got, want in zip(live, ref):
+            for g, w in zip(got, want):
+                if isinstance(w, torch.Tensor):
+                    assert torch.equal(g, w)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("softmax", [False, True])
 def test_prepared_equals_eager_and_follows_inputs(softmax):
     cfg = _cfg(softmax=softmax)
