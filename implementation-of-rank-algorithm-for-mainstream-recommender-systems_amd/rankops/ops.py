@@ -382,8 +382,9 @@ _DIN_L2_WS = {}
 def _din_l2_workspace(device, batch):
     """rk_din_forward's l2 workspace: ceil(batch/16) partials + a completion counter that starts at
     zero and that every launch leaves at zero, so it is allocated (zeroed) once per device and
-    size and reused, also by a hipGraph captured after a warm-up call.  DIN forwards of one batch
-    size on one device therefore must not run concurrently on two streams."""
+    size and reused, also by a hipGraph captured after a warm-up call.  Eager DIN forwards of one
+    batch size on one device therefore must not run concurrently on two streams (prepared plans
+    carry their own: din_forward_plan)."""
     n = (batch + 15) // 16 + 1
     key = (str(torch.device(device)), n)
     ws = _DIN_L2_WS.get(key)
@@ -408,12 +409,20 @@ def din_pack_attention(att_weights, H: int) -> torch.Tensor:
 
 
 def _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax, layers,
-                      head: Epilogue, batch, device, l2_col0, l2_scale, l2_out, att_image):
-    """The rk_din_forward argument list (without the stream) and the ctypes arrays it points into."""
+                      head: Epilogue, batch, device, l2_col0, l2_scale, l2_out, att_image, private_ws=False):
+    """The rk_din_forward argument list (without the stream) and the ctypes arrays it points into.
+    private_ws: an l2 workspace of its own (a prepared plan, which may run concurrently with other
+    plans on other streams) instead of the shared per-(device, batch) one."""
     w1, b1, w2, b2, w3, b3 = att_weights
     arr = _seg_array(segs)
     larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
-    ws = _din_l2_workspace(device, batch) if l2_out is not None else None
+    ws = None
+    if l2_out is not None:
+        if private_ws:
+            ws = torch.zeros((batch + 15) // 16 + 1, device=device, dtype=torch.float32)
+            torch.cuda.current_stream(ws.device).synchronize()  # zeroed before a launch on any stream
+        else:
+            ws = _din_l2_workspace(device, batch)
     args = (arr, len(segs), width, q_col, att_col, ptr(key_table), key_table.shape[0], key_table.stride(0), ptr(seq),
             seq.stride(0), seq.shape[1], ptr(seq_len), batch, H, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(w3),
             ptr(b3), 1 if use_softmax else 0, larr, len(layers), ctypes.byref(head), l2_col0, float(l2_scale),
@@ -464,7 +473,7 @@ def din_forward_plan(segs, width, q_col, att_col, key_table, seq, seq_len, H, at
                      head: Epilogue, batch, device, l2_col0=0, l2_scale=0.0, l2_out=None, att_image=None, keep=()):
     _lib.ensure_device(device)
     args, k = _din_forward_args(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_weights, use_softmax,
-                                layers, head, batch, device, l2_col0, l2_scale, l2_out, att_image)
+                                layers, head, batch, device, l2_col0, l2_scale, l2_out, att_image, private_ws=True)
     return DinPlan(args, (k, tuple(keep)), device)
 
 
