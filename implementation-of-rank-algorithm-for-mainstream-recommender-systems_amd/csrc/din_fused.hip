@@ -19,6 +19,7 @@
 #include <new>
 
 #include "mlp_core.h"
+#include "mlp_stream.h"
 
 namespace rk {
 
@@ -59,6 +60,7 @@ struct DinArgs {
   int nl;
   rk_epilogue head;
   int ld0, ld1;
+  int epi_off;  // streamed phase B (mlp_stream.h): float offset of the epilogue-parameter image
 };
 
 // LDS carve (floats): [Wk | Wqk | Wq] 3 x 64 x (H+4), W2 32 x 68, b1 64, b2 32, w3 32,
@@ -122,7 +124,8 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-template <int H, int NIT>
+// P: the compiled layer plan of phase B (mlp_stream.h), or void for the generic mlp_rows.
+template <int H, int NIT, class P>
 __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   using Ly = DinLds<H>;
   constexpr int NQ = H / 8;
@@ -195,7 +198,12 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       if (i < kImg4) v[r] = reinterpret_cast<const f32x4_t*>(a.att_image)[i];
     }
   }
+  // streamed phase B: its epilogue-parameter image rides with the attention image (phase A is long)
+  using Epi = std::conditional_t<std::is_void_v<P>, NoStage, StreamEpi<std::conditional_t<std::is_void_v<P>, StreamPlanK128, P>>>;
+  Epi epi_img;
+  if constexpr (!std::is_void_v<P>) epi_img.load(a.L, tid);
   auto image_to_lds = [&]() {
+    if constexpr (!std::is_void_v<P>) epi_img.store(sm + a.epi_off, tid);
     if (a.att_image) {
 #pragma unroll
       for (int r = 0; r < kPer; ++r) {
@@ -582,8 +590,12 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
   return;
 #endif
-  mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
-           NIT > 0 ? s_rows : nullptr);
+  if constexpr (std::is_void_v<P>)
+    mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
+             NIT > 0 ? s_rows : nullptr);
+  else
+    mlp_stream_rows<P, false>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid, NoStage(),
+                              nullptr, NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
   // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =
   // MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1 table (measured valid on
@@ -686,7 +698,8 @@ struct DinPlan {
   int64_t blocks;
   size_t shm;
   int H;
-  int nit;  // balanced assignment: seq_len loads per thread (0: contiguous 16-sample blocks)
+  int nit;     // balanced assignment: seq_len loads per thread (0: contiguous 16-sample blocks)
+  int stream;  // phase B on the streamed plan (kStreamK128) or mlp_rows (kStreamNone)
 };
 }  // namespace rk
 
@@ -772,19 +785,36 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   }
   size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
                sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 64 * kMlpRows;
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
   // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
   // by default when the histories span three or more tile counts (T > 64).  Measured (graph
   // replays, batch 4096, lengths uniform in 1..T): T = 128 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us;
   // at T = 50 (two tile counts) the ranking costs ~1% more than it recovers.
-  // RANKOPS_DIN_BALANCE=1 / 0 forces it on / off (tests, A/B timing).
+  // RANKOPS_DIN_BALANCE=1 / 0 forces it on / off (tests, A/B timing).  Only where its LDS (the
+  // batch row of each LDS row and the class masks) still fits: otherwise contiguous samples.
   const char* env = getenv("RANKOPS_DIN_BALANCE");
   a.bal_nb = (T + 31) / 32 + 1;
   const bool want_bal = env && env[0] ? env[0] != '0' : a.bal_nb >= 4;
   if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
-    plan->nit = batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
-    shm += sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
+    const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
+    if (shm + extra <= 160 * 1024) {
+      plan->nit = batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
+      shm += extra;
+    }
   }
-  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
+  // phase B on the streamed plan (hidden units [512, 256, 128] over a row of <= 128): its
+  // epilogue-parameter image goes last, where it still fits
+  plan->stream = stream_plan_for(layers, nlayers, width) == kStreamK128 ? kStreamK128 : kStreamNone;
+  if (plan->stream != kStreamNone) {
+    shm = (shm + 15) / 16 * 16;
+    const size_t bytes = sizeof(float) * stream_plan_epi_floats(kStreamK128);
+    if (shm + bytes <= 160 * 1024) {
+      a.epi_off = (int)(shm / sizeof(float));
+      shm += bytes;
+    } else {
+      plan->stream = kStreamNone;
+    }
+  }
   plan->shm = shm;
   return RK_OK;
 }
@@ -796,16 +826,31 @@ static int din_launch(const DinPlan& p, hipStream_t st) {
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<blocks, kMlpThreads, p.shm, st>>>(p.a);
   };
+  if (p.stream == kStreamK128) {
+    using S = StreamPlanK128;
+    switch (p.H * 16 + p.nit) {
+      case 8 * 16: go(din_forward_kernel<8, 0, S>); break;
+      case 8 * 16 + 4: go(din_forward_kernel<8, 4, S>); break;
+      case 8 * 16 + 8: go(din_forward_kernel<8, 8, S>); break;
+      case 16 * 16: go(din_forward_kernel<16, 0, S>); break;
+      case 16 * 16 + 4: go(din_forward_kernel<16, 4, S>); break;
+      case 16 * 16 + 8: go(din_forward_kernel<16, 8, S>); break;
+      case 32 * 16: go(din_forward_kernel<32, 0, S>); break;
+      case 32 * 16 + 4: go(din_forward_kernel<32, 4, S>); break;
+      default: go(din_forward_kernel<32, 8, S>); break;
+    }
+    return check_launch("rk_din_forward");
+  }
   switch (p.H * 16 + p.nit) {
-    case 8 * 16: go(din_forward_kernel<8, 0>); break;
-    case 8 * 16 + 4: go(din_forward_kernel<8, 4>); break;
-    case 8 * 16 + 8: go(din_forward_kernel<8, 8>); break;
-    case 16 * 16: go(din_forward_kernel<16, 0>); break;
-    case 16 * 16 + 4: go(din_forward_kernel<16, 4>); break;
-    case 16 * 16 + 8: go(din_forward_kernel<16, 8>); break;
-    case 32 * 16: go(din_forward_kernel<32, 0>); break;
-    case 32 * 16 + 4: go(din_forward_kernel<32, 4>); break;
-    default: go(din_forward_kernel<32, 8>); break;
+    case 8 * 16: go(din_forward_kernel<8, 0, void>); break;
+    case 8 * 16 + 4: go(din_forward_kernel<8, 4, void>); break;
+    case 8 * 16 + 8: go(din_forward_kernel<8, 8, void>); break;
+    case 16 * 16: go(din_forward_kernel<16, 0, void>); break;
+    case 16 * 16 + 4: go(din_forward_kernel<16, 4, void>); break;
+    case 16 * 16 + 8: go(din_forward_kernel<16, 8, void>); break;
+    case 32 * 16: go(din_forward_kernel<32, 0, void>); break;
+    case 32 * 16 + 4: go(din_forward_kernel<32, 4, void>); break;
+    default: go(din_forward_kernel<32, 8, void>); break;
   }
   return check_launch("rk_din_forward");
 }

@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include "mlp_core.h"
+#include "mlp_stream.h"
 
 namespace rk {
 
@@ -23,6 +24,7 @@ struct MlpArgs {
   int64_t ldy;
   int ld0, ld1;  // LDS row strides of the two activation buffers (floats)
   int off1;      // float offset of buffer 1
+  int off_epi;   // streamed plans: float offset of the epilogue-parameter image
 };
 
 // RT row tiles of 16 rows per workgroup: every weight element streamed from L2 serves 16*RT rows
@@ -66,6 +68,35 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
   MLP_FLUSH(tid);
 }
 
+// The same tail on a compiled layer plan (mlp_stream.h): one weight stream across the layers.
+template <class P>
+__global__ __launch_bounds__(kMlpThreads) void mlp_stream_kernel(MlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.M - m0);
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.off1;
+  const int K0p = P::KC0 * 16;
+  auto stage = [&]() {
+    if (a.x_vec) {
+      const int q = K0p / 4;
+      for (int i = tid; i < kMlpRows * q; i += kMlpThreads) {
+        const int r = i / q, c = (i % q) * 4;
+        f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+        if (r < rows && c < a.K0) v = *reinterpret_cast<const f32x4_t*>(a.x + (m0 + r) * a.ldx + c);
+        *reinterpret_cast<f32x4_t*>(buf0 + r * a.ld0 + c) = v;
+      }
+    } else {
+      for (int i = tid; i < kMlpRows * K0p; i += kMlpThreads) {
+        const int r = i / K0p, c = i % K0p;
+        buf0[r * a.ld0 + c] = (r < rows && c < a.K0) ? a.x[(m0 + r) * a.ldx + c] : 0.f;
+      }
+    }
+  };
+  mlp_stream_rows<P>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.off_epi, m0, rows, a.head, tid, finish_only(stage));
+}
+
 // Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): per 16-row tile, wave w
 // gathers row m0 + w (dense + category embeddings, dcn.py:163-169) straight into the MLP's LDS
 // input buffer while layer 0's weights are already in flight, runs the cross stack on the row in
@@ -102,7 +133,7 @@ struct DcnArgs {
 };
 
 // NJ = column groups of 64 per lane (1: width <= 64, the DCN wechat row of 50; 4: width <= 256)
-template <int NJ>
+template <int NJ, class P>
 __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -235,8 +266,12 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
     p = wave_sum(p);
     if (lane == 0) part[wave] = p;
   };
-  mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
-           two_phase(stage_issue, stage_finish), part);
+  if constexpr (std::is_void_v<P>)
+    mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
+             two_phase(stage_issue, stage_finish), part);
+  else
+    mlp_stream_rows<P>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
+                       two_phase(stage_issue, stage_finish), part);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
   MLP_FLUSH(tid);
@@ -257,6 +292,40 @@ __global__ void mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int n,
   out[i] = (r < n && col < k) ? w[(int64_t)r * ldw + col] : 0.f;
 }
 
+
+int stream_plan_for(const rk_mlp_layer* layers, int nlayers, int K0) {
+  if (const char* e = getenv("RANKOPS_MLP_STREAM"))
+    if (e[0] == '0') return kStreamNone;
+  if (nlayers < 1 || nlayers > 3 || pad64(K0) > 1024) return kStreamNone;
+  int nt[3] = {0, 0, 0};
+  for (int l = 0; l < nlayers; ++l) {
+    if (layers[l].residual || layers[l].store) return kStreamNone;
+    nt[l] = pad64(layers[l].n) / 16;
+  }
+  const int kc0 = pad64(K0) / 16;
+  if (nlayers == 3 && nt[0] == 32 && nt[1] == 16 && nt[2] == 8) {
+    switch (kc0) {
+      case 4: return kStreamK64;
+      case 8: return kStreamK128;
+      case 12: return kStreamK192;
+      case 16: return kStreamK256;
+      default: return kStreamNone;
+    }
+  }
+  if (nlayers == 2 && kc0 == 32 && nt[0] == 16 && nt[1] == 8) return kStreamTail512;
+  return kStreamNone;
+}
+
+int stream_plan_epi_floats(int id) {
+  switch (id) {
+    case kStreamK64: return StreamPlanK64::epi_floats();
+    case kStreamK128: return StreamPlanK128::epi_floats();
+    case kStreamK192: return StreamPlanK192::epi_floats();
+    case kStreamK256: return StreamPlanK256::epi_floats();
+    case kStreamTail512: return StreamPlanTail512::epi_floats();
+    default: return 0;
+  }
+}
 
 int mlp_validate(const rk_mlp_layer* layers, int nlayers, int K0, const rk_epilogue& head, int* need0, int* need1,
                  const char* what) {
@@ -349,14 +418,30 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward: M too large");
   bool store = false;  // hidden activations written out (training); eval compiles the path out
   for (int l = 0; l < nlayers; ++l) store = store || layers[l].store != nullptr;
-  auto go = [&](auto kern) {
+  auto go = [&](auto kern, size_t bytes) {
     raise_lds_limit((const void*)kern, 160 * 1024);
-    kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+    kern<<<(unsigned)blocks, kMlpThreads, bytes, (hipStream_t)stream>>>(a);
   };
+  // a compiled layer plan: the streamed tail (mlp_stream.h), its epilogue image after the buffers
+  const int plan = rt == 1 ? stream_plan_for(layers, nlayers, K0) : kStreamNone;
+  if (plan != kStreamNone) {
+    a.off_epi = (int)(shm / sizeof(float));
+    const size_t bytes = shm + sizeof(float) * stream_plan_epi_floats(plan);
+    if (bytes <= 160 * 1024) {
+      switch (plan) {
+        case kStreamK64: go(mlp_stream_kernel<StreamPlanK64>, bytes); break;
+        case kStreamK128: go(mlp_stream_kernel<StreamPlanK128>, bytes); break;
+        case kStreamK192: go(mlp_stream_kernel<StreamPlanK192>, bytes); break;
+        case kStreamK256: go(mlp_stream_kernel<StreamPlanK256>, bytes); break;
+        default: go(mlp_stream_kernel<StreamPlanTail512>, bytes); break;
+      }
+      return check_launch("rk_mlp_forward");
+    }
+  }
   if (rt == 2)
-    store ? go(mlp_kernel<2, true>) : go(mlp_kernel<2, false>);
+    store ? go(mlp_kernel<2, true>, shm) : go(mlp_kernel<2, false>, shm);
   else
-    store ? go(mlp_kernel<1, true>) : go(mlp_kernel<1, false>);
+    store ? go(mlp_kernel<1, true>, shm) : go(mlp_kernel<1, false>, shm);
   return check_launch("rk_mlp_forward");
 }
 
@@ -430,15 +515,29 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   a.num_layers = num_layers;
   a.cross_head_w = cross_head_w;
   a.flags = flags;
-  const size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
+  size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
+  // the wechat row (width <= 64) on a compiled layer plan: the streamed tail, its epilogue image
+  // after the cross partials
+  int plan = width <= 64 ? stream_plan_for(layers, nlayers, width) : kStreamNone;
+  if (plan != kStreamNone && plan != kStreamK64) plan = kStreamNone;
+  if (plan != kStreamNone) {
+    a.m.off_epi = (int)(shm / sizeof(float));
+    if (shm + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024)
+      shm += sizeof(float) * stream_plan_epi_floats(plan);
+    else
+      plan = kStreamNone;
+  }
   auto go = [&](auto kern) {
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   };
-  width <= 64 ? go(dcn_fused_kernel<1>) : go(dcn_fused_kernel<kDcnPerLane>);
+  if (plan == kStreamK64)
+    go(dcn_fused_kernel<1, StreamPlanK64>);
+  else
+    width <= 64 ? go(dcn_fused_kernel<1, void>) : go(dcn_fused_kernel<kDcnPerLane, void>);
   return check_launch("rk_dcn_forward");
 }

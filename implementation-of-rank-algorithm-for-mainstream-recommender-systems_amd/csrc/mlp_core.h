@@ -109,6 +109,13 @@ __device__ __forceinline__ ColEpi col_epi(const rk_mlp_layer& L, int n) {
   return e;
 }
 
+// Dice on one element, a*(1-p)*z + p*z with p = sigmoid(z*s + b) (din.py:26-36, BN folded into s, b);
+// the contraction is spelled out so every epilogue that uses it rounds the same way.
+__device__ __forceinline__ float dice_apply(float z, float s, float b, float a) {
+  const float p = sigmoid_fast(__builtin_fmaf(z, s, b));
+  return __builtin_fmaf(p, z, (a * (1.0f - p)) * z);
+}
+
 // The element-wise epilogue in the reference's order (bias, residual, pre-BN, activation,
 // post-BN); `dice` and `has_res` are wave-uniform.  Absent affine parts are the identity (z * 1 + 0
 // is exact), and the piecewise-linear activations one negative-side slope `neg` (ReLU 0,
@@ -121,8 +128,7 @@ __device__ __forceinline__ float col_apply(const rk_mlp_layer& L, const ColEpi& 
   if (has_res) z = res + z;
   z = z * (L.pre_scale ? e.pre_s : 1.f) + (L.pre_scale ? e.pre_b : 0.f);
   if (dice) {
-    const float p = sigmoid_fast(z * e.act_s + e.act_b);
-    z = e.alpha * (1.0f - p) * z + p * z;
+    z = dice_apply(z, e.act_s, e.act_b, e.alpha);
   } else {
     const float neg = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? e.alpha : 1.f;
     z = z > 0.f ? z : z * neg;

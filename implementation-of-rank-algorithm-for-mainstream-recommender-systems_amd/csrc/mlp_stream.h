@@ -1,0 +1,349 @@
+// Streamed fused-MLP tail for fixed layer plans (round 4): mlp_rows (mlp_core.h) restructured so
+// that the weight stream of a wave never stops at a layer boundary.
+//
+// Same work split as mlp_rows — 16 rows per workgroup of 16 waves, wave w owns the 16-column
+// tiles w and w + 16 of every layer, v_mfma_f32_16x16x4_f32 over fragment-major packed weights
+// (rk_mlp_pack_weight), activations ping-ponging between two LDS buffers — with three changes:
+//  * The layer plan (K0 chunks, column tiles per layer) is a template parameter and the whole
+//    layer sequence is unrolled.  Each wave's weight loads of ALL layers form one sequence, and
+//    the R-slot register ring runs over it continuously: consuming a slot of layer l's last chunks
+//    refills it with layer l+1's first chunks.  mlp_rows stopped refilling in a layer's last ring
+//    cycle and issued the next layer's whole ring (128 KiB per CU) after the epilogue, behind the
+//    TA: 1.6-4.4k cycles per boundary (profiles/r03/phases_epi_pf1.log) on the critical path.
+//    With one definition of every ring register per point of the unrolled sequence, the compiler
+//    sees the exact vmcnt of every use (the r03 attempt to spread the ring inside the generic loop
+//    spilled because the ring reached the next layer from two definitions).
+//  * The per-column epilogue parameters of every layer are resolved once per workgroup into an
+//    LDS image ([Np][8] floats per layer) in the prologue, so the vector memory queue holds only
+//    weight loads (ring register k is always the k-th outstanding load) and no parameter VGPRs
+//    are live across a layer.
+//  * Waves that own no tile of a layer (the 128-wide last layer: waves 8..15) are a separate
+//    unrolled class; their stream simply ends earlier.
+// Accumulation order, epilogue arithmetic (col_apply) and the head are those of mlp_rows, so the
+// outputs are bit-identical to it (tests/test_gpu_mlp_stream.py).
+//
+// Eval only (no activation stores), no residual layers: everything else stays on mlp_rows.
+#pragma once
+
+#include <type_traits>
+#include <utility>
+
+#include "mlp_core.h"
+
+namespace rk {
+
+#ifndef RK_STREAM_RING
+#define RK_STREAM_RING 8
+#endif
+
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// KC0: 16-deep K chunks of the input (pad64(K0) / 16); NT: 16-column tiles of each layer
+// (pad64(n_l) / 16, at most 32).  Layer l > 0 contracts over the previous layer's tiles.
+template <int KC0_, int... NT_>
+struct StreamPlan {
+  static constexpr int NL = sizeof...(NT_);
+  static constexpr int KC0 = KC0_;
+  static constexpr int nt(int l) {
+    constexpr int v[] = {NT_...};
+    return v[l];
+  }
+  static constexpr int kc(int l) { return l == 0 ? KC0 : nt(l - 1); }
+  // column tiles of layer l owned by wave w (tiles w, w + 16)
+  static constexpr int tpw(int l, int w) { return w < nt(l) ? (nt(l) - 1 - w) / 16 + 1 : 0; }
+  // first load of layer l in wave w's stream, and the stream's length
+  static constexpr int base(int l, int w) {
+    int b = 0;
+    for (int i = 0; i < l; ++i) b += tpw(i, w) * kc(i);
+    return b;
+  }
+  static constexpr int layer_of(int g, int w) {
+    int l = 0;
+    while (l + 1 < NL && base(l + 1, w) <= g) ++l;
+    return l;
+  }
+  static constexpr bool same_class(int a, int b) {
+    for (int l = 0; l < NL; ++l)
+      if (tpw(l, a) != tpw(l, b)) return false;
+    return true;
+  }
+  // the lowest wave with the same tile counts in every layer (waves are dispatched by class)
+  static constexpr int rep(int w) {
+    int r = 0;
+    while (!same_class(r, w)) ++r;
+    return r;
+  }
+  // LDS epilogue-parameter image: [Np_l][8] floats per layer
+  static constexpr int epi_off(int l) {
+    int o = 0;
+    for (int i = 0; i < l; ++i) o += 16 * nt(i) * 8;
+    return o;
+  }
+  static constexpr int epi_floats() { return epi_off(NL); }
+  static constexpr int epi_cols() { return epi_off(NL) / 8; }
+  static_assert(NL >= 1 && NL <= RK_MLP_MAX_LAYERS, "layer count");
+  static_assert(epi_off(NL) / 8 <= 2 * kMlpThreads, "epilogue image: two columns per thread at most");
+};
+
+// The epilogue-parameter image, in two halves: load() issues the (unconditional) loads of at most
+// two columns per thread into registers, store() writes them to LDS.  Column i of the image is
+// layer l's column i - cols(<l); values are col_epi's (absent vectors read as any valid float and
+// are resolved by col_apply against the layer's flags, exactly as mlp_rows does).
+template <class P>
+struct StreamEpi {
+  ColEpi e[2];
+  static constexpr int kCols = (P::epi_cols() + kMlpThreads - 1) / kMlpThreads;  // per thread, 1 or 2
+  __device__ __forceinline__ void load(const rk_mlp_layer* __restrict__ layers, int tid) {
+#pragma unroll
+    for (int k = 0; k < kCols; ++k) {
+      const int i = tid + kMlpThreads * k;
+      // the thread's layer by selects over the (scalar) layer table: loads under a per-layer
+      // branch would close their joins with vmcnt(0)
+      int l = 0;
+#pragma unroll
+      for (int q = 1; q < P::NL; ++q) l = i >= P::epi_off(q) / 8 ? q : l;
+      rk_mlp_layer L = layers[0];
+#pragma unroll
+      for (int q = 1; q < P::NL; ++q)
+        if (l == q) L = layers[q];
+      const int n = i - P::epi_off(l) / 8;
+      e[k] = col_epi(L, n < L.n ? n : 0);
+      // resolved against the layer's flags here, once: absent affine parts become the identity
+      // (col_apply adds 0 / scales by 1 for them too, so the arithmetic is the same), and the
+      // non-Dice activations one negative-side slope in the alpha slot
+      ColEpi& r = e[k];
+      r.bias = L.bias ? r.bias : 0.f;
+      r.pre_s = L.pre_scale ? r.pre_s : 1.f;
+      r.pre_b = L.pre_scale ? r.pre_b : 0.f;
+      r.post_s = L.post_scale ? r.post_s : 1.f;
+      r.post_b = L.post_scale ? r.post_b : 0.f;
+      if (L.act != RK_ACT_DICE)
+        r.alpha = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? r.alpha : 1.f;
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ img, int tid) const {
+#pragma unroll
+    for (int k = 0; k < kCols; ++k) {
+      const int i = tid + kMlpThreads * k;
+      if (i < P::epi_cols()) {
+        f32x4_t* d = reinterpret_cast<f32x4_t*>(img + 8 * i);
+        d[0] = (f32x4_t){e[k].bias, e[k].pre_s, e[k].pre_b, e[k].act_s};
+        d[1] = (f32x4_t){e[k].act_b, e[k].alpha, e[k].post_s, e[k].post_b};
+      }
+    }
+  }
+};
+
+// One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
+// (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
+// operator() after it, before that barrier).  EPI_HERE: the caller has not stored the image — it is
+// loaded here (after stage.issue(), ahead of the ring) and stored after the stage.
+template <class P, int W, bool EPI_HERE, class Stage>
+__device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
+                                                 float* buf1, int ld1, float* epi, int64_t m0, int rows,
+                                                 const rk_epilogue& h, int tid, int wave, Stage& stage,
+                                                 const float* lds_partial, const int64_t* row_ids) {
+  constexpr int R = RK_STREAM_RING;
+  constexpr int NL = P::NL;
+  constexpr int TOT = P::base(NL, W);
+  const int lane = tid & 63, li = lane & 15, kq = 4 * (lane >> 4);
+  f32x4_t ring[R];
+
+  // load g of the stream: layer l, chunk c of tile j (consumption order: chunk-major)
+  auto issue = [&](auto G) {
+    constexpr int g = G;
+    if constexpr (g < TOT) {
+      constexpr int l = P::layer_of(g, W);
+      constexpr int T = P::tpw(l, W);
+      constexpr int i = g - P::base(l, W), c = i / T, j = i % T;
+      const rk_mlp_layer& L = layers[l];
+      const float* p = L.w + ((int64_t)(wave + kMlpWaves * j) * (L.ldw / 16) + c) * kFragStep;
+      ring[g % R] = *reinterpret_cast<const f32x4_t*>(p + 4 * lane);
+    }
+  };
+
+  const int Kh = layers[NL - 1].n;
+  const bool hpre = h.head_w != nullptr && Kh <= 128;
+  float hw[2] = {0.f, 0.f};
+  float hp = 0.f;
+  auto head_prefetch = [&]() {
+    if (!hpre) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (lane + 64 * c < Kh) hw[c] = h.head_w[lane + 64 * c];
+    if (wave < rows && h.head_partial && !lds_partial) hp = h.head_partial[row_ids ? row_ids[wave] : m0 + wave];
+  };
+
+  StreamEpi<P> ep_stage;
+  stage.issue();
+  if constexpr (EPI_HERE) ep_stage.load(layers, tid);
+  __builtin_amdgcn_sched_barrier(0);  // the stage's and the parameters' loads stay ahead of the ring
+  static_for<0, R>([&](auto G) {
+    issue(G);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  if constexpr (NL == 1) head_prefetch();
+  stage();
+  if constexpr (EPI_HERE) ep_stage.store(epi, tid);
+  mlp_lds_barrier();
+
+  static_for<0, NL>([&](auto LI) {
+    constexpr int l = LI;
+    constexpr int T = P::tpw(l, W), KC = P::kc(l), B0 = P::base(l, W);
+    const rk_mlp_layer& L = layers[l];
+    const float* in = (l & 1) ? buf1 : buf0;
+    float* out = (l & 1) ? buf0 : buf1;
+    const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
+    if constexpr (T == 0) {
+#if RK_MLP_SYNC
+      // no tile in this layer: take part in the active waves' lockstep barriers
+      static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
+#endif
+    } else {
+      f32x4_t acc[T];
+#pragma unroll
+      for (int j = 0; j < T; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const float* arow = in + li * ldin + kq;
+      // A float4s one chunk ahead in two register sets (see mlp_layer)
+      f32x4_t ab[2];
+      ab[0] = *reinterpret_cast<const f32x4_t*>(arow);
+      static_for<0, KC>([&](auto CI) {
+        constexpr int c = CI;
+        if constexpr (c + 1 < KC) ab[(c + 1) & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * (c + 1));
+        __builtin_amdgcn_sched_barrier(0);  // the read goes out before this chunk's MFMAs
+        static_for<0, 4>([&](auto EI) {
+          constexpr int e = EI;
+          static_for<0, T>([&](auto JI) {
+            constexpr int j = JI;
+            acc[j] = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc[j]);
+          });
+        });
+        // refill the slots just read with the stream's next loads (past this layer: the next
+        // layer's first chunks)
+        static_for<0, T>([&](auto JI) {
+          constexpr int j = JI;
+          issue(std::integral_constant<int, B0 + c * T + j + R>{});
+        });
+        __builtin_amdgcn_sched_barrier(0);
+#if RK_MLP_SYNC
+        if constexpr ((c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
+#endif
+      });
+#if RK_MLP_EPI_PRIO
+      __builtin_amdgcn_s_setprio(2);
+#endif
+      const float* img = epi + P::epi_off(l);
+      auto epilogue = [&](auto DICE) {
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+          const int n = 16 * (wave + kMlpWaves * j) + li;
+          const bool real = n < L.n;
+          const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(img + 8 * n);
+          const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(img + 8 * n + 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = (lane >> 4) * 4 + r;
+            // col_apply's arithmetic on the resolved parameters (bias, pre affine, activation,
+            // post affine)
+            float z = acc[j][r] + p0[0];
+            z = z * p0[1] + p0[2];
+            if constexpr (DICE) {
+              z = dice_apply(z, p0[3], p1[0], p1[1]);
+            } else {
+              z = z > 0.f ? z : z * p1[1];
+            }
+            z = z * p1[2] + p1[3];
+            out[row * ldout + n] = real ? z : 0.f;  // padded columns: the next layer's zero K pad
+          }
+        }
+      };
+      if (L.act == RK_ACT_DICE)
+        epilogue(std::true_type{});
+      else
+        epilogue(std::false_type{});
+    }
+    if constexpr (l + 2 == NL) head_prefetch();
+    mlp_lds_barrier();
+#if RK_MLP_EPI_PRIO
+    if constexpr (T > 0) __builtin_amdgcn_s_setprio(0);
+#endif
+  });
+
+  // head: one wave per row, as mlp_rows
+  const float* fin = (NL & 1) ? buf1 : buf0;
+  const int ldf = (NL & 1) ? ld1 : ld0;
+  const int K = Kh;
+  if (h.head_w) {
+    for (int r = wave; r < rows; r += kMlpWaves) {
+      const bool pre = hpre && r == wave;
+      float p = 0.f;
+      if (pre) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (lane + 64 * c < K) p = fmaf(fin[r * ldf + lane + 64 * c], hw[c], p);
+      } else {
+        for (int n = lane; n < K; n += 64) p = fmaf(fin[r * ldf + n], h.head_w[n], p);
+      }
+      p = wave_sum(p);
+      if (lane == 0) {
+        const int64_t m = row_ids ? row_ids[r] : m0 + r;
+        float logit = p + h.head_b[0];
+        if (lds_partial)
+          logit = lds_partial[r] + logit;
+        else if (h.head_partial)
+          logit = (pre ? hp : h.head_partial[m]) + logit;
+        if (h.fm1) {
+          if (h.head_aux) h.head_aux[m] = logit;
+          logit = h.fm1[m] * h.final_w[0] + h.fm2[m] * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];
+        }
+        if (h.head_logit) h.head_logit[m] = logit;
+        if (h.head_prob) h.head_prob[m] = 1.0f / (1.0f + expf(-logit));
+      }
+    }
+  }
+}
+
+// Entry point: dispatches the calling wave to its class's unrolled body.  Must be called by all
+// kMlpThreads threads.  `epi`: P::epi_floats() floats of LDS (16-B aligned).
+template <class P, bool EPI_HERE = true, class Stage = NoStage>
+__device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
+                                                float* buf1, int ld1, float* epi, int64_t m0, int rows,
+                                                const rk_epilogue& h, int tid, Stage stage = Stage(),
+                                                const float* lds_partial = nullptr,
+                                                const int64_t* row_ids = nullptr) {
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  static_for<0, kMlpWaves>([&](auto WI) {
+    constexpr int w = WI;
+    if constexpr (P::rep(w) == w) {
+      bool mine = true;  // is the calling wave in class w?
+#pragma unroll
+      for (int l = 0; l < P::NL; ++l) mine = mine && P::tpw(l, wave) == P::tpw(l, w);
+      if (mine)
+        mlp_stream_class<P, w, EPI_HERE>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
+                                         lds_partial, row_ids);
+    }
+  });
+}
+
+// Plans compiled into the library (hidden units [512, 256, 128], the reference's default for
+// DCN / DIN / BST / DeepFM): by the input's K chunks.  DeepFM's tail after its tiled first layer
+// is [256, 128] over K0 = 512.
+using StreamPlanK64 = StreamPlan<4, 32, 16, 8>;    // DCN (width 50)
+using StreamPlanK128 = StreamPlan<8, 32, 16, 8>;   // DIN (16 + 34 + 2H <= 128)
+using StreamPlanK192 = StreamPlan<12, 32, 16, 8>;  // BST DNN (16 + 34 + d = 178 at d 128)
+using StreamPlanK256 = StreamPlan<16, 32, 16, 8>;
+using StreamPlanTail512 = StreamPlan<32, 16, 8>;   // DeepFM: 512 -> 256 -> 128
+
+// Host: the compiled plan matching a layer stack (0: none — use mlp_rows).  Eval only: no
+// activation stores, no residual layers.  RANKOPS_MLP_STREAM=0 disables the streamed path.
+enum StreamPlanId { kStreamNone = 0, kStreamK64, kStreamK128, kStreamK192, kStreamK256, kStreamTail512 };
+int stream_plan_for(const rk_mlp_layer* layers, int nlayers, int K0);
+int stream_plan_epi_floats(int id);
+
+}  // namespace rk

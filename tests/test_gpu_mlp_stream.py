@@ -1,0 +1,243 @@
+"""GPU: the streamed fused-MLP tail (csrc/mlp_stream.h, round 4) against the generic mlp_rows path
+(RANKOPS_MLP_STREAM=0) — bit for bit, since the accumulation order and the epilogue arithmetic are
+the same — and against a float64 restatement of the layer stack.
+
+Covered: every compiled plan (K0 chunks 4/8/12/16 over [512, 256, 128], and [256, 128] over K0 512),
+every activation (none, ReLU, LeakyReLU, PReLU with one or per-channel alpha, Dice), with and without
+bias and pre-/post-BatchNorm affines, ragged batches (1, 15, 17, 1000), and the model forwards that
+run it: DCN (dcn_fused_kernel), DIN (phase B of din_forward_kernel, contiguous and balanced
+assignment, softmax and PReLU variants), DeepFM (tail after the tiled first layer), BST (DNN tail).
+Reference rows: dcn.py:144-152,175-180; din.py:272-285,312-316; deepfm.py:100-112,143-151;
+bst.py:203-214,245-247."""
+import os
+
+import pytest
+import torch
+
+import helpers as H
+from rankops import ops
+from rankops._lib import Epilogue  # noqa: F401
+
+ATOL = RTOL = 1e-4
+
+
+class _stream_env:
+    """Sets RANKOPS_MLP_STREAM (read by the C library at every launch / plan preparation)."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def __enter__(self):
+        self.old = os.environ.get("RANKOPS_MLP_STREAM")
+        os.environ["RANKOPS_MLP_STREAM"] = "1" if self.on else "0"
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("RANKOPS_MLP_STREAM", None)
+        else:
+            os.environ["RANKOPS_MLP_STREAM"] = self.old
+
+
+def _layers(K0, widths, act, bias, pre, post, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    spec, mls, keep = [], [], []
+    k = K0
+    for n in widths:
+        w = (torch.rand(n, k, generator=g) - 0.5) * (2.0 / k ** 0.5)
+        d = {"w": w}
+        if bias:
+            d["bias"] = torch.rand(n, generator=g) - 0.5
+        if pre:
+            d["pre_scale"], d["pre_shift"] = torch.rand(n, generator=g) + 0.5, torch.rand(n, generator=g) - 0.5
+        if post:
+            d["post_scale"], d["post_shift"] = torch.rand(n, generator=g) + 0.5, torch.rand(n, generator=g) - 0.5
+        if act == "dice":
+            d["act_scale"], d["act_shift"] = torch.rand(n, generator=g) + 0.5, torch.rand(n, generator=g) - 0.5
+            d["act_alpha"] = torch.rand(n, generator=g) - 0.5
+        elif act == "prelu1":
+            d["act_alpha"] = torch.rand(1, generator=g) * 0.5
+        elif act == "prelu":
+            d["act_alpha"] = torch.rand(n, generator=g) * 0.5
+        d = {kk: v.to(dev) for kk, v in d.items()}
+        kw = {kk: v for kk, v in d.items() if kk != "w"}
+        a = {"prelu1": "prelu"}.get(act, act)
+        if act.startswith("prelu"):
+            kw["act_alpha_len"] = d["act_alpha"].numel()
+        packed = ops.pack_mlp_weight(d["w"])
+        mls.append(ops.make_mlp_layer(d["w"], packed, act=a, slope=0.125 if act == "leaky" else 0.0, **kw))
+        keep += [packed, d]
+        spec.append((d, act))
+        k = n
+    return spec, mls, keep
+
+
+def _ref64(x, spec, hw, hb):
+    h = x.double()
+    for d, act in spec:
+        z = h @ d["w"].double().t()
+        if "bias" in d:
+            z = z + d["bias"].double()
+        if "pre_scale" in d:
+            z = z * d["pre_scale"].double() + d["pre_shift"].double()
+        if act == "relu":
+            z = torch.relu(z)
+        elif act == "leaky":
+            z = torch.where(z > 0, z, z * 0.125)
+        elif act.startswith("prelu"):
+            z = torch.where(z > 0, z, z * d["act_alpha"].double())
+        elif act == "dice":
+            p = torch.sigmoid(z * d["act_scale"].double() + d["act_shift"].double())
+            z = d["act_alpha"].double() * (1 - p) * z + p * z
+        if "post_scale" in d:
+            z = z * d["post_scale"].double() + d["post_shift"].double()
+        h = z
+    return h @ hw.double() + hb.double()
+
+
+def _run_mlp(x, mls, hw, hb, on):
+    logit = torch.empty(x.shape[0], device=x.device)
+    prob = torch.empty(x.shape[0], device=x.device)
+    ep = ops.make_epilogue(head_w=hw, head_b=hb, head_logit=logit, head_prob=prob)
+    with _stream_env(on):
+        ops.mlp_forward(x, mls, ep)
+    torch.cuda.synchronize()
+    return logit, prob
+
+
+PLANS = [(50, (512, 256, 128)), (114, (512, 256, 128)), (178, (512, 256, 128)), (256, (512, 256, 128)),
+         (512, (256, 128))]
+ACTS = [("relu", True, True, False), ("none", True, False, False), ("leaky", False, False, True),
+        ("prelu1", True, False, True), ("prelu", True, True, True), ("dice", True, False, True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K0,widths", PLANS)
+@pytest.mark.parametrize("act,bias,pre,post", ACTS)
+def test_stream_mlp_equals_generic_and_float64(K0, widths, act, bias, pre, post):
+    dev = torch.device("cuda")
+    spec, mls, keep = _layers(K0, widths, act, bias, pre, post, seed=K0 + len(act), dev=dev)
+    g = torch.Generator().manual_seed(7)
+    hw = ((torch.rand(widths[-1], generator=g) - 0.5) * 0.2).to(dev)
+    hb = torch.tensor([0.05], device=dev)
+    for B in (1, 17, 1000):
+        x = (torch.rand(B, K0, generator=g) * 2 - 1).to(dev)
+        ls, ps = _run_mlp(x, mls, hw, hb, True)
+        lg, pg = _run_mlp(x, mls, hw, hb, False)
+        assert torch.equal(ls, lg), (B, (ls - lg).abs().max().item())
+        assert torch.equal(ps, pg)
+        ref = _ref64(x.cpu(), [({k: v.cpu() for k, v in d.items()}, a) for d, a in spec], hw.cpu(), hb.cpu())
+        torch.testing.assert_close(ls.cpu().double(), ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+def test_stream_mlp_unaligned_input_stride():
+    """x with a row stride that is not a multiple of 4 (the scalar staging path)."""
+    dev = torch.device("cuda")
+    spec, mls, keep = _layers(50, (512, 256, 128), "relu", True, True, False, seed=3, dev=dev)
+    hw = torch.rand(128, device=dev) - 0.5
+    hb = torch.tensor([0.1], device=dev)
+    base = torch.rand(333, 53, device=dev)
+    x = base[:, 1:51]
+    ls, _ = _run_mlp(x, mls, hw, hb, True)
+    lg, _ = _run_mlp(x, mls, hw, hb, False)
+    assert torch.equal(ls, lg)
+
+
+def _model_pair(name, cfg, B, seed=1000):
+    """The model's eval outputs with the streamed plan and with mlp_rows (fresh modules of the same
+    seed, so no launch cache or prepared plan crosses the two settings), plus the oracle."""
+    inp = H.make_inputs(name, cfg, B, seed=seed)
+    outs = []
+    for on in (True, False):
+        with _stream_env(on):
+            model = H.build(name, cfg).cuda().eval()
+            with torch.no_grad():
+                o = H.as_tuple(H.call_model(model, name, H.to_device(inp, "cuda")))
+            torch.cuda.synchronize()
+            outs.append(tuple(x.clone() if isinstance(x, torch.Tensor) else x for x in o))
+    return outs, inp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 15, 17, 4096])
+def test_dcn_stream_equals_generic(B):
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    (s, g), _ = _model_pair("dcn", cfg, B)
+    for a, b in zip(s, g):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_dcn_stream_matches_oracle():
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    model = H.build("dcn", cfg)
+    p = H.cpu_params(model)
+    inp = H.make_inputs("dcn", cfg, 300)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        ref = H.as_tuple(H.call_oracle("dcn", cfg, p, inp))
+    with _stream_env(True):
+        model = model.cuda().eval()
+        torch.manual_seed(0)
+        with torch.no_grad():
+            out = H.as_tuple(H.call_model(model, "dcn", H.to_device(inp, "cuda")))
+    for o, r in zip(out, ref):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.cpu(), r, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["plain", "softmax", "prelu", "balanced", "T130"])
+def test_din_stream_equals_generic(variant, monkeypatch):
+    cfg = {"T": 50, "dim": 32, "interaction_weights": "frozen", "vocab": H.WECHAT_VOCAB}
+    if variant == "softmax":
+        cfg["softmax"] = True
+    if variant == "prelu":
+        cfg["activation"] = "prelu"
+    if variant == "balanced":
+        monkeypatch.setenv("RANKOPS_DIN_BALANCE", "1")
+    if variant == "T130":
+        cfg["T"] = 130
+    (s, g), inp = _model_pair("din", cfg, 1000)
+    for a, b in zip(s, g):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b), variant
+
+
+@pytest.mark.gpu
+def test_din_stream_matches_oracle():
+    cfg = {"T": 50, "dim": 32, "interaction_weights": "frozen"}
+    model = H.build("din", cfg)
+    H.randomize_eval_stats(model)
+    p = H.cpu_params(model)
+    inp = H.make_inputs("din", cfg, 257)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
+    with _stream_env(True):
+        model = model.cuda().eval()
+        torch.manual_seed(0)
+        with torch.no_grad():
+            out = H.as_tuple(H.call_model(model, "din", H.to_device(inp, "cuda")))
+    for o, r in zip(out, ref):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.cpu(), r, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+def test_deepfm_tail_stream_equals_generic():
+    cfg = {"dim": 32, "fields": {f"field_{i:02d}": 5000 for i in range(30)}}
+    (s, g), _ = _model_pair("deepfm", cfg, 4096)
+    for a, b in zip(s, g):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_bst_tail_stream_equals_generic():
+    cfg = {"T": 64, "dim": 128, "heads": 4, "max_len": 64, "vocab": H.WECHAT_VOCAB}
+    (s, g), _ = _model_pair("bst", cfg, 300)
+    for a, b in zip(s, g):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
