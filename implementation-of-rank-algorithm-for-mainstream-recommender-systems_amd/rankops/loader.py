@@ -103,17 +103,20 @@ class Vocabulary:
         `device` and looked up there.  Returns an int64 device tensor."""
         return _device_lookup(self, _arrow_chunks(column), torch.device(device), None, ",")
 
-    def lookup_sequences_device(self, column, T: int = None, sep=",", device="cuda"):
+    def lookup_sequences_device(self, column, T: int = None, sep=",", device="cuda", null_history="raise"):
         """lookup_sequences() on the GPU (rk_bucketize_sequences_device)."""
         chunks = _arrow_chunks(column)
+        _check_null_history(chunks, null_history, "lookup_sequences_device")
         if T is None:
             T = _max_items(chunks, sep, 0)
         return _device_lookup(self, chunks, torch.device(device), T, sep)
 
-    def lookup_sequences(self, column, T: int = None, sep=",", threads: int = 0):
+    def lookup_sequences(self, column, T: int = None, sep=",", threads: int = 0, null_history="raise"):
         """(idx [n, T] int64 zero padded, lengths [n]) of sep-separated histories; T defaults to
-        the longest row (din_collate_fn)."""
+        the longest row (din_collate_fn).  A null value raises TypeError as the reference's
+        Dataset does (din.py:147-151) unless null_history="empty" (length 0)."""
         chunks = _arrow_chunks(column)
+        _check_null_history(chunks, null_history, "lookup_sequences")
         n = sum(len(c) for c in chunks)
         if T is None:
             T = _max_items(chunks, sep, threads)
@@ -359,6 +362,24 @@ def _dense_into(table, name, out: np.ndarray):
 
 # ---------------------------------------------------------------- batch assembly
 
+NULL_HISTORY = ("raise", "empty")
+
+
+def _check_null_history(chunks, policy: str, what: str):
+    """A null history cell.  The reference's DIN Dataset reads it with row.get(col, []), which
+    returns the null (None / NaN) for a present column, and then iterates it: TypeError
+    (din.py:147-151).  policy "raise" (default) does the same; "empty" reads it as an empty history
+    (length 0), which only a row WITHOUT the column gets in the reference."""
+    if policy not in NULL_HISTORY:
+        raise ValueError(f"{what}: null_history must be one of {NULL_HISTORY}, got {policy!r}")
+    if policy == "raise" and chunks is not None:
+        for c in chunks:
+            if not isinstance(c, _NonString) and c.null_count > 0:
+                raise TypeError(f"{what}: null history value ('NoneType' object is not iterable, as the "
+                                "reference's DIN Dataset raises at din.py:147-151); pass null_history='empty' "
+                                "to read nulls as empty histories")
+
+
 class BatchAssembler:
     """Builds one model's forward arguments for a batch of raw rows.
 
@@ -372,9 +393,11 @@ class BatchAssembler:
     views of device buffers.  With device="cpu" the host path returns host tensors."""
 
     def __init__(self, model: str, vocabs: dict, device="cuda", max_seq_length=50, threads: int = 0,
-                 bucketing: str = None):
+                 bucketing: str = None, null_history: str = "raise"):
         if model not in CATEGORY:
             raise ValueError(f"BatchAssembler: unknown model {model!r}")
+        _check_null_history(None, null_history, "BatchAssembler")
+        self.null_history = null_history  # DIN: a null history raises TypeError (din.py:147-151) or reads as []
         bucketing = bucketing or ("device" if torch.device(device).type == "cuda" else "host")
         if bucketing not in ("host", "device"):
             raise ValueError(f"BatchAssembler: bucketing must be 'host' or 'device', got {bucketing!r}")
@@ -412,6 +435,7 @@ class BatchAssembler:
         hist = None
         if m == "din":
             hist = _arrow_chunks(_column(table, DIN_SEQ)) if _column(table, DIN_SEQ) is not None else None
+            _check_null_history(hist, self.null_history, "BatchAssembler")
             seq_T = _max_items(hist, ",", self.threads) if hist is not None else 0
         elif m == "bst":
             seq_T = self.max_seq_length
@@ -527,6 +551,7 @@ class BatchAssembler:
             if kind == "hist" and chunks is not None:
                 if any(isinstance(c, _NonString) for c in chunks):
                     raise TypeError("rankops.loader: a sequence column must hold strings")
+                _check_null_history(chunks, self.null_history, "BatchAssembler")
                 seq_T = _max_items(chunks, ",", self.threads)
         if m == "bst":
             seq_T = self.max_seq_length

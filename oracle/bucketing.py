@@ -57,8 +57,12 @@ def lookup(indices, value):
     return 0
 
 
-def din_history(indices, value):
-    """din.py:147-157: returns the per-row index list (its length is the row's length)."""
+def din_history(indices, value, null="raise"):
+    """din.py:147-157: returns the per-row index list (its length is the row's length).  A null
+    cell of a present column: row.get returns it and `for item in seq` raises TypeError
+    (din.py:147-151); null="empty" reads it as [] (the engine's opt-in null_history="empty")."""
+    if value is None and null == "raise":
+        raise TypeError("'NoneType' object is not iterable (din.py:147-151)")
     seq = [] if value is None else value
     if isinstance(seq, str):
         seq = seq.split(',')
@@ -100,7 +104,7 @@ def dense_row(row):
     return np.array([row.get(f, 0.0) for f in DENSE_FEATURES], dtype=np.float64).astype(np.float32)
 
 
-def batch(model, rows, vocabs, max_seq_length=50):
+def batch(model, rows, vocabs, max_seq_length=50, null_history="raise"):
     """The collated batch the reference's DataLoader hands to `model.forward` for `rows` (list of
     dicts of raw values), as numpy arrays keyed like the forward's arguments.  `vocabs` maps a
     field to its vocab_indices dict (AFM: built with skip_empty and without manual_tag_list,
@@ -117,7 +121,7 @@ def batch(model, rows, vocabs, max_seq_length=50):
                 "category_input": {c: np.array([lookup(vocabs[c], r.get(c)) if c in vocabs else 0
                                                 for r in rows], dtype=np.int64) for c in AFM_CATEGORY}}
     if model == "din":
-        hist, lens = din_collate([din_history(vocabs["feedid"], r.get(DIN_SEQ)) for r in rows])
+        hist, lens = din_collate([din_history(vocabs["feedid"], r.get(DIN_SEQ), null_history) for r in rows])
         return {"dense": {f: np.array([r.get(f, 0.0) for r in rows], dtype=np.float64).astype(np.float32)
                           for f in DENSE_FEATURES},
                 "category": {c: np.array([lookup(vocabs[c], r.get(c)) for r in rows], dtype=np.int64)

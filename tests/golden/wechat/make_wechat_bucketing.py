@@ -21,7 +21,8 @@ Reads, as text, the only reference-held data on the hot path's input side:
 
 The semantics the tests pin against this data: index = line position, OOV -> 0 (colliding with
 line 0), multi-tag manual_tag_list -> 0, empty history '' -> [0] with length 1, null history ->
-length 0, and AFM's manual_tag_list always 0.  Run in the build container only:
+length 0 (the engine's opt-in null_history="empty"; by default a null history raises TypeError as
+din.py:147-151 does), and AFM's manual_tag_list always 0.  Run in the build container only:
 
     python tests/golden/wechat/make_wechat_bucketing.py
 """
@@ -109,7 +110,7 @@ def main():
                   for f, fn in ob.VOCAB_FILES.items()}
         if model == "afm":
             vocabs.pop("manual_tag_list")
-        b = ob.batch(model, rows, vocabs, max_seq_length=50)
+        b = ob.batch(model, rows, vocabs, max_seq_length=50, null_history="empty")
 
         def put(prefix, v):
             if isinstance(v, dict):

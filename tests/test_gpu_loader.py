@@ -71,12 +71,14 @@ def test_device_history_sequences(tmp_path):
     path, words, idx = _oracle_vocab(tmp_path, "h", b"s\na\nb\nc\n\nzz\n", False)
     v = rankops.Vocabulary(path)
     rows = HISTORIES * 3 + [",".join(["a", "b", "zz", ""] * 500), "c," * 1999 + "a"]
-    want_seq, want_len = ob.din_collate([ob.din_history(idx, r) for r in rows])
-    got_seq, got_len = v.lookup_sequences_device(pa.array(rows))
+    with pytest.raises(TypeError):
+        v.lookup_sequences_device(pa.array(rows))
+    want_seq, want_len = ob.din_collate([ob.din_history(idx, r, "empty") for r in rows])
+    got_seq, got_len = v.lookup_sequences_device(pa.array(rows), null_history="empty")
     np.testing.assert_array_equal(got_len.cpu().numpy(), want_len)
     np.testing.assert_array_equal(got_seq.cpu().numpy(), want_seq)
     for T in (0, 1, 5, 600):
-        s, n = v.lookup_sequences_device(pa.array(rows).slice(2), T=T)
+        s, n = v.lookup_sequences_device(pa.array(rows).slice(2), T=T, null_history="empty")
         np.testing.assert_array_equal(s.cpu().numpy(), want_seq[2:, :T] if T <= want_seq.shape[1] else
                                       np.pad(want_seq[2:], ((0, 0), (0, T - want_seq.shape[1]))))
         np.testing.assert_array_equal(n.cpu().numpy(), np.minimum(want_len[2:], T))
@@ -94,8 +96,8 @@ def test_assembled_batch_feeds_forward(model, bucketing, vocab):
                for f in ob.VOCAB_FILES}
     if model == "afm":
         ovocabs.pop("manual_tag_list")
-    want = ob.batch(model, rows, ovocabs, max_seq_length=50)
-    asm = rankops.BatchAssembler(model, vocabs, device="cuda", bucketing=bucketing)
+    want = ob.batch(model, rows, ovocabs, max_seq_length=50, null_history="empty")
+    asm = rankops.BatchAssembler(model, vocabs, device="cuda", bucketing=bucketing, null_history="empty")
     got = asm(_table(rows))
     for name, g in zip(ARGS[model], got):
         if isinstance(g, dict):
@@ -129,7 +131,7 @@ def test_double_buffered_batches_stay_independent(vocab, bucketing):
     """Consecutive batches reuse the two pinned buffers; earlier results must not change."""
     vocab_dir, words = vocab
     vocabs = rankops.wechat_vocabularies(vocab_dir)
-    asm = rankops.BatchAssembler("din", vocabs, device="cuda", bucketing=bucketing)
+    asm = rankops.BatchAssembler("din", vocabs, device="cuda", bucketing=bucketing, null_history="empty")
     outs = []
     for s in range(5):
         rows = _synthetic_rows(words, 300 + 17 * s, seed=100 + s)
@@ -138,6 +140,6 @@ def test_double_buffered_batches_stay_independent(vocab, bucketing):
     ovocabs = {f: ob.vocab_indices(ob.load_vocabulary(os.path.join(vocab_dir, ob.VOCAB_FILES[f])))
                for f in ob.VOCAB_FILES}
     for rows, got in outs:
-        want = ob.batch("din", rows, ovocabs)
+        want = ob.batch("din", rows, ovocabs, null_history="empty")
         for name, g in zip(ARGS["din"], got):
             _compare(g, want[name])

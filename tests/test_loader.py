@@ -98,12 +98,18 @@ def test_din_history_sequences(tmp_path):
     path, words, idx = _oracle_vocab(tmp_path, "h", b"a\nb\nc\n\nzz\n", False)
     v = rankops.Vocabulary(path)
     rows = HISTORIES * 3
-    want_seq, want_len = ob.din_collate([ob.din_history(idx, r) for r in rows])
-    got_seq, got_len = v.lookup_sequences(rows)
+    # a null history raises as the reference's Dataset does (din.py:147-151) ...
+    with pytest.raises(TypeError):
+        v.lookup_sequences(rows)
+    with pytest.raises(TypeError):
+        ob.din_history(idx, None)
+    # ... or reads as an empty history on request
+    want_seq, want_len = ob.din_collate([ob.din_history(idx, r, "empty") for r in rows])
+    got_seq, got_len = v.lookup_sequences(rows, null_history="empty")
     np.testing.assert_array_equal(got_len, want_len)
     np.testing.assert_array_equal(got_seq, want_seq)
     # capped width (BST-style truncation keeps the first T items and caps the length)
-    got5, len5 = v.lookup_sequences(rows, T=5)
+    got5, len5 = v.lookup_sequences(rows, T=5, null_history="empty")
     np.testing.assert_array_equal(got5, want_seq[:, :5])
     np.testing.assert_array_equal(len5, np.minimum(want_len, 5))
     big = [",".join(np.random.default_rng(i).choice(["a", "b", "c", "zz", "q"], size=i % 70)) for i in range(50000)]
@@ -135,6 +141,28 @@ def _synthetic_rows(vocab_words, B, seed, with_nulls=True):
             r[f] = float(np.log1p(rng.poisson(2.0)) + 1e-9 * rng.random()) if rng.random() > 0.02 else float("nan")
         rows.append(r)
     return rows
+
+
+def test_null_history_raises_like_the_reference(small_vocab):
+    """din.py:147-151: row.get(col, []) returns a present column's null and iterating it raises
+    TypeError; the assembler does the same by default, and reads it as [] with null_history="empty"."""
+    vocab_dir, words = small_vocab
+    vocabs = rankops.wechat_vocabularies(vocab_dir)
+    rows = _synthetic_rows(words, 200, seed=3)
+    assert any(r[ob.DIN_SEQ] is None for r in rows)
+    with pytest.raises(TypeError, match="din.py:147-151"):
+        rankops.BatchAssembler("din", vocabs, device="cpu")(_table(rows))
+    oracle_vocabs = {f: ob.vocab_indices(ob.load_vocabulary(os.path.join(vocab_dir, ob.VOCAB_FILES[f])))
+                     for f in ob.VOCAB_FILES}
+    with pytest.raises(TypeError):
+        ob.batch("din", rows, oracle_vocabs)
+    clean = _synthetic_rows(words, 200, seed=3, with_nulls=False)
+    got = rankops.BatchAssembler("din", vocabs, device="cpu")(_table(clean))
+    want = ob.batch("din", clean, oracle_vocabs)
+    for name, g in zip(ARGS["din"], got):
+        _compare(g, want[name])
+    with pytest.raises(ValueError):
+        rankops.BatchAssembler("din", vocabs, device="cpu", null_history="skip")
 
 
 def _table(rows):
@@ -187,8 +215,8 @@ def test_batch_assembler_matches_reference_dataset(model, small_vocab):
                      for f in ob.VOCAB_FILES}
     if model == "afm":  # AFM's Dataset looks for manual_tag_list.txt (afm.py:31-36): absent
         oracle_vocabs.pop("manual_tag_list")
-    want = ob.batch(model, rows, oracle_vocabs, max_seq_length=50)
-    asm = rankops.BatchAssembler(model, vocabs, device="cpu")
+    want = ob.batch(model, rows, oracle_vocabs, max_seq_length=50, null_history="empty")
+    asm = rankops.BatchAssembler(model, vocabs, device="cpu", null_history="empty")
     got = asm(_table(rows))
     assert len(got) == len(ARGS[model])
     for name, g in zip(ARGS[model], got):

@@ -9,7 +9,10 @@ Semantics checked bit for bit, host (rk_bucketize*) and device (rk_bucketize*_de
   multi-tag manual_tag_list -> 0        the ETL comma-joins tags (DataGenerator.py:365-368); the
                                         vocabulary holds single tags
   '' history -> [0] with length 1       din.py:147-157 (''.split(',') == [''])
-  null history -> length 0              din.py:147 (row.get(col, []) of a missing value)
+  null history -> TypeError             din.py:147-151 (row.get(col, []) returns a present column's
+                                        null, and iterating it raises); null_history="empty" reads it as
+                                        length 0, the mode the fixture's DIN batch was made in (a row
+                                        WITHOUT the column gets [] in the reference)
   AFM manual_tag_list always 0          afm.py:31-36 (its Dataset opens manual_tag_list.txt,
                                         which does not exist)
   table rows = len(vocab) + 1           dcn.py:119-125"""
@@ -78,8 +81,10 @@ def test_unknown_multitag_and_whitespace_probes(wechat):
               tags[5] + " ", "manual_tag_id_999999", tags[5].upper()]
     np.testing.assert_array_equal(mt.lookup(probes), [5, 0, 0, 0, 0, 0, 0, 0, 0])
     feed = _lines(os.path.join(vocab_dir, "feedid.txt"))
-    seqs, lens = vocabs["feedid"].lookup_sequences(["", None, feed[7], f"{feed[7]},{feed[9]}",
-                                                    f"{feed[7]},,feedid_x", f",{feed[3]}"])
+    probes = ["", None, feed[7], f"{feed[7]},{feed[9]}", f"{feed[7]},,feedid_x", f",{feed[3]}"]
+    with pytest.raises(TypeError):
+        vocabs["feedid"].lookup_sequences(probes)
+    seqs, lens = vocabs["feedid"].lookup_sequences(probes, null_history="empty")
     np.testing.assert_array_equal(lens, [1, 0, 1, 2, 3, 2])
     np.testing.assert_array_equal(seqs, [[0, 0, 0], [0, 0, 0], [7, 0, 0], [7, 9, 0], [7, 0, 0], [0, 3, 0]])
 
@@ -88,7 +93,10 @@ def test_unknown_multitag_and_whitespace_probes(wechat):
 def test_reference_vocabulary_batches_host(wechat, model):
     vocab_dir, _, rows, batches = wechat
     vocabs = rankops.wechat_vocabularies(vocab_dir, skip_empty_lines=model == "afm")
-    asm = rankops.BatchAssembler(model, vocabs, device="cpu")
+    if model == "din":  # the fixture holds null histories: the reference raises on them (din.py:147-151)
+        with pytest.raises(TypeError):
+            rankops.BatchAssembler(model, vocabs, device="cpu")(rows)
+    asm = rankops.BatchAssembler(model, vocabs, device="cpu", null_history="empty")
     got = asm(rows)
     for name, g in zip(ARGS[model], got):
         _compare(g, batches[model][name])
@@ -107,7 +115,7 @@ def test_reference_vocabulary_batches_host(wechat, model):
 def test_reference_vocabulary_batches_gpu(wechat, model, bucketing):
     vocab_dir, _, rows, batches = wechat
     vocabs = rankops.wechat_vocabularies(vocab_dir, skip_empty_lines=model == "afm")
-    asm = rankops.BatchAssembler(model, vocabs, device="cuda", bucketing=bucketing)
+    asm = rankops.BatchAssembler(model, vocabs, device="cuda", bucketing=bucketing, null_history="empty")
     got = asm(rows)
     torch.cuda.synchronize()
     for name, g in zip(ARGS[model], got):
