@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the per-model extras")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
+    ap.add_argument("--no-model-curve", action="store_true", help="skip the modelled 1->8 GPU curve of configs[4]")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call,din_zipf,"
                                         "dcn_eager,din_eager,deepfm_eager,bst_eager")
@@ -321,7 +322,7 @@ def bench_sharded(world, rank, steps, warmup):
         step = model.capture_pipeline(cat).step
 
     t = max_over_ranks(world, time_replays(step, steps, warmup, world))
-    wire = B_l * SHARDED_FIELDS * (8 + 4 * row_stride(32)) * (world - 1) / world
+    wire = B_l * SHARDED_FIELDS * (model.index_dtype.itemsize + 4 * row_stride(32)) * (world - 1) / world
     return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
             "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
@@ -329,6 +330,77 @@ def bench_sharded(world, rank, steps, warmup):
             "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
                      f"{len(model.chunk_bounds(B_l))}-chunk pipeline: per chunk 3 hipGraph segments + async RCCL "
                      "all_to_all_single (row exchange of chunk c overlaps the gather of c+1)")}
+
+
+XGMI_LINK_BPS = 153e9   # MI355X: 7 xGMI links x ~153 GB/s per GPU, point to point (fully connected node)
+A2A_LATENCY_S = 20e-6   # assumed fixed cost per RCCL all_to_all_single call (not measured here)
+
+
+def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
+    """A MODEL, not a measurement, of the 1 -> 8 GPU strong-scaling curve of configs[4] (global
+    batch 65536, 1e8 rows), built from what one GPU can time: rank 0's local device work at P
+    ranks — gather_local over its fields for the P x B_c rows it serves per chunk and fm_and_tail
+    for its B_c samples, both captured as hipGraphs and timed here — plus the wire time of the two
+    all-to-alls from their per-link bytes at XGMI_LINK_BPS (each peer pair has its own link) and an
+    assumed A2A_LATENCY_S per collective.  Two bounds: serial (compute + wire) and the chunked
+    pipeline's overlap (the row exchange of chunk c hidden behind chunk c+1's compute, first
+    chunk's exchange exposed)."""
+    import helpers as H
+    from rankops.sharded import ShardedDeepFM, row_stride
+    dev = torch.device("cuda", torch.cuda.current_device())
+    fields = {f"field_{i:02d}": SHARDED_ROWS_PER_FIELD for i in range(SHARDED_FIELDS)}
+    RS = row_stride(32)
+    curve = {"1": {"ms_per_step": p1_ms, "samples_per_s": round(SHARDED_GLOBAL_BATCH / (p1_ms * 1e-3), 1),
+                   "kind": "measured (sharded_deepfm at P = 1)"}}
+    for P in ps:
+        torch.manual_seed(42)
+        with torch.device(dev):
+            model = ShardedDeepFM(fields, 32, [512, 256, 128], rank=0, world_size=P)
+        H.randomize_eval_stats(model, 43)
+        model.eval()
+        B_l = SHARDED_GLOBAL_BATCH // P
+        B_c = B_l // chunks
+        F_me = len(model.local_fields)
+        rng = np.random.default_rng(77 + P)
+        recv_idx = torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, P * B_c * F_me)).to(
+            dev, model.index_dtype)
+        recv_rows = torch.randn(B_c * SHARDED_FIELDS * RS, device=dev)
+        cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_c)).to(dev) for f in fields}
+        with torch.no_grad():
+            g_pack, _ = graph_of(lambda: model.pack_indices(cat))
+            g_gather, _ = graph_of(lambda: model.gather_local(recv_idx, P * B_c))
+            g_fm, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_c))
+        t_pack = kernel_avg_ms(g_pack.replay, iters) * chunks
+        t_gather = kernel_avg_ms(g_gather.replay, iters) * chunks
+        t_fm = kernel_avg_ms(g_fm.replay, iters) * chunks
+        t_comp = t_pack + t_gather + t_fm
+        # per link: this rank's bytes to one peer (F / P fields of its B_l samples, each way)
+        f_peer = SHARDED_FIELDS / P
+        idx_link = B_l * f_peer * model.index_dtype.itemsize
+        rows_link = B_l * f_peer * RS * 4
+        t_idx = 1e3 * (idx_link / XGMI_LINK_BPS + chunks * A2A_LATENCY_S)
+        t_rows = 1e3 * (rows_link / XGMI_LINK_BPS + chunks * A2A_LATENCY_S)
+        serial = t_comp + t_idx + t_rows
+        first = (t_idx + t_rows) / chunks
+        overlap = max(t_comp, t_rows + t_idx) + first
+        curve[str(P)] = {
+            "kind": "model, not a measurement",
+            "B_local": B_l, "fields_rank0": F_me,
+            "compute_ms": {"pack": round(t_pack, 4), "gather_local": round(t_gather, 4),
+                           "fm_and_tail": round(t_fm, 4)},
+            "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4)},
+            "bytes_per_link": {"index": int(idx_link), "rows": int(rows_link)},
+            "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4)},
+            "samples_per_s": {"serial": round(SHARDED_GLOBAL_BATCH / (serial * 1e-3), 1),
+                              "overlapped": round(SHARDED_GLOBAL_BATCH / (overlap * 1e-3), 1)},
+            "speedup_vs_p1": {"serial": round(p1_ms / serial, 2), "overlapped": round(p1_ms / overlap, 2)},
+        }
+        del model, g_pack, g_gather, g_fm
+        torch.cuda.empty_cache()
+    return {"assumptions": f"{chunks}-chunk pipeline; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
+                           f"peer pair; {A2A_LATENCY_S * 1e6:.0f} us per all_to_all_single call (assumed); "
+                           "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter",
+            "curve": curve}
 
 
 # ------------------------------------------------------------------ host input path (SURVEY §8(f) #1)
@@ -715,6 +787,12 @@ def main():
             sh = bench_sharded(world, rank, args.steps, args.warmup)
         except Exception as exc:  # reported, never fatal for the headline line
             sh = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+        if world == 1 and "ms_per_step" in sh and not args.no_model_curve:
+            try:
+                sh["model_curve"] = sharded_model_curve(sh["ms_per_step"])
+            except Exception as exc:
+                sh["model_curve"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+            torch.cuda.empty_cache()
         result["sharded_deepfm"] = sh
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baselines(model.cpu(), cfg, result["value"], result.get("models", {}),

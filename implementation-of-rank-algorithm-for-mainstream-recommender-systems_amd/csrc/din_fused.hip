@@ -594,7 +594,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
              NIT > 0 ? s_rows : nullptr);
   else
-    mlp_stream_rows<P, false>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid, NoStage(),
+    mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid, NoStage(),
                               nullptr, NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
   // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =

@@ -41,7 +41,8 @@ struct LtArgs {
 // The fused DeepFM front end's A source (rk_fm_linear_packed): row b of A is the concatenation of
 // the num_fields packed-table rows idx[f][b] (rk_fm_pack_table layout: dim floats, then the
 // first-order weight), and the same pass produces fm1 / fm2 (deepfm.py:122-140) for the rows it
-// stages.
+// stages.  A field without an index array (idx null) is a dense block of packed rows, row b at
+// src + b * ld: the rows ShardedDeepFM receives from the field's owner rank.
 struct LtFm {
   const float* src[kLtMaxFields];
   const int64_t* idx[kLtMaxFields];
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(kMlpThreads) void linear_tiled_kernel(LtArgs a, LtF
       const int e = tid + kMlpThreads * u;
       const int f = __builtin_amdgcn_readfirstlane(e / kLtRows);  // wave-uniform: scalar descriptor loads
       const int64_t m = m0 + e % kLtRows;
-      iv[u] = (f < fm.F && m < a.M) ? fm.idx[f][m] : -1;
+      iv[u] = (f < fm.F && m < a.M) ? (fm.idx[f] ? fm.idx[f][m] : m) : -1;
     }
   }
 
@@ -394,14 +395,16 @@ RK_API int rk_fm_linear_packed(const rk_segment* fields, int32_t num_fields, int
   LtFm fm = {};
   for (int f = 0; f < num_fields; ++f) {
     const rk_segment& s = fields[f];
-    if (!s.src || !s.idx || s.rows <= 0 || s.idx_stride != 1 || s.dim != dim || s.src_ld < dim + 1 || s.src_ld % 4 ||
-        !aligned16(s.src) || s.out_col != f * dim)
+    if (!s.src || (s.idx && (s.rows <= 0 || s.idx_stride != 1)) || s.dim != dim || s.src_ld < dim + 1 ||
+        s.src_ld % 4 || !aligned16(s.src) || s.out_col != f * dim)
       return fail(RK_ERR_INVALID,
-                  "rk_fm_linear_packed: field %d is not a unit-stride packed [rows, >= dim+1] table at column f*dim", f);
+                  "rk_fm_linear_packed: field %d is not a packed [rows, >= dim+1] table (unit-stride indices, or "
+                  "none: a dense block of packed rows) at column f*dim",
+                  f);
     fm.src[f] = s.src;
     fm.idx[f] = s.idx;
     fm.ld[f] = s.src_ld;
-    fm.rows[f] = s.rows;
+    fm.rows[f] = s.idx ? s.rows : batch;  // dense: row b < batch
   }
   fm.F = num_fields;
   fm.dim_shift = __builtin_ctz((unsigned)dim);

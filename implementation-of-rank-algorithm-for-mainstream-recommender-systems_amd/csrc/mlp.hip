@@ -94,7 +94,14 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_stream_kernel(MlpArgs a) {
       }
     }
   };
-  mlp_stream_rows<P>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.off_epi, m0, rows, a.head, tid, finish_only(stage));
+#ifdef RK_MLP_PHASES
+  const unsigned long long k_t0 = clock64();
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
+#endif
+  mlp_stream_rows<P, RK_STREAM_EPI>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.off_epi, m0, rows, a.head, tid, finish_only(stage));
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
+  MLP_FLUSH(tid);
 }
 
 // Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): per 16-row tile, wave w
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
     mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
              two_phase(stage_issue, stage_finish), part);
   else
-    mlp_stream_rows<P>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
+    mlp_stream_rows<P, RK_STREAM_EPI>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
                        two_phase(stage_issue, stage_finish), part);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);

@@ -35,6 +35,10 @@ namespace rk {
 #ifndef RK_STREAM_RING
 #define RK_STREAM_RING 8
 #endif
+// epilogue parameters of the rk_mlp_forward / DCN streamed tails (StreamEpiMode below)
+#ifndef RK_STREAM_EPI
+#define RK_STREAM_EPI 2
+#endif
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -91,6 +95,39 @@ struct StreamPlan {
   static_assert(epi_off(NL) / 8 <= 2 * kMlpThreads, "epilogue image: two columns per thread at most");
 };
 
+// col_epi's raw values resolved against the layer's flags: absent affine parts become the identity
+// (col_apply adds 0 / scales by 1 for them too, so the arithmetic is the same), and the non-Dice
+// activations one negative-side slope in the alpha slot.
+__device__ __forceinline__ ColEpi resolve_epi(const rk_mlp_layer& L, ColEpi r) {
+  r.bias = L.bias ? r.bias : 0.f;
+  r.pre_s = L.pre_scale ? r.pre_s : 1.f;
+  r.pre_b = L.pre_scale ? r.pre_b : 0.f;
+  r.post_s = L.post_scale ? r.post_s : 1.f;
+  r.post_b = L.post_scale ? r.post_b : 0.f;
+  if (L.act != RK_ACT_DICE)
+    r.alpha = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? r.alpha : 1.f;
+  return r;
+}
+
+// col_apply on resolved parameters (bias, pre affine, activation, post affine).
+template <bool DICE>
+__device__ __forceinline__ float apply_epi(const ColEpi& e, float z) {
+  z = z + e.bias;
+  z = z * e.pre_s + e.pre_b;
+  if constexpr (DICE)
+    z = dice_apply(z, e.act_s, e.act_b, e.alpha);
+  else
+    z = z > 0.f ? z : z * e.alpha;
+  return z * e.post_s + e.post_b;
+}
+
+// Where a streamed tail finds its per-column epilogue parameters.
+enum StreamEpiMode {
+  kEpiLdsHere = 0,    // LDS image, loaded and stored by mlp_stream_rows in its prologue
+  kEpiLdsCaller = 1,  // LDS image stored by the caller before the barrier that opens layer 0 (DIN)
+  kEpiRegs = 2,       // registers: layer 0's after the ring in the prologue, layer l+1's after layer l's epilogue
+};
+
 // The epilogue-parameter image, in two halves: load() issues the (unconditional) loads of at most
 // two columns per thread into registers, store() writes them to LDS.  Column i of the image is
 // layer l's column i - cols(<l); values are col_epi's (absent vectors read as any valid float and
@@ -113,18 +150,7 @@ struct StreamEpi {
       for (int q = 1; q < P::NL; ++q)
         if (l == q) L = layers[q];
       const int n = i - P::epi_off(l) / 8;
-      e[k] = col_epi(L, n < L.n ? n : 0);
-      // resolved against the layer's flags here, once: absent affine parts become the identity
-      // (col_apply adds 0 / scales by 1 for them too, so the arithmetic is the same), and the
-      // non-Dice activations one negative-side slope in the alpha slot
-      ColEpi& r = e[k];
-      r.bias = L.bias ? r.bias : 0.f;
-      r.pre_s = L.pre_scale ? r.pre_s : 1.f;
-      r.pre_b = L.pre_scale ? r.pre_b : 0.f;
-      r.post_s = L.post_scale ? r.post_s : 1.f;
-      r.post_b = L.post_scale ? r.post_b : 0.f;
-      if (L.act != RK_ACT_DICE)
-        r.alpha = L.act == RK_ACT_RELU ? 0.f : L.act == RK_ACT_LEAKY ? L.slope : L.act == RK_ACT_PRELU ? r.alpha : 1.f;
+      e[k] = resolve_epi(L, col_epi(L, n < L.n ? n : 0));
     }
   }
   __device__ __forceinline__ void store(float* __restrict__ img, int tid) const {
@@ -142,9 +168,8 @@ struct StreamEpi {
 
 // One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
 // (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
-// operator() after it, before that barrier).  EPI_HERE: the caller has not stored the image — it is
-// loaded here (after stage.issue(), ahead of the ring) and stored after the stage.
-template <class P, int W, bool EPI_HERE, class Stage>
+// operator() after it, before that barrier).  EPI: StreamEpiMode.
+template <class P, int W, int EPI, class Stage>
 __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                  float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                  const rk_epilogue& h, int tid, int wave, Stage& stage,
@@ -180,22 +205,45 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     if (wave < rows && h.head_partial && !lds_partial) hp = h.head_partial[row_ids ? row_ids[wave] : m0 + wave];
   };
 
+#ifdef RK_MLP_PHASES
+  const unsigned long long t_start = clock64();
+#endif
   StreamEpi<P> ep_stage;
+  // kEpiRegs: the parameters of the wave's columns of one layer (tiles j = 0, 1)
+  ColEpi epr[2];
+  auto load_epr = [&](auto LI) {
+    constexpr int l = LI;
+    if constexpr (l < NL) {
+      const rk_mlp_layer& L = layers[l];
+#pragma unroll
+      for (int j = 0; j < P::tpw(l, W); ++j) {
+        const int n = 16 * (wave + kMlpWaves * j) + li;
+        epr[j] = col_epi(L, n < L.n ? n : 0);
+      }
+    }
+  };
   stage.issue();
-  if constexpr (EPI_HERE) ep_stage.load(layers, tid);
+  if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
   __builtin_amdgcn_sched_barrier(0);  // the stage's and the parameters' loads stay ahead of the ring
   static_for<0, R>([&](auto G) {
     issue(G);
     __builtin_amdgcn_sched_barrier(0);
   });
+  // layer 0's parameters behind the ring (needed only at its epilogue)
+  if constexpr (EPI == kEpiRegs) load_epr(std::integral_constant<int, 0>{});
   if constexpr (NL == 1) head_prefetch();
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS - 4, t_start);  // (timing builds) ring issued
   stage();
-  if constexpr (EPI_HERE) ep_stage.store(epi, tid);
+  if constexpr (EPI == kEpiLdsHere) ep_stage.store(epi, tid);
   mlp_lds_barrier();
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS, t_start);  // prologue done
 
   static_for<0, NL>([&](auto LI) {
     constexpr int l = LI;
     constexpr int T = P::tpw(l, W), KC = P::kc(l), B0 = P::base(l, W);
+#ifdef RK_MLP_PHASES
+    const unsigned long long t0 = clock64();
+#endif
     const rk_mlp_layer& L = layers[l];
     const float* in = (l & 1) ? buf1 : buf0;
     float* out = (l & 1) ? buf0 : buf1;
@@ -235,6 +283,10 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         if constexpr ((c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
 #endif
       });
+      MLP_MARK(4 * l, t0);
+#ifdef RK_MLP_PHASES
+      if (lane == 0 && l < 4) s_mlp_wave_marks[l][wave][0] = (unsigned)(clock64() - t0);
+#endif
 #if RK_MLP_EPI_PRIO
       __builtin_amdgcn_s_setprio(2);
 #endif
@@ -244,21 +296,25 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         for (int j = 0; j < T; ++j) {
           const int n = 16 * (wave + kMlpWaves * j) + li;
           const bool real = n < L.n;
-          const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(img + 8 * n);
-          const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(img + 8 * n + 4);
+          ColEpi e;
+          if constexpr (EPI == kEpiRegs) {
+            e = resolve_epi(L, epr[j]);
+          } else {
+            const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(img + 8 * n);
+            const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(img + 8 * n + 4);
+            e.bias = p0[0];
+            e.pre_s = p0[1];
+            e.pre_b = p0[2];
+            e.act_s = p0[3];
+            e.act_b = p1[0];
+            e.alpha = p1[1];
+            e.post_s = p1[2];
+            e.post_b = p1[3];
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = (lane >> 4) * 4 + r;
-            // col_apply's arithmetic on the resolved parameters (bias, pre affine, activation,
-            // post affine)
-            float z = acc[j][r] + p0[0];
-            z = z * p0[1] + p0[2];
-            if constexpr (DICE) {
-              z = dice_apply(z, p0[3], p1[0], p1[1]);
-            } else {
-              z = z > 0.f ? z : z * p1[1];
-            }
-            z = z * p1[2] + p1[3];
+            const float z = apply_epi<decltype(DICE)::value>(e, acc[j][r]);
             out[row * ldout + n] = real ? z : 0.f;  // padded columns: the next layer's zero K pad
           }
         }
@@ -267,9 +323,18 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         epilogue(std::true_type{});
       else
         epilogue(std::false_type{});
+#ifdef RK_MLP_PHASES
+      if (lane == 0 && l < 4) s_mlp_wave_marks[l][wave][1] = (unsigned)(clock64() - t0);
+#endif
     }
+    MLP_MARK(4 * l + 1, t0);
+    // the next layer's parameters (this layer's are consumed): in flight across the barrier, behind
+    // that layer's first ring loads
+    if constexpr (EPI == kEpiRegs) load_epr(std::integral_constant<int, l + 1>{});
     if constexpr (l + 2 == NL) head_prefetch();
+    MLP_MARK(4 * l + 2, t0);
     mlp_lds_barrier();
+    MLP_MARK(4 * l + 3, t0);
 #if RK_MLP_EPI_PRIO
     if constexpr (T > 0) __builtin_amdgcn_s_setprio(0);
 #endif
@@ -311,7 +376,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
 
 // Entry point: dispatches the calling wave to its class's unrolled body.  Must be called by all
 // kMlpThreads threads.  `epi`: P::epi_floats() floats of LDS (16-B aligned).
-template <class P, bool EPI_HERE = true, class Stage = NoStage>
+template <class P, int EPI = kEpiRegs, class Stage = NoStage>
 __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                 float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                 const rk_epilogue& h, int tid, Stage stage = Stage(),
@@ -325,7 +390,7 @@ __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__
 #pragma unroll
       for (int l = 0; l < P::NL; ++l) mine = mine && P::tpw(l, wave) == P::tpw(l, w);
       if (mine)
-        mlp_stream_class<P, w, EPI_HERE>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
+        mlp_stream_class<P, w, EPI>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
                                          lds_partial, row_ids);
     }
   });

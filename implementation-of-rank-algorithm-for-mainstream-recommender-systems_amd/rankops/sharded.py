@@ -6,21 +6,26 @@ second-order [V_f, D] and first-order [V_f, 1] tables; the dense layers are repl
 rank holds a data-parallel slice of B_l samples with the indices of all F fields.  One forward:
 
   1. index exchange   all_to_all_single: rank r receives, from every source s, the indices of
-                      r's fields for s's samples, laid out [s][b][f_r] (int64)
+                      r's fields for s's samples, laid out [s][b][f_r] (int32 on the wire while
+                      every table has < 2^31 rows — configs[4]: 3.3M per field — else int64)
   2. local gather     one rk_concat_gather from r's packed tables (rk_fm_pack_table: per field
                       one [V_f, RS] table, the D second-order floats at 0..D-1 and the
                       first-order weight at D, RS = D + 1 rounded up to 4 floats so every row
                       stays 16-B aligned) -> rows [s][b][f_r][RS], one contiguous read per row
   3. row exchange     all_to_all_single back: each source gets [r][b][f_r][RS] from every owner
-  4. FM + MLP         rk_fm_gather over the received rows (dense segments, field order restored
-                      through out_col = f * D), then the fused MLP tail exactly as DeepFM
+  4. FM + MLP         rk_fm_linear_packed over the received rows, read in place as dense blocks of
+                      packed rows (field order restored through out_col = f * D): fm1, fm2 and the
+                      first deep layer in one launch, the [B, F*D] deep input never written to
+                      HBM; then the streamed MLP tail (DeepFM's two-launch forward)
 
 At P > 1 the steps run per chunk of the local batch (run_steps): each chunk's row all-to-all is
 issued asynchronously and overlaps the next chunk's gather and the previous chunk's FM + tail.
-At P = 1 there is nothing to exchange: the forward is one rk_fm_gather_packed pass over the
-packed tables plus the tail, i.e. `DeepFM.forward` on the same weights.
-The exchange volume per rank and step is B_l * F * (8 + 4 * RS) bytes, (P-1)/P of it on the
-wire.  Reference: DeepFM.forward, deepfm.py:121-151 (the reference is single-device; the
+At P = 1 there is nothing to exchange: the forward is rk_fm_linear_packed over the packed tables
+plus the tail, i.e. `DeepFM.forward` on the same weights.
+The exchange volume per rank and step is B_l * F * (4 + 4 * RS) bytes (int32 indices), (P-1)/P of
+it on the wire.  Rows travel at RS = 36 floats (144 B, 132 live): the receiver's fused front end
+reads them in place with 16-B loads, which a 132-B stride would misalign for three rows in four,
+and the row exchange overlaps the next chunk's gather.  Reference: DeepFM.forward, deepfm.py:121-151 (the reference is single-device; the
 sharding is the MI355X build's own).
 """
 from __future__ import annotations
@@ -66,6 +71,11 @@ class ShardedDeepFM(EngineModule):
         # otherwise a callable (out, inp, out_splits, in_splits, async_op) -> out | (out, work)
         # with the same semantics (tests drive P shards in one process through an emulator)
         self.exchange_fn = None
+        # index wire format: int32 while every table fits (the receiver widens before its gather)
+        self.index_dtype = torch.int32 if max(self.field_rows.values()) < 2 ** 31 else torch.int64
+        # gather + FM + first deep layer in one rk_fm_linear_packed launch (False: the three-launch
+        # rk_fm_gather(_packed) + tiled first layer + tail path, kept for A/B)
+        self.fused_front = True
         self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
                                                      for f in self.local_fields})
         self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
@@ -135,19 +145,21 @@ class ShardedDeepFM(EngineModule):
         return [B_l * len(self.fields_of[r]) * RS for r in range(self.world)], [B_l * F_me * RS] * self.world
 
     def pack_indices(self, category: dict) -> torch.Tensor:
-        """Send buffer of step 1: [r][b][f_r] index blocks (a small int64 permute)."""
+        """Send buffer of step 1: [r][b][f_r] index blocks (a small permute, in index_dtype)."""
         blocks = []
         for r in range(self.world):
             fr = self.fields_of[r]
             if fr:
                 blocks.append(torch.stack([category[f] for f in fr], 1).reshape(-1))
-        return torch.cat(blocks) if blocks else torch.empty(0, dtype=torch.int64, device=self._device())
+        if not blocks:
+            return torch.empty(0, dtype=self.index_dtype, device=self._device())
+        return torch.cat(blocks).to(self.index_dtype)
 
     def exchange_indices(self, category: dict, B_l: int, async_op: bool = False):
         """Step 1: send [r][b][f_r] index blocks; receive [s][b][f_me]."""
         send = self.pack_indices(category)
         out_s, in_s = self.index_splits(B_l)
-        recv = torch.empty(sum(out_s), dtype=torch.int64, device=send.device)
+        recv = torch.empty(sum(out_s), dtype=self.index_dtype, device=send.device)
         return self._exchange(recv, send, out_s, in_s, async_op)
 
     def gather_local(self, recv_idx: torch.Tensor, rows_total: int) -> torch.Tensor:
@@ -156,6 +168,8 @@ class ShardedDeepFM(EngineModule):
         out = torch.empty(rows_total, F_me * RS, device=recv_idx.device, dtype=torch.float32)
         if F_me == 0 or rows_total == 0:
             return out
+        if recv_idx.dtype != torch.int64:  # int32 wire format
+            recv_idx = recv_idx.to(torch.int64)
         segs = []
         for j, f in enumerate(self.local_fields):
             idx = recv_idx[j:]  # element (R, j) sits at R * F_me + j
@@ -169,6 +183,30 @@ class ShardedDeepFM(EngineModule):
         recv = torch.empty(sum(out_s), device=rows.device, dtype=torch.float32)
         return self._exchange(recv, rows.reshape(-1), out_s, in_s, async_op)
 
+    def _front_ok(self, B_l: int) -> bool:
+        D, l0 = self.embedding_dim, self._tail[0]
+        return (self.fused_front and B_l > 0 and len(self._tail) >= 2 and len(self.fields) <= 32
+                and 4 <= D <= 256 and D & (D - 1) == 0)
+
+    def _front_and_tail(self, segs, B_l: int):
+        """rk_fm_linear_packed (gather, fm1, fm2 and deep layer 0, deepfm.py:122-142 + 100-112)
+        then the rest of the tail and the head (deepfm.py:143-151)."""
+        from . import common
+        dev = self._device()
+        l0 = self._tail[0]
+        ml0 = ops.make_mlp_layer(l0.linear.weight, common.PACKED(l0.linear.weight), **l0.epilogue_kwargs())
+        y = torch.empty(B_l, l0.linear.out_features, device=dev, dtype=torch.float32)
+        fm1 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        fm2 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        ops.fm_linear_packed(segs, self.embedding_dim, B_l, ml0, y, fm1, fm2)
+        deep = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        total = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
+        run_tail(y, self._tail[1:], self.deep_output_layer,
+                 dict(fm1=fm1, fm2=fm2, final_w=self.final_layer.weight, final_b=self.final_layer.bias,
+                      head_aux=deep), total, prob)
+        return prob, total, fm1, fm2, deep
+
     def fm_and_tail(self, recv_rows: torch.Tensor, B_l: int):
         """Step 4: FM + deep tail on the received rows (field order restored by out_col)."""
         D, RS = self.embedding_dim, row_stride(self.embedding_dim)
@@ -180,6 +218,11 @@ class ShardedDeepFM(EngineModule):
             for j, f in enumerate(self.fields_of[r]):
                 base[f] = (off + j * RS, len(self.fields_of[r]) * RS)
             off += B_l * len(self.fields_of[r]) * RS
+        if self._front_ok(B_l):  # the received packed rows read in place (dense segments)
+            from ._lib import Segment
+            segs = [Segment(recv_rows.data_ptr() + base[f][0] * 4, None, 0, base[f][1], 0, D, i * D)
+                    for i, f in enumerate(self.fields)]
+            return self._front_and_tail(segs, B_l)
         for i, f in enumerate(self.fields):
             o, ld = base[f]
             second.append(_lib_dense(recv_rows, o, ld, D, i * D))
@@ -199,6 +242,8 @@ class ShardedDeepFM(EngineModule):
         for i, f in enumerate(self.fields):
             idx = cat[f] if cat[f].stride(0) == 1 else cat[f].contiguous()
             segs.append(ops.packed_segment(self.packed_table(f), idx, D, i * D))
+        if self._front_ok(B_l):
+            return self._front_and_tail(segs, B_l)
         deep_in = torch.empty(B_l, len(self.fields) * D, device=dev, dtype=torch.float32)
         fm1 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
         fm2 = torch.empty(B_l, 1, device=dev, dtype=torch.float32)
@@ -301,7 +346,7 @@ class CapturedPipeline:
             cc = {f: v[b0:b1] for f, v in cat.items()}
             out_i, in_i = model.index_splits(Bc)
             out_r, in_r = model.row_splits(Bc)
-            recv_idx = torch.zeros(sum(out_i), dtype=torch.int64, device=dev)  # valid rows for the warm-up gathers
+            recv_idx = torch.zeros(sum(out_i), dtype=model.index_dtype, device=dev)  # valid rows for the warm-ups
             recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
             g1, send = _graph_of(lambda cc=cc: model.pack_indices(cc))
             g2, rows = _graph_of(lambda ri=recv_idx, Bc=Bc: model.gather_local(ri, model.world * Bc))

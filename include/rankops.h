@@ -362,6 +362,8 @@ int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_
  * ((sum_f e_f)^2 - sum_f e_f^2)[d], and y[b, :] = epilogue(concat_f(e_f) . W^T) with
  * e_f = row idx_f[b] of field f's packed table (rk_fm_pack_table layout, as rk_fm_gather_packed:
  * segment f = {packed table, unit-stride index, rows, dim, src_ld >= dim + 1, out_col = f * dim}).
+ * A segment with idx = NULL is a dense block of packed rows (row b at src + b * src_ld, b < batch):
+ * the rows ShardedDeepFM receives from a field's owner rank over the row all-to-all.
  * The layer is packed by rk_mlp_pack_weight for K = num_fields * dim (no residual).  dim a power of
  * two in [4, 256], num_fields <= 32.  The concatenated deep input is staged in LDS only.
  * Out-of-range indices read zero rows and raise RK_FLAG_INDEX_OOB.                               */

@@ -138,8 +138,9 @@ def test_sharded_step_functions_emulated_on_gpu(world):
     for r, (recv_idx, rows, got) in enumerate(outs):
         mine = shards[r].local_fields
         ri = recv_idx.view(world * B_l, len(mine))
+        assert ri.dtype == torch.int32  # int32 on the wire (every table < 2^31 rows)
         want_idx = torch.stack([inp["category"][f].cpu() for f in mine], 1)  # sources in order = global rows
-        assert torch.equal(ri, want_idx)
+        assert torch.equal(ri.long(), want_idx)
         rv = rows.view(world * B_l, len(mine), RS)
         for j, f in enumerate(mine):
             w2 = full.second_order_embeddings[f].weight.detach().cpu()
@@ -181,3 +182,32 @@ def test_captured_pipeline_emulated_on_gpu(world):
     assert emu.calls == 2 * 2 * 4
     import rankops
     assert rankops.error_flags() == 0  # the capture's warm-up gathers read valid (zeroed) indices
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 8])
+@pytest.mark.parametrize("fused", [True, False])
+def test_fused_front_and_unfused_path_match_oracle(world, fused):
+    """fm_and_tail / local_fm_and_tail through rk_fm_linear_packed (the received rows read in place
+    as dense blocks of packed rows; P = 1 from the packed tables) and through the three-launch
+    rk_fm_gather path (fused_front = False), against the oracle; ragged local batch."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 333
+    inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=600 + world), "cuda")
+    expect = _oracle(full, CFG30, inp["category"])
+    shards, emu = _shards(full, world)
+
+    def rank_fn(r):
+        sh = shards[r]
+        sh.fused_front = fused
+        mine = {f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in inp["category"].items()}
+        with torch.no_grad():
+            out = sh.run_steps(mine, chunks=1)
+        torch.cuda.synchronize()
+        return tuple(o.cpu() for o in out)
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    for r, got in enumerate(outs):
+        _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
+    import rankops
+    assert rankops.error_flags() == 0

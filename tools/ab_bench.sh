@@ -2,7 +2,7 @@
 # A/B of library builds on the headline legs: for each .so given, the bench's forward legs with
 # RANKOPS_LIB pointing at it.  Usage (on the box): bash tools/ab_bench.sh <tag> <lib.so>...
 set -o pipefail
-T=$1; shift; O=gpurun_out/r03; mkdir -p $O
+T=$1; shift; O=${ABDIR:-gpurun_out/r03}; mkdir -p $O
 for L in "$@"; do
   N=$(basename $L .so)
   RANKOPS_LIB=$PWD/$L timeout -k 10 300 python bench.py --no-cpu --no-loader --no-train --no-sharded --models dcn,deepfm,bst > $O/ab_${T}_$N.json 2> $O/ab_${T}_$N.err || { echo "bench $N failed"; tail -5 $O/ab_${T}_$N.err; exit 1; }
