@@ -339,7 +339,7 @@ A2A_LATENCY_S = 20e-6   # assumed fixed cost per RCCL all_to_all_single call (no
 def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
     """A MODEL, not a measurement, of the 1 -> 8 GPU strong-scaling curve of configs[4] (global
     batch 65536, 1e8 rows), built from what one GPU can time: rank 0's local device work at P
-    ranks — gather_local over its fields for the P x B_c rows it serves per chunk and fm_and_tail
+    ranks — gather_rows over its fields for the P x B_c rows it serves per chunk and fm_and_tail
     for its B_c samples, both captured as hipGraphs and timed here — plus the wire time of the two
     all-to-alls from their per-link bytes at XGMI_LINK_BPS (each peer pair has its own link) and an
     assumed A2A_LATENCY_S per collective.  Two bounds: serial (compute + wire) and the chunked
@@ -359,33 +359,35 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         H.randomize_eval_stats(model, 43)
         model.eval()
         B_l = SHARDED_GLOBAL_BATCH // P
-        B_c = B_l // chunks
+        C = len(model.chunk_bounds(B_l, chunks))
+        B_c = B_l // C
         F_me = len(model.local_fields)
         rng = np.random.default_rng(77 + P)
-        recv_idx = torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, P * B_c * F_me)).to(
+        recv_idx = torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, P * B_l * F_me)).to(
             dev, model.index_dtype)
         recv_rows = torch.randn(B_c * SHARDED_FIELDS * RS, device=dev)
-        cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_c)).to(dev) for f in fields}
+        cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l)).to(dev) for f in fields}
         with torch.no_grad():
             g_pack, _ = graph_of(lambda: model.pack_indices(cat))
-            g_gather, _ = graph_of(lambda: model.gather_local(recv_idx, P * B_c))
+            g_gather, _ = graph_of(lambda: model.gather_rows(recv_idx, B_l, 0, B_c))
             g_fm, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_c))
-        t_pack = kernel_avg_ms(g_pack.replay, iters) * chunks
-        t_gather = kernel_avg_ms(g_gather.replay, iters) * chunks
-        t_fm = kernel_avg_ms(g_fm.replay, iters) * chunks
+        t_pack = kernel_avg_ms(g_pack.replay, iters)
+        t_gather = kernel_avg_ms(g_gather.replay, iters) * C
+        t_fm = kernel_avg_ms(g_fm.replay, iters) * C
         t_comp = t_pack + t_gather + t_fm
         # per link: this rank's bytes to one peer (F / P fields of its B_l samples, each way)
         f_peer = SHARDED_FIELDS / P
         idx_link = B_l * f_peer * model.index_dtype.itemsize
         rows_link = B_l * f_peer * RS * 4
-        t_idx = 1e3 * (idx_link / XGMI_LINK_BPS + chunks * A2A_LATENCY_S)
-        t_rows = 1e3 * (rows_link / XGMI_LINK_BPS + chunks * A2A_LATENCY_S)
+        t_idx = 1e3 * (idx_link / XGMI_LINK_BPS + A2A_LATENCY_S)  # one index exchange per step
+        t_rows = 1e3 * (rows_link / XGMI_LINK_BPS + C * A2A_LATENCY_S)
         serial = t_comp + t_idx + t_rows
-        first = (t_idx + t_rows) / chunks
-        overlap = max(t_comp, t_rows + t_idx) + first
+        # pipeline: pack + index exchange, then chunk c's rows travel behind chunk c+1's gather and
+        # chunk c-1's FM + tail; the first chunk's gather and the last chunk's exchange stay exposed
+        overlap = t_pack + t_idx + max(t_gather + t_fm, t_rows) + (t_gather + t_rows) / C
         curve[str(P)] = {
             "kind": "model, not a measurement",
-            "B_local": B_l, "fields_rank0": F_me,
+            "B_local": B_l, "fields_rank0": F_me, "chunks": C,
             "compute_ms": {"pack": round(t_pack, 4), "gather_local": round(t_gather, 4),
                            "fm_and_tail": round(t_fm, 4)},
             "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4)},
@@ -397,7 +399,7 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         }
         del model, g_pack, g_gather, g_fm
         torch.cuda.empty_cache()
-    return {"assumptions": f"{chunks}-chunk pipeline; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
+    return {"assumptions": f"up to {chunks} chunks of >= 4096 samples; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
                            f"peer pair; {A2A_LATENCY_S * 1e6:.0f} us per all_to_all_single call (assumed); "
                            "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter",
             "curve": curve}

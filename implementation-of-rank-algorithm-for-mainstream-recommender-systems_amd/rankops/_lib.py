@@ -283,6 +283,9 @@ SIGNATURES = {
     "rk_auc_workspace_size": (ctypes.c_int, [c_int64, POINTER(c_int64)]),
     "rk_auc": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rk_linear_tiled": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_void_p, c_int64, c_void_p]),
+    "rk_shard_pack_indices": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
+    "rk_shard_gather_rows": (ctypes.c_int, [_SEG_P, c_int32, c_int32, c_void_p, c_int32, c_int64, c_int64, c_int64,
+                                            c_void_p, c_void_p]),
     "rk_fm_linear_packed": (ctypes.c_int, [_SEG_P, c_int32, c_int32, c_int64, _MLP_P, c_void_p, c_int64, c_void_p,
                                            c_void_p, c_void_p]),
     "rk_bn_fold": (

@@ -18,7 +18,9 @@ rank holds a data-parallel slice of B_l samples with the indices of all F fields
                       first deep layer in one launch, the [B, F*D] deep input never written to
                       HBM; then the streamed MLP tail (DeepFM's two-launch forward)
 
-At P > 1 the steps run per chunk of the local batch (run_steps): each chunk's row all-to-all is
+At P > 1 the index exchange covers the whole local batch (one rk_shard_pack_indices launch, one
+all-to-all), then steps 2-4 run per chunk of the local batch (run_steps): each chunk's gather
+(rk_shard_gather_rows, straight from the received int32 indices) feeds a row all-to-all that is
 issued asynchronously and overlaps the next chunk's gather and the previous chunk's FM + tail.
 At P = 1 there is nothing to exchange: the forward is rk_fm_linear_packed over the packed tables
 plus the tail, i.e. `DeepFM.forward` on the same weights.
@@ -66,7 +68,9 @@ class ShardedDeepFM(EngineModule):
         self.fields_of = [[f for i, f in enumerate(self.fields) if self.owner[i] == r] for r in range(world_size)]
         self.local_fields = self.fields_of[rank]
         self.pipeline_chunks = 4  # exchange pipeline depth at P > 1 (chunk_bounds)
-        self.min_chunk = 512
+        # smallest chunk: 4096 samples keep the fused front end's 64 x 128 tiles on every CU
+        # (rk_fm_linear_packed at 2048 rows leaves half the chip idle)
+        self.min_chunk = 4096
         # all-to-all transport: None = torch.distributed.all_to_all_single on `group` (RCCL);
         # otherwise a callable (out, inp, out_splits, in_splits, async_op) -> out | (out, work)
         # with the same semantics (tests drive P shards in one process through an emulator)
@@ -145,7 +149,12 @@ class ShardedDeepFM(EngineModule):
         return [B_l * len(self.fields_of[r]) * RS for r in range(self.world)], [B_l * F_me * RS] * self.world
 
     def pack_indices(self, category: dict) -> torch.Tensor:
-        """Send buffer of step 1: [r][b][f_r] index blocks (a small permute, in index_dtype)."""
+        """Send buffer of step 1: [r][b][f_r] index blocks in index_dtype (on the GPU with int32:
+        one rk_shard_pack_indices launch)."""
+        first = category[self.fields[0]]
+        if self.index_dtype == torch.int32 and first.is_cuda and all(
+                category[f].dtype == torch.int64 and category[f].stride(0) == 1 for f in self.fields):
+            return self._pack_indices_kernel(category, first.shape[0])
         blocks = []
         for r in range(self.world):
             fr = self.fields_of[r]
@@ -155,12 +164,52 @@ class ShardedDeepFM(EngineModule):
             return torch.empty(0, dtype=self.index_dtype, device=self._device())
         return torch.cat(blocks).to(self.index_dtype)
 
+    def _pack_indices_kernel(self, category: dict, B: int) -> torch.Tensor:
+        import ctypes
+        n = len(self.fields)
+        ptrs, base, stride = (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)(), (ctypes.c_int32 * n)()
+        q, start = 0, 0
+        for r in range(self.world):
+            fr = self.fields_of[r]
+            for j, f in enumerate(fr):
+                ptrs[q], base[q], stride[q] = category[f].data_ptr(), B * start + j, len(fr)
+                q += 1
+            start += len(fr)
+        out = torch.empty(B * n, dtype=torch.int32, device=category[self.fields[0]].device)
+        lib = ops._lib.load()
+        ops._lib.ensure_device(out.device)
+        ops.check(lib.rk_shard_pack_indices(ptrs, base, stride, n, B, out.data_ptr(), ops._lib.stream_of(out)),
+                  "rk_shard_pack_indices")
+        return out
+
     def exchange_indices(self, category: dict, B_l: int, async_op: bool = False):
         """Step 1: send [r][b][f_r] index blocks; receive [s][b][f_me]."""
         send = self.pack_indices(category)
         out_s, in_s = self.index_splits(B_l)
         recv = torch.empty(sum(out_s), dtype=self.index_dtype, device=send.device)
         return self._exchange(recv, send, out_s, in_s, async_op)
+
+    def gather_rows(self, recv_idx: torch.Tensor, B_src: int, b0: int, bc: int) -> torch.Tensor:
+        """Step 2 for samples [b0, b0 + bc) of every source: rows [s][b'][f_me][RS] from this rank's
+        packed tables at the received indices (recv_idx: [s][B_src][f_me] as exchanged).  int32:
+        one rk_shard_gather_rows launch; int64: rk_concat_gather over the chunk's copy."""
+        RS, F_me = row_stride(self.embedding_dim), len(self.local_fields)
+        if recv_idx.dtype == torch.int32 and F_me > 0:
+            out = torch.empty(self.world * bc, F_me * RS, device=recv_idx.device, dtype=torch.float32)
+            if bc == 0:
+                return out
+            from ._lib import Segment
+            segs = [Segment(self.packed_table(f).data_ptr(), None, 0, self.packed_table(f).stride(0),
+                            self.packed_table(f).shape[0], RS, 0) for f in self.local_fields]
+            lib = ops._lib.load()
+            ops._lib.ensure_device(out.device)
+            ops.check(lib.rk_shard_gather_rows(ops._seg_array(segs), F_me, RS, recv_idx.data_ptr(), self.world, B_src,
+                                               b0, bc, out.data_ptr(), ops._lib.stream_of(out)), "rk_shard_gather_rows")
+            return out
+        if b0 == 0 and bc == B_src:
+            return self.gather_local(recv_idx, self.world * B_src)
+        sel = recv_idx.view(self.world, B_src, F_me)[:, b0:b0 + bc].reshape(-1)
+        return self.gather_local(sel, self.world * bc)
 
     def gather_local(self, recv_idx: torch.Tensor, rows_total: int) -> torch.Tensor:
         """Step 2: rows [s*B_l + b][f_me][RS] from this rank's tables (rk_concat_gather)."""
@@ -281,23 +330,21 @@ class ShardedDeepFM(EngineModule):
         return [(edges[i], edges[i + 1]) for i in range(C)]
 
     def run_steps(self, cat: dict, chunks: int = None):
-        """P > 1: the four steps per chunk of the local batch, pipelined — every chunk's index
-        all-to-all is issued first; then each chunk's gather runs on the compute stream while the
-        previous chunk's row all-to-all is in flight on the collective stream; the FM + tail of a
-        chunk waits only for its own rows.  Outputs are the chunks' results in sample order (each
-        sample's math is independent of the chunking)."""
+        """P > 1: one index all-to-all for the whole local batch, then steps 2-4 per chunk,
+        pipelined — each chunk's gather runs on the compute stream while the previous chunk's row
+        all-to-all is in flight on the collective stream; the FM + tail of a chunk waits only for
+        its own rows.  Outputs are the chunks' results in sample order (each sample's math is
+        independent of the chunking)."""
         if self.world == 1:
             return self.local_fm_and_tail(cat)
         B_l = cat[self.fields[0]].shape[0]
         parts = self.chunk_bounds(B_l, chunks)
-        sub = [{f: v[b0:b1] for f, v in cat.items()} for b0, b1 in parts]
-        idx = [self.exchange_indices(c, b1 - b0, async_op=True) for c, (b0, b1) in zip(sub, parts)]
+        recv_idx, work = self.exchange_indices(cat, B_l, async_op=True)
+        if work is not None:
+            work.wait()
         rows = []
-        for (recv_idx, work), (b0, b1) in zip(idx, parts):
-            if work is not None:
-                work.wait()
-            rows.append(self.exchange_rows(self.gather_local(recv_idx, self.world * (b1 - b0)), b1 - b0,
-                                           async_op=True))
+        for b0, b1 in parts:
+            rows.append(self.exchange_rows(self.gather_rows(recv_idx, B_l, b0, b1 - b0), b1 - b0, async_op=True))
         outs = []
         for (recv_rows, work), (b0, b1) in zip(rows, parts):
             if work is not None:
@@ -330,9 +377,9 @@ def _graph_of(fn):
 
 class CapturedPipeline:
     """The P > 1 exchange pipeline of ShardedDeepFM.run_steps as replayable segments.  step()
-    issues, per chunk: pack graph -> async index all-to-all; then per chunk: wait -> gather graph
-    -> async row all-to-all; then per chunk: wait -> FM + tail graph.  `outputs` are the five
-    forward outputs of the last step (concatenated over chunks by result())."""
+    issues: pack graph -> index all-to-all (whole local batch) -> per chunk: gather graph -> async
+    row all-to-all; then per chunk: wait -> FM + tail graph.  `outputs` are the five forward outputs
+    of the last step (concatenated over chunks by result())."""
 
     def __init__(self, model: ShardedDeepFM, cat: dict, chunks: int = None):
         if model.world == 1:
@@ -340,30 +387,27 @@ class CapturedPipeline:
         self.model = model
         dev = model._device()
         B_l = cat[model.fields[0]].shape[0]
+        out_i, in_i = model.index_splits(B_l)
+        self.idx_splits = (out_i, in_i)
+        self.recv_idx = torch.zeros(sum(out_i), dtype=model.index_dtype, device=dev)  # valid rows for the warm-ups
+        self.g_pack, self.send = _graph_of(lambda: model.pack_indices(cat))
         self.segs = []
         for b0, b1 in model.chunk_bounds(B_l, chunks):
             Bc = b1 - b0
-            cc = {f: v[b0:b1] for f, v in cat.items()}
-            out_i, in_i = model.index_splits(Bc)
             out_r, in_r = model.row_splits(Bc)
-            recv_idx = torch.zeros(sum(out_i), dtype=model.index_dtype, device=dev)  # valid rows for the warm-ups
             recv_rows = torch.empty(sum(out_r), dtype=torch.float32, device=dev)
-            g1, send = _graph_of(lambda cc=cc: model.pack_indices(cc))
-            g2, rows = _graph_of(lambda ri=recv_idx, Bc=Bc: model.gather_local(ri, model.world * Bc))
+            g2, rows = _graph_of(lambda b0=b0, Bc=Bc: model.gather_rows(self.recv_idx, B_l, b0, Bc))
             g3, outs = _graph_of(lambda rr=recv_rows, Bc=Bc: model.fm_and_tail(rr, Bc))
-            self.segs.append(dict(g1=g1, send=send, g2=g2, rows=rows, g3=g3, outs=outs, recv_idx=recv_idx,
-                                  recv_rows=recv_rows, idx_splits=(out_i, in_i), row_splits=(out_r, in_r)))
+            self.segs.append(dict(g2=g2, rows=rows, g3=g3, outs=outs, recv_rows=recv_rows, row_splits=(out_r, in_r)))
 
     def step(self):
         m = self.model
-        works = []
-        for s in self.segs:
-            s["g1"].replay()
-            works.append(m._exchange(s["recv_idx"], s["send"], *s["idx_splits"], async_op=True)[1])
+        self.g_pack.replay()
+        w = m._exchange(self.recv_idx, self.send, *self.idx_splits, async_op=True)[1]
+        if w is not None:
+            w.wait()
         rworks = []
-        for s, w in zip(self.segs, works):
-            if w is not None:
-                w.wait()
+        for s in self.segs:
             s["g2"].replay()
             rworks.append(m._exchange(s["recv_rows"], s["rows"].reshape(-1), *s["row_splits"], async_op=True)[1])
         for s, w in zip(self.segs, rworks):

@@ -371,6 +371,21 @@ int rk_fm_linear_packed(const rk_segment* fields, int32_t num_fields, int32_t di
                         const rk_mlp_layer* layer, float* y, int64_t ldy, float* fm1, float* fm2,
                         void* stream);
 
+/* ---- table-sharded DeepFM, the local steps around the all-to-alls (rankops.sharded; the
+ * reference's DeepFM.forward, deepfm.py:121-151, runs on one device) ---- */
+/* The index all-to-all's send buffer in one launch: slot q (fields in owner-major order) copies
+ * idx[q][0..batch) as int32 to out[base[q] + b * stride[q]] (base = batch * start_r + j,
+ * stride = F_r: blocks [r][b][f_r]).  Indices must fit int32 (the caller checks table rows). */
+int rk_shard_pack_indices(const int64_t* const* idx, const int64_t* base, const int32_t* stride,
+                          int32_t num_fields, int64_t batch, int32_t* out, void* stream);
+/* The row all-to-all's send buffer for samples [b0, b0 + bc) of every source: out[s][b'][j][0..row_floats)
+ * = packed row idx[(s * source_batch + b0 + b') * num_fields + j] of table j (tables[j]: packed
+ * rk_fm_pack_table layout, src_ld >= row_floats, 16-B aligned; idx / out / dim fields unused).
+ * Out-of-range indices write zero rows and raise RK_FLAG_INDEX_OOB. */
+int rk_shard_gather_rows(const rk_segment* tables, int32_t num_fields, int32_t row_floats, const int32_t* idx,
+                         int32_t num_sources, int64_t source_batch, int64_t b0, int64_t bc, float* out,
+                         void* stream);
+
 /* FwFM.forward (fwfm.py:114-139): per sample, logit = sum_f linear[f] row + sum_{i<j} field_weight[p]
  * <embeddings[i] row, embeddings[j] row> + bias[0] (p runs i-major over i < j, fwfm.py:129-136),
  * prob = sigmoid(logit).  embeddings[f]: table segments of width dim (out_col ignored);

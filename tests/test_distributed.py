@@ -24,6 +24,10 @@ class CpuStepsSharded(sharded.ShardedDeepFM):
     """Device steps done with torch CPU ops (test stand-ins for rk_concat_gather / rk_fm_gather /
     rk_mlp_forward); the exchange steps are inherited unchanged."""
 
+    def gather_rows(self, recv_idx, B_src, b0, bc):
+        sel = recv_idx.view(self.world, B_src, len(self.local_fields))[:, b0:b0 + bc].reshape(-1)
+        return self.gather_local(sel, self.world * bc)
+
     def gather_local(self, recv_idx, rows_total):
         D, RS, Fm = self.embedding_dim, sharded.row_stride(self.embedding_dim), len(self.local_fields)
         out = torch.full((rows_total, Fm * RS), float("nan"))

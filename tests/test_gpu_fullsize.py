@@ -104,7 +104,7 @@ def test_configs4_sharded_p1_full_tables(sharded_1e8):
 @pytest.mark.timeout(900)
 def test_configs4_sharded_p8_emulated_full_size(sharded_1e8):
     """configs[4] at full size on one GPU: 8 shards (4/4/4/4/4/4/3/3 fields of 3,333,334 rows),
-    local batch 8192 each (global 65536), the 4-chunk exchange pipeline through the emulator."""
+    local batch 8192 each (global 65536), the chunked exchange pipeline through the emulator."""
     full, fields, p = sharded_1e8
     world, B_l = 8, 8192
     emu = InProcessAllToAll(world)
@@ -125,7 +125,7 @@ def test_configs4_sharded_p8_emulated_full_size(sharded_1e8):
         return tuple(o.cpu() for o in out)
 
     outs = run_ranks(world, rank_fn, on_error=emu.abort)
-    assert emu.calls == 2 * 4
+    assert emu.calls == 1 + 2  # one index exchange, then 2 chunks of 4096 (min_chunk) of rows
     with torch.no_grad():
         expect = ref.deepfm_forward(p, cat, list(fields), 3)
     for r, got in enumerate(outs):

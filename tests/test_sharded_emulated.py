@@ -1,5 +1,5 @@
 """The P > 1 table-sharded DeepFM (rankops.sharded, BASELINE configs[4]) with P shards in one
-process on one device: every device step is the real one — pack_indices, gather_local
+process on one device: every device step is the real one — pack_indices, gather_rows / gather_local
 (rk_concat_gather over the packed tables), fm_and_tail (rk_fm_gather over the received rows'
 dense segments + the fused tail) and run_steps' chunk pipeline — and only the RCCL transport is
 replaced by the in-process all-to-all emulator (tests/a2a_emulator.py).  Outputs are compared
@@ -72,7 +72,7 @@ def test_emulator_routes_like_gloo_cpu(world, chunks):
     outs = run_ranks(world, rank_fn, on_error=emu.abort)
     for r, got in enumerate(outs):
         _check(got, expect, r * B, (r + 1) * B, 1e-5)
-    assert emu.calls == 2 * chunks
+    assert emu.calls == 1 + chunks  # one index exchange, then one row exchange per chunk
 
 
 @pytest.mark.gpu
@@ -179,7 +179,7 @@ def test_captured_pipeline_emulated_on_gpu(world):
     outs = run_ranks(world, rank_fn, on_error=emu.abort)
     for r, got in enumerate(outs):
         _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
-    assert emu.calls == 2 * 2 * 4
+    assert emu.calls == 2 * (1 + 4)
     import rankops
     assert rankops.error_flags() == 0  # the capture's warm-up gathers read valid (zeroed) indices
 
@@ -211,3 +211,36 @@ def test_fused_front_and_unfused_path_match_oracle(world, fused):
         _check(got, expect, r * B_l, (r + 1) * B_l, 1e-4)
     import rankops
     assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shard_pack_and_gather_kernels(world):
+    """rk_shard_pack_indices equals the torch stack/cat/cast permute; rk_shard_gather_rows equals
+    the packed-table rows at the received indices for a chunk [b0, b0 + bc) of every source, and an
+    out-of-range index gives a zero row and raises RK_FLAG_INDEX_OOB."""
+    import rankops
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    shards, _ = _shards(full, world)
+    sh = shards[0]
+    B = 777
+    g = torch.Generator().manual_seed(world)
+    cat = {f: torch.randint(0, n, (B,), generator=g).cuda() for f, n in FIELDS30.items()}
+    got = sh.pack_indices(cat)
+    want = torch.cat([torch.stack([cat[f] for f in fr], 1).reshape(-1) for fr in sh.fields_of if fr]).to(torch.int32)
+    assert got.dtype == torch.int32 and torch.equal(got, want)
+    F_me = len(sh.local_fields)
+    recv = torch.stack([torch.randint(0, FIELDS30[f], (world, B), generator=g) for f in sh.local_fields], 2)
+    recv[1, 5, 0] = sh.packed_table(sh.local_fields[0]).shape[0]  # one past the table's last row: OOB
+    recv_d = recv.reshape(-1).to(torch.int32).cuda()
+    rankops.error_flags(reset=True)
+    RS = sharded.row_stride(32)
+    for b0, bc in ((0, B), (100, 333), (776, 1)):
+        rows = sh.gather_rows(recv_d, B, b0, bc).view(world, bc, F_me, RS).cpu()
+        for j, f in enumerate(sh.local_fields):
+            tab = sh.packed_table(f).cpu()
+            idx = recv[:, b0:b0 + bc, j]
+            ok = idx < tab.shape[0]
+            exp = tab[idx.clamp(max=tab.shape[0] - 1)] * ok[..., None]
+            assert torch.equal(rows[:, :, j, :], exp[:, :, :RS])
+    assert rankops.error_flags(reset=True) & 1
