@@ -198,13 +198,42 @@ def graph_kernel_avg_ms(launch, per_graph=20, iters=10):
 
 # ------------------------------------------------------------------ PMC traffic (profiles/traffic.json)
 
-def load_traffic(kernel: str, workload_name: str):
-    path = os.path.join(REPO, "profiles", "traffic.json")
+COUNTERS_FILE = os.path.join("profiles", "counters.json")  # tools/r04_counters.sh -> tools/pmc_counters.py
+
+
+def load_counters(kernel: str, workload_name: str):
+    """The committed counter digest of `kernel` under `workload_name` (profiles/counters.json: SQ
+    MFMA-busy and wait counters, the profiled average duration, PMC HBM bytes), or None."""
     try:
-        with open(path) as f:
-            return json.load(f).get(f"{workload_name}:{kernel}")
+        with open(os.path.join(REPO, COUNTERS_FILE)) as f:
+            e = json.load(f).get(f"{workload_name}:{kernel}")
     except (OSError, ValueError):
         return None
+    if e is not None:
+        e = dict(e, file=COUNTERS_FILE)
+    return e
+
+
+def load_traffic(kernel: str, workload_name: str):
+    """PMC-measured HBM bytes per launch of `kernel` (profiles/counters.json)."""
+    e = load_counters(kernel, workload_name)
+    if not e or "traffic" not in e:
+        return None
+    return dict(e["traffic"], file=COUNTERS_FILE, session=e.get("session"))
+
+
+def counter_fields(kernel: str, workload_name: str, flop_per_launch: float = None):
+    """mfma_busy_frac and the profiled duration (plus the roofline fraction at that duration)
+    from the committed counter digest, for a bench roofline block."""
+    e = load_counters(kernel, workload_name)
+    if not e:
+        return {"mfma_busy_frac": None, "counters": None}
+    out = {"mfma_busy_frac": e.get("mfma_busy_frac"),
+           "counters": {k: e.get(k) for k in ("file", "session", "mfma_busy_cycles_per_simd", "busy_cycles_per_se",
+                                              "clock_ghz", "trace_avg_ns")}}
+    if flop_per_launch and e.get("trace_avg_ns"):
+        out["frac_at_profiled_duration"] = round(flop_per_launch / (e["trace_avg_ns"] * 1e-9) / PEAK_FP32_MFMA, 4)
+    return out
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
@@ -637,6 +666,43 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
     return out
 
 
+# ------------------------------------------------------------------ DCN / BST kernel rooflines
+
+DCN_EXEC_FLOP = 2 * (64 * 512 + 512 * 256 + 256 * 128 + 128) + 3 * 4 * 50  # padded MLP widths + head + cross
+
+
+def dcn_roofline(model, inp, batch):
+    """dcn_fused_kernel (the whole DCN forward, one launch): 20 back-to-back forwards captured in
+    one hipGraph, HIP events on the replay stream (the ~1.5 us dependent-launch boundary included)."""
+    import helpers as H
+    ms = graph_kernel_avg_ms(lambda: H.call_model(model, "dcn", inp))
+    flop = DCN_FLOP * batch
+    r = {"kernel": "dcn_fused_kernel<1, StreamPlan<4,32,16,8>>", "bound": "mfma", "unit": "TFLOP/s",
+         "peak": PEAK_FP32_MFMA / 1e12, "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
+         "flop_basis": "reference formulation per sample: 379,236 (cross 3 x 4 x 50 + 50->512->256->128->1 MLP, "
+                       "SURVEY §8d)",
+         "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4),
+         "executed_flop_per_launch": DCN_EXEC_FLOP * batch,
+         "frac_executed": round(DCN_EXEC_FLOP * batch / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
+    r.update(counter_fields("dcn_fused_kernel", "dcn", flop))
+    return r
+
+
+def bst_roofline(model, inp, batch):
+    """bst_block_kernel (every transformer block + pooling of the BST forward, one launch) timed
+    alone: back-to-back launches, HIP events on the stream they run on."""
+    launch = model.blocks_kernel_launcher(inp["seq_feedid"], inp["seq_length"])
+    ms = kernel_avg_ms(launch, 20)
+    flop = BST_BLOCK_FLOP * batch
+    r = {"kernel": "bst_block_kernel", "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_FP32_MFMA / 1e12,
+         "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
+         "flop_basis": "14,680,064 per sample per block: QKV/O projections, QK^T and AV over T = 64, FFN "
+                       "(d_model 128, 4 heads; SURVEY §8d)",
+         "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
+    r.update(counter_fields("bst_block_kernel", "bst", flop))
+    return r
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
@@ -742,7 +808,9 @@ def main():
                               "flop_basis": "reference formulation per sample: att-MLP 1,027,200 + cross/"
                                             "weighted sum 6,400 + fcn 444,672 (SURVEY §8d)",
                               "executed_flop_per_launch": DIN_FWD_EXEC_FLOP * args.batch,
+                              "frac_executed": round(DIN_FWD_EXEC_FLOP * args.batch / (ms * 1e-3) / PEAK_FP32_MFMA, 4),
                               "traffic": load_traffic("din_forward_kernel", "din")}
+        result["roofline"].update(counter_fields("din_forward_kernel", "din", flop))
     if rank == 0 and world == 1 and not args.no_extras:
         extras = {}
         for name in [m for m in args.models.split(",") if m]:
@@ -754,6 +822,11 @@ def main():
                 r["eager_over_graph"] = round(r["ms_per_step"] / extras[name[:-6]]["ms_per_step"], 3)
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
+                r["roofline"] = bst_roofline(m2, inp2, batch)
+            if name == "dcn":
+                r["roofline"] = dcn_roofline(m2, inp2, batch)
+            if name == "deepfm":
+                r["mfma_busy"] = {k: counter_fields(k, "deepfm") for k in ("linear_tiled_kernel", "mlp_stream_kernel")}
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob

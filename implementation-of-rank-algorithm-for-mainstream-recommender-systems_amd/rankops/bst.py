@@ -256,6 +256,21 @@ class BSTModel(EngineModule):
         run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
         return probs, logits
 
+    def blocks_kernel_launcher(self, seq_feedid, seq_length):
+        """Zero-argument re-launch of this forward's rk_bst_forward_blocks kernel (every block +
+        pooling) into a scratch DNN row, for kernel-level timing (bench.py BST roofline)."""
+        seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
+        seq_length = ops.as_index(seq_length, "seq_length")
+        B, T = seq_feedid.shape
+        blocks = self._fused_blocks(T)
+        if blocks is None or not self.transformer_blocks:
+            raise RuntimeError("BST configuration outside rk_bst_forward_blocks' envelope")
+        d = self.d_model
+        row = torch.empty(B, d, device=seq_feedid.device, dtype=torch.float32)
+        return lambda: ops.bst_forward_blocks(self.embeddings['feedid'].weight, seq_feedid, seq_length, d,
+                                              self.transformer_blocks[0].nhead, blocks, ops._lib.fptr(row, 0), d,
+                                              self.pooling_method != 'sum')
+
     def _fused_blocks(self, T):
         """Parameters for rk_bst_forward_blocks, or None outside its envelope (d_model 128,
         4 heads, T <= 64, <= 4 blocks, contiguous 16-B aligned fp32 parameters)."""

@@ -27,7 +27,11 @@ def main():
     import rankops
     rankops.load_library()
     batch = args.batch or (2048 if args.workload == "bst" else 4096)
-    model, inp, fn, cfg, name = bench.workload(args.workload, batch, 0)
+    gather = args.workload == "deepfm_gather"  # rk_fm_gather_packed alone (bench.py gather_roofline)
+    model, inp, fn, cfg, name = bench.workload("deepfm" if gather else args.workload, batch, 0)
+    if gather:
+        launch = model.gather_launcher(inp["category"])
+        fn = lambda: [launch() for _ in range(20)]  # noqa: E731
     torch.cuda.synchronize()
     if args.eager:
         with torch.no_grad():
