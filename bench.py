@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--no-model-curve", action="store_true", help="skip the modelled 1->8 GPU curve of configs[4]")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,fwfm,din_per_call,din_zipf,"
+    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,bst_ref,fwfm,din_per_call,din_zipf,"
                                         "dcn_eager,din_eager,deepfm_eager,bst_eager")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step legs")
@@ -123,6 +123,9 @@ def workload(name: str, batch: int, seed: int, zipf: float = None):
         model_name = "deepfm"
     elif name == "bst":
         cfg = {"vocab": H.WECHAT_VOCAB, "T": 64, "dim": 128, "heads": 4, "max_len": 64}
+        model_name = "bst"
+    elif name == "bst_ref":  # the reference script's own shape: d_model 16 (bst.py:192,339-349), 4 heads, T 50
+        cfg = {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 16, "heads": 4, "max_len": 50}
         model_name = "bst"
     elif name == "fwfm":
         cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8}

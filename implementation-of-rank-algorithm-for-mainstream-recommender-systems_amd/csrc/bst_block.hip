@@ -503,8 +503,12 @@ RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t
                                  int32_t heads, int32_t nblocks, const float* const* block_params,
                                  const float* block_scalars, float* pool_out, int64_t ld_pool, int32_t pool_mean,
                                  void* stream) {
+  if (d_model == 16)  // the reference script's own width (bst.py:192): bst_small.hip
+    return bst_small_forward(table, table_rows, ld_table, seq, ld_seq, T, seq_len, batch, heads, nblocks, block_params,
+                             block_scalars, pool_out, ld_pool, pool_mean, (hipStream_t)stream);
   if (d_model != kBD || heads != 4)
-    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: d_model=%d heads=%d (fused path: 128/4)", d_model, heads);
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: d_model=%d heads=%d (fused paths: 128/4, 16/1-8)", d_model,
+                heads);
   if (T <= 0 || T > kBT) return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: T=%d outside [1, %d]", T, kBT);
   if (nblocks <= 0 || nblocks > kBMaxBlocks)
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: %d blocks (max %d)", nblocks, kBMaxBlocks);

@@ -1,0 +1,296 @@
+// Fused BST transformer block(s) + pooling at the reference script's own width: d_model 16
+// (bst.py:192 hard-codes it; heads 1/2/4/8, T <= 64).  Reference: BSTTransformer.forward
+// bst.py:66-91, the pooling of BSTModel.forward bst.py:224-241.
+//
+// At d 16 a sample's whole block is ~0.3 MFLOP over 3.2 KB of gathered rows: the per-layer path
+// (five rk_linear GEMMs of K = N = 16 and the attention kernel, the sequence round-tripping
+// through HBM between them, ~370 us per 4096-sample batch) is launch- and traffic-bound.  Here one
+// wave owns one sample and lane t owns position t: the position's 16-wide rows (x, q, k, v,
+// context, the FFN activations) live in registers, every projection is a per-lane 16 x 16
+// matrix-vector product, and only K and V go through LDS (broadcast ds_read_b128: each query lane
+// walks every key).  Softmax is two-pass
+// (max, then exp-sum and P.V) per head, masked keys at -inf as bst.py:80 (an all-masked row gives
+// NaN as torch's softmax does).  f32 VALU throughout; the block is ~3k FMAs per lane.
+//
+// Weights and biases are read with uniform addresses straight from global memory, so they come in
+// through the scalar cache into SGPRs (s_load), one operand of each v_fma: LDS carries only K and V.
+//
+// Work split: 256-thread workgroups (4 waves), persistent — each wave walks samples
+// b = (blockIdx.x * 4 + wave) + k * gridDim.x * 4.
+#include "common.h"
+
+namespace rk {
+
+constexpr int kSD = 16;        // d_model
+constexpr int kST = 64;        // positions (one per lane)
+constexpr int kSMaxBlocks = 4;
+constexpr int kSWaves = 4;
+
+struct BstSmallW {
+  const float* p[17];  // the header's order: pos, wq, bq, wk, bk, wv, bv, wo, bo, w1, b1, w2, b2, g1, be1, g2, be2
+  float eps1, eps2, slope;
+};
+
+struct BstSmallArgs {
+  const float* table;
+  int64_t rows, ld;
+  const int64_t* seq;
+  int64_t ld_seq;
+  int T;
+  const int64_t* seq_len;
+  int64_t batch;
+  int nblocks;
+  BstSmallW blk[kSMaxBlocks];
+  float* pool_out;
+  int64_t ld_pool;
+  int pool_mean;
+  uint32_t* flags;
+};
+
+typedef float f4s __attribute__((ext_vector_type(4)));
+// read-only parameters through the constant address space: uniform loads become s_load (SGPRs)
+typedef const __attribute__((address_space(4))) float cfloat;
+typedef const __attribute__((address_space(4))) f4s cf4s;
+
+// y = W x + b for one lane (W row-major [16][16], nn.Linear layout; uniform loads -> SGPRs)
+__device__ __forceinline__ void matvec16(const float* Wg, const float* bg, const float (&x)[kSD], float (&y)[kSD]) {
+  const cfloat* bias = (const cfloat*)bg;
+#pragma unroll
+  for (int o = 0; o < kSD; ++o) {
+    // row o's address waits for row o - 2's result: at most two 16-float rows in SGPRs at a time
+    // (the scheduler otherwise issues all 16 row loads up front and spills SGPRs to VGPR lanes)
+    const float* row = Wg + o * kSD;
+    if (o >= 2) asm volatile("" : "+s"(row) : "v"(y[o - 2]));
+    const cfloat* W = (const cfloat*)row;
+    float s = bias[o];
+#pragma unroll
+    for (int q = 0; q < kSD / 4; ++q) {
+      const f4s w = *(const cf4s*)(W + 4 * q);
+      s = fmaf(w[0], x[4 * q], s);
+      s = fmaf(w[1], x[4 * q + 1], s);
+      s = fmaf(w[2], x[4 * q + 2], s);
+      s = fmaf(w[3], x[4 * q + 3], s);
+    }
+    y[o] = s;
+  }
+}
+
+// LayerNorm over the lane's 16 values (biased variance, as torch.nn.LayerNorm)
+__device__ __forceinline__ void layernorm16(float (&x)[kSD], const float* gg, const float* bg, float eps) {
+  const cfloat* g = (const cfloat*)gg;
+  const cfloat* be = (const cfloat*)bg;
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSD; ++i) m += x[i];
+  m = m / (float)kSD;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSD; ++i) {
+    const float d = x[i] - m;
+    v = fmaf(d, d, v);
+  }
+  v = v / (float)kSD;
+  const float r = 1.0f / sqrtf(v + eps);
+#pragma unroll
+  for (int i = 0; i < kSD; ++i) x[i] = (x[i] - m) * r * g[i] + be[i];
+}
+
+template <int NH>
+__global__ __launch_bounds__(kSWaves * 64, 4) void bst_small_kernel(BstSmallArgs a) {
+  constexpr int DH = kSD / NH;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* const kv = sm + wave * 2 * kST * kSD;  // this wave's K [64][16], V [64][16]
+  float* const Ks = kv;
+  float* const Vs = kv + kST * kSD;
+  const float qscale = 1.0f / sqrtf((float)DH);
+
+  for (int64_t b = (int64_t)blockIdx.x * kSWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kSWaves) {
+    const int T = a.T;
+    const bool pos_live = lane < T;
+    const int64_t len = a.seq_len[b];
+    float x[kSD];
+    {
+      const int64_t r = pos_live ? a.seq[b * a.ld_seq + lane] : 0;
+      const bool ok = r >= 0 && r < a.rows;
+      if (pos_live && !ok) flag_oob(a.flags);
+      const float* src = a.table + (ok ? r : 0) * a.ld;
+#pragma unroll
+      for (int q = 0; q < kSD / 4; ++q) {
+        const f4s v = *reinterpret_cast<const f4s*>(src + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[4 * q + e] = (pos_live && ok) ? v[e] : 0.f;
+      }
+    }
+    for (int blk = 0; blk < a.nblocks; ++blk) {
+      // the parameter pointers laundered per sample and block: loads through them stay inside the
+      // loop (hoisted out of the sample loop, all 1.7k weights would be live in SGPRs and spill)
+      BstSmallW w;
+#pragma unroll
+      for (int k = 0; k < 17; ++k) {
+        const float* pk = a.blk[blk].p[k];
+        asm volatile("" : "+s"(pk));
+        w.p[k] = pk;
+      }
+      w.eps1 = a.blk[blk].eps1;
+      w.eps2 = a.blk[blk].eps2;
+      w.slope = a.blk[blk].slope;
+      // queries / keys get the position embedding, values do not (bst.py:69-71)
+      float qin[kSD];
+      {
+        const float* pp = w.p[0] + (pos_live ? lane : 0) * kSD;
+#pragma unroll
+        for (int q4 = 0; q4 < kSD / 4; ++q4) {
+          const f4s v = *reinterpret_cast<const f4s*>(pp + 4 * q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) qin[4 * q4 + e] = x[4 * q4 + e] + (pos_live ? v[e] : 0.f);
+        }
+      }
+      float q[kSD], t16[kSD];
+      matvec16(w.p[3], w.p[4], qin, t16);  // k
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < kSD / 4; ++i)
+        *reinterpret_cast<f4s*>(Ks + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
+      matvec16(w.p[5], w.p[6], x, t16);  // v
+#pragma unroll
+      for (int i = 0; i < kSD / 4; ++i)
+        *reinterpret_cast<f4s*>(Vs + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
+      matvec16(w.p[1], w.p[2], qin, q);  // q
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      // scores s_h[j] = q_h . k_h[j] / sqrt(dh), keys j >= len masked (-inf); two-pass softmax
+      float m[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) m[h] = -INFINITY;
+      for (int j = 0; j < T; ++j) {
+        float k[kSD];
+#pragma unroll
+        for (int i = 0; i < kSD / 4; ++i) {
+          const f4s v = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
+          k[4 * i] = v[0], k[4 * i + 1] = v[1], k[4 * i + 2] = v[2], k[4 * i + 3] = v[3];
+        }
+        const bool masked = (int64_t)j >= len;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
+          s = masked ? -INFINITY : s * qscale;
+          m[h] = fmaxf(m[h], s);
+        }
+      }
+      float l[NH], ctx[kSD];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) l[h] = 0.f;
+#pragma unroll
+      for (int i = 0; i < kSD; ++i) ctx[i] = 0.f;
+      for (int j = 0; j < T; ++j) {
+        float k[kSD], v[kSD];
+#pragma unroll
+        for (int i = 0; i < kSD / 4; ++i) {
+          const f4s kv4 = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
+          const f4s vv4 = *reinterpret_cast<const f4s*>(Vs + j * kSD + 4 * i);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) k[4 * i + e] = kv4[e], v[4 * i + e] = vv4[e];
+        }
+        const bool masked = (int64_t)j >= len;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
+          s = masked ? -INFINITY : s * qscale;
+          const float p = expf(s - m[h]);
+          l[h] += p;
+#pragma unroll
+          for (int e = 0; e < DH; ++e) ctx[h * DH + e] = fmaf(p, v[h * DH + e], ctx[h * DH + e]);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int e = 0; e < DH; ++e) ctx[h * DH + e] = ctx[h * DH + e] / l[h];
+      // out1 = norm1(queries + W_o ctx) (dropout: identity in eval)
+      float o[kSD];
+      matvec16(w.p[7], w.p[8], ctx, o);
+#pragma unroll
+      for (int i = 0; i < kSD; ++i) o[i] = qin[i] + o[i];
+      layernorm16(o, w.p[13], w.p[14], w.eps1);
+      // out = norm2(out1 + ffn(out1)), ffn = Linear, LeakyReLU, (Dropout), Linear
+      matvec16(w.p[9], w.p[10], o, t16);
+      const float slope = w.slope;
+#pragma unroll
+      for (int i = 0; i < kSD; ++i) t16[i] = t16[i] >= 0.f ? t16[i] : t16[i] * slope;
+      matvec16(w.p[11], w.p[12], t16, x);
+#pragma unroll
+      for (int i = 0; i < kSD; ++i) x[i] = o[i] + x[i];
+      layernorm16(x, w.p[15], w.p[16], w.eps2);
+      __builtin_amdgcn_wave_barrier();  // K / V are rewritten by the next block (or sample)
+    }
+    // pooling over all T positions (bst.py:236-241: the padded positions' outputs included)
+    float pooled = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSD; ++i) {
+      const float s = wave_sum(pos_live ? x[i] : 0.f);
+      pooled = lane == i ? s : pooled;
+    }
+    if (lane < kSD) {
+      const float v = a.pool_mean ? pooled / (float)len : pooled;
+      a.pool_out[b * a.ld_pool + lane] = v;
+    }
+  }
+}
+
+int bst_small_forward(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq, int64_t ld_seq,
+                      int32_t T, const int64_t* seq_len, int64_t batch, int32_t heads, int32_t nblocks,
+                      const float* const* block_params, const float* block_scalars, float* pool_out, int64_t ld_pool,
+                      int32_t pool_mean, hipStream_t st) {
+  if (heads != 1 && heads != 2 && heads != 4 && heads != 8)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: d_model 16 with %d heads (1, 2, 4 or 8)", heads);
+  if (T <= 0 || T > kST) return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: T=%d outside [1, %d]", T, kST);
+  if (nblocks <= 0 || nblocks > kSMaxBlocks)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: %d blocks (max %d)", nblocks, kSMaxBlocks);
+  if (!table || !seq || !seq_len || !block_params || !block_scalars || !pool_out || ld_table % 4 ||
+      ((uintptr_t)table & 15u) || ld_seq < T || ld_pool < kSD || table_rows <= 0)
+    return fail(RK_ERR_INVALID, "rk_bst_forward_blocks: bad arguments");
+  BstSmallArgs a = {};
+  a.table = table;
+  a.rows = table_rows;
+  a.ld = ld_table;
+  a.seq = seq;
+  a.ld_seq = ld_seq;
+  a.T = T;
+  a.seq_len = seq_len;
+  a.batch = batch;
+  a.nblocks = nblocks;
+  for (int i = 0; i < nblocks; ++i) {
+    for (int k = 0; k < 17; ++k) {
+      const float* p = block_params[17 * i + k];
+      if (!p || ((uintptr_t)p & 15u))
+        return fail(RK_ERR_INVALID, "rk_bst_forward_blocks: block %d parameter %d null or misaligned", i, k);
+      a.blk[i].p[k] = p;
+    }
+    a.blk[i].eps1 = block_scalars[3 * i];
+    a.blk[i].eps2 = block_scalars[3 * i + 1];
+    a.blk[i].slope = block_scalars[3 * i + 2];
+  }
+  a.pool_out = pool_out;
+  a.ld_pool = ld_pool;
+  a.pool_mean = pool_mean;
+  a.flags = device_flags();
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_bst_forward_blocks: negative batch");
+  const size_t shm = (size_t)(kSWaves * 2 * kST * kSD) * sizeof(float);
+  const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / shm)));
+  const int64_t need = (batch + kSWaves - 1) / kSWaves;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)num_cus() * per_cu));
+  switch (heads) {
+    case 1: bst_small_kernel<1><<<grid, kSWaves * 64, shm, st>>>(a); break;
+    case 2: bst_small_kernel<2><<<grid, kSWaves * 64, shm, st>>>(a); break;
+    case 4: bst_small_kernel<4><<<grid, kSWaves * 64, shm, st>>>(a); break;
+    default: bst_small_kernel<8><<<grid, kSWaves * 64, shm, st>>>(a); break;
+  }
+  return check_launch("rk_bst_forward_blocks (d_model 16)");
+}
+
+}  // namespace rk

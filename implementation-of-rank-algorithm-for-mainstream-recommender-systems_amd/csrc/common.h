@@ -38,6 +38,12 @@ bool gemm_rows_try(const float* A, int64_t lda, const float* A_mask, const float
                    int64_t ldb, int b_trans, int64_t M, int N, int K, float* C, int64_t ldc, int accumulate,
                    const rk_epilogue* ep, hipStream_t st);
 
+// rk_bst_forward_blocks at d_model 16 (bst_small.hip)
+int bst_small_forward(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq, int64_t ld_seq,
+                      int32_t T, const int64_t* seq_len, int64_t batch, int32_t heads, int32_t nblocks,
+                      const float* const* block_params, const float* block_scalars, float* pool_out, int64_t ld_pool,
+                      int32_t pool_mean, hipStream_t st);
+
 // ---- device helpers ----
 // Wave index of the calling thread in its workgroup, as a wave-uniform (SGPR) value: branches and
 // addresses that depend only on it compile to scalar code.

@@ -272,12 +272,16 @@ class BSTModel(EngineModule):
                                               self.pooling_method != 'sum')
 
     def _fused_blocks(self, T):
-        """Parameters for rk_bst_forward_blocks, or None outside its envelope (d_model 128,
-        4 heads, T <= 64, <= 4 blocks, contiguous 16-B aligned fp32 parameters)."""
+        """Parameters for rk_bst_forward_blocks, or None outside its envelope: d_model 128 with 4
+        heads (bst_block_kernel) or the reference script's d_model 16 with 1/2/4/8 heads
+        (bst_small_kernel); T <= 64, <= 4 blocks, contiguous 16-B aligned fp32 parameters."""
         blks = self.transformer_blocks
-        if not (common.FUSED_BST and self.d_model == 128 and 1 <= T <= 64 and len(blks) <= 4
-                and self.embeddings['feedid'].weight.stride(0) == 128
-                and all(b.nhead == 4 for b in blks)):
+        d = self.d_model
+        heads_ok = (lambda h: h == 4) if d == 128 else (lambda h: h in (1, 2, 4, 8))
+        if not (common.FUSED_BST and d in (16, 128) and 1 <= T <= 64 and len(blks) <= 4
+                and self.embeddings['feedid'].weight.stride(0) == d
+                and self.embeddings['feedid'].weight.data_ptr() % 16 == 0
+                and all(heads_ok(b.nhead) for b in blks)):
             return None
         out = []
         for b in blks:

@@ -53,54 +53,134 @@ def table_rows(vocab_dir, field: str, vocab_sizes: Optional[dict] = None) -> int
 
 # ---------------------------------------------------------------- per-call random weights (H2)
 # The reference re-creates these layers inside forward() from the default CPU generator on
-# every call; the draw order below is the reference's construction order.
+# every call; the draw order below is the reference's construction order.  Each draw is an
+# H2Spec: the tensor shapes, a `fill` that makes exactly the reference's generator calls into
+# preallocated tensors (nn.Linear.reset_parameters' kaiming_uniform_ then uniform_, or
+# cross_layer's xavier_normal_ / zeros_), and a `pack` that returns them in the models' layout.
+# Drawing into preallocated views instead of constructing nn.Linear modules gives bit-identical
+# values (the same generator calls on the same shapes) without the module overhead, and lets the
+# per-call mode draw straight into a pinned staging buffer (H2Stage).
+
+@dataclass
+class H2Spec:
+    shapes: list
+    fill: object
+    pack: object
+
+
+def linear_fill(w: torch.Tensor, b: torch.Tensor):
+    """nn.Linear.reset_parameters' draws into preallocated tensors: kaiming_uniform_(a=sqrt(5))
+    on the weight, then uniform_(-1/sqrt(fan_in), 1/sqrt(fan_in)) on the bias."""
+    nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    fan_in = w.shape[1]
+    bound = 1 / math.sqrt(fan_in) if fan_in > 0 else 0
+    nn.init.uniform_(b, -bound, bound)
+
+
+def cross_spec(dim: int, num_layers: int) -> H2Spec:
+    """cross_layer(): w ~ xavier_normal_ on a (d, 1) tensor, b = 0, per layer (dcn.py:37-41)."""
+    def fill(v):
+        for l in range(num_layers):
+            nn.init.xavier_normal_(v[0][l].view(dim, 1))
+            nn.init.zeros_(v[1][l].view(dim, 1))
+    return H2Spec([(num_layers, dim), (num_layers, dim)], fill, lambda v: (v[0], v[1]))
+
+
+def din_attention_spec(embedding_dim: int) -> H2Spec:
+    """din_attention(): Linear(4H,64), Linear(64,32), Linear(32,1) in order (din.py:61-67)."""
+    H = embedding_dim
+
+    def fill(v):
+        linear_fill(v[0], v[1])
+        linear_fill(v[2], v[3])
+        linear_fill(v[4], v[5])
+    return H2Spec([(64, 4 * H), (64,), (32, 64), (32,), (1, 32), (1,)], fill, list)
+
+
+def residual_spec(dim: int, internal_dim: int, num_units: int) -> H2Spec:
+    """residual_unit(): Linear(d, I) then Linear(I, d), per unit (deepcrossing.py:37-39)."""
+    def fill(v):
+        for u in range(num_units):
+            linear_fill(v[4 * u], v[4 * u + 1])
+            linear_fill(v[4 * u + 2], v[4 * u + 3])
+    shapes = [(internal_dim, dim), (internal_dim,), (dim, internal_dim), (dim,)] * num_units
+    return H2Spec(shapes, fill, lambda v: [list(v[4 * u:4 * u + 4]) for u in range(num_units)])
+
+
+def draw_spec(spec: H2Spec):
+    """The spec's draws into fresh host tensors."""
+    views = [torch.empty(s) for s in spec.shapes]
+    spec.fill(views)
+    return spec.pack(views)
+
 
 def draw_cross_layers(dim: int, num_layers: int):
-    """cross_layer(): w ~ xavier_normal_ on a (d, 1) tensor, b = 0, per layer (dcn.py:37-41)."""
-    ws, bs = [], []
-    for _ in range(num_layers):
-        w = torch.zeros(dim, 1)
-        b = torch.zeros(dim, 1)
-        nn.init.xavier_normal_(w)
-        nn.init.zeros_(b)
-        ws.append(w.reshape(dim))
-        bs.append(b.reshape(dim))
-    if not ws:
-        return torch.zeros(0, dim), torch.zeros(0, dim)
-    return torch.stack(ws), torch.stack(bs)
+    return draw_spec(cross_spec(dim, num_layers))
 
 
 def draw_din_attention(embedding_dim: int):
-    """din_attention(): Linear(4H,64), Linear(64,32), Linear(32,1) in order (din.py:61-67)."""
-    l1 = nn.Linear(4 * embedding_dim, 64)
-    l2 = nn.Linear(64, 32)
-    l3 = nn.Linear(32, 1)
-    return [t.detach() for t in (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)]
+    return draw_spec(din_attention_spec(embedding_dim))
 
 
 def draw_residual_units(dim: int, internal_dim: int, num_units: int):
-    """residual_unit(): Linear(d, I) then Linear(I, d), per unit (deepcrossing.py:37-39)."""
-    units = []
-    for _ in range(num_units):
-        a = nn.Linear(dim, internal_dim)
-        b = nn.Linear(internal_dim, dim)
-        units.append([t.detach() for t in (a.weight, a.bias, b.weight, b.bias)])
-    return units
+    return draw_spec(residual_spec(dim, internal_dim, num_units))
+
+
+class H2Stage:
+    """Per-call draws for a GPU forward: the generator calls write straight into one of two pinned
+    host buffers, one asynchronous host-to-device copy per forward moves them into a fresh device
+    buffer (stream-ordered before the forward's kernels; the caching allocator keeps it alive for
+    them), and the device views are returned in the model's layout.  A buffer is reused only after
+    the copy that read it has completed (its event)."""
+
+    def __init__(self):
+        self._host = [None, None]
+        self._events = [None, None]
+        self._turn = 0
+
+    def draw(self, spec: H2Spec, device):
+        sizes = [math.prod(s) for s in spec.shapes]
+        n = sum(sizes)
+        i = self._turn
+        self._turn ^= 1
+        if self._events[i] is not None:
+            self._events[i].synchronize()
+        host = self._host[i]
+        if host is None or host.numel() < n:
+            host = torch.empty(max(n, 1024), dtype=torch.float32, pin_memory=True)
+            self._host[i] = host
+        views, off = [], 0
+        for s, k in zip(spec.shapes, sizes):
+            views.append(host[off:off + k].view(s))
+            off += k
+        spec.fill(views)
+        dev = torch.empty(max(n, 1), dtype=torch.float32, device=device)
+        dev[:n].copy_(host[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._events[i] = ev
+        out, off = [], 0
+        for s, k in zip(spec.shapes, sizes):
+            out.append(dev[off:off + k].view(s))
+            off += k
+        return spec.pack(out)
 
 
 class InteractionWeights:
     """Holds the H2 weights for one model.  mode 'per_call' redraws them on every forward
     exactly like the reference; 'frozen' draws them once (on the first forward, with the same
-    generator calls) and keeps them resident on the device."""
+    generator calls) and keeps them resident on the device.  `spec` returns the H2Spec of the
+    draws (shapes, the reference's generator calls, layout)."""
 
     MODES = ("per_call", "frozen")
 
-    def __init__(self, mode: str, draw):
+    def __init__(self, mode: str, spec):
         if mode not in self.MODES:
             raise ValueError(f"interaction_weights must be one of {self.MODES}, got {mode!r}")
         self.mode = mode
-        self._draw = draw
+        self._spec = spec
         self._cached = None
+        self._stage = H2Stage()
 
     def get(self, device):
         if self.mode == "frozen" and self._cached is not None and self._cached[0] == device:
@@ -109,8 +189,9 @@ class InteractionWeights:
             raise RuntimeError("per-call interaction weights are drawn on the host each forward and cannot be "
                                "captured in a hipGraph; use interaction_weights='frozen' (or run the forward once "
                                "before capturing)")
-        host = self._draw()
-        dev = _to_device(host, device)
+        if self.mode == "per_call" and torch.device(device).type == "cuda":
+            return self._stage.draw(self._spec(), device)
+        dev = _to_device(draw_spec(self._spec()), device)
         if self.mode == "frozen":
             self._cached = (device, dev)
         return dev

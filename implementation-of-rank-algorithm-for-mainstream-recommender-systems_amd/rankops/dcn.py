@@ -22,7 +22,8 @@ import torch
 import torch.nn as nn
 
 from . import common, ops, train
-from .common import EngineModule, InteractionWeights, Layer, draw_cross_layers, load_vocabulary, run_tail, table_rows
+from .common import (EngineModule, InteractionWeights, Layer, cross_spec, draw_cross_layers, load_vocabulary, run_tail,
+                     table_rows)
 
 
 def cross_layer(x0: torch.Tensor, xl: torch.Tensor, index: int) -> torch.Tensor:
@@ -66,7 +67,7 @@ class DCNModel(EngineModule):
         self.output_layer = nn.Linear(self.input_dim + hidden_units[-1], 1)
         self._tail = [Layer(m, act="relu") for m in self.dnn if isinstance(m, nn.Linear)]
         self.cross_weights = InteractionWeights(
-            interaction_weights, lambda: draw_cross_layers(self.input_dim, self.num_cross_layer))
+            interaction_weights, lambda: cross_spec(self.input_dim, self.num_cross_layer))
 
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)

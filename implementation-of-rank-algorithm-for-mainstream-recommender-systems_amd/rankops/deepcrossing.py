@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from . import ops, train
 from . import common
-from .common import InteractionWeights, check_eval, const, draw_residual_units, fused_mlp_fits, load_vocabulary, \
+from .common import InteractionWeights, check_eval, const, draw_residual_units, fused_mlp_fits, load_vocabulary, residual_spec, \
     table_rows
 
 
@@ -56,7 +56,7 @@ class DeepCrossingModel(common.EngineModule):
         self.output_layer = nn.Linear(self.input_dim, 1)
         self.residual_weights = InteractionWeights(
             interaction_weights,
-            lambda: draw_residual_units(self.input_dim, self.residual_internal_dim, self.residual_network_num))
+            lambda: residual_spec(self.input_dim, self.residual_internal_dim, self.residual_network_num))
 
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)

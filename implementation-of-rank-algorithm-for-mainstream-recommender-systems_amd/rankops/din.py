@@ -22,7 +22,8 @@ import torch.nn as nn
 
 from . import common, ops, train
 from .common import PACKED, fused_mlp_fits
-from .common import EngineModule, InteractionWeights, Layer, check_eval, draw_din_attention, load_vocabulary, run_tail, \
+from .common import EngineModule, InteractionWeights, Layer, check_eval, din_attention_spec, draw_din_attention, \
+    load_vocabulary, run_tail, \
     table_rows
 
 FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_singer_id", "manual_tag_list")
@@ -180,7 +181,7 @@ class DIN(EngineModule):
             width = unit
         self.output_layer = nn.Linear(width, 1)
         self.att_weights = InteractionWeights(
-            interaction_weights, lambda: draw_din_attention(self.embeddings[SEQ_KEY].embedding_dim))
+            interaction_weights, lambda: din_attention_spec(self.embeddings[SEQ_KEY].embedding_dim))
         self._dropout = train.DropoutStreams()
 
     def _load_vocabulary(self, vocab_dir, filename):

@@ -1,0 +1,60 @@
+"""GPU: rk_bst_forward_blocks at the reference script's own width, d_model 16 (bst.py:192 hard-codes
+it; bst_small_kernel in csrc/bst_small.hip: one wave per sample, lane = position), against the CPU
+oracle (oracle.reference_forward: bst.py:66-91, 216-247) and against the per-layer path
+(common.FUSED_BST = False).  Heads 1/2/4/8, T 1..64, 1-3 blocks, sum and mean pooling, lengths
+0 (NaN, as torch's all-masked softmax) / 1 / T / past T, out-of-range sequence indices."""
+import pytest
+import torch
+
+import helpers as H
+import rankops
+from test_gpu_parity import _compare, run_pair
+
+ATOL = RTOL = 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [
+    {"T": 50, "heads": 4},                      # the reference script's defaults
+    {"T": 50, "heads": 4, "pooling": "mean"},
+    {"T": 64, "heads": 1, "max_len": 64},
+    {"T": 33, "heads": 2, "blocks": 2},
+    {"T": 17, "heads": 8, "blocks": 3, "batch_norm": False},
+    {"T": 1, "heads": 4},
+])
+def test_small_bst_matches_oracle(cfg):
+    model = H.build("bst", cfg)
+    assert model._fused_blocks(cfg["T"]) is not None  # the d_model 16 fused path is taken
+    inp = H.make_inputs("bst", cfg, 200, seed=31)
+    inp["seq_length"][:3] = torch.tensor([0, 1, cfg["T"]])
+    if cfg["T"] > 1:
+        inp["seq_length"][3] = cfg["T"] + 5  # longer than the padded width: every key valid
+    out, ref = run_pair("bst", cfg, B=200, inputs=inp, model=model)
+    _compare(out, ref, f"bst16-{cfg}")
+    assert torch.isnan(out[1][0].cpu()).all()  # length 0: all keys masked -> NaN like the reference
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+def test_small_bst_equals_per_layer_path_at_bench_shape(monkeypatch):
+    cfg = {"T": 50, "heads": 4, "vocab": H.WECHAT_VOCAB}
+    model = H.build("bst", cfg).cuda()
+    inp = H.to_device(H.make_inputs("bst", cfg, 4096, seed=5), "cuda")
+    with torch.no_grad():
+        fused = H.as_tuple(H.call_model(model, "bst", inp))
+        monkeypatch.setattr(rankops.common, "FUSED_BST", False)
+        plain = H.as_tuple(H.call_model(model, "bst", inp))
+    for a, b in zip(fused, plain):
+        torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_small_bst_oob_sequence_index_is_flagged():
+    cfg = {"T": 16, "heads": 4}
+    model = H.build("bst", cfg).cuda()
+    inp = H.to_device(H.make_inputs("bst", cfg, 64, seed=9), "cuda")
+    inp["seq_feedid"][5, 2] = model.embeddings["feedid"].num_embeddings  # one past the table
+    rankops.error_flags(reset=True)
+    with torch.no_grad():
+        H.call_model(model, "bst", inp)
+    assert rankops.error_flags(reset=True) & 1

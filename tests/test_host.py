@@ -179,9 +179,11 @@ def test_fused_mlp_envelope():
 def test_interaction_weight_modes():
     calls = []
 
-    def draw():
-        calls.append(1)
-        return torch.randn(3)
+    def draw():  # an H2Spec whose fill counts its draws
+        def fill(v):
+            calls.append(1)
+            v[0].normal_()
+        return common.H2Spec([(3,)], fill, lambda v: v[0])
 
     iw = common.InteractionWeights("frozen", draw)
     a = iw.get("cpu")
@@ -202,3 +204,40 @@ def test_interaction_weight_modes():
 def test_package_layout():
     assert os.path.isdir(os.path.join(H.PKG_DIR, "csrc"))
     assert os.path.isfile(os.path.join(H.REPO, "include", "rankops.h"))
+
+
+def test_h2_spec_draws_equal_module_construction():
+    """The per-call H2 draws (common.*_spec: the reference's generator calls into preallocated
+    tensors, which the GPU path makes straight into a pinned staging buffer) are bit-identical to
+    constructing the reference's layers: din_attention's three nn.Linear (din.py:61-67),
+    cross_layer's xavier_normal_ / zeros_ (dcn.py:37-41), residual_unit's two nn.Linear
+    (deepcrossing.py:37-39)."""
+    import math
+    import torch.nn as nn
+    from rankops import common
+    torch.manual_seed(11)
+    mods = [nn.Linear(4 * 16, 64), nn.Linear(64, 32), nn.Linear(32, 1)]
+    want = [t.detach() for m in mods for t in (m.weight, m.bias)]
+    torch.manual_seed(11)
+    got = common.draw_din_attention(16)
+    assert all(torch.equal(a, b) for a, b in zip(want, got))
+    torch.manual_seed(12)
+    ws, bs = [], []
+    for _ in range(2):
+        w, b = torch.zeros(50, 1), torch.zeros(50, 1)
+        nn.init.xavier_normal_(w)
+        nn.init.zeros_(b)
+        ws.append(w.reshape(50))
+        bs.append(b.reshape(50))
+    torch.manual_seed(12)
+    W, B = common.draw_cross_layers(50, 2)
+    assert torch.equal(W, torch.stack(ws)) and torch.equal(B, torch.stack(bs))
+    torch.manual_seed(13)
+    units = []
+    for _ in range(3):
+        a, b = nn.Linear(50, 128), nn.Linear(128, 50)
+        units.append([t.detach() for t in (a.weight, a.bias, b.weight, b.bias)])
+    torch.manual_seed(13)
+    got = common.draw_residual_units(50, 128, 3)
+    assert all(torch.equal(x, y) for u, v in zip(units, got) for x, y in zip(u, v))
+    assert math.isclose(float(torch.empty(0).numel()), 0.0)
