@@ -10,10 +10,14 @@
 //     u = q.(W1a+W1c)^T + b1 is a per-sample bias (64 values, one per lane), and the MFMA A
 //     operand Weff[j][h] = (W1b-W1c)[j][h] + W1d[j][h]*q[h] is formed on the fly from two LDS
 //     rows and the query — layer 1 contracts over H instead of 4H (4x fewer MFMAs than the
-//     reference formulation); layers 2/3, the mask, the online softmax and the weighted key sum
-//     are those of din_attention_kernel (din.hip);
+//     reference formulation).  Round 4: the history is processed in tiles of 16 positions on
+//     v_mfma_f32_16x16x4_f32 (lane = position x key quarter), so a sample pads to a multiple of 16
+//     positions, not 32 (T = 50, lengths U[1, 50]: 33 instead of 44 positions per sample); the
+//     layer-1 accumulators feed layer 2 as its B operand in place, layer 3, the mask and the
+//     (online) softmax and weighted key sum follow per tile;
 //   * the attention output goes into the LDS row; the row's l2 norm (din.py:318-322) is taken.
-//  Phase B: the fcn tail + output layer + sigmoid over the 16 LDS rows (mlp_core.h).
+//  Phase B: the fcn tail + output layer + sigmoid over the 16 LDS rows (mlp_stream.h for the
+//  compiled [512, 256, 128] plan, mlp_core.h otherwise).
 // The l2 term is finished by a one-wave reduction over the per-workgroup partial sums.
 #include <cstdlib>
 #include <new>
@@ -23,10 +27,6 @@
 
 namespace rk {
 
-// tile 1's history keys prefetched into LDS by LDS-DMA during tile 0 (phase A below)
-#ifndef RK_DIN_PF1
-#define RK_DIN_PF1 1
-#endif
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -110,7 +110,7 @@ __device__ __forceinline__ void din_marks_flush(int tid) {
 // a counting sort over the ceil(T/32) + 1 tile classes: per 64-sample block a ballot mask per
 // class in LDS, then each wave finds its rank's sample by a prefix over the blocks' popcounts.
 constexpr int kDinBalMax = 8;  // NIT <= 8: batch <= 8192
-constexpr int kDinBalClasses = 9;  // T <= 256
+constexpr int kDinBalClasses = 17;  // T <= 256 (16-position tiles)
 
 // Inclusive prefix sum over the 64 lanes on the DPP network (no LDS round trips): row_shr 1/2/4/8
 // within each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals forward.
@@ -155,15 +155,15 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
   if (tid < seg_words) sw_v = reinterpret_cast<const int*>(&a.segs)[tid];
 
-  // ---- per-sample tile counts: a sample needs ceil(min(len, T) / 32) attention tiles — positions
-  // past its length contribute exactly 0 (plain: masked weight 0; softmax: exp(pad / sqrt(H) - max)
-  // underflows to 0) — except with softmax and len <= 0, where every position carries the same pad
-  // score and all T count.
+  // ---- per-sample tile counts: a sample needs ceil(min(len, T) / 16) attention tiles of 16
+  // positions — positions past its length contribute exactly 0 (plain: masked weight 0; softmax:
+  // exp(pad / sqrt(H) - max) underflows to 0) — except with softmax and len <= 0, where every
+  // position carries the same pad score and all T count.
   const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int ntiles_all = (a.T + 31) / 32;
+  const int ntiles_all = (a.T + 15) / 16;
   auto clamp_len = [&](int64_t len) { return len <= 0 ? 0 : (len >= a.T ? a.T : (int)len); };  // 32-bit math
-  auto tiles_of = [&](int lc) { return lc ? (lc + 31) >> 5 : (a.use_softmax ? ntiles_all : 0); };
-  // LDS after the descriptors: the history indices of tiles 0 and 1 per LDS row ([16][64]), then
+  auto tiles_of = [&](int lc) { return lc ? (lc + 15) >> 4 : (a.use_softmax ? ntiles_all : 0); };
+  // LDS after the descriptors: the history indices of positions 0..63 per LDS row ([16][64]), then
   // (NIT > 0) the batch row of each LDS row and the class masks
   int64_t* const kpre0 = reinterpret_cast<int64_t*>(col_seg + kDinSegLdsOff + sizeof(rk_segment) * kDinSegs);
   int64_t* const s_rows = kpre0 + 64 * kMlpRows;
@@ -234,19 +234,14 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   uint32_t* flags = a.flags;
 
   // ---- the feature row of one sample (zero padded to pad64(width)) and its history indices of
-  // tiles 0 and 1: the indices, the row's segment indices, then the row values (two dependent
-  // rounds); rowp / kslot: its LDS row and index slot
+  // positions 0..63 (lane = position, the first four tiles): the indices, the row's segment
+  // indices, then the row values (two dependent rounds); rowp / kslot: its LDS row and index slot
   const int wp = pad64(a.width);
   constexpr int kColIt = 4;  // width <= 255: at most four 64-column passes
-  int64_t kidx[2] = {0, 0};  // history index of position tt * 32 + l32, tiles 0 and 1
+  int64_t kidx = 0;          // history index of position `lane`
   float cval[kColIt];
   auto gather_issue = [&](int64_t bs, bool lv_, int nt_) {
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int t = tt * 32 + l32;
-      kidx[tt] = 0;
-      if (lv_ && tt < nt_ && t < a.T) kidx[tt] = a.seq[bs * a.ld_seq + t];
-    }
+    if (lv_ && lane < 16 * nt_ && lane < a.T) kidx = a.seq[bs * a.ld_seq + lane];
     int64_t cidx[kColIt];
     int cseg[kColIt];
 #pragma unroll
@@ -270,10 +265,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     }
   };
   auto gather_store = [&](float* rowp, int64_t* kslot) {
-    if (half == 0) {
-      kslot[l32] = kidx[0];
-      kslot[32 + l32] = kidx[1];
-    }
+    kslot[lane] = kidx;
 #pragma unroll
     for (int i = 0; i < kColIt; ++i) {
       const int c = lane + 64 * i;
@@ -395,43 +387,58 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #endif
   DIN_TS(4);
   float* row = buf0 + loc * a.ld0;
-  // tile 1's index waits in LDS (a register across tile 0 spills at the 128-VGPR budget)
-  int64_t* const kpre = kpre0 + 64 * loc + 32;
-
-  // tile-1 key prefetch slots (see phase A below): NQ KiB per wave in buf1
-  const int pf_slots = min(kMlpRows, (kMlpRows * a.ld1) / (256 * NQ));
-#if RK_DIN_PF1
-  const bool pf1 = live && ntiles > 1 && wave < pf_slots;
-#else
-  const bool pf1 = false;
-#endif
-  float* const pf_slot = buf1 + 256 * NQ * wave;
-
-  f32x4_t k[NQ];
-  // key rows of position t (index r) into k; positions past T read as zeros
-  auto load_keys = [&](int64_t r, int t) {
+  // ---- Phase A on tiles of 16 history positions (v_mfma_f32_16x16x4_f32): lane l holds position
+  // p16 = l & 15 of the tile and the key elements h in [HG g, HG g + HG), g = l >> 4, so a tile's 16
+  // key rows are one 128-B load round per lane group.  Per tile (64 MFMAs, 128 MFMA-cycles per
+  // position as the 32 x 32 form, but a sample pads only to 16 positions: 33 instead of 44
+  // positions per sample at T = 50, lengths U[1, 50]):
+  //   layer 1  acc1[jt] (j = 16 jt + 4 g + r, position p16) = Weff[j][h] . k[h], K = H: the A operand
+  //            Weff = (W1b - W1c) + W1d diag(q) (rows 16 jt + p16, lane group g's h), built per sample
+  //   ReLU(+ u[j])  on the accumulators; they are layer 2's B operands as they stand (K-step (jt, r)
+  //            takes j = 16 jt + 4 g + r from lane group g)
+  //   layer 2  acc2[jt2] (j2 = 16 jt2 + 4 g + r) = W2[j2][j] . h1[j], 16 K-steps
+  //   layer 3  the score of each position: ReLU(acc2 + b2) . w3 over the lane's 8 values, summed over
+  //            the 4 lane groups
+  // then the masked (online) softmax and the weighted key sum o[h] over the tile's positions.
+  constexpr int HG = H / 4;
+  const int p16 = lane & 15, g = lane >> 4;
+  const int64_t* const kslot = kpre0 + 64 * loc;  // indices of positions 0..63 (staged with the row)
+  float kk[HG];  // keys of the current tile: position p16, elements HG g + e
+  // key row of position t (index r) into kv; positions past T read as zeros, out-of-range rows too
+  // (flagged)
+  auto load_keys16 = [&](int64_t r, int t, float (&kv)[HG]) {
     const float* krow = nullptr;
     if (t < a.T) {
       if (r >= 0 && r < a.key_rows)
-        krow = a.key_table + r * a.ld_key;
+        krow = a.key_table + r * a.ld_key + HG * g;
       else
         flag_oob(flags);
-#ifdef RK_DIN_NO_GATHER  // timing experiment only: the keys come from 32 cache-resident rows
-      krow = a.key_table + (int64_t)l32 * a.ld_key;
+#ifdef RK_DIN_NO_GATHER  // timing experiment only: the keys come from 16 cache-resident rows
+      krow = a.key_table + (int64_t)p16 * a.ld_key + HG * g;
 #endif
     }
+    if constexpr (HG >= 4) {
 #pragma unroll
-    for (int c = 0; c < NQ; ++c)
-      k[c] = krow ? *reinterpret_cast<const f32x4_t*>(krow + 8 * c + hk) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < HG / 4; ++c) {
+        const f32x4_t v4 = krow ? *reinterpret_cast<const f32x4_t*>(krow + 4 * c) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kv[4 * c + e] = v4[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < HG; ++e) kv[e] = krow ? krow[e] : 0.f;
+    }
   };
-  // ---- Phase A.1: the first attention tile's keys.  NIT == 0: the row and the indices are in LDS
-  // already (gathered before the barrier above).  NIT > 0: the row, the indices and then the keys
-  // for the assigned sample, the row going to LDS while the key rows are still in flight.
+  auto index_of = [&](int t) -> int64_t { return t < 64 ? kslot[t] : (t < a.T ? a.seq[b * a.ld_seq + t] : 0); };
+  // ---- Phase A.1: the first tile's keys.  NIT == 0: the row and the indices are in LDS already
+  // (gathered before the barrier above).  NIT > 0: the row, the indices and then the keys for the
+  // assigned sample, the row going to LDS while the key rows are still in flight.
   if constexpr (NIT == 0) {
-    if (live && ntiles > 0) load_keys(kpre0[64 * loc + l32], l32);
+    if (live && ntiles > 0) load_keys16(kslot[p16], p16, kk);
   } else {
     gather_issue(b, live, ntiles);
-    if (live && ntiles > 0) load_keys(kidx[0], l32);
+    const uint32_t lo = __shfl((uint32_t)kidx, p16, kWave), hi = __shfl((uint32_t)((uint64_t)kidx >> 32), p16, kWave);
+    if (live && ntiles > 0) load_keys16((int64_t)(((uint64_t)hi << 32) | lo), p16, kk);
     gather_store(row, kpre0 + 64 * loc);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -456,119 +463,109 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-
-    // ---- tile 1's key rows straight into LDS (LDS-DMA: no VGPRs, the kernel is at its 128-register
-    // budget) while tile 0 computes: loaded at tile 1's start they cost the wave a full gather
-    // latency, uncovered once the SIMD's shorter samples are done.  Slots (NQ KiB per wave) live in
-    // buf1, which phase B first writes after the barrier that closes phase A; the ranking puts the
-    // longest samples on the lowest waves, so the slots go to waves 0 .. pf_slots - 1.
-    if (pf1) {
-      const int t1 = 32 + l32;
-      const int64_t r1 = NIT == 0 ? kpre[l32] : kidx[1];
-      const bool ok = t1 < a.T && r1 >= 0 && r1 < a.key_rows;
-      if (t1 < a.T && !ok) flag_oob(flags);
-      const float* src = a.key_table + (ok ? r1 * a.ld_key : 0) + hk;
+    float qv[HG];  // the query elements of lane group g
 #pragma unroll
-      for (int c = 0; c < NQ; ++c)
-        __builtin_amdgcn_global_load_lds((glb_void*)(src + 8 * c), (lds_void*)(pf_slot + 256 * c), 16, 0, 0);
-    }
+    for (int e = 0; e < HG; ++e) qv[e] = row[a.q_col + HG * g + e];
 
     const float sqrt_h = (float)__builtin_sqrt((double)H);
     const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
+    const float b3 = a.b3[0];
     float m_run = -INFINITY, l_run = 0.f;
-    f32x4_t o[NQ];
+    float o[HG];
 #pragma unroll
-    for (int c = 0; c < NQ; ++c) o[c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < HG; ++e) o[e] = 0.f;
     for (int tt = 0; tt < ntiles; ++tt) {
-      // the weight/bias LDS reads below are loop-invariant; hoisting them out of the tile loop
-      // costs ~96 VGPRs and spills at the 128-register budget of a 16-wave workgroup
+      // the weight LDS reads below are loop-invariant; hoisted out of the tile loop (32 more VGPRs
+      // for the layer-1 A operand alone) they spill at the 128-register budget
       asm volatile("" ::: "memory");
-      const int t = tt * 32 + l32;
+      const int t = 16 * tt + p16;
       const bool in_seq = t < a.T;
-      if (tt == 1 && pf1) {  // tile 1's keys from the LDS-DMA slot (zeros past T / out of range)
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only: the DMA went out a tile ago
-        const int64_t r1 = NIT == 0 ? kpre[l32] : kidx[1];
-        const bool ok = in_seq && r1 >= 0 && r1 < a.key_rows;
+      // the next tile's keys go out before this tile's MFMAs
+      float kn[HG];
+      const bool more = tt + 1 < ntiles;
+      if (more) load_keys16(index_of(t + 16), t + 16, kn);
+      f32x4_t acc1[4];
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(pf_slot + 256 * c + 4 * lane);
-          k[c] = ok ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        }
-      } else if (tt > 0) {  // tile 0's keys were loaded with the row; tile 1's index was prefetched
-        load_keys(tt == 1 ? kpre[l32] : (in_seq ? a.seq[b * a.ld_seq + t] : 0), t);
+      for (int jt = 0; jt < 4; ++jt) acc1[jt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      // layer 1's A operand, Weff[16 jt + p16][HG g + e] = Wk + Wqk q (rows of the LDS image)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+        const float* wk = sm + Ly::WK + (16 * jt + p16) * Ly::LDH + HG * g;
+        const float* wqk = sm + Ly::WQK + (16 * jt + p16) * Ly::LDH + HG * g;
+#pragma unroll
+        for (int e = 0; e < HG; ++e) acc1[jt] = mfma16(fmaf(wqk[e], qv[e], wk[e]), kk[e], acc1[jt]);
       }
-
-      // layer 1 (transposed) one 32-row block jt at a time, each folded straight into layer 2
-      // (acc2 = W2 . h1^T with the layer-1 accumulator as the B operand): one layer-1
-      // accumulator is live at a time.
-      f32x16 acc2;
+      // ReLU(layer 1 + u) in place, then layer 2 with the accumulators as its B operands
+      f32x4_t acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+      for (int jt = 0; jt < 4; ++jt) {
+        const f32x4_t uu = *reinterpret_cast<const f32x4_t*>(sm + Ly::U + wave * 64 + 16 * jt + 4 * g);
+        f32x4_t w2[2];
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        f32x16 acc1;
+        for (int jt2 = 0; jt2 < 2; ++jt2)
+          w2[jt2] = *reinterpret_cast<const f32x4_t*>(sm + Ly::W2 + (16 * jt2 + p16) * 68 + 16 * jt + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
-        const int j = jt * 32 + l32;
+        for (int r = 0; r < 4; ++r) {
+          const float z = acc1[jt][r] + uu[r];
+          const float h1 = z < 0.f ? 0.f : z;
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-          const f32x4_t wk = *reinterpret_cast<const f32x4_t*>(sm + Ly::WK + j * Ly::LDH + 8 * c + hk);
-          const f32x4_t wqk = *reinterpret_cast<const f32x4_t*>(sm + Ly::WQK + j * Ly::LDH + 8 * c + hk);
-          f32x4_t qc;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) qc[e] = row[a.q_col + 8 * c + hk + e];
-          const f32x4_t weff = wk + wqk * qc;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc1 = mfma32(weff[e], k[c][e], acc1);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float z = acc1[r] + sm[Ly::U + wave * 64 + jt * 32 + acc_row(r, lane)];
-          acc1[r] = z < 0.f ? 0.f : z;
-        }
-#pragma unroll
-        for (int uu = 0; uu < 4; ++uu) {
-          const f32x4_t av = *reinterpret_cast<const f32x4_t*>(sm + Ly::W2 + l32 * 68 + jt * 32 + 8 * uu + hk);
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc2 = mfma32(av[v], acc1[4 * uu + v], acc2);
+          for (int jt2 = 0; jt2 < 2; ++jt2) acc2[jt2] = mfma16(w2[jt2][r], h1, acc2[jt2]);
         }
       }
-      // layer 3: score[t]
+      // layer 3: the position's score
       float sc = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j2 = acc_row(r, lane);
-        float z = acc2[r] + sm[Ly::B2 + j2];
-        z = z < 0.f ? 0.f : z;
-        sc = fmaf(z, sm[Ly::W3 + j2], sc);
+      for (int jt2 = 0; jt2 < 2; ++jt2) {
+        const f32x4_t b2v = *reinterpret_cast<const f32x4_t*>(sm + Ly::B2 + 16 * jt2 + 4 * g);
+        const f32x4_t w3v = *reinterpret_cast<const f32x4_t*>(sm + Ly::W3 + 16 * jt2 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float z = acc2[jt2][r] + b2v[r];
+          z = z < 0.f ? 0.f : z;
+          sc = fmaf(z, w3v[r], sc);
+        }
       }
+      sc += __shfl_xor(sc, 16, kWave);
       sc += __shfl_xor(sc, 32, kWave);
-      sc = sc + a.b3[0];
+      sc = sc + b3;
 
       const bool valid = in_seq && (int64_t)t < len;
       if (a.use_softmax) {
-        const float s = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
-        const float m_new = fmaxf(m_run, wave_max(s));
+        const float sv = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
+        float mt = sv;
+#pragma unroll
+        for (int x = 1; x < 16; x <<= 1) mt = fmaxf(mt, __shfl_xor(mt, x, kWave));
+        const float m_new = fmaxf(m_run, mt);
         const float scale_old = expf(m_run - m_new);
-        const float p = in_seq ? expf(s - m_new) : 0.f;
-        l_run = l_run * scale_old + wave_sum(half == 0 ? p : 0.f);
+        const float p = in_seq ? expf(sv - m_new) : 0.f;
+        float ps = p;
+#pragma unroll
+        for (int x = 1; x < 16; x <<= 1) ps += __shfl_xor(ps, x, kWave);
+        l_run = l_run * scale_old + ps;
         m_run = m_new;
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) o[c] = o[c] * scale_old + p * k[c];
+        for (int e = 0; e < HG; ++e) o[e] = o[e] * scale_old + p * kk[e];
       } else {
         const float w = valid ? sc : 0.f;
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) o[c] = o[c] + w * k[c];
+        for (int e = 0; e < HG; ++e) o[e] = o[e] + w * kk[e];
+      }
+      if (more) {
+#pragma unroll
+        for (int e = 0; e < HG; ++e) kk[e] = kn[e];
       }
     }
+    // the weighted key sum over the positions (the 16 lanes of a group), into the LDS row
     const float inv_l = a.use_softmax ? 1.0f / l_run : 1.0f;
+    float mine = 0.f;
 #pragma unroll
-    for (int c = 0; c < NQ; ++c)
+    for (int e = 0; e < HG; ++e) {
+      float v = o[e];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = half_sum(o[c][e]);
-        if (l32 == 4 * c + e) row[a.att_col + 8 * c + hk + e] = a.use_softmax ? v * inv_l : v;
-      }
+      for (int x = 1; x < 16; x <<= 1) v += __shfl_xor(v, x, kWave);
+      mine = p16 == e ? v : mine;
+    }
+    if (p16 < HG) row[a.att_col + HG * g + p16] = a.use_softmax ? mine * inv_l : mine;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     if (a.l2_part) {
@@ -793,8 +790,8 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   // RANKOPS_DIN_BALANCE=1 / 0 forces it on / off (tests, A/B timing).  Only where its LDS (the
   // batch row of each LDS row and the class masks) still fits: otherwise contiguous samples.
   const char* env = getenv("RANKOPS_DIN_BALANCE");
-  a.bal_nb = (T + 31) / 32 + 1;
-  const bool want_bal = env && env[0] ? env[0] != '0' : a.bal_nb >= 4;
+  a.bal_nb = (T + 15) / 16 + 1;  // tile-count classes 0 .. ceil(T / 16)
+  const bool want_bal = env && env[0] ? env[0] != '0' : T > 64;
   if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
     const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
     if (shm + extra <= 160 * 1024) {

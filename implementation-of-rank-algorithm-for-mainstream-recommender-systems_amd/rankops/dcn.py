@@ -82,8 +82,9 @@ class DCNModel(EngineModule):
             idx = [category[n] for n in self.embeddings]
         except (KeyError, TypeError):
             return None
-        if not isinstance(dense, torch.Tensor) or dense.device.type != "cuda":
-            return None
+        if not isinstance(dense, torch.Tensor) or dense.device.type != "cuda" or \
+                not all(isinstance(t, torch.Tensor) for t in idx):
+            return None  # lists / arrays take the normal path (as_index's descriptive errors)
         dev = dense.device
         stream = ops._lib.raw_stream(dev)
         calls = self.__dict__.setdefault("_eager", common.EagerCalls())

@@ -188,14 +188,16 @@ class DeepFM(EngineModule):
             tl, ep, keep = tail
             front = ["rk_fm_linear_packed", [arr, len(second), D, B, ops.ctypes.byref(ml0), y.data_ptr(), y.stride(0),
                                              None, None, None]]
-            return [front] + tl, (7, 8), ep, B, (keep, arr, plan, w0, ml0, y)
+            # keep-alive: what the argument blocks point into (not the caller's index tensors: the
+            # cache key's address / shape / stride check makes those pointers valid on a hit)
+            return [front] + tl, (7, 8), ep, B, (keep, arr, packed, w0, ml0, y)
         tail = common.tail_launches(deep_in, self._tail, self.deep_output_layer, head_kwargs)
         if tail is None:
             return None
         tl, ep, keep = tail
         gather = ["rk_fm_gather_packed", [arr, len(second), D, B, deep_in.data_ptr(), deep_in.stride(0), None, None,
                                           None]]
-        return [gather] + tl, (6, 7), ep, B, (keep, arr, plan)
+        return [gather] + tl, (6, 7), ep, B, (keep, arr, packed, deep_in)
 
     def forward(self, category):
         if not self.training:

@@ -341,7 +341,10 @@ class DIN(EngineModule):
                                            self.use_softmax, layers, head, B, dev, l2_col0=pl["cat_col0"],
                                            l2_scale=float(self.l2_lambda), l2_out=zero[0] if want_l2 else None,
                                            att_image=zero[0])
-        return calls.put(key, (list(args), head, B, want_l2, H, (keep, packed, pl, layers)))
+        # the entry keeps what its argument block points into (segment / layer arrays, packed
+        # images, the l2 workspace) but not the caller's input tensors: the key's address, shape
+        # and stride check already makes the raw input pointers valid on a hit
+        return calls.put(key, (list(args), head, B, want_l2, H, (keep, packed, layers)))
 
     def forward(self, dense, category, sequence, target):
         if not self.training:

@@ -1121,9 +1121,13 @@ class Adam(torch.optim.Optimizer):
                 ops._lib.AdamTensor(e[0].data_ptr(), e[1].data_ptr(), e[2].data_ptr(), e[3].data_ptr(), e[0].numel(),
                                     None) for e in entries])
             bumped = [t for e in entries for t in (e[0], e[2], e[3])]
-            hit = [key, arr, len(entries), shared, int(counts.pop()), bumped, entries, params[0].device]
+            # the block keeps raw gradient pointers only: holding the gradient tensors would keep
+            # last step's storages alive across zero_grad(set_to_none=True), so the next backward
+            # could never get the same addresses and the key would miss every step
+            hit = [key, arr, len(entries), shared, int(counts.pop()), bumped, params[0].device]
             cache[gi] = hit
-        _key, arr, n, step_t, count, bumped, _entries, dev = hit
+            self._fast_builds = getattr(self, "_fast_builds", 0) + 1
+        _key, arr, n, step_t, count, bumped, dev = hit
         step_t.add_(1.0)
         hit[4] = count = count + 1
         beta1, beta2 = group["betas"]

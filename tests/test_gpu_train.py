@@ -1170,3 +1170,29 @@ def test_linear_res_dropout_ln_matches_two_launch_path(M, K, p):
     rr = r1.double()
     want = torch.nn.functional.layer_norm(rr, (d,), ln.weight.double(), ln.bias.double(), ln.eps)
     torch.testing.assert_close(y1.double(), want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_adam_fast_step_cache_hits_with_set_to_none_and_frees_old_grads():
+    """the cached eager step must not keep the previous step's gradients alive.  With the
+    reference's loop body (zero_grad(set_to_none=True), forward, backward, step) the old gradient
+    storages are freed, the caching allocator hands the same addresses back, and the argument block
+    is reused instead of rebuilt every step."""
+    import weakref
+    torch.manual_seed(0)
+    model = H.build("dcn", {"interaction_weights": "frozen"}).cuda().train()
+    inp = H.to_device(H.make_inputs("dcn", {}, 256, seed=3), "cuda")
+    label = (torch.rand(256, device="cuda") < 0.3).float()
+    opt = rankops.Adam(model.parameters(), lr=1e-3)
+    crit = torch.nn.BCEWithLogitsLoss()
+    old = []
+    for step in range(6):
+        opt.zero_grad(set_to_none=True)
+        out = H.as_tuple(H.call_model(model, "dcn", inp))
+        crit(out[1].squeeze(), label).backward()
+        old.append([weakref.ref(p.grad) for p in model.parameters() if p.grad is not None])
+        opt.step()
+    opt.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+    assert all(r() is None for refs in old for r in refs)  # no step's gradient is held by the cache
+    assert getattr(opt, "_fast_builds", 0) <= 2  # built on the first fast step, then reused
