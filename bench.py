@@ -716,8 +716,8 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
         def run():
             with torch.no_grad():
                 fn()
-        n = max(5, steps // 5) if name.endswith("per_call") else steps
-        t = time_replays(run, n, 2 if name.endswith("per_call") else warmup, 1)
+        n = max(20, steps // 2) if name.endswith("per_call") else steps
+        t = time_replays(run, n, 5 if name.endswith("per_call") else warmup, 1)
         mode = "eager, per-call H2 draws" if name.endswith("per_call") else "eager (no graph), frozen H2"
         return {"samples_per_s": round(batch * n / t, 1), "mode": mode,
                 "ms_per_step": round(1e3 * t / n, 4)}, model, inp, cfg, model_name

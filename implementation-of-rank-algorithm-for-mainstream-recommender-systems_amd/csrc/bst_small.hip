@@ -9,8 +9,8 @@
 // context, the FFN activations) live in registers, every projection is a per-lane 16 x 16
 // matrix-vector product, and only K and V go through LDS (broadcast ds_read_b128: each query lane
 // walks every key).  Softmax is two-pass
-// (max, then exp-sum and P.V) per head, masked keys at -inf as bst.py:80 (an all-masked row gives
-// NaN as torch's softmax does).  f32 VALU throughout; the block is ~3k FMAs per lane.
+// (max, then exp-sum and P.V) per head on the hardware exp2 (v_exp_f32), masked keys at -inf as
+// bst.py:80 (an all-masked row gives NaN as torch's softmax does).  f32 VALU throughout; the block is ~3k FMAs per lane.
 //
 // Weights and biases are read with uniform addresses straight from global memory, so they come in
 // through the scalar cache into SGPRs (s_load), one operand of each v_fma: LDS carries only K and V.
@@ -103,7 +103,8 @@ __global__ __launch_bounds__(kSWaves * 64, 4) void bst_small_kernel(BstSmallArgs
   float* const kv = sm + wave * 2 * kST * kSD;  // this wave's K [64][16], V [64][16]
   float* const Ks = kv;
   float* const Vs = kv + kST * kSD;
-  const float qscale = 1.0f / sqrtf((float)DH);
+  // scores in log2 units: exp(s / sqrt(dh) - max) = exp2(s * log2(e) / sqrt(dh) - max2) on v_exp_f32
+  const float qscale = 1.4426950408889634f / sqrtf((float)DH);
 
   for (int64_t b = (int64_t)blockIdx.x * kSWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kSWaves) {
     const int T = a.T;
@@ -201,16 +202,18 @@ __global__ __launch_bounds__(kSWaves * 64, 4) void bst_small_kernel(BstSmallArgs
 #pragma unroll
           for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
           s = masked ? -INFINITY : s * qscale;
-          const float p = expf(s - m[h]);
+          const float p = __builtin_amdgcn_exp2f(s - m[h]);
           l[h] += p;
 #pragma unroll
           for (int e = 0; e < DH; ++e) ctx[h * DH + e] = fmaf(p, v[h * DH + e], ctx[h * DH + e]);
         }
       }
 #pragma unroll
-      for (int h = 0; h < NH; ++h)
+      for (int h = 0; h < NH; ++h) {
+        const float inv = 1.0f / l[h];
 #pragma unroll
-        for (int e = 0; e < DH; ++e) ctx[h * DH + e] = ctx[h * DH + e] / l[h];
+        for (int e = 0; e < DH; ++e) ctx[h * DH + e] = ctx[h * DH + e] * inv;
+      }
       // out1 = norm1(queries + W_o ctx) (dropout: identity in eval)
       float o[kSD];
       matvec16(w.p[7], w.p[8], ctx, o);

@@ -161,21 +161,24 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   // stage state carried from issue() (before layer 0's weight prefetch) to the finish
   const int nl = a.num_layers;
   float x0[NJ], xl[NJ], cw[kDcnPreLayers][NJ], cb[kDcnPreLayers][NJ], hw[NJ];
+  const int64_t b = m0 + wave;
+  const bool live = wave < rows;
+  const int64_t bb = live ? b : m0;
+  // round trip 1: the sample's row in every segment — lane t loads segment t's index (one vector
+  // load per wave; 8 scalar loads measured ~2.4 us at kernel start), then every lane reads them
+  // back (wave-uniform).  The streamed tail issues it ahead of its weight ring (stage.early()).
+  int64_t mine = 0;
+  auto stage_index = [&]() {
+    const int64_t* ip = a.segs[0].idx;
+    int64_t st = a.segs[0].idx_stride;
+#pragma unroll
+    for (int t = 1; t < kDcnSegs; ++t)
+      if (lane == t) ip = a.segs[t].idx, st = a.segs[t].idx_stride;
+    mine = ip[bb * st];
+  };
   auto stage_issue = [&]() {
-    const int64_t b = m0 + wave;
-    const bool live = wave < rows;
-    const int64_t bb = live ? b : m0;
-    // round trip 1: the sample's row in every segment — lane t loads segment t's index (one vector
-    // load per wave; 8 scalar loads measured ~2.4 us at kernel start), then every lane reads them
-    // back (wave-uniform)
     int64_t rix[kDcnSegs];
     {
-      const int64_t* ip = a.segs[0].idx;
-      int64_t st = a.segs[0].idx_stride;
-#pragma unroll
-      for (int t = 1; t < kDcnSegs; ++t)
-        if (lane == t) ip = a.segs[t].idx, st = a.segs[t].idx_stride;
-      const int64_t mine = ip[bb * st];
 #pragma unroll
       for (int t = 0; t < kDcnSegs; ++t) {
         const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, t);
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
       }
     }
   };
-  auto stage_finish = [&]() {
+  auto stage_store = [&]() {
     const int K0p = pad64(width);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -237,6 +240,10 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
       xl[j] = x0[j];
       if (c < K0p) buf0[wave * a.m.ld0 + c] = x0[j];
     }
+  };
+  // the cross stack and the cross half of output_layer: needed only by the head, so the streamed
+  // tail runs it inside its second layer (stage.side()), off the prologue's critical path
+  auto stage_cross = [&]() {
     auto cross = [&](const float* w, const float* bl) {
       float d = 0.f;
 #pragma unroll
@@ -275,10 +282,19 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   };
   if constexpr (std::is_void_v<P>)
     mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
-             two_phase(stage_issue, stage_finish), part);
+             two_phase(
+                 [&]() {
+                   stage_index();
+                   stage_issue();
+                 },
+                 [&]() {
+                   stage_store();
+                   stage_cross();
+                 }),
+             part);
   else
     mlp_stream_rows<P, RK_STREAM_EPI>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
-                       two_phase(stage_issue, stage_finish), part);
+                                      staged(stage_index, stage_issue, stage_store, stage_cross), part);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
   MLP_FLUSH(tid);

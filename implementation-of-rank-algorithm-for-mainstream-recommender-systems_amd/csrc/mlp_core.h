@@ -420,9 +420,13 @@ __device__ __forceinline__ void mlp_lds_barrier() { asm volatile("s_waitcnt lgkm
 // The stage fills buf0 in two calls around layer 0's weight prefetch: stage.issue() runs first
 // (the gather's own loads go out ahead of the 8 ring loads per wave, which would otherwise queue
 // in front of them in the CU's memory pipeline), stage() after it (the rest, then a barrier).
+// side(): optional work the streamed tail (mlp_stream.h) runs inside its second layer, after the
+// MFMAs of an early chunk are issued — stage work no layer needs before the head (DCN's cross
+// network) then fills the wave's idle issue slots beside the matrix pipe instead of the prologue.
 struct NoStage {
   __device__ void issue() const {}
   __device__ void operator()() const {}
+  __device__ void side() const {}
 };
 template <class I, class F>
 struct TwoPhaseStage {
@@ -430,7 +434,31 @@ struct TwoPhaseStage {
   F f;
   __device__ void issue() { i(); }
   __device__ void operator()() { f(); }
+  __device__ void side() {}
 };
+// early() (streamed tail only, kEarly): the stage's first, independent loads (DCN: the sample's
+// indices) go out before the weight ring, whose issue then overlaps their latency; issue() (the
+// dependent loads) follows the ring.
+template <class E, class I, class F, class S>
+struct StagedStage {
+  static constexpr bool kEarly = true;
+  E e;
+  I i;
+  F f;
+  S s;
+  __device__ void early() { e(); }
+  __device__ void issue() { i(); }
+  __device__ void operator()() { f(); }
+  __device__ void side() { s(); }
+};
+template <class E, class I, class F, class S>
+__device__ __forceinline__ StagedStage<E, I, F, S> staged(E e, I i, F f, S s) {
+  return StagedStage<E, I, F, S>{e, i, f, s};
+}
+template <class T, class = void>
+struct stage_has_early : std::false_type {};
+template <class T>
+struct stage_has_early<T, std::void_t<decltype(T::kEarly)>> : std::true_type {};
 template <class I, class F>
 __device__ __forceinline__ TwoPhaseStage<I, F> two_phase(I i, F f) {
   return TwoPhaseStage<I, F>{i, f};

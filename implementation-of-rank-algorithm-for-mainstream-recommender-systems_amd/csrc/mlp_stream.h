@@ -169,6 +169,24 @@ struct StreamEpi {
 // One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
 // (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
 // operator() after it, before that barrier).  EPI: StreamEpiMode.
+// Chunk of the side layer at which wave position k (0..3 on its SIMD) runs stage.side(), and the
+// positions that run it at chunk c.
+constexpr int side_chunk(int KC, int k) {
+  const int step = KC / 4 > 0 ? KC / 4 : 1;
+  const int c = (KC > 2 ? 2 : KC - 1) + step * k;
+  return c < KC - 1 ? c : KC - 1;
+}
+constexpr int side_first_pos(int KC, int c) {
+  for (int k = 0; k < 4; ++k)
+    if (side_chunk(KC, k) == c) return k;
+  return 4;
+}
+constexpr int side_last_pos(int KC, int c) {
+  for (int k = 3; k >= 0; --k)
+    if (side_chunk(KC, k) == c) return k;
+  return -1;
+}
+
 template <class P, int W, int EPI, class Stage>
 __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                  float* buf1, int ld1, float* epi, int64_t m0, int rows,
@@ -209,6 +227,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   const unsigned long long t_start = clock64();
 #endif
   StreamEpi<P> ep_stage;
+  constexpr bool kEarly = stage_has_early<Stage>::value;
   // kEpiRegs: the parameters of the wave's columns of one layer (tiles j = 0, 1)
   ColEpi epr[2];
   auto load_epr = [&](auto LI) {
@@ -222,13 +241,23 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       }
     }
   };
-  stage.issue();
-  if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
-  __builtin_amdgcn_sched_barrier(0);  // the stage's and the parameters' loads stay ahead of the ring
+  if constexpr (kEarly) {
+    stage.early();
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
+    stage.issue();
+    if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
+    __builtin_amdgcn_sched_barrier(0);  // the stage's and the parameters' loads stay ahead of the ring
+  }
   static_for<0, R>([&](auto G) {
     issue(G);
     __builtin_amdgcn_sched_barrier(0);
   });
+  if constexpr (kEarly) {
+    stage.issue();
+    if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // layer 0's parameters behind the ring (needed only at its epilogue)
   if constexpr (EPI == kEpiRegs) load_epr(std::integral_constant<int, 0>{});
   if constexpr (NL == 1) head_prefetch();
@@ -249,6 +278,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
     if constexpr (T == 0) {
+      if constexpr (l == (NL > 1 ? 1 : 0)) stage.side();  // (no tile here: the side work all the same)
 #if RK_MLP_SYNC
       // no tile in this layer: take part in the active waves' lockstep barriers
       static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
@@ -279,6 +309,19 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           issue(std::integral_constant<int, B0 + c * T + j + R>{});
         });
         __builtin_amdgcn_sched_barrier(0);
+        // the stage's side work, once, beside the second layer's MFMAs (the first layer's with one),
+        // staggered over the SIMD's four waves (wave w sits at position w / 4 of SIMD w % 4): wave
+        // position k at chunk side_chunk(k), one per lockstep window when the layer has 32 chunks, so
+        // three of a SIMD's waves keep the matrix pipe fed while the fourth waits on the side work's
+        // cross-lane reductions (all four at one chunk left the pipe idle for that latency)
+        if constexpr (l == (NL > 1 ? 1 : 0)) {
+          constexpr int kFirst = side_first_pos(KC, c), kLast = side_last_pos(KC, c);
+          if constexpr (kFirst <= kLast) {
+            const int pos = wave >> 2;
+            if (pos >= kFirst && pos <= kLast) stage.side();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
 #if RK_MLP_SYNC
         if constexpr ((c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
 #endif

@@ -143,8 +143,9 @@ class H2Stage:
         n = sum(sizes)
         i = self._turn
         self._turn ^= 1
-        if self._events[i] is not None:
-            self._events[i].synchronize()
+        ev = self._events[i]
+        if ev is not None:
+            ev.synchronize()
         host = self._host[i]
         if host is None or host.numel() < n:
             host = torch.empty(max(n, 1024), dtype=torch.float32, pin_memory=True)
@@ -156,9 +157,9 @@ class H2Stage:
         spec.fill(views)
         dev = torch.empty(max(n, 1), dtype=torch.float32, device=device)
         dev[:n].copy_(host[:n], non_blocking=True)
-        ev = torch.cuda.Event()
+        if ev is None:
+            ev = self._events[i] = torch.cuda.Event()  # one event per buffer, re-recorded per use
         ev.record(torch.cuda.current_stream(device))
-        self._events[i] = ev
         out, off = [], 0
         for s, k in zip(spec.shapes, sizes):
             out.append(dev[off:off + k].view(s))
