@@ -691,6 +691,24 @@ def dcn_roofline(model, inp, batch):
     return r
 
 
+DEEPFM_FLOP = 1_310_976  # 960->512->256->128->1 (+ the FM sums' 2 x 960 + final 3 -> 1), SURVEY §8d
+
+
+def deepfm_roofline(model, inp, batch):
+    """deepfm_fused_kernel (the whole DeepFM forward, one launch, rk_deepfm_forward): 20 back-to-back
+    forwards captured in one hipGraph, HIP events on the replay stream."""
+    import helpers as H
+    ms = graph_kernel_avg_ms(lambda: H.call_model(model, "deepfm", inp))
+    flop = DEEPFM_FLOP * batch
+    r = {"kernel": "deepfm_fused_kernel<StreamPlan<60,32,16,8>>", "bound": "mfma", "unit": "TFLOP/s",
+         "peak": PEAK_FP32_MFMA / 1e12, "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
+         "flop_basis": "reference formulation per sample: 1,310,976 (30 x 32 -> 512 -> 256 -> 128 -> 1 deep layers; "
+                       "every width a multiple of 64, so also the executed count; SURVEY §8d)",
+         "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
+    r.update(counter_fields("deepfm_fused_kernel", "deepfm", flop))
+    return r
+
+
 def bst_roofline(model, inp, batch):
     """bst_block_kernel (every transformer block + pooling of the BST forward, one launch) timed
     alone: back-to-back launches, HIP events on the stream they run on."""
@@ -759,6 +777,14 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
                 plans[i].launch_on(handles[i])
             res["step"] = (f"prepared single-kernel launches (rk_din_plan_launch), {streams} batches in flight "
                            f"on {streams} HIP streams (round-robin, own inputs/outputs/workspaces)")
+    elif model_name in ("dcn", "deepfm") and not zipf:
+        # DCN and (at configs[1]'s shape) DeepFM are single-kernel forwards too: a prepared launch
+        # (DCNModel.prepare / DeepFM.prepare: the cached ctypes call of rk_dcn_forward /
+        # rk_deepfm_forward bound to the inputs), the graph replay of the same forward beside it
+        run = model.prepare(inp["dense"], inp["category"]) if model_name == "dcn" else model.prepare(inp["category"])
+        tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
+        res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
+        res["step"] = "prepared launch (%s)" % ("rk_dcn_forward" if model_name == "dcn" else "rk_deepfm_forward")
     else:
         run = g.replay
     t = time_replays(run, steps, warmup, world)
@@ -829,7 +855,7 @@ def main():
             if name == "dcn":
                 r["roofline"] = dcn_roofline(m2, inp2, batch)
             if name == "deepfm":
-                r["mfma_busy"] = {k: counter_fields(k, "deepfm") for k in ("linear_tiled_kernel", "mlp_stream_kernel")}
+                r["roofline"] = deepfm_roofline(m2, inp2, batch)
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob

@@ -1,0 +1,218 @@
+// Whole DeepFM eval forward in one launch (DeepFM.forward, deepfm.py:121-151) on the streamed tail
+// (mlp_stream.h): per 16-row tile, wave w gathers sample m0 + w's packed rows (rk_fm_pack_table
+// layout: the dim second-order values, then the first-order weight) of every field straight into
+// the MLP's LDS input row, the three deep layers (Linear + BatchNorm folded + ReLU,
+// deepfm.py:100-112) run on one weight stream across the layers, and the head evaluates
+// deep_output_layer, final_layer over [fm1, fm2, deep] and the sigmoid (deepfm.py:143-151).
+//
+// Replaces rk_fm_linear_packed (the gather + FM + first layer as a 64 x 128-tiled GEMM) +
+// rk_mlp_forward (the rest of the tail): one launch, no [B, 512] round trip through HBM, no
+// K-block barriers (the whole 960-wide row of 16 samples, 61 KB, stays in LDS for layer 0), and
+// the FM sums (deepfm.py:122-140) are taken beside layer 0's MFMAs from the staged row instead of
+// in the prologue.  The cost: every workgroup streams the whole first-layer weight (1.97 MB) for 16
+// rows, from L2 (the 2D tiling streamed a quarter of it for 64 rows).
+//
+// Gather in three dependent rounds, all issued around layer 0's weight ring: (1) lane f loads the
+// sample's index in field f (before the ring); (2) lane f forms the row address, every lane
+// fetches its float4s of the row through a cross-lane read of the owning field's address, and lane
+// f the first-order weight (after the ring); (3) the LDS store before the barrier that opens
+// layer 0.
+#include "mlp_core.h"
+#include "mlp_stream.h"
+
+namespace rk {
+
+constexpr int kDfMaxFields = 32;
+constexpr int kDfLayers = 3;
+
+struct DfArgs {
+  rk_mlp_layer L[kDfLayers];
+  rk_epilogue head;
+  // per field: packed table (or dense block of packed rows), its index column (a dense field
+  // reads the flag word with stride 0 and uses the sample's own row), bounds
+  const float* src[kDfMaxFields];
+  const int64_t* idx[kDfMaxFields];
+  int64_t istride[kDfMaxFields];
+  int64_t ld[kDfMaxFields];
+  int64_t rows[kDfMaxFields];
+  uint32_t dense_mask;
+  int F, dim_shift;
+  int64_t M;
+  int ld0, ld1, off1, off_fm;
+  float* fm1;
+  float* fm2;
+  uint32_t* flags;
+};
+
+template <class P>
+__global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+#ifdef RK_MLP_PHASES
+  const unsigned long long k_t0 = clock64();
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
+#endif
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.M - m0);
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.off1;
+  float* const fm_lds = sm + a.off_fm;  // [fm1 x 16][fm2 x 16]
+  const bool live = wave < rows;
+  const int64_t b = live ? m0 + wave : m0;
+  const int dim = 1 << a.dim_shift, G = dim >> 2;  // float4 quads per field
+  const int nq = a.F * G;                            // float4s of the row
+  constexpr int kQ = (P::KC0 * 4 + 63) / 64;         // float4s per lane (the padded row)
+  const int f_me = lane < a.F ? lane : 0;
+
+  int64_t idx_v = 0;
+  f32x4_t v[kQ];
+  float fw = 0.f;
+  unsigned long long okmask = 0;
+  // round 1: lane f's index in field f
+  auto st_index = [&]() { idx_v = a.idx[f_me][b * a.istride[f_me]]; };
+  // round 2: the row address in lane f, the row's float4s (quad q of the row = quad q % G of field
+  // q / G) and the first-order weight; loads unconditional from valid addresses, masks applied at
+  // the store
+  auto st_issue = [&]() {
+    const int64_t r = (a.dense_mask >> f_me) & 1u ? b : idx_v;
+    const bool ok = r >= 0 && r < a.rows[f_me];
+    const bool bad = lane < a.F && !ok;
+    if (live && __builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) flag_oob(a.flags);
+    okmask = __builtin_amdgcn_ballot_w64(ok && live && lane < a.F);
+    const float* p = a.src[f_me] + (ok ? r : 0) * a.ld[f_me];
+    const uint64_t pu = reinterpret_cast<uint64_t>(p);
+    const uint32_t plo = (uint32_t)pu, phi = (uint32_t)(pu >> 32);
+#pragma unroll
+    for (int i = 0; i < kQ; ++i) {
+      const int q = lane + 64 * i;
+      const int f = min(q >> (a.dim_shift - 2), a.F - 1);
+      const uint32_t lo = __shfl(plo, f, kWave), hi = __shfl(phi, f, kWave);
+      const float* row = reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+      v[i] = *reinterpret_cast<const f32x4_t*>(row + 4 * (q & (G - 1)));
+    }
+    fw = p[dim];
+  };
+  // round 3: the row into buf0 (zeros for padding quads, out-of-range rows and rows past the batch)
+  auto st_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < kQ; ++i) {
+      const int q = lane + 64 * i;
+      if (q < P::KC0 * 4) {
+        const int f = q >> (a.dim_shift - 2);
+        const bool keep = q < nq && ((okmask >> f) & 1ull);
+        *reinterpret_cast<f32x4_t*>(buf0 + wave * a.ld0 + 4 * q) = keep ? v[i] : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  // beside layer 0's MFMAs (buf0 is read-only until layer 1's epilogue): fm1 = sum_f w1_f, fm2 =
+  // 0.5 sum_d ((sum_f e_fd)^2 - sum_f e_fd^2) over the staged row, as rk_fm_linear_packed
+  auto st_fm = [&]() {
+    f32x4_t s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < kQ; ++i) {
+      const int q = lane + 64 * i;
+      if (q < nq) {
+        const f32x4_t x = *reinterpret_cast<const f32x4_t*>(buf0 + wave * a.ld0 + 4 * q);
+        s += x;
+        sq += x * x;
+      }
+    }
+    float o = ((okmask >> lane) & 1ull) ? fw : 0.f;  // lanes < F
+    // lanes of equal lane % G hold the same dims: sum over lane / G
+    for (int x = G; x < 64; x <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += __shfl_xor(s[e], x, kWave);
+        sq[e] += __shfl_xor(sq[e], x, kWave);
+      }
+    }
+    float part = (s[0] * s[0] - sq[0]) + (s[1] * s[1] - sq[1]) + (s[2] * s[2] - sq[2]) + (s[3] * s[3] - sq[3]);
+    for (int x = G / 2; x > 0; x >>= 1) part += __shfl_xor(part, x, kWave);
+    o = wave_sum(o);
+    if (lane == 0) {
+      const float f2 = 0.5f * part;
+      fm_lds[wave] = o;
+      fm_lds[kMlpRows + wave] = f2;
+      if (live) {
+        a.fm1[b] = o;
+        a.fm2[b] = f2;
+      }
+    }
+  };
+  mlp_stream_rows<P, RK_STREAM_EPI>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid,
+                                    side_at<0>(staged(st_index, st_issue, st_store, st_fm)), nullptr, nullptr,
+                                    fm_lds);
+  MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);
+  MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
+  MLP_FLUSH(tid);
+}
+
+}  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                             const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, float* fm1,
+                             float* fm2, void* stream) {
+  if (!fields || num_fields <= 0 || num_fields > kDfMaxFields)
+    return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: %d fields (max %d)", num_fields, kDfMaxFields);
+  if (dim < 4 || dim > 256 || (dim & (dim - 1)))
+    return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: dim %d must be a power of two in [4, 256]", dim);
+  if (!layers || !head || !head->head_w || !head->head_b || !head->final_w || !head->final_b || !fm1 || !fm2 ||
+      batch < 0)
+    return fail(RK_ERR_INVALID, "rk_deepfm_forward: bad arguments (head with final_w / final_b, fm1, fm2)");
+  const int K0 = num_fields * dim;
+  DfArgs a = {};
+  a.head = *head;
+  a.head.fm1 = fm1;  // selects the FM combine; the values come from LDS
+  a.head.fm2 = fm2;
+  a.head.head_partial = nullptr;
+  int need0 = 0, need1 = 0;
+  if (int e = mlp_validate(layers, nlayers, K0, a.head, &need0, &need1, "rk_deepfm_forward")) return e;
+  // the compiled plan: 960 -> 512 -> 256 -> 128 (configs[1]: 30 fields x 32, hidden [512, 256, 128])
+  if (nlayers != kDfLayers || pad64(K0) != StreamPlanK960::KC0 * 16 || stream_plan_for(layers, nlayers, 64) != kStreamK64)
+    return fail(RK_ERR_UNSUPPORTED,
+                "rk_deepfm_forward: no compiled plan for K0 %d and this layer stack (960 -> 512 -> 256 -> 128)", K0);
+  uint32_t* flags = device_flags();
+  if (!flags) return fail(RK_ERR_RUNTIME, "rk_deepfm_forward: device not initialised (rk_init)");
+  for (int f = 0; f < num_fields; ++f) {
+    const rk_segment& s = fields[f];
+    if (!s.src || (s.idx && (s.rows <= 0 || s.idx_stride != 1)) || s.dim != dim || s.src_ld < dim + 1 ||
+        s.src_ld % 4 || !aligned16(s.src) || s.out_col != f * dim)
+      return fail(RK_ERR_INVALID,
+                  "rk_deepfm_forward: field %d is not a packed [rows, >= dim+1] table (unit-stride indices, or "
+                  "none: a dense block of packed rows) at column f*dim",
+                  f);
+    a.src[f] = s.src;
+    a.ld[f] = s.src_ld;
+    if (s.idx) {
+      a.idx[f] = s.idx;
+      a.istride[f] = 1;
+      a.rows[f] = s.rows;
+    } else {
+      a.idx[f] = reinterpret_cast<const int64_t*>(flags);
+      a.istride[f] = 0;
+      a.rows[f] = batch;
+      a.dense_mask |= 1u << f;
+    }
+  }
+  for (int l = 0; l < kDfLayers; ++l) a.L[l] = layers[l];
+  a.F = num_fields;
+  a.dim_shift = __builtin_ctz((unsigned)dim);
+  a.M = batch;
+  a.ld0 = need0 + kMlpLdPad;
+  a.ld1 = need1 + kMlpLdPad;
+  a.off1 = kMlpRows * a.ld0;
+  a.off_fm = a.off1 + kMlpRows * a.ld1;
+  a.fm1 = fm1;
+  a.fm2 = fm2;
+  a.flags = flags;
+  const size_t shm = (size_t)(a.off_fm + 2 * kMlpRows) * sizeof(float);
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
+  if (batch == 0) return RK_OK;
+  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: batch too large");
+  raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960>, 160 * 1024);
+  deepfm_fused_kernel<StreamPlanK960><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  return check_launch("rk_deepfm_forward");
+}

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   float* const buf0 = sm;
   float* const buf1 = sm + a.m.off1;
   float* const part = buf1 + kMlpRows * a.m.ld1;
+  float* const x0s = part + kMlpRows;  // streamed path: the staged rows [16][64], for the side work
   const int width = a.m.K0;
   // Two memory round trips per row instead of one dependent index -> row chain per column: (1) the
   // sample's row index in every segment (wave-uniform loads), (2) the row values of the lane's
@@ -240,9 +241,10 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
       xl[j] = x0[j];
       if (c < K0p) buf0[wave * a.m.ld0 + c] = x0[j];
     }
+    if constexpr (!std::is_void_v<P>) x0s[wave * 64 + lane] = x0[0];
   };
-  // the cross stack and the cross half of output_layer: needed only by the head, so the streamed
-  // tail runs it inside its second layer (stage.side()), off the prologue's critical path
+  // the cross stack and the cross half of output_layer (generic path, after the stage; the
+  // streamed path runs cross_row below as side work instead)
   auto stage_cross = [&]() {
     auto cross = [&](const float* w, const float* bl) {
       float d = 0.f;
@@ -280,6 +282,41 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
     p = wave_sum(p);
     if (lane == 0) part[wave] = p;
   };
+  // streamed path (NJ = 1): the cross stack of staged row s, by any wave (the same arithmetic as
+  // stage_cross); the side work of the third layer, whose 8 column tiles leave waves 8..15 idle:
+  // wave w takes rows w - 8 and w, off the second layer's critical path
+  auto cross_row = [&](int r) {
+    const float x0v = x0s[r * 64 + lane];
+    float xlv = x0v;
+    const bool in = lane < width;
+    auto cross1 = [&](float w, float bl) {
+      float d = 0.f;
+      if (in) d = fmaf(xlv, w, d);
+      d = wave_sum(d);
+      if (in) {
+        float t = x0v * d;
+        t = t + bl;
+        xlv = t + xlv;
+      }
+    };
+#pragma unroll
+    for (int l = 0; l < kDcnPreLayers; ++l)
+      if (l < nl) cross1(cw[l][0], cb[l][0]);
+    for (int l = kDcnPreLayers; l < nl; ++l) {
+      const int c = min(lane, width - 1);
+      cross1(a.cross_w[(int64_t)l * width + c], a.cross_b[(int64_t)l * width + c]);
+    }
+    float p = 0.f;
+    if (in) p = fmaf(xlv, hw[0], p);
+    p = wave_sum(p);
+    if (lane == 0) part[r] = p;
+  };
+  auto side_cross = [&]() {
+    if (wave >= kMlpWaves / 2) {
+      cross_row(wave - kMlpWaves / 2);
+      cross_row(wave);
+    }
+  };
   if constexpr (std::is_void_v<P>)
     mlp_rows(a.m.L, a.m.nl, width, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, nullptr, 0, tid,
              two_phase(
@@ -294,7 +331,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
              part);
   else
     mlp_stream_rows<P, RK_STREAM_EPI>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
-                                      staged(stage_index, stage_issue, stage_store, stage_cross), part);
+                                      side_at<2>(staged(stage_index, stage_issue, stage_store, side_cross)), part);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
   MLP_FLUSH(tid);
@@ -539,6 +576,7 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   a.cross_head_w = cross_head_w;
   a.flags = flags;
   size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
+  const size_t x0_bytes = (size_t)kMlpRows * 64 * sizeof(float);  // streamed path: x0s
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
@@ -548,9 +586,9 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   int plan = width <= 64 ? stream_plan_for(layers, nlayers, width) : kStreamNone;
   if (plan != kStreamNone && plan != kStreamK64) plan = kStreamNone;
   if (plan != kStreamNone) {
-    a.m.off_epi = (int)(shm / sizeof(float));
-    if (shm + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024)
-      shm += sizeof(float) * stream_plan_epi_floats(plan);
+    a.m.off_epi = (int)((shm + x0_bytes) / sizeof(float));
+    if (shm + x0_bytes + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024)
+      shm += x0_bytes + sizeof(float) * stream_plan_epi_floats(plan);
     else
       plan = kStreamNone;
   }

@@ -459,6 +459,24 @@ template <class T, class = void>
 struct stage_has_early : std::false_type {};
 template <class T>
 struct stage_has_early<T, std::void_t<decltype(T::kEarly)>> : std::true_type {};
+// The layer a stage's side work runs beside (mlp_stream.h), when the stage names one: SideAt<L, S>
+// (DeepFM's FM sums read the staged input row, which stays in LDS only through layer 0).
+template <class T, class = void>
+struct stage_side_layer {
+  static constexpr int value = -1;
+};
+template <class T>
+struct stage_side_layer<T, std::void_t<decltype(T::kSideLayer)>> {
+  static constexpr int value = T::kSideLayer;
+};
+template <int L, class S>
+struct SideAt : S {
+  static constexpr int kSideLayer = L;
+};
+template <int L, class S>
+__device__ __forceinline__ SideAt<L, S> side_at(S s) {
+  return SideAt<L, S>{s};
+}
 template <class I, class F>
 __device__ __forceinline__ TwoPhaseStage<I, F> two_phase(I i, F f) {
   return TwoPhaseStage<I, F>{i, f};

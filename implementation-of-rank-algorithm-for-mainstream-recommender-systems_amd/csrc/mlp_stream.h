@@ -166,9 +166,6 @@ struct StreamEpi {
   }
 };
 
-// One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
-// (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
-// operator() after it, before that barrier).  EPI: StreamEpiMode.
 // Chunk of the side layer at which wave position k (0..3 on its SIMD) runs stage.side(), and the
 // positions that run it at chunk c.
 constexpr int side_chunk(int KC, int k) {
@@ -187,11 +184,15 @@ constexpr int side_last_pos(int KC, int c) {
   return -1;
 }
 
+// One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
+// (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
+// operator() after it, before that barrier).  EPI: StreamEpiMode.
 template <class P, int W, int EPI, class Stage>
 __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                  float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                  const rk_epilogue& h, int tid, int wave, Stage& stage,
-                                                 const float* lds_partial, const int64_t* row_ids) {
+                                                 const float* lds_partial, const int64_t* row_ids,
+                                                 const float* lds_fm) {
   constexpr int R = RK_STREAM_RING;
   constexpr int NL = P::NL;
   constexpr int TOT = P::base(NL, W);
@@ -228,6 +229,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
 #endif
   StreamEpi<P> ep_stage;
   constexpr bool kEarly = stage_has_early<Stage>::value;
+  // the layer whose MFMAs the stage's side work runs beside: the stage's choice, else the second
+  constexpr int kSideL = stage_side_layer<Stage>::value >= 0 ? stage_side_layer<Stage>::value : (NL > 1 ? 1 : 0);
   // kEpiRegs: the parameters of the wave's columns of one layer (tiles j = 0, 1)
   ColEpi epr[2];
   auto load_epr = [&](auto LI) {
@@ -278,7 +281,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
     if constexpr (T == 0) {
-      if constexpr (l == (NL > 1 ? 1 : 0)) stage.side();  // (no tile here: the side work all the same)
+      if constexpr (l == kSideL) stage.side();  // (no tile here: the side work all the same)
 #if RK_MLP_SYNC
       // no tile in this layer: take part in the active waves' lockstep barriers
       static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
@@ -309,12 +312,12 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           issue(std::integral_constant<int, B0 + c * T + j + R>{});
         });
         __builtin_amdgcn_sched_barrier(0);
-        // the stage's side work, once, beside the second layer's MFMAs (the first layer's with one),
+        // the stage's side work, once, beside the MFMAs of layer kSideL (default: the second),
         // staggered over the SIMD's four waves (wave w sits at position w / 4 of SIMD w % 4): wave
         // position k at chunk side_chunk(k), one per lockstep window when the layer has 32 chunks, so
         // three of a SIMD's waves keep the matrix pipe fed while the fourth waits on the side work's
         // cross-lane reductions (all four at one chunk left the pipe idle for that latency)
-        if constexpr (l == (NL > 1 ? 1 : 0)) {
+        if constexpr (l == kSideL) {
           constexpr int kFirst = side_first_pos(KC, c), kLast = side_last_pos(KC, c);
           if constexpr (kFirst <= kLast) {
             const int pos = wave >> 2;
@@ -408,7 +411,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           logit = (pre ? hp : h.head_partial[m]) + logit;
         if (h.fm1) {
           if (h.head_aux) h.head_aux[m] = logit;
-          logit = h.fm1[m] * h.final_w[0] + h.fm2[m] * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];
+          const float f1 = lds_fm ? lds_fm[r] : h.fm1[m], f2 = lds_fm ? lds_fm[kMlpRows + r] : h.fm2[m];
+          logit = f1 * h.final_w[0] + f2 * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];
         }
         if (h.head_logit) h.head_logit[m] = logit;
         if (h.head_prob) h.head_prob[m] = 1.0f / (1.0f + expf(-logit));
@@ -424,7 +428,7 @@ __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__
                                                 float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                 const rk_epilogue& h, int tid, Stage stage = Stage(),
                                                 const float* lds_partial = nullptr,
-                                                const int64_t* row_ids = nullptr) {
+                                                const int64_t* row_ids = nullptr, const float* lds_fm = nullptr) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   static_for<0, kMlpWaves>([&](auto WI) {
     constexpr int w = WI;
@@ -434,7 +438,7 @@ __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__
       for (int l = 0; l < P::NL; ++l) mine = mine && P::tpw(l, wave) == P::tpw(l, w);
       if (mine)
         mlp_stream_class<P, w, EPI>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
-                                         lds_partial, row_ids);
+                                         lds_partial, row_ids, lds_fm);
     }
   });
 }
@@ -447,6 +451,7 @@ using StreamPlanK128 = StreamPlan<8, 32, 16, 8>;   // DIN (16 + 34 + 2H <= 128)
 using StreamPlanK192 = StreamPlan<12, 32, 16, 8>;  // BST DNN (16 + 34 + d = 178 at d 128)
 using StreamPlanK256 = StreamPlan<16, 32, 16, 8>;
 using StreamPlanTail512 = StreamPlan<32, 16, 8>;   // DeepFM: 512 -> 256 -> 128
+using StreamPlanK960 = StreamPlan<60, 32, 16, 8>;  // DeepFM whole (30 fields x 32: deepfm_fused.hip)
 
 // Host: the compiled plan matching a layer stack (0: none — use mlp_rows).  Eval only: no
 // activation stores, no residual layers.  RANKOPS_MLP_STREAM=0 disables the streamed path.

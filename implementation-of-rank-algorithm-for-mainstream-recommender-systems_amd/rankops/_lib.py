@@ -288,6 +288,8 @@ SIGNATURES = {
                                             c_void_p, c_void_p]),
     "rk_fm_linear_packed": (ctypes.c_int, [_SEG_P, c_int32, c_int32, c_int64, _MLP_P, c_void_p, c_int64, c_void_p,
                                            c_void_p, c_void_p]),
+    "rk_deepfm_forward": (ctypes.c_int, [_SEG_P, c_int32, c_int32, c_int64, _MLP_P, c_int32, _EPI_P, c_void_p,
+                                         c_void_p, c_void_p]),
     "rk_bn_fold": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),
     # include/rankops_io.h (host input path)

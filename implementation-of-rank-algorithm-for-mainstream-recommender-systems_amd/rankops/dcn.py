@@ -126,6 +126,36 @@ class DCNModel(EngineModule):
         # holds their raw pointers (cross weights and outputs are patched in per call)
         return calls.put(key, (args, ep, B, (packed, head, segs)))
 
+    def prepare(self, dense, category):
+        """An eval forward bound to these input tensors (as DIN.prepare: the single-kernel analogue of
+        capturing the forward in a hipGraph): returns `run()` that recomputes the whole forward from
+        the current contents of the inputs with one rk_dcn_forward launch and returns the same
+        (prob, logit) tensors each time.  Binds the current weights (frozen interaction weights only:
+        per-call mode redraws them every forward)."""
+        if self.training:
+            raise RuntimeError("DCNModel.prepare: eval mode only (call .eval() first)")
+        if self.cross_weights.mode != "frozen":
+            raise RuntimeError("DCNModel.prepare: per-call interaction weights are redrawn every forward; "
+                               "use interaction_weights='frozen'")
+        calls = common.EagerCalls(1)
+        dev = dense.device
+        stream = ops._lib.raw_stream(dev)
+        if self._eager_build(dense, category, 0, calls) is None:
+            raise RuntimeError("DCNModel.prepare: configuration outside rk_dcn_forward's envelope")
+        args, head, B, keep = calls.get(0)
+        cw, cb = self.cross_weights.get(dev)
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head.head_logit, head.head_prob = logit.data_ptr(), prob.data_ptr()
+        args[4], args[5], args[-1] = cw.data_ptr(), cb.data_ptr(), stream
+        fn, out = ops._lib.load().rk_dcn_forward, (prob, logit)
+
+        def run():
+            ops.check(fn(*args), "rk_dcn_forward")
+            return out
+        run.keep = (keep, head, cw, cb, dense, category)
+        return run
+
     def forward(self, dense, category):
         if not self.training:
             out = self._eager_eval(dense, category)

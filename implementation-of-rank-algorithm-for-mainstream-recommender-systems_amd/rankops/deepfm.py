@@ -17,7 +17,9 @@ the deep layers on rk_linear with BatchNorm folded into the epilogue; the last o
 evaluates deep_output_layer, final_layer(3->1) and the sigmoid.  When the first deep layer runs as a
 2D-tiled GEMM (common.tiled_layer: the 30-field benchmark configuration), the gather, fm1, fm2 and
 that layer are one rk_fm_linear_packed launch (FUSED_FRONT): the deep input is staged in LDS and
-never written to HBM, and the eval forward is two launches.
+never written to HBM, and the eval forward is two launches.  At configs[1]'s shape (30 fields x 32,
+hidden [512, 256, 128]) the whole eval forward is one rk_deepfm_forward launch (FUSED_WHOLE): the
+gather, the FM sums, the three deep layers on one weight stream and the head per 16-row tile.
 """
 from __future__ import annotations
 
@@ -34,6 +36,9 @@ WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_s
 PACKED_TABLES = True
 # Gather + FM + first deep layer in one rk_fm_linear_packed launch when that layer is tiled.
 FUSED_FRONT = True
+# The whole eval forward in one rk_deepfm_forward launch where a plan is compiled for the shape
+# (960 -> 512 -> 256 -> 128: configs[1]); otherwise FUSED_FRONT's two launches.
+FUSED_WHOLE = True
 
 
 class DeepFM(EngineModule):
@@ -169,6 +174,12 @@ class DeepFM(EngineModule):
         first = category[names[0]]
         B, dev, D = first.shape[0], first.device, self.embedding_dim
         head_kwargs = dict(final_w=self.final_layer.weight, final_b=self.final_layer.bias)
+        widths = [l.linear.out_features for l in self._tail]
+        if (FUSED_WHOLE and PACKED_TABLES and first.dim() == 1 and len(names) <= 32
+                and ops.deepfm_whole_plan(len(names) * D, widths)):
+            whole = self._whole_build(names, category, head_kwargs)
+            if whole is not None:
+                return whole
         l0, fused = self._tail[0], None
         if FUSED_FRONT and len(self._tail) >= 2 and len(names) <= 32 and first.dim() == 1:
             w0 = common.PACKED(l0.linear.weight)
@@ -198,6 +209,57 @@ class DeepFM(EngineModule):
         gather = ["rk_fm_gather_packed", [arr, len(second), D, B, deep_in.data_ptr(), deep_in.stride(0), None, None,
                                           None]]
         return [gather] + tl, (6, 7), ep, B, (keep, arr, packed, deep_in)
+
+    def _whole_build(self, names, category, head_kwargs):
+        """rk_deepfm_forward's launch (gather, FM, deep layers, head in one): the _eager_build tuple,
+        or None off its path."""
+        plan = self._gather_plan(names, category, deep=False)
+        packed, second, first, D, B, _, fm1, fm2 = plan
+        if not packed or any(t.data_ptr() != category[n].data_ptr() for t, n in zip(first, names)):
+            return None
+        dev = fm1.device
+        ops._lib.ensure_device(dev)
+        arr = ops._seg_array(second)
+        weights = [common.PACKED(l.linear.weight) for l in self._tail]
+        mls = [ops.make_mlp_layer(l.linear.weight, w, **l.epilogue_kwargs()) for l, w in zip(self._tail, weights)]
+        la = (ops._lib.MlpLayer * len(mls))(*mls)
+        ep = ops.make_epilogue(head_w=self.deep_output_layer.weight, head_b=self.deep_output_layer.bias,
+                               **head_kwargs)
+        launch = ["rk_deepfm_forward", [arr, len(second), D, B, la, len(mls), ops.ctypes.byref(ep), None, None, None]]
+        return [launch], (7, 8), ep, B, (arr, packed, weights, mls, la)
+
+    def prepare(self, category):
+        """An eval forward bound to these input tensors (as DIN.prepare: the single-kernel analogue of
+        capturing the forward in a hipGraph): returns `run()` that recomputes the whole forward from
+        the current contents of the inputs with the cached launches (one rk_deepfm_forward at
+        configs[1]'s shape) and returns the same (prob, total, fm1, fm2, deep) tensors each time.
+        Binds the current weights: prepare again after changing them."""
+        if self.training:
+            raise RuntimeError("DeepFM.prepare: eval mode only (call .eval() first)")
+        hit = self._eager_build(category)
+        if hit is None:
+            raise RuntimeError("DeepFM.prepare: configuration outside the cached eval path")
+        launches, fm_slots, ep, B, keep = hit
+        dev = category[next(iter(self.second_order_embeddings))].device
+        out = tuple(torch.empty(B, 1, device=dev, dtype=torch.float32) for _ in range(5))
+        prob, total, fm1, fm2, deep = out
+        front = launches[0][1]
+        front[fm_slots[0]], front[fm_slots[1]] = fm1.data_ptr(), fm2.data_ptr()
+        ep.fm1, ep.fm2, ep.head_aux = fm1.data_ptr(), fm2.data_ptr(), deep.data_ptr()
+        ep.head_logit, ep.head_prob = total.data_ptr(), prob.data_ptr()
+        stream = ops._lib.raw_stream(dev)
+        lib = ops._lib.load()
+        calls = []
+        for name, args in launches:
+            args[-1] = stream
+            calls.append((name, getattr(lib, name), args))
+
+        def run():
+            for name, fn, args in calls:
+                ops.check(fn(*args), name)
+            return out
+        run.keep = (keep, ep, category)
+        return run
 
     def forward(self, category):
         if not self.training:

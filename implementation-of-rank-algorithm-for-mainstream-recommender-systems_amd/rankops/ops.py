@@ -8,6 +8,7 @@ CPU path: a CPU tensor is an error (the CPU restatement in oracle/ is test-only)
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -199,6 +200,25 @@ def fm_linear_packed(fields, dim, batch, layer: "_lib.MlpLayer", y, fm1, fm2):
     arr = _seg_array(fields)
     check(lib.rk_fm_linear_packed(arr, len(fields), dim, batch, ctypes.byref(layer), ptr(y), y.stride(0), ptr(fm1),
                                   ptr(fm2), _lib.stream_of(y)), "rk_fm_linear_packed")
+
+
+def deepfm_whole_plan(k0: int, widths) -> bool:
+    """Whether rk_deepfm_forward has a compiled plan for this DeepFM (deep input k0 wide, hidden
+    widths): 960 -> 512 -> 256 -> 128 (configs[1]); RANKOPS_MLP_STREAM=0 turns it off, as in C."""
+    return (os.environ.get("RANKOPS_MLP_STREAM", "1")[:1] != "0" and (k0 + 63) // 64 * 64 == 960
+            and list(widths) == [512, 256, 128])
+
+
+def deepfm_forward(fields, dim, batch, layers, ep, fm1, fm2):
+    """rk_deepfm_forward: the whole DeepFM eval forward in one launch (packed gather, FM, the deep
+    layers and the head); fields = packed_segment(table, idx, dim, f * dim) per field, layers the
+    three MlpLayer structs, ep the head epilogue (head_w/b, final_w/b, head_logit/prob/aux)."""
+    lib = _lib.load()
+    _lib.ensure_device(fm1.device)
+    arr = _seg_array(fields)
+    la = (_lib.MlpLayer * len(layers))(*layers)
+    check(lib.rk_deepfm_forward(arr, len(fields), dim, batch, la, len(layers), ctypes.byref(ep), ptr(fm1), ptr(fm2),
+                                _lib.stream_of(fm1)), "rk_deepfm_forward")
 
 
 def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, use_softmax, out_ptr, ld_out,

@@ -13,17 +13,18 @@ rank holds a data-parallel slice of B_l samples with the indices of all F fields
                       first-order weight at D, RS = D + 1 rounded up to 4 floats so every row
                       stays 16-B aligned) -> rows [s][b][f_r][RS], one contiguous read per row
   3. row exchange     all_to_all_single back: each source gets [r][b][f_r][RS] from every owner
-  4. FM + MLP         rk_fm_linear_packed over the received rows, read in place as dense blocks of
-                      packed rows (field order restored through out_col = f * D): fm1, fm2 and the
-                      first deep layer in one launch, the [B, F*D] deep input never written to
-                      HBM; then the streamed MLP tail (DeepFM's two-launch forward)
+  4. FM + MLP         rk_deepfm_forward over the received rows, read in place as dense blocks of
+                      packed rows (field order restored through out_col = f * D): fm1, fm2, the
+                      deep layers and the head in one launch, the [B, F*D] deep input never
+                      written to HBM (configs[4]'s shape; other shapes: rk_fm_linear_packed,
+                      then the streamed MLP tail — DeepFM's two-launch forward)
 
 At P > 1 the index exchange covers the whole local batch (one rk_shard_pack_indices launch, one
 all-to-all), then steps 2-4 run per chunk of the local batch (run_steps): each chunk's gather
 (rk_shard_gather_rows, straight from the received int32 indices) feeds a row all-to-all that is
 issued asynchronously and overlaps the next chunk's gather and the previous chunk's FM + tail.
-At P = 1 there is nothing to exchange: the forward is rk_fm_linear_packed over the packed tables
-plus the tail, i.e. `DeepFM.forward` on the same weights.
+At P = 1 there is nothing to exchange: the forward is rk_deepfm_forward over the packed tables,
+i.e. `DeepFM.forward` on the same weights.
 The exchange volume per rank and step is B_l * F * (4 + 4 * RS) bytes (int32 indices), (P-1)/P of
 it on the wire.  Rows travel at RS = 36 floats (144 B, 132 live): the receiver's fused front end
 reads them in place with 16-B loads, which a 132-B stride would misalign for three rows in four,
@@ -80,6 +81,9 @@ class ShardedDeepFM(EngineModule):
         # gather + FM + first deep layer in one rk_fm_linear_packed launch (False: the three-launch
         # rk_fm_gather(_packed) + tiled first layer + tail path, kept for A/B)
         self.fused_front = True
+        # ... and, where a plan is compiled for the shape (960 -> 512 -> 256 -> 128), the whole
+        # forward in one rk_deepfm_forward launch (False: rk_fm_linear_packed + the tail)
+        self.fused_whole = True
         self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
                                                      for f in self.local_fields})
         self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
@@ -242,6 +246,17 @@ class ShardedDeepFM(EngineModule):
         then the rest of the tail and the head (deepfm.py:143-151)."""
         from . import common
         dev = self._device()
+        widths = [l.linear.out_features for l in self._tail]
+        if self.fused_whole and ops.deepfm_whole_plan(len(self.fields) * self.embedding_dim, widths):
+            # the whole forward in one rk_deepfm_forward launch (configs[4]: 30 fields x 32, 512-256-128)
+            mls = [ops.make_mlp_layer(l.linear.weight, common.PACKED(l.linear.weight), **l.epilogue_kwargs())
+                   for l in self._tail]
+            fm1, fm2, deep, total, prob = (torch.empty(B_l, 1, device=dev, dtype=torch.float32) for _ in range(5))
+            ep = ops.make_epilogue(head_w=self.deep_output_layer.weight, head_b=self.deep_output_layer.bias,
+                                   final_w=self.final_layer.weight, final_b=self.final_layer.bias, head_logit=total,
+                                   head_prob=prob, head_aux=deep)
+            ops.deepfm_forward(segs, self.embedding_dim, B_l, mls, ep, fm1, fm2)
+            return prob, total, fm1, fm2, deep
         l0 = self._tail[0]
         ml0 = ops.make_mlp_layer(l0.linear.weight, common.PACKED(l0.linear.weight), **l0.epilogue_kwargs())
         y = torch.empty(B_l, l0.linear.out_features, device=dev, dtype=torch.float32)

@@ -34,6 +34,7 @@
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_fm_linear_packed  the DeepFM front end in one launch: packed-table gather, fm1, fm2 and the
  *                      first deep layer (the deep input never reaches HBM)  deepfm.py:100-112,122-142
+ *   rk_deepfm_forward  DeepFM.forward() in one launch at configs[1]'s shape   deepfm.py:121-151
  *   rk_eval_batch, rk_auc  evaluate(): loss / accuracy / AUC on the device  dcn.py:214-239
  *   rk_fwfm_forward    FwFM.forward()                        fwfm.py:114-139
  *   training (loss.backward() + optimizer.step() of the train() loops, dcn.py:196-201):
@@ -370,6 +371,17 @@ int rk_linear_tiled(const float* x, int64_t ldx, int64_t M, int32_t K, const rk_
 int rk_fm_linear_packed(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                         const rk_mlp_layer* layer, float* y, int64_t ldy, float* fm1, float* fm2,
                         void* stream);
+
+/* The whole DeepFM eval forward in one launch (DeepFM.forward, deepfm.py:121-151): fields as for
+ * rk_fm_linear_packed (packed tables with unit-stride indices, or dense blocks of packed rows),
+ * layers = the three deep layers (Linear + BatchNorm folded + ReLU, deepfm.py:100-112), head =
+ * deep_output_layer (head_w, head_b) with final_layer (final_w, final_b) and the outputs
+ * head_logit / head_prob / head_aux (the deep logit); fm1 / fm2 [batch] are written (its own
+ * fm1 / fm2 fields are ignored).  Compiled plan: 960 -> 512 -> 256 -> 128 (configs[1]: 30 fields
+ * x 32); other shapes return RK_ERR_UNSUPPORTED (use rk_fm_linear_packed + rk_mlp_forward). */
+int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                      const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, float* fm1,
+                      float* fm2, void* stream);
 
 /* ---- table-sharded DeepFM, the local steps around the all-to-alls (rankops.sharded; the
  * reference's DeepFM.forward, deepfm.py:121-151, runs on one device) ---- */

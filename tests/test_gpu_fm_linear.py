@@ -104,10 +104,12 @@ def test_fm_linear_packed_rejects_bad_layouts():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [4096, 4100])
-def test_deepfm_fused_front_against_oracle(B):
+def test_deepfm_fused_front_against_oracle(B, monkeypatch):
     """rankops.DeepFM at configs[1]'s field shape (30 fields x 32, 512-256-128) and a batch that
-    tiles the first layer: the eval forward is rk_fm_linear_packed + rk_mlp_forward, equal to the
-    oracle and to the unfused gather + tiled-layer path."""
+    tiles the first layer, with the one-launch forward off (FUSED_WHOLE, tests/test_gpu_deepfm_fused.py):
+    the eval forward is rk_fm_linear_packed + rk_mlp_forward, equal to the oracle and to the unfused
+    gather + tiled-layer path."""
+    monkeypatch.setattr(deepfm_mod, "FUSED_WHOLE", False)
     cfg = {"dim": 32, "fields": FIELDS30}
     model = H.build("deepfm", cfg)
     H.randomize_eval_stats(model, 5)

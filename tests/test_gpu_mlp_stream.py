@@ -226,7 +226,11 @@ def test_din_stream_matches_oracle():
 
 
 @pytest.mark.gpu
-def test_deepfm_tail_stream_equals_generic():
+def test_deepfm_tail_stream_equals_generic(monkeypatch):
+    """The tail after rk_fm_linear_packed (the one-launch rk_deepfm_forward off: it has no generic
+    twin to be bit-identical to)."""
+    from rankops import deepfm as deepfm_mod
+    monkeypatch.setattr(deepfm_mod, "FUSED_WHOLE", False)
     cfg = {"dim": 32, "fields": {f"field_{i:02d}": 5000 for i in range(30)}}
     (s, g), _ = _model_pair("deepfm", cfg, 4096)
     for a, b in zip(s, g):
@@ -241,3 +245,26 @@ def test_bst_tail_stream_equals_generic():
     for a, b in zip(s, g):
         if isinstance(a, torch.Tensor):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_dcn_prepare_equals_forward():
+    """DCNModel.prepare: the bound rk_dcn_forward launch recomputes from the inputs' current contents."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    model = H.build("dcn", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("dcn", cfg, 1000, seed=8), "cuda")
+    run = model.prepare(d["dense"], d["category"])
+    with torch.no_grad():
+        a = tuple(o.clone() for o in run())
+        ref = model(d["dense"], d["category"])
+    for x, y in zip(a, ref):
+        assert torch.equal(x, y)
+    e = H.to_device(H.make_inputs("dcn", cfg, 1000, seed=9), "cuda")
+    d["dense"].copy_(e["dense"])
+    for k in d["category"]:
+        d["category"][k].copy_(e["category"][k])
+    with torch.no_grad():
+        b = run()
+        ref = model(e["dense"], e["category"])
+    for x, y in zip(b, ref):
+        assert torch.equal(x, y)

@@ -186,11 +186,12 @@ def test_captured_pipeline_emulated_on_gpu(world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [1, 2, 8])
-@pytest.mark.parametrize("fused", [True, False])
-def test_fused_front_and_unfused_path_match_oracle(world, fused):
-    """fm_and_tail / local_fm_and_tail through rk_fm_linear_packed (the received rows read in place
-    as dense blocks of packed rows; P = 1 from the packed tables) and through the three-launch
-    rk_fm_gather path (fused_front = False), against the oracle; ragged local batch."""
+@pytest.mark.parametrize("mode", ["whole", "front", "unfused"])
+def test_fused_front_and_unfused_path_match_oracle(world, mode):
+    """fm_and_tail / local_fm_and_tail through rk_deepfm_forward (whole: the received rows read in
+    place as dense blocks of packed rows; P = 1 from the packed tables), through rk_fm_linear_packed
+    + the tail (front) and through the three-launch rk_fm_gather path (unfused), against the oracle;
+    ragged local batch."""
     full = H.build("deepfm", CFG30, seed=42).cuda()
     B_l = 333
     inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=600 + world), "cuda")
@@ -199,7 +200,8 @@ def test_fused_front_and_unfused_path_match_oracle(world, fused):
 
     def rank_fn(r):
         sh = shards[r]
-        sh.fused_front = fused
+        sh.fused_whole = mode == "whole"
+        sh.fused_front = mode != "unfused"
         mine = {f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in inp["category"].items()}
         with torch.no_grad():
             out = sh.run_steps(mine, chunks=1)
