@@ -825,6 +825,11 @@ def main():
                    "single_stream_samples_per_s": head.get("single_stream_samples_per_s"),
                    "single_stream_ms_per_step": head.get("single_stream_ms_per_step")},
     }
+    from rankops import _lib as rk_lib
+    bi = rk_lib.build_info()
+    result["build"] = {"lib_src_hash": bi.get("src"), "tree_src_hash": bi.get("tree_src"), "arch": bi.get("arch"),
+                       "extra_flags": bi.get("extra"),
+                       "lib_matches_tree": bi.get("tree_src") is not None and bi.get("src") == bi.get("tree_src")}
     if rank == 0:
         launch = model.fused_kernel_launcher(inp["dense"], inp["category"], inp["sequence"], inp["target"])
         ms = kernel_avg_ms(launch)

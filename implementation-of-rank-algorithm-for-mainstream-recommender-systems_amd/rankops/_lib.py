@@ -111,6 +111,7 @@ _MLP_P = POINTER(MlpLayer)
 # name -> (restype, argtypes); the exact set declared in include/*.h
 SIGNATURES = {
     "rk_abi_version": (c_int32, []),
+    "rk_build_info": (c_char_p, []),
     "rk_last_error": (c_char_p, []),
     "rk_init": (ctypes.c_int, [c_int32]),
     "rk_error_flags": (ctypes.c_int, [c_int32, POINTER(c_uint32), c_int32]),
@@ -365,6 +366,33 @@ def load():
         raise RankOpsError(f"rankops: two HIP runtimes mapped in one process: {sorted(runtimes)}")
     _lib = lib
     return lib
+
+
+def build_info() -> dict:
+    """The loaded library's provenance (rk_build_info): {"src": hash of the sources it was built
+    from, "arch", "extra": extra compile flags (timing builds)}, plus "path" and "tree_src" (the
+    same hash over the csrc/ and include/ files next to this package; None without them)."""
+    d = dict(kv.split("=", 1) for kv in load().rk_build_info().decode().split())
+    d["path"] = LIB_PATH
+    d["tree_src"] = tree_source_hash()
+    return d
+
+
+def tree_source_hash():
+    """sha256[:16] over csrc/{*.hip,*.h,*.cpp} (name order) + include/rankops.h + rankops_io.h,
+    as the Makefile computes SRC_HASH."""
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(os.path.dirname(here), "csrc")
+    inc = os.path.join(os.path.dirname(os.path.dirname(here)), "include")
+    if not os.path.isdir(csrc) or not os.path.isdir(inc):
+        return None
+    h = hashlib.sha256()
+    names = sorted(n for n in os.listdir(csrc) if os.path.splitext(n)[1] in (".hip", ".h", ".cpp"))
+    for path in [os.path.join(csrc, n) for n in names] + [os.path.join(inc, n) for n in ("rankops.h", "rankops_io.h")]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def last_error() -> str:

@@ -185,6 +185,8 @@ typedef struct rk_mlp_layer {
 
 /* ---- runtime ---- */
 int32_t rk_abi_version(void);
+/* Provenance of this build: "src=<sha256[:16] of the sources> arch=<gfx> extra=<flags>". */
+const char* rk_build_info(void);
 const char* rk_last_error(void);
 int rk_init(int32_t device);
 /* Reads (and optionally clears) the device flag word; synchronises the device. */

@@ -12,3 +12,5 @@ find $O/trace_deepfm_$1 -name "*kernel_trace.csv" -delete
 RANKOPS_LIB=$PWD/$P/librankops_phases.so timeout -k 10 120 python tools/dcn_phases.py > $O/dcn_phases_$1.log 2>&1 || exit 1
 RANKOPS_LIB=$PWD/$P/librankops_phases.so timeout -k 10 120 python tools/din_phases.py > $O/din_phases_$1.log 2>&1 || exit 1
 head -14 $O/dcn_phases_$1.log; tail -12 $O/din_phases_$1.log
+RANKOPS_LIB=$PWD/$P/librankops_phases.so MODEL=deepfm timeout -k 10 120 python tools/dcn_phases.py > $O/deepfm_phases_$1.log 2>&1 || exit 1
+head -14 $O/deepfm_phases_$1.log
