@@ -55,6 +55,25 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// The same all-lane sum with the in-row steps on DPP (xor 1, xor 2 by quad_perm; 8- and 16-lane
+// mirrors) and only the two cross-row steps through ds_bpermute: 4 VALU ops + 2 LDS round trips
+// instead of 6.  Every step adds two partial sums that are equal in both lanes, so all lanes end
+// with the same bits (a different association from wave_sum: the two are not interchangeable
+// where results must match bit for bit).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f32<0x141>(v);  // row_half_mirror
+  v += dpp_f32<0x140>(v);  // row_mirror
+  v += __shfl_xor(v, 16, kWave);
+  v += __shfl_xor(v, 32, kWave);
+  return v;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

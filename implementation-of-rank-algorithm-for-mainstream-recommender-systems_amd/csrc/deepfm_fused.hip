@@ -151,6 +151,18 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
 
 using namespace rk;
 
+#ifdef RK_MLP_PHASES
+// Timing build only (tools/dcn_phases.py, MODEL=deepfm): this module's phase counters.
+RK_API int rk_debug_deepfm_phases(unsigned long long* marks, int32_t nwg, unsigned* wave_marks) {
+  if (nwg < 0 || nwg > kMlpMarkWG) return 1;
+  if (hipMemcpyFromSymbol(marks, HIP_SYMBOL(g_mlp_marks), sizeof(g_mlp_marks[0]) * nwg) != hipSuccess) return 1;
+  if (wave_marks &&
+      hipMemcpyFromSymbol(wave_marks, HIP_SYMBOL(g_mlp_wave_marks), sizeof(g_mlp_wave_marks[0]) * nwg) != hipSuccess)
+    return 1;
+  return 0;
+}
+#endif
+
 RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                              const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, float* fm1,
                              float* fm2, void* stream) {

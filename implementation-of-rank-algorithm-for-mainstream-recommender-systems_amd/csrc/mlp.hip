@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         if (lane + 64 * j < width) d = fmaf(xl[j], w[j], d);
-      d = wave_sum(d);
+      d = wave_sum_dpp(d);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         if (lane + 64 * j < width) {
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       if (lane + 64 * j < width) p = fmaf(xl[j], hw[j], p);
-    p = wave_sum(p);
+    p = wave_sum_dpp(p);
     if (lane == 0) part[wave] = p;
   };
   // streamed path (NJ = 1): the cross stack of staged row s, by any wave (the same arithmetic as
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
     auto cross1 = [&](float w, float bl) {
       float d = 0.f;
       if (in) d = fmaf(xlv, w, d);
-      d = wave_sum(d);
+      d = wave_sum_dpp(d);
       if (in) {
         float t = x0v * d;
         t = t + bl;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
     }
     float p = 0.f;
     if (in) p = fmaf(xlv, hw[0], p);
-    p = wave_sum(p);
+    p = wave_sum_dpp(p);
     if (lane == 0) part[r] = p;
   };
   auto side_cross = [&]() {

@@ -277,6 +277,9 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     const unsigned long long t0 = clock64();
 #endif
     const rk_mlp_layer& L = layers[l];
+    // lockstep barriers, except in a layer the stage chose for side work that leaves waves without
+    // a tile: those waves do the side work instead, and a barrier would make the others wait for it
+    constexpr bool kSync = !(stage_side_layer<Stage>::value == l && P::nt(l) < kMlpWaves);
     const float* in = (l & 1) ? buf1 : buf0;
     float* out = (l & 1) ? buf0 : buf1;
     const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
@@ -284,7 +287,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       if constexpr (l == kSideL) stage.side();  // (no tile here: the side work all the same)
 #if RK_MLP_SYNC
       // no tile in this layer: take part in the active waves' lockstep barriers
-      static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
+      if constexpr (kSync)
+        static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
 #endif
     } else {
       f32x4_t acc[T];
@@ -326,7 +330,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           }
         }
 #if RK_MLP_SYNC
-        if constexpr ((c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
+        if constexpr (kSync && (c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
 #endif
       });
       MLP_MARK(4 * l, t0);

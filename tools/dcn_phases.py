@@ -28,8 +28,10 @@ M = 4 * 8 + 4
 nwg = (batch + 15) // 16
 buf = (ctypes.c_ulonglong * (nwg * M))()
 wbuf = (ctypes.c_uint * (nwg * 4 * 16 * 2))()
-lib.rk_debug_mlp_phases.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
-assert lib.rk_debug_mlp_phases(buf, nwg, wbuf) == 0
+# each kernel module keeps its own counters: the one-launch DeepFM forward reads deepfm_fused.hip's
+dbg = lib.rk_debug_deepfm_phases if name == "deepfm" and hasattr(lib, "rk_debug_deepfm_phases") else lib.rk_debug_mlp_phases
+dbg.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+assert dbg(buf, nwg, wbuf) == 0
 wm = np.array(wbuf, dtype=np.float64).reshape(nwg, 4, 16, 2) / 1e3
 m = np.array(buf, dtype=np.float64).reshape(nwg, M)
 

@@ -14,3 +14,4 @@ RANKOPS_LIB=$PWD/$P/librankops_phases.so timeout -k 10 120 python tools/din_phas
 head -14 $O/dcn_phases_$1.log; tail -12 $O/din_phases_$1.log
 RANKOPS_LIB=$PWD/$P/librankops_phases.so MODEL=deepfm timeout -k 10 120 python tools/dcn_phases.py > $O/deepfm_phases_$1.log 2>&1 || exit 1
 head -14 $O/deepfm_phases_$1.log
+if [ -n "$AB_BAL" ]; then bash tools/ab_env.sh bal RANKOPS_DIN_BALANCE 0 1 0 1 || exit 1; fi
