@@ -784,14 +784,15 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
                sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 64 * kMlpRows;
   if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
   // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
-  // by default when the histories span three or more tile counts (T > 64).  Measured (graph
-  // replays, batch 4096, lengths uniform in 1..T): T = 128 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us;
-  // at T = 50 (two tile counts) the ranking costs ~1% more than it recovers.
+  // by default when the histories span three or more 16-position tile counts (T > 32).  Measured
+  // (round 3, 32-position tiles, graph replays, batch 4096, lengths uniform in 1..T): T = 128
+  // 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us; round 4 (16-position tiles) at T = 50, kernel averages
+  // over two interleaved A/B pairs: 45.18 / 44.22 -> 44.05 / 43.59 us (profiles/r04/ab_bal_*).
   // RANKOPS_DIN_BALANCE=1 / 0 forces it on / off (tests, A/B timing).  Only where its LDS (the
   // batch row of each LDS row and the class masks) still fits: otherwise contiguous samples.
   const char* env = getenv("RANKOPS_DIN_BALANCE");
   a.bal_nb = (T + 15) / 16 + 1;  // tile-count classes 0 .. ceil(T / 16)
-  const bool want_bal = env && env[0] ? env[0] != '0' : T > 64;
+  const bool want_bal = env && env[0] ? env[0] != '0' : T > 32;
   if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
     const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
     if (shm + extra <= 160 * 1024) {
