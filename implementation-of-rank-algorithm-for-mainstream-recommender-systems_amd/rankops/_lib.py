@@ -401,7 +401,9 @@ def last_error() -> str:
 
 def check(rc: int, what: str):
     if rc != RK_OK:
-        raise RankOpsError(f"{what} failed (code {rc}): {last_error()}")
+        err = RankOpsError(f"{what} failed (code {rc}): {last_error()}")
+        err.code = rc
+        raise err
 
 
 def ensure_device(device: torch.device):

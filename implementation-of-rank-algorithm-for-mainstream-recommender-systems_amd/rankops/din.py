@@ -214,7 +214,8 @@ class DIN(EngineModule):
         seq_len = ops.as_index(sequence[f"{SEQ_KEY}_length"], "sequence length")
         fused = (common.FUSED_DIN and H in (8, 16, 32) and width <= 255 and len(segs) <= 32
                  and self.embeddings[SEQ_KEY].embedding_dim == H
-                 and fused_mlp_fits(width, [l.linear.out_features for l in self._tail]))
+                 and fused_mlp_fits(width, [l.linear.out_features for l in self._tail])
+                 and (width, seq.shape[1], H) not in self.__dict__.get("_unfusable", ()))
         return dict(B=B, dev=dev, segs=segs, cat_col0=cat_col0, q_col=q_col, att_col=att_col, width=width, H=H,
                     seq=seq, seq_len=seq_len, fused=fused, keep=(dense_cols, category, target), lookups=lookups,
                     seq_key=SEQ_KEY, want_l2=self.mini_batch_aware_regularization and self.l2_lambda > 0)
@@ -321,8 +322,21 @@ class DIN(EngineModule):
         args[14:20] = [t.data_ptr() for t in w]
         args[27] = l2_reg.data_ptr() if want_l2 else None
         args[28] = img.data_ptr()
-        ops.check(ops._lib.load().rk_din_forward(*args, stream), "rk_din_forward")
+        rc = ops._lib.load().rk_din_forward(*args, stream)
+        if rc == ops._lib.RK_ERR_UNSUPPORTED:  # e.g. past the kernel's LDS budget: the unfused path
+            self._mark_unfusable(sequence[SEQ_KEY].shape[1], H)
+            calls._d.pop(key, None)
+            return None
+        ops.check(rc, "rk_din_forward")
         return prob, logit, l2_reg
+
+    def _mark_unfusable(self, T, H):
+        """rk_din_forward refused this shape (RK_ERR_UNSUPPORTED, e.g. its LDS carve past 160 KiB with
+        wide fcn layers): later forwards of the shape take the unfused launches."""
+        width = None
+        for l in self._tail[:1]:
+            width = l.linear.in_features
+        self.__dict__.setdefault("_unfusable", set()).add((width, T, H))
 
     def _eager_build(self, dense, category, sequence, target, key, calls):
         if not all(t.dtype == torch.int64 for t in list(category.values()) + [target["feedid"]] + list(sequence.values())):
@@ -371,8 +385,13 @@ class DIN(EngineModule):
         if pl["fused"]:
             # the whole forward in one launch (rk_din_forward)
             l2_reg = torch.empty((), device=dev, dtype=torch.float32) if want_l2 else 0.0
-            self._launch_fused(pl, w, logit, prob, l2_reg)
-            return prob, logit, l2_reg
+            try:
+                self._launch_fused(pl, w, logit, prob, l2_reg)
+                return prob, logit, l2_reg
+            except ops._lib.RankOpsError as e:
+                if getattr(e, "code", None) != ops._lib.RK_ERR_UNSUPPORTED:
+                    raise
+                self._mark_unfusable(T, H)
 
         row = torch.empty(B, width, device=dev, dtype=torch.float32)
         ops.concat_gather(segs, B, row)

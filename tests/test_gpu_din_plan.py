@@ -160,3 +160,36 @@ def test_balanced_assignment_matches_contiguous_blocks(monkeypatch, softmax, bat
     torch.cuda.synchronize()
     assert torch.equal(bal[0], ctg[0]) and torch.equal(bal[1], ctg[1])
     torch.testing.assert_close(bal[2], ctg[2], rtol=1e-6, atol=0)
+
+
+@pytest.mark.gpu
+def test_unsupported_fused_shape_falls_back_to_unfused(monkeypatch):
+    """When rk_din_forward refuses a configuration (RK_ERR_UNSUPPORTED, e.g. an LDS carve past 160
+    KiB), the forward takes the unfused launches for that shape from then on: simulated
+    by refusing every fused launch; the outputs still match the oracle."""
+    import rankops
+    from rankops import common
+    cfg = _cfg(T=80)
+    model = H.build("din", cfg)
+    inp = H.make_inputs("din", cfg, 300)
+    p = H.cpu_params(model)
+    model = model.cuda().eval()
+    d = H.to_device(inp, "cuda")
+
+    def refuse(*a, **k):
+        err = rankops._lib.RankOpsError("rk_din_forward failed (code 4): simulated")
+        err.code = rankops._lib.RK_ERR_UNSUPPORTED
+        raise err
+    monkeypatch.setattr(ops, "din_forward", refuse)
+    monkeypatch.setattr(common, "EAGER_CACHE", False)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        out = H.as_tuple(model(d["dense"], d["category"], d["sequence"], d["target"]))
+        assert model.__dict__.get("_unfusable")  # the shape is marked: no second fused attempt
+        again = H.as_tuple(model(d["dense"], d["category"], d["sequence"], d["target"]))
+        torch.manual_seed(5)
+        ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
+    for o, a, r in zip(out, again, ref):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.cpu(), r, atol=ATOL, rtol=RTOL)
+            assert torch.equal(o, a)
