@@ -415,10 +415,13 @@ class PackedWeights:
     """rk_mlp_pack_weight images, held weakly per weight tensor object and rebuilt when its
     storage or version changes (load_state_dict, .to(), optimizer steps).  Keying on the
     object — not the address — keeps a freed model's packed image from being served to a new
-    tensor that reuses its memory."""
+    tensor that reuses its memory.  After an optimizer step the image is rewritten in place, on
+    the current stream, unless a prepared forward (DIN / DCN / DeepFM .prepare) pinned it: such a
+    plan keeps the image it was prepared with (it binds the weights of that moment; prepare again
+    after changing them), and its launches on other streams never see a half-rewritten image."""
 
     def __init__(self):
-        self._d = {}  # id(tensor) -> (weakref, key, packed); the weakref callback drops the entry
+        self._d = {}  # id(tensor) -> (weakref, key, packed, pinned); the weakref callback drops the entry
 
     def __call__(self, w: torch.Tensor) -> torch.Tensor:
         key = (_GENERATION[0], w.data_ptr(), w._version, tuple(w.shape), w.device)
@@ -426,15 +429,23 @@ class PackedWeights:
         if hit is None or hit[0]() is not w or hit[1] != key:
             d, i = self._d, id(w)
             if hit is not None and hit[0]() is w and hit[1][:2] == key[:2] and hit[1][3:] == key[3:] \
-                    and not torch.cuda.is_current_stream_capturing():
+                    and not hit[3] and not torch.cuda.is_current_stream_capturing():
                 # only the version moved (an optimizer step): rewrite the image in place, on the
                 # stream, behind every launch already reading it
-                hit = (hit[0], key, ops.pack_mlp_weight(w, out=hit[2]))
+                hit = (hit[0], key, ops.pack_mlp_weight(w, out=hit[2]), False)
             else:
                 ref = weakref.ref(w, lambda _r, d=d, i=i: d.pop(i, None) if d.get(i, (None,))[0] is _r else None)
-                hit = (ref, key, ops.pack_mlp_weight(w))
+                hit = (ref, key, ops.pack_mlp_weight(w), False)
             self._d[i] = hit
         return hit[2]
+
+    def pin(self, w: torch.Tensor) -> torch.Tensor:
+        """The current image of `w`, never rewritten in place from now on (a later version of `w`
+        gets a fresh image)."""
+        img = self(w)
+        h = self._d[id(w)]
+        self._d[id(w)] = (h[0], h[1], h[2], True)
+        return img
 
 
 PACKED = PackedWeights()

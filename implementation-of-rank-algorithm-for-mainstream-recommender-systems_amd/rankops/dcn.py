@@ -143,6 +143,8 @@ class DCNModel(EngineModule):
         if self._eager_build(dense, category, 0, calls) is None:
             raise RuntimeError("DCNModel.prepare: configuration outside rk_dcn_forward's envelope")
         args, head, B, keep = calls.get(0)
+        for l in self._tail:  # the images the plan binds are never rewritten in place under it
+            common.PACKED.pin(l.linear.weight)
         cw, cb = self.cross_weights.get(dev)
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)

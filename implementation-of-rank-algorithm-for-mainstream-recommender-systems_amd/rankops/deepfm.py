@@ -240,6 +240,8 @@ class DeepFM(EngineModule):
         if hit is None:
             raise RuntimeError("DeepFM.prepare: configuration outside the cached eval path")
         launches, fm_slots, ep, B, keep = hit
+        for l in self._tail:  # the images the plan binds are never rewritten in place under it
+            common.PACKED.pin(l.linear.weight)
         dev = category[next(iter(self.second_order_embeddings))].device
         out = tuple(torch.empty(B, 1, device=dev, dtype=torch.float32) for _ in range(5))
         prob, total, fm1, fm2, deep = out

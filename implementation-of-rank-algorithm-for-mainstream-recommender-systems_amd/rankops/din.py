@@ -261,7 +261,7 @@ class DIN(EngineModule):
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
         want_l2 = pl["want_l2"]
         l2_reg = torch.empty((), device=dev, dtype=torch.float32) if want_l2 else None
-        packed = [PACKED(l.linear.weight) for l in self._tail]
+        packed = [PACKED.pin(l.linear.weight) for l in self._tail]  # never rewritten under the plan
         layers = [ops.make_mlp_layer(l.linear.weight, pk, **l.epilogue_kwargs()) for l, pk in zip(self._tail, packed)]
         head = ops.make_epilogue(head_w=self.output_layer.weight, head_b=self.output_layer.bias,
                                  head_logit=logit, head_prob=prob)

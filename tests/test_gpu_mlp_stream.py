@@ -268,3 +268,21 @@ def test_dcn_prepare_equals_forward():
         ref = model(e["dense"], e["category"])
     for x, y in zip(b, ref):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_prepared_plan_keeps_its_weight_images_after_an_update():
+    """A prepared forward pins the packed images it binds: a weight update followed by a forward
+    (which repacks) gives the forward the new weights and leaves the plan on the old ones (ADVICE r3:
+    no in-place rewrite under a plan that may run on another stream)."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    model = H.build("dcn", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("dcn", cfg, 500, seed=12), "cuda")
+    run = model.prepare(d["dense"], d["category"])
+    with torch.no_grad():
+        before = run()[0].clone()
+        model._tail[0].linear.weight.mul_(0.5)  # an in-place update: version bump
+        after_fwd = model(d["dense"], d["category"])[0].clone()
+        plan_again = run()[0].clone()
+    assert torch.equal(plan_again, before)
+    assert not torch.equal(after_fwd, before)
