@@ -39,6 +39,11 @@ namespace rk {
 #ifndef RK_STREAM_EPI
 #define RK_STREAM_EPI 2
 #endif
+// experiment: single-tile layers accumulate odd K-steps into a second register set (two
+// independent MFMA chains per wave), summed before the epilogue — not bit-identical to mlp_rows
+#ifndef RK_STREAM_SPLITACC
+#define RK_STREAM_SPLITACC 0
+#endif
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -294,6 +299,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       f32x4_t acc[T];
 #pragma unroll
       for (int j = 0; j < T; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      constexpr bool kSplit = RK_STREAM_SPLITACC && T == 1;
+      f32x4_t acc_odd = {0.f, 0.f, 0.f, 0.f};
       const float* arow = in + li * ldin + kq;
       // A float4s one chunk ahead in two register sets (see mlp_layer)
       f32x4_t ab[2];
@@ -306,7 +313,10 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           constexpr int e = EI;
           static_for<0, T>([&](auto JI) {
             constexpr int j = JI;
-            acc[j] = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc[j]);
+            if constexpr (kSplit && (e & 1))
+              acc_odd = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc_odd);
+            else
+              acc[j] = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc[j]);
           });
         });
         // refill the slots just read with the stream's next loads (past this layer: the next
@@ -333,6 +343,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         if constexpr (kSync && (c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
 #endif
       });
+      if constexpr (kSplit) acc[0] += acc_odd;
       MLP_MARK(4 * l, t0);
 #ifdef RK_MLP_PHASES
       if (lane == 0 && l < 4) s_mlp_wave_marks[l][wave][0] = (unsigned)(clock64() - t0);
