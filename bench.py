@@ -709,6 +709,26 @@ def deepfm_roofline(model, inp, batch):
     return r
 
 
+def bst_small_roofline(model, inp, batch, cfg):
+    """bst_small_kernel (every block + pooling of BST at the reference's own shape, d_model 16, one
+    launch) timed alone: back-to-back launches, HIP events on the stream they run on.  VALU-bound:
+    priced against the FP32 vector peak (157.3 TF needs packed FMAs; the kernel's scalar fmaf chain
+    tops out at half of it)."""
+    launch = model.blocks_kernel_launcher(inp["seq_feedid"], inp["seq_length"])
+    ms = kernel_avg_ms(launch, 20)
+    T, d = cfg["max_len"], cfg["dim"]
+    per = 8 * T * d * d + 4 * T * T * d + 4 * T * d * d  # projections, QK^T + AV, FFN (as BST_BLOCK_FLOP)
+    nb = len(getattr(model, "transformer_blocks", [None]))
+    flop = per * nb * batch
+    r = {"kernel": "bst_small_kernel", "bound": "valu", "unit": "TFLOP/s", "peak": PEAK_FP32_MFMA / 1e12,
+         "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
+         "flop_basis": f"{per:,} per sample per block (T = {T}, d_model {d}) x {nb} block(s)",
+         "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4),
+         "frac_of_unpacked_fma_peak": round(2 * flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
+    r.update(counter_fields("bst_small_kernel", "bst_ref", flop))
+    return r
+
+
 def bst_roofline(model, inp, batch):
     """bst_block_kernel (every transformer block + pooling of the BST forward, one launch) timed
     alone: back-to-back launches, HIP events on the stream they run on."""
@@ -857,6 +877,8 @@ def main():
             if name == "bst":
                 r["gflop_per_s_block"] = round(BST_BLOCK_FLOP * r["samples_per_s"] / 1e9, 1)
                 r["roofline"] = bst_roofline(m2, inp2, batch)
+            if name == "bst_ref":
+                r["roofline"] = bst_small_roofline(m2, inp2, batch, cfg2)
             if name == "dcn":
                 r["roofline"] = dcn_roofline(m2, inp2, batch)
             if name == "deepfm":

@@ -5,7 +5,7 @@
 # Usage (on the box): bash tools/r04_counters.sh <tag> [workloads...]
 set -o pipefail
 T=${1:-base}; shift
-WL=${@:-din dcn deepfm bst}
+WL=${@:-din dcn deepfm bst bst_ref}
 O=gpurun_out/r04/$T; mkdir -p $O
 export TMPDIR=/tmp
 for w in $WL; do
@@ -25,7 +25,7 @@ if [ -z "$NO_PMC" ]; then
   pmc deepfm_gather --workload deepfm_gather --iters 3 || { echo "pmc gather failed"; exit 1; }
   pmc deepfm_gather65536 --workload deepfm_gather --iters 3 --batch 65536 || { echo "pmc gather 65536 failed"; exit 1; }
 fi
-python3 tools/pmc_counters.py $O din:din_forward_kernel dcn:dcn_fused_kernel deepfm:linear_tiled_kernel \
-  deepfm:mlp_stream_kernel bst:bst_block_kernel bst:mlp_stream_kernel deepfm_gather:fm_gather_kernel \
-  deepfm_gather65536:fm_gather_kernel > $O/digest.log 2>&1 || { echo "digest failed"; tail $O/digest.log; exit 1; }
+python3 tools/pmc_counters.py $O din:din_forward_kernel dcn:dcn_fused_kernel deepfm:deepfm_fused_kernel \
+  bst:bst_block_kernel bst:mlp_stream_kernel bst_ref:bst_small_kernel bst_ref:mlp_stream_kernel \
+  deepfm_gather:fm_gather_kernel deepfm_gather65536:fm_gather_kernel > $O/digest.log 2>&1 || { echo "digest failed"; tail $O/digest.log; exit 1; }
 cat $O/digest.log | cut -c1-300
