@@ -206,8 +206,6 @@ class BSTModel(EngineModule):
         seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
         seq_length = ops.as_index(seq_length, "seq_length")
         if self.training:  # Dropout in the blocks and the dnn, BatchNorm batch statistics, HIP backward
-            if len(self.transformer_blocks) == 0:
-                raise NotImplementedError("BSTModel with zero transformer blocks")
             for blk in self.transformer_blocks:
                 if seq_feedid.shape[1] > blk.position_embedding.num_embeddings:
                     raise IndexError(f"BSTTransformer: sequence length {seq_feedid.shape[1]} exceeds max_len "

@@ -817,6 +817,8 @@ class _BSTTrain(torch.autograd.Function):
             saves.append((x, xp, qkv, probs, cx, r1, out1, m1, s1, f1, a, r2, m2, s2))
             x = out
         mean_pool = model.pooling_method != "sum"
+        if not saves:  # no blocks: transformer_output = seq_emb (bst.py:229), pooled over all T positions
+            ops.concat_gather([ops.table_segment(feed, seq.view(-1), 0)], M, x)
         ops.bst_pool(x, B, T, seq_len, mean_pool, row, col)
         units, last = bst_units(model)
         saved = deep_stack_forward(row, units, seed, slot)
@@ -893,6 +895,9 @@ class _BSTTrain(torch.autograd.Function):
             dWv, dbv, _ = _lin_grads(dV, x, blk.w_v.weight, dx=dxp, accumulate=True)
             block_grads[i] = [gpos, dWq, dbq, dWk, dbk, dWv, dbv, dWo, dbo, dg1, dbe1, dg2, dbe2, dW1, db1, dW2, db2]
             dx = dxp
+        if nb == 0:  # no blocks: the pooling gradient goes straight to the gathered sequence rows
+            dx = torch.empty(M, d, **f32)
+            ops.bst_pool_backward(d_row, col, B, T, d, seq_len, mean_pool, dx)
         # embedding tables: the category lookups from the dnn input row, the behaviour sequence from dx
         segs = [ops.table_segment(tgrads[k], idx, c) for k, idx, c in looks]
         if segs:
@@ -1088,18 +1093,29 @@ class Adam(torch.optim.Optimizer):
 
     def _fast_step(self, gi, group) -> bool:
         """The eager step with the marshalled rk_adam_step argument block reused: valid while the
-        group's parameters, their states and their gradients' storages stay the same and every
-        parameter is at the same step count (the reference's loop: every parameter gets a gradient
-        every step).  Per step: one foreach increment of the CPU step tensors, one launch, one
-        version bump.  Anything else (first step, a missing gradient, new gradient storage, mixed
-        step counts) takes the general path, which rebuilds the block next time."""
+        group's parameters and their states stay the same and every parameter is at the same step
+        count (the reference's loop: every parameter gets a gradient every step); new gradient
+        storages are patched into the block.  Per step: one increment of the shared CPU step tensor,
+        one launch, one version bump.  Anything else (first step, a missing gradient, mixed step
+        counts) takes the general path, which rebuilds the block next time."""
         params = group["params"]
         grads = [p.grad for p in params]
         if not params or any(g is None for g in grads):
             return False
         cache = self.__dict__.setdefault("_fast", {})
-        key = tuple(g.data_ptr() for g in grads) + tuple(p.data_ptr() for p in params)
+        key = tuple(p.data_ptr() for p in params)
+        gkey = tuple(g.data_ptr() for g in grads)
         hit = cache.get(gi)
+        if hit is not None and hit[0] == key and hit[7] != gkey:
+            # new gradient storages (the caching allocator need not hand last step's addresses back
+            # after zero_grad(set_to_none=True)): patch the pointers into the block, no rebuild
+            if any(g.dtype != torch.float32 or not g.is_contiguous() or g.is_sparse or g.numel() != p.numel()
+                   or g.device != p.device for g, p in zip(grads, params)):
+                return False
+            arr = hit[1]
+            for i, g in enumerate(grads):
+                arr[i].grad = g.data_ptr()
+            hit[7] = gkey
         if hit is None or hit[0] != key:
             states = [self.state.get(p) for p in params]
             if any(not st for st in states) or any(st["step"].device.type != "cpu" for st in states):
@@ -1124,10 +1140,10 @@ class Adam(torch.optim.Optimizer):
             # the block keeps raw gradient pointers only: holding the gradient tensors would keep
             # last step's storages alive across zero_grad(set_to_none=True), so the next backward
             # could never get the same addresses and the key would miss every step
-            hit = [key, arr, len(entries), shared, int(counts.pop()), bumped, params[0].device]
+            hit = [key, arr, len(entries), shared, int(counts.pop()), bumped, params[0].device, gkey]
             cache[gi] = hit
             self._fast_builds = getattr(self, "_fast_builds", 0) + 1
-        _key, arr, n, step_t, count, bumped, dev = hit
+        _key, arr, n, step_t, count, bumped, dev, _gkey = hit
         step_t.add_(1.0)
         hit[4] = count = count + 1
         beta1, beta2 = group["betas"]

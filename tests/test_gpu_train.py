@@ -740,8 +740,10 @@ def _bst_step_check(cfg, B, seed, steps):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [{"T": 20}, {"T": 20, "dim": 32, "blocks": 2, "pooling": "mean"},
                                  {"T": 64, "dim": 128, "max_len": 64, "vocab": H.WECHAT_VOCAB},
-                                 {"T": 50, "dim": 32, "max_len": 50}],
-                         ids=["reference", "two_blocks_mean", "bench_shape", "reference_T50"])
+                                 {"T": 50, "dim": 32, "max_len": 50}, {"T": 20, "blocks": 0},
+                                 {"T": 20, "blocks": 0, "pooling": "mean"}],
+                         ids=["reference", "two_blocks_mean", "bench_shape", "reference_T50", "zero_blocks",
+                              "zero_blocks_mean"])
 def test_bst_train_steps_match_autograd(cfg):
     _bst_step_check(cfg, 256, seed=2600, steps=2)
 
