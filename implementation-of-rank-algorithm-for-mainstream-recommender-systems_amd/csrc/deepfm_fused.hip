@@ -220,7 +220,7 @@ RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32
   a.fm2 = fm2;
   a.flags = flags;
   const size_t shm = (size_t)(a.off_fm + 2 * kMlpRows) * sizeof(float);
-  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
+  if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: batch too large");

@@ -806,7 +806,7 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   if (plan->stream != kStreamNone) {
     shm = (shm + 15) / 16 * 16;
     const size_t bytes = sizeof(float) * stream_plan_epi_floats(kStreamK128);
-    if (shm + bytes <= 160 * 1024) {
+    if (shm + bytes <= 160 * 1024 - kStreamStaticLds) {
       a.epi_off = (int)(shm / sizeof(float));
       shm += bytes;
     } else {

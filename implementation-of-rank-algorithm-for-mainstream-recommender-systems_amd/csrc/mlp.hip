@@ -487,7 +487,7 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   if (plan != kStreamNone) {
     a.off_epi = (int)(shm / sizeof(float));
     const size_t bytes = shm + sizeof(float) * stream_plan_epi_floats(plan);
-    if (bytes <= 160 * 1024) {
+    if (bytes <= 160 * 1024 - kStreamStaticLds) {
       switch (plan) {
         case kStreamK64: go(mlp_stream_kernel<StreamPlanK64>, bytes); break;
         case kStreamK128: go(mlp_stream_kernel<StreamPlanK128>, bytes); break;
@@ -587,7 +587,7 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   if (plan != kStreamNone && plan != kStreamK64) plan = kStreamNone;
   if (plan != kStreamNone) {
     a.m.off_epi = (int)((shm + x0_bytes) / sizeof(float));
-    if (shm + x0_bytes + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024)
+    if (shm + x0_bytes + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024 - kStreamStaticLds)
       shm += x0_bytes + sizeof(float) * stream_plan_epi_floats(plan);
     else
       plan = kStreamNone;

@@ -44,6 +44,25 @@ namespace rk {
 #ifndef RK_STREAM_SPLITACC
 #define RK_STREAM_SPLITACC 0
 #endif
+// Layer hand-off by per-tile ready flags instead of a workgroup barrier: after its epilogue a wave
+// sets the bits of its output tiles in an LDS word (rk_stream_ready[l]); a wave of layer l+1 waits
+// for bit c only before it reads K-chunk c (= layer l's tile c).  The matrix pipe serves a SIMD's
+// waves oldest-first, so waves 0-3 finish a layer first and, with a barrier, idled through the
+// younger waves' last MFMAs and epilogues (DCN 512->256 boundary: waves 0-3 done at 4.9k, barrier
+// at 7.4k cycles, tools/dcn_phases.py); with the flags they start the next layer's chunks in the
+// order the older waves produce them.  The accumulation order is unchanged (bit-identical to
+// mlp_rows).  The barrier before the head stays.  Measured no gain (DIN 88.1 / 88.0 M against
+// 89.3 / 89.9 M with the barrier, DCN and DeepFM within noise: profiles/r04/ab_flags_*.json): the
+// lockstep barriers 8 chunks into the next layer pull the early waves back, so off.
+#ifndef RK_STREAM_FLAGS
+#define RK_STREAM_FLAGS 0
+#endif
+// LDS that the streamed tail adds to its kernel beyond the caller's carve (the ready words); host
+// LDS budgets leave room for it
+constexpr int kStreamStaticLds = 64;
+#if RK_STREAM_FLAGS
+static __shared__ unsigned rk_stream_ready[RK_MLP_MAX_LAYERS];
+#endif
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -272,6 +291,9 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   MLP_MARK(4 * RK_MLP_MAX_LAYERS - 4, t_start);  // (timing builds) ring issued
   stage();
   if constexpr (EPI == kEpiLdsHere) ep_stage.store(epi, tid);
+#if RK_STREAM_FLAGS
+  if (tid < NL) rk_stream_ready[tid] = 0u;  // read only after the barrier below
+#endif
   mlp_lds_barrier();
   MLP_MARK(4 * RK_MLP_MAX_LAYERS, t_start);  // prologue done
 
@@ -302,12 +324,32 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       constexpr bool kSplit = RK_STREAM_SPLITACC && T == 1;
       f32x4_t acc_odd = {0.f, 0.f, 0.f, 0.f};
       const float* arow = in + li * ldin + kq;
+      // layer l > 0, flag hand-off: K-chunk c is layer l-1's output tile c; `ready` caches the bits
+      // seen set (wave-uniform), the LDS word is re-read only for a chunk not seen yet
+      unsigned ready = 0u;
+      auto wait_chunk = [&](int c) {
+#if RK_STREAM_FLAGS
+        if constexpr (l > 0) {
+          if (!((ready >> c) & 1u)) {
+            do {
+              ready = __builtin_amdgcn_readfirstlane(
+                  __hip_atomic_load(&rk_stream_ready[l - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            } while (!((ready >> c) & 1u));
+            asm volatile("" ::: "memory");  // the chunk's activation reads stay behind the flag
+          }
+        }
+#endif
+      };
       // A float4s one chunk ahead in two register sets (see mlp_layer)
       f32x4_t ab[2];
+      wait_chunk(0);
       ab[0] = *reinterpret_cast<const f32x4_t*>(arow);
       static_for<0, KC>([&](auto CI) {
         constexpr int c = CI;
-        if constexpr (c + 1 < KC) ab[(c + 1) & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * (c + 1));
+        if constexpr (c + 1 < KC) {
+          wait_chunk(c + 1);
+          ab[(c + 1) & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * (c + 1));
+        }
         __builtin_amdgcn_sched_barrier(0);  // the read goes out before this chunk's MFMAs
         static_for<0, 4>([&](auto EI) {
           constexpr int e = EI;
@@ -384,6 +426,16 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         epilogue(std::true_type{});
       else
         epilogue(std::false_type{});
+#if RK_STREAM_FLAGS
+      if constexpr (l + 1 < NL) {
+        // this wave's output tiles are in LDS (its own LDS ops complete in order): publish them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        unsigned bits = 0u;
+#pragma unroll
+        for (int j = 0; j < T; ++j) bits |= 1u << (wave + kMlpWaves * j);
+        if (lane == 0) __hip_atomic_fetch_or(&rk_stream_ready[l], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#endif
 #ifdef RK_MLP_PHASES
       if (lane == 0 && l < 4) s_mlp_wave_marks[l][wave][1] = (unsigned)(clock64() - t0);
 #endif
@@ -394,7 +446,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     if constexpr (EPI == kEpiRegs) load_epr(std::integral_constant<int, l + 1>{});
     if constexpr (l + 2 == NL) head_prefetch();
     MLP_MARK(4 * l + 2, t0);
-    mlp_lds_barrier();
+    if constexpr (!RK_STREAM_FLAGS || l + 1 == NL) mlp_lds_barrier();  // (flags: only before the head)
     MLP_MARK(4 * l + 3, t0);
 #if RK_MLP_EPI_PRIO
     if constexpr (T > 0) __builtin_amdgcn_s_setprio(0);
