@@ -652,7 +652,8 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
     for key, b, cat in legs:
         ms = graph_kernel_avg_ms(model.gather_launcher(cat))
         achieved = DEEPFM_GATHER_BYTES * b / (ms * 1e-3)
-        tr = load_traffic("fm_gather_kernel", "deepfm" if key == f"batch_{batch}" else f"deepfm@{b}") \
+        # (tools/r04_counters.sh: workloads deepfm_gather at the config's batch, deepfm_gather65536)
+        tr = load_traffic("fm_gather_kernel", "deepfm_gather" if b == batch else f"deepfm_gather{b}") \
             if not key.startswith("zipf") else None
         out[key] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
                     "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
