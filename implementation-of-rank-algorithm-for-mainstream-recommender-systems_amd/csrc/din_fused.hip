@@ -124,8 +124,36 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// Phase B's layer-0 K-chunks that run before the barrier closing phase A (mlp_stream.h
+// PreChunks): the row's columns [0, 16 KS) — dense, category and query columns with the reference's
+// layout [dense 16 | category 34 | query H | attention H] — are in LDS before any attention output
+// is, so a wave that finishes its sample early accumulates them while the slowest sample is still
+// in phase A (the matrix pipe is half idle there), and phase B opens with 8 - KS chunks of layer 0.
+template <int H>
+constexpr int din_pre_chunks() {
+  return (16 + 34 + H) / 16 < 7 ? (16 + 34 + H) / 16 : 7;
+}
+// balanced launches gather each wave's row inside phase A: the waves count their rows in here
+static __shared__ unsigned s_din_rows_ready;
+// WAIT: balanced launches only (contiguous ones stage every row before the first barrier); a
+// compile-time flag — a runtime member would be read back from scratch behind the weight ring
+template <bool WAIT>
+struct DinRowsReady {
+  __device__ void issue() const {}
+  __device__ void operator()() const {
+    if constexpr (WAIT) {
+      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_din_rows_ready, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP)) < (unsigned)kMlpWaves)
+        __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");  // the rows are read after the count
+    }
+  }
+  __device__ void side() const {}
+};
+
 // P: the compiled layer plan of phase B (mlp_stream.h), or void for the generic mlp_rows.
-template <int H, int NIT, class P>
+// KS: phase B's layer-0 chunks run before the phase-A barrier (streamed plans; 0: none).
+template <int H, int NIT, class P, int KS = 0>
 __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   using Ly = DinLds<H>;
   constexpr int NQ = H / 8;
@@ -302,6 +330,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     }
   }
   DIN_TS(6);
+  if (KS > 0 && tid == 0) s_din_rows_ready = 0u;
   __syncthreads();
   DIN_TS(1);
 #ifdef RK_DIN_PHASES
@@ -443,6 +472,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+  if constexpr (NIT > 0 && KS > 0) {  // this wave's row is in LDS (its stores completed above)
+    if (lane == 0) __hip_atomic_fetch_add(&s_din_rows_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 #ifdef RK_DIN_PHASES
   if (tid == 0) {  // wave 0: its row in LDS and its first tile's keys landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -590,6 +622,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   if constexpr (std::is_void_v<P>)
     mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
              NIT > 0 ? s_rows : nullptr);
+  else if constexpr (KS > 0)
+    mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid,
+                                      PreChunks<KS, DinRowsReady<(NIT > 0)>>{}, nullptr, NIT > 0 ? s_rows : nullptr);
   else
     mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid, NoStage(),
                               nullptr, NIT > 0 ? s_rows : nullptr);
@@ -697,6 +732,7 @@ struct DinPlan {
   int H;
   int nit;     // balanced assignment: seq_len loads per thread (0: contiguous 16-sample blocks)
   int stream;  // phase B on the streamed plan (kStreamK128) or mlp_rows (kStreamNone)
+  int pre;     // streamed plan: phase B's layer-0 chunks before the phase-A barrier (din_pre_chunks)
 };
 }  // namespace rk
 
@@ -782,7 +818,7 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   }
   size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
                sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 64 * kMlpRows;
-  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
+  if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
   // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
   // by default when the histories span three or more 16-position tile counts (T > 32).  Measured
   // (round 3, 32-position tiles, graph replays, batch 4096, lengths uniform in 1..T): T = 128
@@ -795,7 +831,7 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   const bool want_bal = env && env[0] ? env[0] != '0' : T > 32;
   if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
     const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
-    if (shm + extra <= 160 * 1024) {
+    if (shm + extra <= 160 * 1024 - kStreamStaticLds) {
       plan->nit = batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
       shm += extra;
     }
@@ -813,6 +849,13 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
       plan->stream = kStreamNone;
     }
   }
+  // the pre-barrier chunks need every column they read outside the attention output (the only
+  // columns phase A writes); RANKOPS_DIN_PRE=0 turns them off (A/B timing)
+  if (plan->stream != kStreamNone) {
+    const int ks = H == 8 ? din_pre_chunks<8>() : H == 16 ? din_pre_chunks<16>() : din_pre_chunks<32>();
+    const char* pe = getenv("RANKOPS_DIN_PRE");
+    plan->pre = (pe && pe[0] == '0') || att_col < 16 * ks ? 0 : ks;
+  }
   plan->shm = shm;
   return RK_OK;
 }
@@ -824,6 +867,21 @@ static int din_launch(const DinPlan& p, hipStream_t st) {
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<blocks, kMlpThreads, p.shm, st>>>(p.a);
   };
+  if (p.stream == kStreamK128 && p.pre > 0) {
+    using S = StreamPlanK128;
+    switch (p.H * 16 + p.nit) {
+      case 8 * 16: go(din_forward_kernel<8, 0, S, din_pre_chunks<8>()>); break;
+      case 8 * 16 + 4: go(din_forward_kernel<8, 4, S, din_pre_chunks<8>()>); break;
+      case 8 * 16 + 8: go(din_forward_kernel<8, 8, S, din_pre_chunks<8>()>); break;
+      case 16 * 16: go(din_forward_kernel<16, 0, S, din_pre_chunks<16>()>); break;
+      case 16 * 16 + 4: go(din_forward_kernel<16, 4, S, din_pre_chunks<16>()>); break;
+      case 16 * 16 + 8: go(din_forward_kernel<16, 8, S, din_pre_chunks<16>()>); break;
+      case 32 * 16: go(din_forward_kernel<32, 0, S, din_pre_chunks<32>()>); break;
+      case 32 * 16 + 4: go(din_forward_kernel<32, 4, S, din_pre_chunks<32>()>); break;
+      default: go(din_forward_kernel<32, 8, S, din_pre_chunks<32>()>); break;
+    }
+    return check_launch("rk_din_forward");
+  }
   if (p.stream == kStreamK128) {
     using S = StreamPlanK128;
     switch (p.H * 16 + p.nit) {

@@ -469,6 +469,21 @@ template <class T>
 struct stage_side_layer<T, std::void_t<decltype(T::kSideLayer)>> {
   static constexpr int value = T::kSideLayer;
 };
+// Layer-0 K-chunks the streamed tail (mlp_stream.h) runs before the barrier that opens layer 0,
+// after stage() (PreChunks<KS, S>): the stage guarantees that input columns [0, 16 KS) of every row
+// are in LDS by then (DIN: the feature and query columns, before the slowest sample's attention).
+template <class T, class = void>
+struct stage_pre_chunks {
+  static constexpr int value = 0;
+};
+template <class T>
+struct stage_pre_chunks<T, std::void_t<decltype(T::kPreChunks)>> {
+  static constexpr int value = T::kPreChunks;
+};
+template <int KS, class S>
+struct PreChunks : S {
+  static constexpr int kPreChunks = KS;
+};
 template <int L, class S>
 struct SideAt : S {
   static constexpr int kSideLayer = L;

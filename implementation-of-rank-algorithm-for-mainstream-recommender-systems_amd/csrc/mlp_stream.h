@@ -290,6 +290,37 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   if constexpr (NL == 1) head_prefetch();
   MLP_MARK(4 * RK_MLP_MAX_LAYERS - 4, t_start);  // (timing builds) ring issued
   stage();
+  // layer 0's first KS K-chunks before the barrier (PreChunks: their input columns are staged
+  // already), accumulated in order into the accumulators layer 0 continues from — bit-identical
+  constexpr int KS = stage_pre_chunks<Stage>::value;
+  constexpr int T0 = P::tpw(0, W);
+  static_assert(KS == 0 || (KS < kMlpSyncChunks && KS < P::kc(0) && kSideL != 0 && !RK_STREAM_SPLITACC),
+                "pre-barrier chunks: no lockstep barrier or side work among them");
+  f32x4_t acc0[T0 > 0 ? T0 : 1];
+  if constexpr (KS > 0 && T0 > 0) {
+#pragma unroll
+    for (int j = 0; j < T0; ++j) acc0[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const float* arow = buf0 + li * ld0 + kq;
+    f32x4_t ab[2];
+    ab[0] = *reinterpret_cast<const f32x4_t*>(arow);
+    static_for<0, KS>([&](auto CI) {
+      constexpr int c = CI;
+      if constexpr (c + 1 < KS) ab[(c + 1) & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * (c + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, 4>([&](auto EI) {
+        constexpr int e = EI;
+        static_for<0, T0>([&](auto JI) {
+          constexpr int j = JI;
+          acc0[j] = mfma16(ab[c & 1][e], ring[(c * T0 + j) % R][e], acc0[j]);
+        });
+      });
+      static_for<0, T0>([&](auto JI) {
+        constexpr int j = JI;
+        issue(std::integral_constant<int, c * T0 + j + R>{});
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
   if constexpr (EPI == kEpiLdsHere) ep_stage.store(epi, tid);
 #if RK_STREAM_FLAGS
   if (tid < NL) rk_stream_ready[tid] = 0u;  // read only after the barrier below
@@ -318,9 +349,15 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
 #endif
     } else {
+      constexpr int CB = l == 0 ? KS : 0;  // first chunk of this section (layer 0: after the pre-chunks)
       f32x4_t acc[T];
 #pragma unroll
-      for (int j = 0; j < T; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < T; ++j) {
+        if constexpr (CB > 0)
+          acc[j] = acc0[j];
+        else
+          acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      }
       constexpr bool kSplit = RK_STREAM_SPLITACC && T == 1;
       f32x4_t acc_odd = {0.f, 0.f, 0.f, 0.f};
       const float* arow = in + li * ldin + kq;
@@ -342,9 +379,9 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       };
       // A float4s one chunk ahead in two register sets (see mlp_layer)
       f32x4_t ab[2];
-      wait_chunk(0);
-      ab[0] = *reinterpret_cast<const f32x4_t*>(arow);
-      static_for<0, KC>([&](auto CI) {
+      wait_chunk(CB);
+      ab[CB & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * CB);
+      static_for<CB, KC>([&](auto CI) {
         constexpr int c = CI;
         if constexpr (c + 1 < KC) {
           wait_chunk(c + 1);

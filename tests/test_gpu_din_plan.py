@@ -163,6 +163,34 @@ def test_balanced_assignment_matches_contiguous_blocks(monkeypatch, softmax, bat
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dim", [8, 16, 32])
+@pytest.mark.parametrize("softmax", [False, True])
+@pytest.mark.parametrize("balance", ["0", "1"])
+def test_pre_barrier_layer0_chunks_bit_identical(monkeypatch, dim, softmax, balance):
+    """Phase B's first layer-0 K-chunks (the dense, category and query columns) accumulated by each
+    wave before the barrier that closes phase A (din_fused.hip PreChunks; RANKOPS_DIN_PRE=0 turns
+    them off): the same chunks in the same order into the same accumulators, so every output is
+    bit-identical to the launch without them — contiguous and balanced launches (the balanced one
+    waits on the rows-ready count), zero / short / full histories, a partial last workgroup."""
+    cfg = _cfg(softmax=softmax, dim=dim)
+    model = H.build("din", cfg).cuda().eval()
+    batch = 4096 + 37
+    inp = H.make_inputs("din", cfg, batch, seed=77 + dim)
+    L = inp["sequence"]["his_read_comment_7d_seq_length"]
+    L[:6] = torch.tensor([0, 1, 16, 17, 50, 0])
+    d = H.to_device(inp, "cuda")
+    monkeypatch.setenv("RANKOPS_DIN_BALANCE", balance)
+    with torch.no_grad():
+        monkeypatch.setenv("RANKOPS_DIN_PRE", "1")
+        pre = H.as_tuple(H.call_model(model, "din", d))
+        monkeypatch.setenv("RANKOPS_DIN_PRE", "0")
+        ref = H.as_tuple(H.call_model(model, "din", d))
+    torch.cuda.synchronize()
+    assert torch.equal(pre[0], ref[0]) and torch.equal(pre[1], ref[1])
+    torch.testing.assert_close(pre[2], ref[2], rtol=1e-6, atol=0)
+
+
+@pytest.mark.gpu
 def test_unsupported_fused_shape_falls_back_to_unfused(monkeypatch):
     """When rk_din_forward refuses a configuration (RK_ERR_UNSUPPORTED, e.g. an LDS carve past 160
     KiB), the forward takes the unfused launches for that shape from then on: simulated
