@@ -61,6 +61,10 @@ struct DinArgs {
   rk_epilogue head;
   int ld0, ld1;
   int epi_off;  // streamed phase B (mlp_stream.h): float offset of the epilogue-parameter image
+  // balanced launches of a plan (rk_din_plan_set_epilogue_image): that image packed in global
+  // memory (rk_mlp_pack_epilogue), copied into LDS by LDS-DMA after phase A instead of resolved
+  // per column at launch (≈ 1.6 us of the staging: profiles/r04/din_phases_stage*.log)
+  const float* epi_image;
 };
 
 // LDS carve (floats): [Wk | Wqk | Wq] 3 x 64 x (H+4), W2 32 x 68, b1 64, b2 32, w3 32,
@@ -137,10 +141,14 @@ constexpr int din_pre_chunks() {
 static __shared__ unsigned s_din_rows_ready;
 // WAIT: balanced launches only (contiguous ones stage every row before the first barrier); a
 // compile-time flag — a runtime member would be read back from scratch behind the weight ring
-template <bool WAIT>
+// DMA: balanced launches, whose last four waves may have copied the epilogue image into LDS by
+// LDS-DMA after their phase A: the copies retire before the barrier that opens phase B (loads
+// retire in order; exactly the RK_STREAM_RING ring loads were issued after them).
+template <bool WAIT, bool DMA>
 struct DinRowsReady {
   __device__ void issue() const {}
   __device__ void operator()() const {
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RK_STREAM_RING) : "memory");
     if constexpr (WAIT) {
       while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_din_rows_ready, __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_WORKGROUP)) < (unsigned)kMlpWaves)
@@ -229,9 +237,16 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   // streamed phase B: its epilogue-parameter image rides with the attention image (phase A is long)
   using Epi = std::conditional_t<std::is_void_v<P>, NoStage, StreamEpi<std::conditional_t<std::is_void_v<P>, StreamPlanK128, P>>>;
   Epi epi_img;
-  if constexpr (!std::is_void_v<P>) epi_img.load(a.L, tid);
+  const bool epi_dma = NIT > 0 && a.epi_image != nullptr;  // copied after phase A instead (see DinArgs)
+#ifndef RK_DIN_EXP_NOEPI  // timing experiment only: phase B without its epilogue parameters (wrong outputs)
+  if constexpr (!std::is_void_v<P>)
+    if (!epi_dma) epi_img.load(a.L, tid);
+#endif
   auto image_to_lds = [&]() {
-    if constexpr (!std::is_void_v<P>) epi_img.store(sm + a.epi_off, tid);
+#ifndef RK_DIN_EXP_NOEPI
+    if constexpr (!std::is_void_v<P>)
+      if (!epi_dma) epi_img.store(sm + a.epi_off, tid);
+#endif
     if (a.att_image) {
 #pragma unroll
       for (int r = 0; r < kPer; ++r) {
@@ -619,15 +634,24 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
   return;
 #endif
+  if constexpr (!std::is_void_v<P> && NIT > 0) {
+    // the epilogue image by LDS-DMA (1 KiB per wave instruction) from the four waves with the
+    // shortest samples (balanced: wave j holds the j-th longest), which reach this point first
+    constexpr int kBlocks = P::epi_floats() / 256;
+    static_assert(P::epi_floats() % 256 == 0, "epilogue image of whole 1 KiB blocks");
+    if (epi_dma && wave >= kMlpWaves - 4) {
+      for (int k = wave - (kMlpWaves - 4); k < kBlocks; k += 4)
+        __builtin_amdgcn_global_load_lds((glb_void*)(a.epi_image + 256 * k + 4 * lane),
+                                         (lds_void*)(sm + a.epi_off + 256 * k), 16, 0, 0);
+    }
+  }
   if constexpr (std::is_void_v<P>)
     mlp_rows(a.L, a.nl, a.width, buf0, a.ld0, buf1, a.ld1, m0, rows, a.head, nullptr, 0, tid, NoStage(), nullptr,
              NIT > 0 ? s_rows : nullptr);
-  else if constexpr (KS > 0)
-    mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid,
-                                      PreChunks<KS, DinRowsReady<(NIT > 0)>>{}, nullptr, NIT > 0 ? s_rows : nullptr);
   else
-    mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid, NoStage(),
-                              nullptr, NIT > 0 ? s_rows : nullptr);
+    mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid,
+                                      PreChunks<KS, DinRowsReady<(NIT > 0 && KS > 0), (NIT > 0)>>{}, nullptr,
+                                      NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
   // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =
   // MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1 table (measured valid on
@@ -952,6 +976,16 @@ RK_API int rk_din_plan_launch(const void* plan, void* stream) {
 }
 
 RK_API void rk_din_plan_destroy(void* plan) { delete static_cast<DinPlan*>(plan); }
+
+RK_API int rk_din_plan_set_epilogue_image(void* plan, const float* image) {
+  if (!plan) return fail(RK_ERR_INVALID, "rk_din_plan_set_epilogue_image: null plan");
+  DinPlan& p = *static_cast<DinPlan*>(plan);
+  if (image && ((uintptr_t)image & 15u)) return fail(RK_ERR_INVALID, "rk_din_plan_set_epilogue_image: misaligned image");
+  if (image && (p.stream != kStreamK128 || p.nit == 0))
+    return fail(RK_ERR_UNSUPPORTED, "rk_din_plan_set_epilogue_image: the plan has no balanced streamed phase B");
+  p.a.epi_image = image;
+  return RK_OK;
+}
 
 #ifdef RK_DIN_PHASES
 RK_API int rk_debug_din_phases(unsigned long long* ts, unsigned long long* waves, unsigned long long* mlp) {

@@ -443,6 +443,45 @@ RK_API int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k,
   return check_launch("rk_mlp_pack_weight");
 }
 
+// The streamed tail's epilogue-parameter image ([column][8] resolved floats: mlp_stream.h
+// StreamEpi, the layout of its LDS image) written to global memory once, for kernels that copy it
+// into LDS with LDS-DMA instead of resolving every column's parameters at launch (DIN plans).
+struct EpiPackArgs {
+  rk_mlp_layer L[RK_MLP_MAX_LAYERS];
+  float* out;
+};
+template <class P>
+__global__ __launch_bounds__(kMlpThreads) void mlp_pack_epilogue_kernel(EpiPackArgs a) {
+  StreamEpi<P> e;
+  e.load(a.L, threadIdx.x);
+  e.store(a.out, threadIdx.x);
+}
+
+RK_API int rk_mlp_epilogue_image_floats(const rk_mlp_layer* layers, int32_t nlayers, int32_t K0) {
+  if (!layers || nlayers <= 0 || nlayers > RK_MLP_MAX_LAYERS || K0 <= 0) return 0;
+  return stream_plan_epi_floats(stream_plan_for(layers, nlayers, K0));
+}
+
+RK_API int rk_mlp_pack_epilogue(const rk_mlp_layer* layers, int32_t nlayers, int32_t K0, float* out, void* stream) {
+  if (!out || ((uintptr_t)out & 15u)) return fail(RK_ERR_INVALID, "rk_mlp_pack_epilogue: output null or misaligned");
+  int need0 = 0, need1 = 0;
+  const rk_epilogue none = {};
+  if (int e = mlp_validate(layers, nlayers, K0, none, &need0, &need1, "rk_mlp_pack_epilogue")) return e;
+  EpiPackArgs a = {};
+  for (int l = 0; l < nlayers; ++l) a.L[l] = layers[l];
+  a.out = out;
+  const hipStream_t st = (hipStream_t)stream;
+  switch (stream_plan_for(layers, nlayers, K0)) {
+    case kStreamK64: mlp_pack_epilogue_kernel<StreamPlanK64><<<1, kMlpThreads, 0, st>>>(a); break;
+    case kStreamK128: mlp_pack_epilogue_kernel<StreamPlanK128><<<1, kMlpThreads, 0, st>>>(a); break;
+    case kStreamK192: mlp_pack_epilogue_kernel<StreamPlanK192><<<1, kMlpThreads, 0, st>>>(a); break;
+    case kStreamK256: mlp_pack_epilogue_kernel<StreamPlanK256><<<1, kMlpThreads, 0, st>>>(a); break;
+    case kStreamTail512: mlp_pack_epilogue_kernel<StreamPlanTail512><<<1, kMlpThreads, 0, st>>>(a); break;
+    default: return fail(RK_ERR_UNSUPPORTED, "rk_mlp_pack_epilogue: no compiled layer plan for this stack");
+  }
+  return check_launch("rk_mlp_pack_epilogue");
+}
+
 RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_mlp_layer* layers,
                           int32_t nlayers, const rk_epilogue* head, float* y, int64_t ldy, void* stream) {
   if (!x || M < 0 || ldx < K0) return fail(RK_ERR_INVALID, "rk_mlp_forward: bad input (M=%lld)", (long long)M);

@@ -177,6 +177,9 @@ SIGNATURES = {
          c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
          c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p, POINTER(c_void_p)]),
     "rk_din_plan_launch": (ctypes.c_int, [c_void_p, c_void_p]),
+    "rk_din_plan_set_epilogue_image": (ctypes.c_int, [c_void_p, c_void_p]),
+    "rk_mlp_epilogue_image_floats": (ctypes.c_int, [_MLP_P, c_int32, c_int32]),
+    "rk_mlp_pack_epilogue": (ctypes.c_int, [_MLP_P, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_din_plan_destroy": (None, [c_void_p]),
     "rk_din_attention_image_floats": (c_int64, [c_int32]),
     "rk_din_pack_attention": (

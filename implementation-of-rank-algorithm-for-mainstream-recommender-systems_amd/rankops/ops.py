@@ -472,6 +472,19 @@ class DinPlan:
         self._handle = ctypes.c_void_p()
         check(self._lib.rk_din_forward_plan(*args, ctypes.byref(self._handle)), "rk_din_forward_plan")
         self._keep = keep
+        self._epi = None
+        # phase B's epilogue parameters packed once (rk_mlp_pack_epilogue) and copied into LDS by
+        # the kernel, for plans whose launches use them (balanced streamed plans); the image is a
+        # snapshot of the current BatchNorm / Dice parameters, as the plan binds the weights
+        larr, nl, width = args[21], args[22], args[2]
+        # (RANKOPS_DIN_EPI_DMA=0: resolved per column at launch, as the eager forward does)
+        n = self._lib.rk_mlp_epilogue_image_floats(larr, nl, width)
+        if n > 0 and os.environ.get("RANKOPS_DIN_EPI_DMA", "1") != "0":
+            img = torch.empty(n, device=device, dtype=torch.float32)
+            check(self._lib.rk_mlp_pack_epilogue(larr, nl, width, img.data_ptr(), _lib.raw_stream(device)),
+                  "rk_mlp_pack_epilogue")
+            if self._lib.rk_din_plan_set_epilogue_image(self._handle, img.data_ptr()) == _lib.RK_OK:
+                self._epi = img  # (RK_ERR_UNSUPPORTED: contiguous launches keep resolving at launch)
 
     def launch(self):
         check(self._lib.rk_din_plan_launch(self._handle, _lib.raw_stream(self._device)),

@@ -291,6 +291,11 @@ int rk_din_forward_plan(const rk_segment* row_segs, int32_t nseg, int32_t width,
                         const float* att_image, void** plan);
 int rk_din_plan_launch(const void* plan, void* stream);
 void rk_din_plan_destroy(void* plan);
+/* Binds the plan's phase-B epilogue-parameter image, packed by rk_mlp_pack_epilogue from the same
+ * layer stack (NULL unbinds): balanced launches (T > 32 by default) then copy it into LDS by
+ * LDS-DMA after the attention phase instead of resolving every column's bias / BatchNorm / Dice
+ * parameters at launch.  RK_ERR_UNSUPPORTED for a plan without a balanced streamed phase B.      */
+int rk_din_plan_set_epilogue_image(void* plan, const float* image);
 
 int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
                    const float* dense, int64_t ld_dense, int32_t num_dense,
@@ -336,6 +341,13 @@ int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_pe
  * time; rows/cols of rk_mlp_packed_size give the size and ldw = cols.                       */
 int rk_mlp_packed_size(int32_t n, int32_t k, int64_t* rows, int64_t* cols);
 int rk_mlp_pack_weight(const float* w, int64_t ldw, int32_t n, int32_t k, float* out, void* stream);
+
+/* The per-column epilogue parameters of a layer stack with a compiled streamed plan (hidden units
+ * [512, 256, 128] over an input of <= 256, or [256, 128] over 512), resolved and laid out as the
+ * streamed tail's LDS image ([column][8] floats: bias, pre scale/shift, Dice scale/shift, slope,
+ * post scale/shift).  rk_mlp_epilogue_image_floats: its size in floats (0: no compiled plan).    */
+int rk_mlp_epilogue_image_floats(const rk_mlp_layer* layers, int32_t nlayers, int32_t K0);
+int rk_mlp_pack_epilogue(const rk_mlp_layer* layers, int32_t nlayers, int32_t K0, float* out, void* stream);
 
 /* Whole MLP tail in one launch: layers[0..nlayers) on x [M, K0] (K0 <= 1024, widths <= 512;
  * every layers[l].w packed by rk_mlp_pack_weight, ldw = pad64(K)), then the head of `head`

@@ -191,6 +191,43 @@ def test_pre_barrier_layer0_chunks_bit_identical(monkeypatch, dim, softmax, bala
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dim", [16, 32])
+@pytest.mark.parametrize("batch", [4096, 4133])
+def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch):
+    """A prepared plan binds phase B's epilogue parameters packed once (rk_mlp_pack_epilogue,
+    rk_din_plan_set_epilogue_image); balanced launches copy them into LDS by LDS-DMA after phase A
+    instead of resolving each column at launch.  Same values, same arithmetic: the plan's outputs
+    equal the plan without the image (RANKOPS_DIN_EPI_DMA=0) and the eager forward bit for bit,
+    and match the oracle."""
+    cfg = _cfg(dim=dim, T=50)
+    model = H.build("din", cfg)
+    p = H.cpu_params(model)
+    model = model.cuda().eval()
+    inp = H.make_inputs("din", cfg, batch, seed=5 + batch)
+    d = H.to_device(inp, "cuda")
+    monkeypatch.setenv("RANKOPS_DIN_BALANCE", "1")
+    args = (d["dense"], d["category"], d["sequence"], d["target"])
+    torch.manual_seed(5)  # the frozen H2 draw happens on the first forward, as the oracle's per-call draw
+    with torch.no_grad():
+        monkeypatch.setenv("RANKOPS_DIN_EPI_DMA", "1")
+        run = model.prepare(*args)
+        assert run.plan._epi is not None  # the image is bound
+        dma = [t.clone() for t in H.as_tuple(run())[:2]]
+        monkeypatch.setenv("RANKOPS_DIN_EPI_DMA", "0")
+        run0 = model.prepare(*args)
+        assert run0.plan._epi is None
+        res = [t.clone() for t in H.as_tuple(run0())[:2]]
+        eager = H.as_tuple(H.call_model(model, "din", d))
+    torch.cuda.synchronize()
+    for a, b, c in zip(dma, res, eager):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
+    torch.testing.assert_close(dma[0].cpu(), ref[0], atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
 def test_unsupported_fused_shape_falls_back_to_unfused(monkeypatch):
     """When rk_din_forward refuses a configuration (RK_ERR_UNSUPPORTED, e.g. an LDS carve past 160
     KiB), the forward takes the unfused launches for that shape from then on: simulated
