@@ -61,7 +61,7 @@ struct DinArgs {
   rk_epilogue head;
   int ld0, ld1;
   int epi_off;  // streamed phase B (mlp_stream.h): float offset of the epilogue-parameter image
-  // balanced launches of a plan (rk_din_plan_set_epilogue_image): that image packed in global
+  // a plan's launches (rk_din_plan_set_epilogue_image): that image packed in global
   // memory (rk_mlp_pack_epilogue), copied into LDS by LDS-DMA after phase A instead of resolved
   // per column at launch (≈ 1.6 us of the staging: profiles/r04/din_phases_stage*.log)
   const float* epi_image;
@@ -141,8 +141,8 @@ constexpr int din_pre_chunks() {
 static __shared__ unsigned s_din_rows_ready;
 // WAIT: balanced launches only (contiguous ones stage every row before the first barrier); a
 // compile-time flag — a runtime member would be read back from scratch behind the weight ring
-// DMA: balanced launches, whose last four waves may have copied the epilogue image into LDS by
-// LDS-DMA after their phase A: the copies retire before the barrier that opens phase B (loads
+// DMA: the last four waves may have copied the epilogue image into LDS by LDS-DMA after their
+// phase A: the copies retire before the barrier that opens phase B (loads
 // retire in order; exactly the RK_STREAM_RING ring loads were issued after them).
 template <bool WAIT, bool DMA>
 struct DinRowsReady {
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   // streamed phase B: its epilogue-parameter image rides with the attention image (phase A is long)
   using Epi = std::conditional_t<std::is_void_v<P>, NoStage, StreamEpi<std::conditional_t<std::is_void_v<P>, StreamPlanK128, P>>>;
   Epi epi_img;
-  const bool epi_dma = NIT > 0 && a.epi_image != nullptr;  // copied after phase A instead (see DinArgs)
+  const bool epi_dma = a.epi_image != nullptr;  // copied after phase A instead (see DinArgs)
 #ifndef RK_DIN_EXP_NOEPI  // timing experiment only: phase B without its epilogue parameters (wrong outputs)
   if constexpr (!std::is_void_v<P>)
     if (!epi_dma) epi_img.load(a.L, tid);
@@ -634,9 +634,10 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #ifdef RK_DIN_SKIP_B  // timing experiment only (tools/din_phase_time.py)
   return;
 #endif
-  if constexpr (!std::is_void_v<P> && NIT > 0) {
+  if constexpr (!std::is_void_v<P>) {
     // the epilogue image by LDS-DMA (1 KiB per wave instruction) from the four waves with the
-    // shortest samples (balanced: wave j holds the j-th longest), which reach this point first
+    // shortest samples (either assignment gives wave j the j-th longest sample of the workgroup),
+    // which reach this point first
     constexpr int kBlocks = P::epi_floats() / 256;
     static_assert(P::epi_floats() % 256 == 0, "epilogue image of whole 1 KiB blocks");
     if (epi_dma && wave >= kMlpWaves - 4) {
@@ -650,7 +651,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
              NIT > 0 ? s_rows : nullptr);
   else
     mlp_stream_rows<P, kEpiLdsCaller>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.epi_off, m0, rows, a.head, tid,
-                                      PreChunks<KS, DinRowsReady<(NIT > 0 && KS > 0), (NIT > 0)>>{}, nullptr,
+                                      PreChunks<KS, DinRowsReady<(NIT > 0 && KS > 0), true>>{}, nullptr,
                                       NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
   // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =
@@ -981,8 +982,8 @@ RK_API int rk_din_plan_set_epilogue_image(void* plan, const float* image) {
   if (!plan) return fail(RK_ERR_INVALID, "rk_din_plan_set_epilogue_image: null plan");
   DinPlan& p = *static_cast<DinPlan*>(plan);
   if (image && ((uintptr_t)image & 15u)) return fail(RK_ERR_INVALID, "rk_din_plan_set_epilogue_image: misaligned image");
-  if (image && (p.stream != kStreamK128 || p.nit == 0))
-    return fail(RK_ERR_UNSUPPORTED, "rk_din_plan_set_epilogue_image: the plan has no balanced streamed phase B");
+  if (image && p.stream != kStreamK128)
+    return fail(RK_ERR_UNSUPPORTED, "rk_din_plan_set_epilogue_image: the plan has no streamed phase B");
   p.a.epi_image = image;
   return RK_OK;
 }

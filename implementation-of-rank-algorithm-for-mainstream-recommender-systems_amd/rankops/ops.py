@@ -484,7 +484,7 @@ class DinPlan:
             check(self._lib.rk_mlp_pack_epilogue(larr, nl, width, img.data_ptr(), _lib.raw_stream(device)),
                   "rk_mlp_pack_epilogue")
             if self._lib.rk_din_plan_set_epilogue_image(self._handle, img.data_ptr()) == _lib.RK_OK:
-                self._epi = img  # (RK_ERR_UNSUPPORTED: contiguous launches keep resolving at launch)
+                self._epi = img  # (RK_ERR_UNSUPPORTED: no streamed phase B)
 
     def launch(self):
         check(self._lib.rk_din_plan_launch(self._handle, _lib.raw_stream(self._device)),

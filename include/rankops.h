@@ -292,9 +292,9 @@ int rk_din_forward_plan(const rk_segment* row_segs, int32_t nseg, int32_t width,
 int rk_din_plan_launch(const void* plan, void* stream);
 void rk_din_plan_destroy(void* plan);
 /* Binds the plan's phase-B epilogue-parameter image, packed by rk_mlp_pack_epilogue from the same
- * layer stack (NULL unbinds): balanced launches (T > 32 by default) then copy it into LDS by
- * LDS-DMA after the attention phase instead of resolving every column's bias / BatchNorm / Dice
- * parameters at launch.  RK_ERR_UNSUPPORTED for a plan without a balanced streamed phase B.      */
+ * layer stack (NULL unbinds): its launches then copy it into LDS by LDS-DMA after the attention
+ * phase instead of resolving every column's bias / BatchNorm / Dice parameters at launch.
+ * RK_ERR_UNSUPPORTED for a plan without a streamed phase B.                                     */
 int rk_din_plan_set_epilogue_image(void* plan, const float* image);
 
 int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,

@@ -193,10 +193,12 @@ def test_pre_barrier_layer0_chunks_bit_identical(monkeypatch, dim, softmax, bala
 @pytest.mark.gpu
 @pytest.mark.parametrize("dim", [16, 32])
 @pytest.mark.parametrize("batch", [4096, 4133])
-def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch):
+@pytest.mark.parametrize("balance", ["0", "1"])
+def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch, balance):
     """A prepared plan binds phase B's epilogue parameters packed once (rk_mlp_pack_epilogue,
     rk_din_plan_set_epilogue_image); balanced launches copy them into LDS by LDS-DMA after phase A
-    instead of resolving each column at launch.  Same values, same arithmetic: the plan's outputs
+    instead of resolving each column at launch (balanced and contiguous launches).  Same values, same
+    arithmetic: the plan's outputs
     equal the plan without the image (RANKOPS_DIN_EPI_DMA=0) and the eager forward bit for bit,
     and match the oracle."""
     cfg = _cfg(dim=dim, T=50)
@@ -205,7 +207,7 @@ def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch):
     model = model.cuda().eval()
     inp = H.make_inputs("din", cfg, batch, seed=5 + batch)
     d = H.to_device(inp, "cuda")
-    monkeypatch.setenv("RANKOPS_DIN_BALANCE", "1")
+    monkeypatch.setenv("RANKOPS_DIN_BALANCE", balance)
     args = (d["dense"], d["category"], d["sequence"], d["target"])
     torch.manual_seed(5)  # the frozen H2 draw happens on the first forward, as the oracle's per-call draw
     with torch.no_grad():
