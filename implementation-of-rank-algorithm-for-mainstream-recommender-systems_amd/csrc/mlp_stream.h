@@ -57,6 +57,12 @@ namespace rk {
 #ifndef RK_STREAM_FLAGS
 #define RK_STREAM_FLAGS 0
 #endif
+// Weight-stream loads with the nontemporal hint (experiment): every weight element is read once
+// per CU, so its L1 line is never reused; the memory-pipe counters show the CU's TCP stalled on
+// pending requests 32-43 % of the kernel (profiles/r04/ta).
+#ifndef RK_STREAM_NT
+#define RK_STREAM_NT 0
+#endif
 // LDS that the streamed tail adds to its kernel beyond the caller's carve (the ready words); host
 // LDS budgets leave room for it
 constexpr int kStreamStaticLds = 64;
@@ -232,7 +238,11 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       constexpr int i = g - P::base(l, W), c = i / T, j = i % T;
       const rk_mlp_layer& L = layers[l];
       const float* p = L.w + ((int64_t)(wave + kMlpWaves * j) * (L.ldw / 16) + c) * kFragStep;
+#if RK_STREAM_NT
+      ring[g % R] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p + 4 * lane));
+#else
       ring[g % R] = *reinterpret_cast<const f32x4_t*>(p + 4 * lane);
+#endif
     }
   };
 
