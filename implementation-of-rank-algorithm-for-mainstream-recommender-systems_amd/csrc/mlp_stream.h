@@ -63,6 +63,12 @@ namespace rk {
 #ifndef RK_STREAM_NT
 #define RK_STREAM_NT 0
 #endif
+// Ring loads issued ahead of a kEarly stage's dependent loads (the rest right after them).  A/B
+// over two interleaved runs (profiles/r04/ab_re*.json): DCN 176.0 / 179.8 M with the whole ring
+// ahead (8), 181.0 / 183.0 M at 2, 181.4 / 179.5 at 0, 179.0 / 180.6 at 4; DeepFM within noise.
+#ifndef RK_STREAM_RING_EARLY
+#define RK_STREAM_RING_EARLY 2
+#endif
 // LDS that the streamed tail adds to its kernel beyond the caller's carve (the ready words); host
 // LDS budgets leave room for it
 constexpr int kStreamStaticLds = 64;
@@ -286,7 +292,11 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
     __builtin_amdgcn_sched_barrier(0);  // the stage's and the parameters' loads stay ahead of the ring
   }
-  static_for<0, R>([&](auto G) {
+  // kEarly stages: only the first R0 ring loads go out before the stage's dependent loads (DCN /
+  // DeepFM: the row gather), so those queue behind R0 KiB per wave in the CU's memory pipe instead
+  // of the whole ring (16 waves x 8 KiB); the rest of the ring follows them
+  constexpr int R0 = kEarly ? (RK_STREAM_RING_EARLY < R ? RK_STREAM_RING_EARLY : R) : R;
+  static_for<0, R0>([&](auto G) {
     issue(G);
     __builtin_amdgcn_sched_barrier(0);
   });
@@ -294,6 +304,10 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     stage.issue();
     if constexpr (EPI == kEpiLdsHere) ep_stage.load(layers, tid);
     __builtin_amdgcn_sched_barrier(0);
+    static_for<R0, R>([&](auto G) {
+      issue(G);
+      __builtin_amdgcn_sched_barrier(0);
+    });
   }
   // layer 0's parameters behind the ring (needed only at its epilogue)
   if constexpr (EPI == kEpiRegs) load_epr(std::integral_constant<int, 0>{});
