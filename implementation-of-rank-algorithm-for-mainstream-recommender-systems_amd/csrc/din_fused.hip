@@ -952,6 +952,20 @@ RK_API int rk_din_forward(const rk_segment* row_segs, int32_t nseg, int32_t widt
   return din_launch(p, (hipStream_t)stream);
 }
 
+RK_API int rk_din_forward_ex(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
+                             const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
+                             int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,
+                             const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                             const float* b3, int32_t use_softmax, const rk_mlp_layer* layers, int32_t nlayers,
+                             const rk_epilogue* head, int32_t l2_col0, float l2_scale, float* l2_workspace,
+                             float* l2_out, const float* att_image, const float* epi_image, void* stream) {
+  if (epi_image && ((uintptr_t)epi_image & 15u)) return fail(RK_ERR_INVALID, "rk_din_forward_ex: misaligned epi_image");
+  DinPlan p;
+  if (int e = din_prepare(RK_DIN_ARG_NAMES, &p)) return e;
+  if (p.stream == kStreamK128) p.a.epi_image = epi_image;  // (other phase-B paths resolve at launch)
+  return din_launch(p, (hipStream_t)stream);
+}
+
 RK_API int rk_din_forward_plan(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col, int32_t att_col,
                           const float* key_table, int64_t key_rows, int64_t ld_key, const int64_t* seq,
                           int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t H,

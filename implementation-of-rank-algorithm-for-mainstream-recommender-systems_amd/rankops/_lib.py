@@ -171,6 +171,11 @@ SIGNATURES = {
         [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
          c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
          c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_din_forward_ex": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
+         c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, _MLP_P,
+         c_int32, _EPI_P, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_din_forward_plan": (
         ctypes.c_int,
         [_SEG_P, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,

@@ -322,7 +322,7 @@ class DIN(EngineModule):
         args[14:20] = [t.data_ptr() for t in w]
         args[27] = l2_reg.data_ptr() if want_l2 else None
         args[28] = img.data_ptr()
-        rc = ops._lib.load().rk_din_forward(*args, stream)
+        rc = ops._lib.load().rk_din_forward_ex(*args, stream)
         if rc == ops._lib.RK_ERR_UNSUPPORTED:  # e.g. past the kernel's LDS budget: the unfused path
             self._mark_unfusable(sequence[SEQ_KEY].shape[1], H)
             calls._d.pop(key, None)
@@ -355,10 +355,13 @@ class DIN(EngineModule):
                                            self.use_softmax, layers, head, B, dev, l2_col0=pl["cat_col0"],
                                            l2_scale=float(self.l2_lambda), l2_out=zero[0] if want_l2 else None,
                                            att_image=zero[0])
+        # phase B's epilogue image packed once per entry (the key covers every parameter's
+        # version) and copied into LDS by the kernel (rk_din_forward_ex), as a prepared plan does
+        epi = ops.pack_epilogue_image(args[21], args[22], args[2], dev)
         # the entry keeps what its argument block points into (segment / layer arrays, packed
         # images, the l2 workspace) but not the caller's input tensors: the key's address, shape
         # and stride check already makes the raw input pointers valid on a hit
-        return calls.put(key, (list(args), head, B, want_l2, H, (keep, packed, layers)))
+        return calls.put(key, (list(args) + [ops.ptr(epi)], head, B, want_l2, H, (keep, packed, layers, epi)))
 
     def forward(self, dense, category, sequence, target):
         if not self.training:

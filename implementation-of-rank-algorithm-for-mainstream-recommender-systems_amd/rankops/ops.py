@@ -460,6 +460,19 @@ def din_forward(segs, width, q_col, att_col, key_table, seq, seq_len, H, att_wei
     check(lib.rk_din_forward(*args, _lib.raw_stream(device)), "rk_din_forward")
 
 
+def pack_epilogue_image(larr, nlayers, K0, device):
+    """The per-column epilogue parameters of a layer stack with a compiled streamed plan, packed
+    in the streamed tail's LDS layout (rk_mlp_pack_epilogue), or None (no plan;
+    RANKOPS_DIN_EPI_DMA=0: the DIN kernel resolves them per column at launch instead)."""
+    lib = _lib.load()
+    n = lib.rk_mlp_epilogue_image_floats(larr, nlayers, K0)
+    if n <= 0 or os.environ.get("RANKOPS_DIN_EPI_DMA", "1") == "0":
+        return None
+    img = torch.empty(n, device=device, dtype=torch.float32)
+    check(lib.rk_mlp_pack_epilogue(larr, nlayers, K0, img.data_ptr(), _lib.raw_stream(device)), "rk_mlp_pack_epilogue")
+    return img
+
+
 class DinPlan:
     """rk_din_forward_plan: the fused DIN forward with its arguments validated once; calling it
     launches the kernel on the current stream (one launch, no per-call host work besides the
@@ -477,14 +490,9 @@ class DinPlan:
         # the kernel, for plans whose launches use them (balanced streamed plans); the image is a
         # snapshot of the current BatchNorm / Dice parameters, as the plan binds the weights
         larr, nl, width = args[21], args[22], args[2]
-        # (RANKOPS_DIN_EPI_DMA=0: resolved per column at launch, as the eager forward does)
-        n = self._lib.rk_mlp_epilogue_image_floats(larr, nl, width)
-        if n > 0 and os.environ.get("RANKOPS_DIN_EPI_DMA", "1") != "0":
-            img = torch.empty(n, device=device, dtype=torch.float32)
-            check(self._lib.rk_mlp_pack_epilogue(larr, nl, width, img.data_ptr(), _lib.raw_stream(device)),
-                  "rk_mlp_pack_epilogue")
-            if self._lib.rk_din_plan_set_epilogue_image(self._handle, img.data_ptr()) == _lib.RK_OK:
-                self._epi = img  # (RK_ERR_UNSUPPORTED: no streamed phase B)
+        img = pack_epilogue_image(larr, nl, width, device)
+        if img is not None and self._lib.rk_din_plan_set_epilogue_image(self._handle, img.data_ptr()) == _lib.RK_OK:
+            self._epi = img  # (RK_ERR_UNSUPPORTED: no streamed phase B)
 
     def launch(self):
         check(self._lib.rk_din_plan_launch(self._handle, _lib.raw_stream(self._device)),

@@ -276,6 +276,19 @@ int64_t rk_din_attention_image_floats(int32_t H);
 int rk_din_pack_attention(const float* w1, const float* b1, const float* w2, const float* b2,
                           const float* w3, int32_t H, float* image, void* stream);
 
+/* rk_din_forward with phase B's epilogue-parameter image packed by rk_mlp_pack_epilogue from the
+ * same layer stack (NULL: resolved per column at launch, as rk_din_forward): the kernel copies it
+ * into LDS by LDS-DMA after the attention phase.  Ignored when phase B does not run on the
+ * compiled [512, 256, 128] plan.  Same outputs, bit for bit.                                  */
+int rk_din_forward_ex(const rk_segment* row_segs, int32_t nseg, int32_t width, int32_t q_col,
+                      int32_t att_col, const float* key_table, int64_t key_rows, int64_t ld_key,
+                      const int64_t* seq, int64_t ld_seq, int32_t T, const int64_t* seq_len,
+                      int64_t batch, int32_t H, const float* w1, const float* b1, const float* w2,
+                      const float* b2, const float* w3, const float* b3, int32_t use_softmax,
+                      const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head,
+                      int32_t l2_col0, float l2_scale, float* l2_workspace, float* l2_out,
+                      const float* att_image, const float* epi_image, void* stream);
+
 /* A prepared rk_din_forward: the same arguments, validated once, launched later by
  * rk_din_plan_launch on any stream at the cost of one kernel launch — the one-kernel analogue of
  * a captured hipGraph without the graph's per-replay launch gap (~9 us on this forward).  Like a

@@ -219,10 +219,16 @@ def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch, b
         run0 = model.prepare(*args)
         assert run0.plan._epi is None
         res = [t.clone() for t in H.as_tuple(run0())[:2]]
-        eager = H.as_tuple(H.call_model(model, "din", d))
+        model.__dict__.pop("_eager", None)
+        eager = [t.clone() for t in H.as_tuple(H.call_model(model, "din", d))[:2]]  # rk_din_forward_ex, no image
+        monkeypatch.setenv("RANKOPS_DIN_EPI_DMA", "1")
+        model.__dict__.pop("_eager", None)
+        eager_dma = H.as_tuple(H.call_model(model, "din", d))  # the cached eager entry packs its image
+        entry = next(iter(model._eager._d.values()))
+        assert entry[-1][-1] is not None
     torch.cuda.synchronize()
-    for a, b, c in zip(dma, res, eager):
-        assert torch.equal(a, b) and torch.equal(a, c)
+    for a, b, c, e in zip(dma, res, eager, eager_dma):
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, e)
     torch.manual_seed(5)
     with torch.no_grad():
         ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
