@@ -40,7 +40,11 @@ namespace rk {
 #define RK_STREAM_EPI 2
 #endif
 // experiment: single-tile layers accumulate odd K-steps into a second register set (two
-// independent MFMA chains per wave), summed before the epilogue — not bit-identical to mlp_rows
+// independent MFMA chains per wave), summed before the epilogue — not bit-identical to mlp_rows.
+// A compute-and-stream probe gains 12 % from two chains (tools/stream_probe.hip,
+// profiles/r04/stream_probe3.log), but this form makes hipcc spill ~400 VGPRs (DCN 3x slower,
+// profiles/r04/ab_split_*.json), and alternating the chains per K-chunk instead is within noise
+// (ab_split2_*.json).  Off.
 #ifndef RK_STREAM_SPLITACC
 #define RK_STREAM_SPLITACC 0
 #endif
@@ -318,7 +322,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   // already), accumulated in order into the accumulators layer 0 continues from — bit-identical
   constexpr int KS = stage_pre_chunks<Stage>::value;
   constexpr int T0 = P::tpw(0, W);
-  static_assert(KS == 0 || (KS < kMlpSyncChunks && KS < P::kc(0) && kSideL != 0 && !RK_STREAM_SPLITACC),
+  static_assert(KS == 0 || (KS < kMlpSyncChunks && KS < P::kc(0) && kSideL != 0 && !(RK_STREAM_SPLITACC && T0 == 1)),
                 "pre-barrier chunks: no lockstep barrier or side work among them");
   f32x4_t acc0[T0 > 0 ? T0 : 1];
   if constexpr (KS > 0 && T0 > 0) {
