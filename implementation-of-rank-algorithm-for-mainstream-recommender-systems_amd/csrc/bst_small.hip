@@ -18,6 +18,7 @@
 // Work split: 256-thread workgroups (4 waves), persistent — each wave walks samples
 // b = (blockIdx.x * 4 + wave) + k * gridDim.x * 4.
 #include "common.h"
+#include "mlp_stream.h"
 
 namespace rk {
 
@@ -95,154 +96,298 @@ __device__ __forceinline__ void layernorm16(float (&x)[kSD], const float* gg, co
   for (int i = 0; i < kSD; ++i) x[i] = (x[i] - m) * r * g[i] + be[i];
 }
 
+// One sample's blocks and pooling by one wave (lane t = position t): returns the pooled value of
+// column `lane` in lanes 0..15.  Ks / Vs: the wave's [64][16] LDS slices.
+template <int NH>
+__device__ __forceinline__ float bst_small_sample(const BstSmallArgs& a, int64_t b, float* Ks, float* Vs, int lane) {
+  constexpr int DH = kSD / NH;
+  // scores in log2 units: exp(s / sqrt(dh) - max) = exp2(s * log2(e) / sqrt(dh) - max2) on v_exp_f32
+  const float qscale = 1.4426950408889634f / sqrtf((float)DH);
+  const int T = a.T;
+  const bool pos_live = lane < T;
+  const int64_t len = a.seq_len[b];
+  float x[kSD];
+  {
+    const int64_t r = pos_live ? a.seq[b * a.ld_seq + lane] : 0;
+    const bool ok = r >= 0 && r < a.rows;
+    if (pos_live && !ok) flag_oob(a.flags);
+    const float* src = a.table + (ok ? r : 0) * a.ld;
+#pragma unroll
+    for (int q = 0; q < kSD / 4; ++q) {
+      const f4s v = *reinterpret_cast<const f4s*>(src + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[4 * q + e] = (pos_live && ok) ? v[e] : 0.f;
+    }
+  }
+  for (int blk = 0; blk < a.nblocks; ++blk) {
+    // the parameter pointers laundered per sample and block: loads through them stay inside the
+    // loop (hoisted out of the sample loop, all 1.7k weights would be live in SGPRs and spill)
+    BstSmallW w;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+      const float* pk = a.blk[blk].p[k];
+      asm volatile("" : "+s"(pk));
+      w.p[k] = pk;
+    }
+    w.eps1 = a.blk[blk].eps1;
+    w.eps2 = a.blk[blk].eps2;
+    w.slope = a.blk[blk].slope;
+    // queries / keys get the position embedding, values do not (bst.py:69-71)
+    float qin[kSD];
+    {
+      const float* pp = w.p[0] + (pos_live ? lane : 0) * kSD;
+#pragma unroll
+      for (int q4 = 0; q4 < kSD / 4; ++q4) {
+        const f4s v = *reinterpret_cast<const f4s*>(pp + 4 * q4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qin[4 * q4 + e] = x[4 * q4 + e] + (pos_live ? v[e] : 0.f);
+      }
+    }
+    float q[kSD], t16[kSD];
+    matvec16(w.p[3], w.p[4], qin, t16);  // k
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < kSD / 4; ++i)
+      *reinterpret_cast<f4s*>(Ks + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
+    matvec16(w.p[5], w.p[6], x, t16);  // v
+#pragma unroll
+    for (int i = 0; i < kSD / 4; ++i)
+      *reinterpret_cast<f4s*>(Vs + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
+    matvec16(w.p[1], w.p[2], qin, q);  // q
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // scores s_h[j] = q_h . k_h[j] / sqrt(dh), keys j >= len masked (-inf); two-pass softmax
+    float m[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) m[h] = -INFINITY;
+    for (int j = 0; j < T; ++j) {
+      float k[kSD];
+#pragma unroll
+      for (int i = 0; i < kSD / 4; ++i) {
+        const f4s v = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
+        k[4 * i] = v[0], k[4 * i + 1] = v[1], k[4 * i + 2] = v[2], k[4 * i + 3] = v[3];
+      }
+      const bool masked = (int64_t)j >= len;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
+        s = masked ? -INFINITY : s * qscale;
+        m[h] = fmaxf(m[h], s);
+      }
+    }
+    float l[NH], ctx[kSD];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) l[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSD; ++i) ctx[i] = 0.f;
+    for (int j = 0; j < T; ++j) {
+      float k[kSD], v[kSD];
+#pragma unroll
+      for (int i = 0; i < kSD / 4; ++i) {
+        const f4s kv4 = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
+        const f4s vv4 = *reinterpret_cast<const f4s*>(Vs + j * kSD + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) k[4 * i + e] = kv4[e], v[4 * i + e] = vv4[e];
+      }
+      const bool masked = (int64_t)j >= len;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
+        s = masked ? -INFINITY : s * qscale;
+        const float p = __builtin_amdgcn_exp2f(s - m[h]);
+        l[h] += p;
+#pragma unroll
+        for (int e = 0; e < DH; ++e) ctx[h * DH + e] = fmaf(p, v[h * DH + e], ctx[h * DH + e]);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const float inv = 1.0f / l[h];
+#pragma unroll
+      for (int e = 0; e < DH; ++e) ctx[h * DH + e] = ctx[h * DH + e] * inv;
+    }
+    // out1 = norm1(queries + W_o ctx) (dropout: identity in eval)
+    float o[kSD];
+    matvec16(w.p[7], w.p[8], ctx, o);
+#pragma unroll
+    for (int i = 0; i < kSD; ++i) o[i] = qin[i] + o[i];
+    layernorm16(o, w.p[13], w.p[14], w.eps1);
+    // out = norm2(out1 + ffn(out1)), ffn = Linear, LeakyReLU, (Dropout), Linear
+    matvec16(w.p[9], w.p[10], o, t16);
+    const float slope = w.slope;
+#pragma unroll
+    for (int i = 0; i < kSD; ++i) t16[i] = t16[i] >= 0.f ? t16[i] : t16[i] * slope;
+    matvec16(w.p[11], w.p[12], t16, x);
+#pragma unroll
+    for (int i = 0; i < kSD; ++i) x[i] = o[i] + x[i];
+    layernorm16(x, w.p[15], w.p[16], w.eps2);
+    __builtin_amdgcn_wave_barrier();  // K / V are rewritten by the next block (or sample)
+  }
+  // pooling over all T positions (bst.py:236-241: the padded positions' outputs included)
+  float pooled = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSD; ++i) {
+    const float s = wave_sum(pos_live ? x[i] : 0.f);
+    pooled = lane == i ? s : pooled;
+  }
+  return a.pool_mean ? pooled / (float)len : pooled;
+}
+
 template <int NH>
 __global__ __launch_bounds__(kSWaves * 64, 4) void bst_small_kernel(BstSmallArgs a) {
-  constexpr int DH = kSD / NH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* const kv = sm + wave * 2 * kST * kSD;  // this wave's K [64][16], V [64][16]
-  float* const Ks = kv;
-  float* const Vs = kv + kST * kSD;
-  // scores in log2 units: exp(s / sqrt(dh) - max) = exp2(s * log2(e) / sqrt(dh) - max2) on v_exp_f32
-  const float qscale = 1.4426950408889634f / sqrtf((float)DH);
-
   for (int64_t b = (int64_t)blockIdx.x * kSWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kSWaves) {
-    const int T = a.T;
-    const bool pos_live = lane < T;
-    const int64_t len = a.seq_len[b];
-    float x[kSD];
-    {
-      const int64_t r = pos_live ? a.seq[b * a.ld_seq + lane] : 0;
-      const bool ok = r >= 0 && r < a.rows;
-      if (pos_live && !ok) flag_oob(a.flags);
-      const float* src = a.table + (ok ? r : 0) * a.ld;
+    const float v = bst_small_sample<NH>(a, b, kv, kv + kST * kSD, lane);
+    if (lane < kSD) a.pool_out[b * a.ld_pool + lane] = v;
+  }
+}
+
+// The whole BSTModel eval forward at d_model 16 in one launch (bst.py:216-247): per 16-sample
+// workgroup, wave w gathers sample m0 + w's DNN-row columns [dense | category embeddings] into LDS
+// (bst.py:218-222), runs its transformer blocks and pooling (bst_small_sample, K / V in the wave's
+// LDS slices) and writes the pooled 16 columns after them (bst.py:238-243); then the DNN tail and
+// its output layer + sigmoid (bst.py:245-246) on the streamed plan over the 16 LDS rows.  The K / V
+// slices alias phase B's second activation buffer: phase B writes it only after the barrier that
+// opens it.  Replaces rk_concat_gather + rk_bst_forward_blocks + rk_mlp_forward (three launches and
+// the DNN row's round trip through HBM).
+constexpr int kBfSegs = 8;
+constexpr int kBfCols = 128;  // row columns [0, width + 16) within one 128-wide K plan
+struct BstFwdArgs {
+  BstSmallArgs s;  // blocks, sequence, flags (pool_out unused)
+  rk_segment segs[kBfSegs];
+  uint8_t col_seg[kBfCols], col_off[kBfCols];  // row column -> (segment, offset); 255: zero
+  int width;                                   // pooled columns at [width, width + 16)
+  rk_mlp_layer L[RK_MLP_MAX_LAYERS];
+  rk_epilogue head;
+  int ld0, ld1, off1;  // LDS (floats): buf0 [16][ld0]; at off1 buf1 [16][ld1] / the K, V slices
+};
+static_assert(sizeof(BstFwdArgs) <= 4096, "kernel arguments beyond 4 KiB");
+
+template <int NH>
+__global__ __launch_bounds__(kMlpThreads) void bst_small_fwd_kernel(BstFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.s.batch - m0);
+  const int64_t b = m0 + wave;
+  const bool live = wave < rows;
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.off1;
+  float* const kv = buf1 + wave * 2 * kST * kSD;
+  float* const row = buf0 + wave * a.ld0;
+  // the row's gathered columns (zero past `width` and for a sample past the batch)
 #pragma unroll
-      for (int q = 0; q < kSD / 4; ++q) {
-        const f4s v = *reinterpret_cast<const f4s*>(src + 4 * q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) x[4 * q + e] = (pos_live && ok) ? v[e] : 0.f;
+  for (int i = 0; i < kBfCols / 64; ++i) {
+    const int c = lane + 64 * i;
+    float v = 0.f;
+    const int sg = live && c < a.width ? a.col_seg[c] : 255;
+    if (sg != 255) {
+      const rk_segment& g = a.segs[sg];
+      int64_t r = b;
+      if (g.idx) {
+        r = g.idx[b * g.idx_stride];
+        if (r < 0 || r >= g.rows) {
+          flag_oob(a.s.flags);
+          r = -1;
+        }
       }
+      if (r >= 0) v = g.src[r * g.src_ld + a.col_off[c]];
     }
-    for (int blk = 0; blk < a.nblocks; ++blk) {
-      // the parameter pointers laundered per sample and block: loads through them stay inside the
-      // loop (hoisted out of the sample loop, all 1.7k weights would be live in SGPRs and spill)
-      BstSmallW w;
-#pragma unroll
-      for (int k = 0; k < 17; ++k) {
-        const float* pk = a.blk[blk].p[k];
-        asm volatile("" : "+s"(pk));
-        w.p[k] = pk;
-      }
-      w.eps1 = a.blk[blk].eps1;
-      w.eps2 = a.blk[blk].eps2;
-      w.slope = a.blk[blk].slope;
-      // queries / keys get the position embedding, values do not (bst.py:69-71)
-      float qin[kSD];
-      {
-        const float* pp = w.p[0] + (pos_live ? lane : 0) * kSD;
-#pragma unroll
-        for (int q4 = 0; q4 < kSD / 4; ++q4) {
-          const f4s v = *reinterpret_cast<const f4s*>(pp + 4 * q4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) qin[4 * q4 + e] = x[4 * q4 + e] + (pos_live ? v[e] : 0.f);
-        }
-      }
-      float q[kSD], t16[kSD];
-      matvec16(w.p[3], w.p[4], qin, t16);  // k
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < kSD / 4; ++i)
-        *reinterpret_cast<f4s*>(Ks + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
-      matvec16(w.p[5], w.p[6], x, t16);  // v
-#pragma unroll
-      for (int i = 0; i < kSD / 4; ++i)
-        *reinterpret_cast<f4s*>(Vs + lane * kSD + 4 * i) = (f4s){t16[4 * i], t16[4 * i + 1], t16[4 * i + 2], t16[4 * i + 3]};
-      matvec16(w.p[1], w.p[2], qin, q);  // q
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      // scores s_h[j] = q_h . k_h[j] / sqrt(dh), keys j >= len masked (-inf); two-pass softmax
-      float m[NH];
-#pragma unroll
-      for (int h = 0; h < NH; ++h) m[h] = -INFINITY;
-      for (int j = 0; j < T; ++j) {
-        float k[kSD];
-#pragma unroll
-        for (int i = 0; i < kSD / 4; ++i) {
-          const f4s v = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
-          k[4 * i] = v[0], k[4 * i + 1] = v[1], k[4 * i + 2] = v[2], k[4 * i + 3] = v[3];
-        }
-        const bool masked = (int64_t)j >= len;
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          float s = 0.f;
-#pragma unroll
-          for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
-          s = masked ? -INFINITY : s * qscale;
-          m[h] = fmaxf(m[h], s);
-        }
-      }
-      float l[NH], ctx[kSD];
-#pragma unroll
-      for (int h = 0; h < NH; ++h) l[h] = 0.f;
-#pragma unroll
-      for (int i = 0; i < kSD; ++i) ctx[i] = 0.f;
-      for (int j = 0; j < T; ++j) {
-        float k[kSD], v[kSD];
-#pragma unroll
-        for (int i = 0; i < kSD / 4; ++i) {
-          const f4s kv4 = *reinterpret_cast<const f4s*>(Ks + j * kSD + 4 * i);
-          const f4s vv4 = *reinterpret_cast<const f4s*>(Vs + j * kSD + 4 * i);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) k[4 * i + e] = kv4[e], v[4 * i + e] = vv4[e];
-        }
-        const bool masked = (int64_t)j >= len;
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          float s = 0.f;
-#pragma unroll
-          for (int e = 0; e < DH; ++e) s = fmaf(q[h * DH + e], k[h * DH + e], s);
-          s = masked ? -INFINITY : s * qscale;
-          const float p = __builtin_amdgcn_exp2f(s - m[h]);
-          l[h] += p;
-#pragma unroll
-          for (int e = 0; e < DH; ++e) ctx[h * DH + e] = fmaf(p, v[h * DH + e], ctx[h * DH + e]);
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        const float inv = 1.0f / l[h];
-#pragma unroll
-        for (int e = 0; e < DH; ++e) ctx[h * DH + e] = ctx[h * DH + e] * inv;
-      }
-      // out1 = norm1(queries + W_o ctx) (dropout: identity in eval)
-      float o[kSD];
-      matvec16(w.p[7], w.p[8], ctx, o);
-#pragma unroll
-      for (int i = 0; i < kSD; ++i) o[i] = qin[i] + o[i];
-      layernorm16(o, w.p[13], w.p[14], w.eps1);
-      // out = norm2(out1 + ffn(out1)), ffn = Linear, LeakyReLU, (Dropout), Linear
-      matvec16(w.p[9], w.p[10], o, t16);
-      const float slope = w.slope;
-#pragma unroll
-      for (int i = 0; i < kSD; ++i) t16[i] = t16[i] >= 0.f ? t16[i] : t16[i] * slope;
-      matvec16(w.p[11], w.p[12], t16, x);
-#pragma unroll
-      for (int i = 0; i < kSD; ++i) x[i] = o[i] + x[i];
-      layernorm16(x, w.p[15], w.p[16], w.eps2);
-      __builtin_amdgcn_wave_barrier();  // K / V are rewritten by the next block (or sample)
-    }
-    // pooling over all T positions (bst.py:236-241: the padded positions' outputs included)
-    float pooled = 0.f;
-#pragma unroll
-    for (int i = 0; i < kSD; ++i) {
-      const float s = wave_sum(pos_live ? x[i] : 0.f);
-      pooled = lane == i ? s : pooled;
-    }
-    if (lane < kSD) {
-      const float v = a.pool_mean ? pooled / (float)len : pooled;
-      a.pool_out[b * a.ld_pool + lane] = v;
+    row[c] = v;
+  }
+  const float pooled = live ? bst_small_sample<NH>(a.s, b, kv, kv + kST * kSD, lane) : 0.f;
+  if (lane < kSD) row[a.width + lane] = pooled;
+  mlp_stream_rows<StreamPlanK128, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
+}
+
+RK_API int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, const float* table,
+                                int64_t table_rows, int64_t ld_table, const int64_t* seq, int64_t ld_seq, int32_t T,
+                                const int64_t* seq_len, int64_t batch, int32_t heads, int32_t nblocks,
+                                const float* const* block_params, const float* block_scalars, int32_t pool_mean,
+                                const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, void* stream) {
+  if (heads != 1 && heads != 2 && heads != 4 && heads != 8)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: %d heads (1, 2, 4 or 8)", heads);
+  if (T <= 0 || T > kST) return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: T=%d outside [1, %d]", T, kST);
+  if (nblocks <= 0 || nblocks > kSMaxBlocks)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: %d blocks (1..%d)", nblocks, kSMaxBlocks);
+  if (!row_segs || nseg <= 0 || nseg > kBfSegs || width <= 0 || width + kSD > kBfCols)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: %d row segments over %d columns", nseg, width);
+  if (!table || !seq || !seq_len || !block_params || !block_scalars || !head || !head->head_w || ld_table % 4 ||
+      ((uintptr_t)table & 15u) || ld_seq < T || table_rows <= 0 || batch < 0)
+    return fail(RK_ERR_INVALID, "rk_bst_small_forward: bad arguments");
+  const int K0 = width + kSD;
+  if (stream_plan_for(layers, nlayers, K0) != kStreamK128)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: the DNN tail has no compiled plan over %d columns", K0);
+  BstFwdArgs a = {};
+  int need0 = 0, need1 = 0;
+  a.head = *head;
+  if (int e = mlp_validate(layers, nlayers, K0, a.head, &need0, &need1, "rk_bst_small_forward")) return e;
+  for (int l = 0; l < nlayers; ++l) a.L[l] = layers[l];
+  for (int c = 0; c < kBfCols; ++c) {  // the last covering segment wins (rk_concat_gather)
+    a.col_seg[c] = 255;
+    a.col_off[c] = 0;
+  }
+  for (int sg = 0; sg < nseg; ++sg) {
+    const rk_segment& g = row_segs[sg];
+    if (!g.src || g.dim <= 0 || g.out_col < 0 || g.out_col + g.dim > width || (g.idx && g.rows <= 0))
+      return fail(RK_ERR_INVALID, "rk_bst_small_forward: row segment %d invalid", sg);
+    a.segs[sg] = g;
+    for (int c = g.out_col; c < g.out_col + g.dim; ++c) {
+      a.col_seg[c] = (uint8_t)sg;
+      a.col_off[c] = (uint8_t)(c - g.out_col);
     }
   }
+  a.width = width;
+  BstSmallArgs& s = a.s;
+  s.table = table;
+  s.rows = table_rows;
+  s.ld = ld_table;
+  s.seq = seq;
+  s.ld_seq = ld_seq;
+  s.T = T;
+  s.seq_len = seq_len;
+  s.batch = batch;
+  s.nblocks = nblocks;
+  for (int i = 0; i < nblocks; ++i) {
+    for (int k = 0; k < 17; ++k) {
+      const float* p = block_params[17 * i + k];
+      if (!p || ((uintptr_t)p & 15u))
+        return fail(RK_ERR_INVALID, "rk_bst_small_forward: block %d parameter %d null or misaligned", i, k);
+      s.blk[i].p[k] = p;
+    }
+    s.blk[i].eps1 = block_scalars[3 * i];
+    s.blk[i].eps2 = block_scalars[3 * i + 1];
+    s.blk[i].slope = block_scalars[3 * i + 2];
+  }
+  s.pool_mean = pool_mean;
+  s.flags = device_flags();
+  a.ld0 = need0 + kMlpLdPad;
+  a.ld1 = need1 + kMlpLdPad;
+  a.off1 = kMlpRows * a.ld0;
+  const size_t region = std::max<size_t>((size_t)kMlpWaves * 2 * kST * kSD, (size_t)kMlpRows * a.ld1);
+  const size_t shm = ((size_t)a.off1 + region) * sizeof(float);
+  if (shm > 160 * 1024 - kStreamStaticLds)
+    return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: %zu B of LDS needed", shm);
+  if (batch == 0) return RK_OK;
+  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: batch too large");
+  auto go = [&](auto kern) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  };
+  switch (heads) {
+    case 1: go(bst_small_fwd_kernel<1>); break;
+    case 2: go(bst_small_fwd_kernel<2>); break;
+    case 4: go(bst_small_fwd_kernel<4>); break;
+    default: go(bst_small_fwd_kernel<8>); break;
+  }
+  return check_launch("rk_bst_small_forward");
 }
 
 int bst_small_forward(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq, int64_t ld_seq,

@@ -157,6 +157,10 @@ SIGNATURES = {
     "rk_bst_attention_masked": (
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64,
                        c_void_p]),
+    "rk_bst_small_forward": (
+        ctypes.c_int,
+        [_SEG_P, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32,
+         c_int32, POINTER(c_void_p), POINTER(ctypes.c_float), c_int32, _MLP_P, c_int32, _EPI_P, c_void_p]),
     "rk_bst_forward_blocks": (
         ctypes.c_int,
         [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32, c_int32,

@@ -223,10 +223,11 @@ class BSTModel(EngineModule):
                 segs.append(ops.table_segment(emb.weight, idx, col))
                 col += emb.embedding_dim
         width = col + d
-        row = torch.empty(B, width, device=dev, dtype=torch.float32)
-        ops.concat_gather(segs, B, row)
         nblk = len(self.transformer_blocks)
+        row = None
         if nblk == 0:
+            row = torch.empty(B, width, device=dev, dtype=torch.float32)
+            ops.concat_gather(segs, B, row)
             # no transformer blocks (bst.py:228-235 leaves transformer_output = seq_emb): gather the
             # history rows, then sum / mean pooling over all T positions into the DNN row
             seq = torch.empty(B * T, d, device=dev, dtype=torch.float32)
@@ -242,6 +243,21 @@ class BSTModel(EngineModule):
                 raise IndexError(f"BSTTransformer: sequence length {T} exceeds max_len "
                                  f"{blk.position_embedding.num_embeddings}")
         blocks = self._fused_blocks(T)
+        if blocks is not None and d == 16 and common.FUSED_BST_FWD:
+            # the whole forward in one launch (rk_bst_small_forward): row gather, blocks, pooling,
+            # DNN tail and head; outside its envelope the three launches below
+            logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
+            probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
+            mls = [ops.make_mlp_layer(l.linear.weight, common.PACKED(l.linear.weight), **l.epilogue_kwargs())
+                   for l in self._tail]
+            head = ops.make_epilogue(head_w=self.dnn[-1].weight, head_b=self.dnn[-1].bias, head_logit=logits,
+                                     head_prob=probs)
+            if ops.bst_small_forward(segs, col, self.embeddings['feedid'].weight, seq_feedid, seq_length,
+                                     self.transformer_blocks[0].nhead, blocks, self.pooling_method != 'sum', mls,
+                                     head):
+                return probs, logits
+        row = torch.empty(B, width, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, row)
         if blocks is not None:
             # every block + pooling in one launch, activations in LDS (rk_bst_forward_blocks)
             ops.bst_forward_blocks(self.embeddings['feedid'].weight, seq_feedid, seq_length, d,

@@ -383,6 +383,7 @@ EAGER_CACHE = True  # eval forwards reuse their marshalled launches (EagerCalls)
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
 FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
 FUSED_BST = True  # BST: all transformer blocks + pooling in one rk_bst_forward_blocks launch
+FUSED_BST_FWD = True  # BST at d_model 16: row gather + blocks + pooling + DNN tail in one rk_bst_small_forward
 # A first layer this wide runs as its own 2D-tiled GEMM (rk_linear_tiled) before the fused tail:
 # in the 16-row fused kernel every CU would stream the whole weight (DeepFM 960 -> 512: 2 MB)
 TILED_FIRST_MIN_K = 512

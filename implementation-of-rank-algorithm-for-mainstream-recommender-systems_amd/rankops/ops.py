@@ -319,6 +319,29 @@ def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr
                                     ld_pool, 1 if pool_mean else 0, _lib.stream_of(table)), "rk_bst_forward_blocks")
 
 
+def bst_small_forward(segs, width, table, seq, seq_len, heads, blocks, pool_mean, layers, head: Epilogue) -> bool:
+    """rk_bst_small_forward: the whole BST eval forward at d_model 16 in one launch.  False (nothing
+    launched) outside its envelope (RK_ERR_UNSUPPORTED), for the three-launch path."""
+    lib = _lib.load()
+    B, T = seq.shape
+    params = (ctypes.c_void_p * (BST_BLOCK_PARAMS * len(blocks)))()
+    scalars = (ctypes.c_float * (3 * len(blocks)))()
+    for i, (tensors, sc) in enumerate(blocks):
+        for k, t in enumerate(tensors):
+            params[BST_BLOCK_PARAMS * i + k] = ptr(t)
+        for k in range(3):
+            scalars[3 * i + k] = float(sc[k])
+    arr = _seg_array(segs)
+    larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
+    rc = lib.rk_bst_small_forward(arr, len(segs), width, ptr(table), table.shape[0], table.stride(0), ptr(seq),
+                                  seq.stride(0), T, ptr(seq_len), B, heads, len(blocks), params, scalars,
+                                  1 if pool_mean else 0, larr, len(layers), ctypes.byref(head), _lib.stream_of(table))
+    if rc == _lib.RK_ERR_UNSUPPORTED:
+        return False
+    check(rc, "rk_bst_small_forward")
+    return True
+
+
 def bn_fold(mean, var, weight, bias, eps, scale, shift):
     lib = _lib.load()
     check(lib.rk_bn_fold(ptr(mean), ptr(var), ptr(weight), ptr(bias), float(eps), mean.numel(), ptr(scale),

@@ -326,6 +326,21 @@ int rk_bst_attention_masked(const float* qkv, int64_t ld_qkv, int64_t batch, int
                             int32_t d_model, int32_t heads, const uint8_t* key_padding_mask,
                             int64_t ld_mask, float* ctx, int64_t ld_ctx, void* stream);
 
+/* The whole BSTModel eval forward at the reference script's d_model 16 (bst.py:192, 216-247) in one
+ * launch: the DNN row [dense | category embeddings] gathered by `row_segs` over columns
+ * [0, width), every transformer block and the pooling (as rk_bst_forward_blocks at d_model 16)
+ * written to columns [width, width + 16), then `layers` (packed by rk_mlp_pack_weight, BatchNorm
+ * folded, LeakyReLU) and the output layer + sigmoid of `head` (head_w/head_b/head_logit/head_prob).
+ * Envelope: heads 1/2/4/8, 1 <= T <= 64, nblocks <= 4, nseg <= 8, width + 16 in (64, 128] with
+ * hidden units [512, 256, 128] (else RK_ERR_UNSUPPORTED: rk_concat_gather +
+ * rk_bst_forward_blocks + rk_mlp_forward compute the same).                                  */
+int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, const float* table,
+                         int64_t table_rows, int64_t ld_table, const int64_t* seq, int64_t ld_seq,
+                         int32_t T, const int64_t* seq_len, int64_t batch, int32_t heads,
+                         int32_t nblocks, const float* const* block_params,
+                         const float* block_scalars, int32_t pool_mean, const rk_mlp_layer* layers,
+                         int32_t nlayers, const rk_epilogue* head, void* stream);
+
 /* Every transformer block of BSTModel.forward plus the pooling (bst.py:66-91, 224-241) in one
  * launch, one workgroup per sample, activations kept in LDS:
  *   x = table[seq[b, :T]];  for each block i: x = block_i(x)  (mask keys >= seq_len[b])

@@ -58,3 +58,44 @@ def test_small_bst_oob_sequence_index_is_flagged():
     with torch.no_grad():
         H.call_model(model, "bst", inp)
     assert rankops.error_flags(reset=True) & 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,batch", [
+    ({"T": 50, "heads": 4, "vocab": H.WECHAT_VOCAB}, 4096),   # the bench leg (models.bst_ref)
+    ({"T": 50, "heads": 4, "pooling": "mean"}, 4133),           # a partial last workgroup
+    ({"T": 64, "heads": 1, "max_len": 64}, 300),
+    ({"T": 33, "heads": 2, "blocks": 2}, 17),
+    ({"T": 17, "heads": 8, "blocks": 3, "batch_norm": False}, 64),
+])
+def test_small_bst_one_launch_equals_three_launches(monkeypatch, cfg, batch):
+    """rk_bst_small_forward (the whole d_model-16 forward in one launch: row gather, blocks, pooling,
+    DNN tail, head) against rk_concat_gather + rk_bst_forward_blocks + rk_mlp_forward on the same
+    inputs: the same gather, the same per-sample block code and the same streamed tail, so the
+    outputs agree bit for bit (NaN rows of length-0 sequences included)."""
+    model = H.build("bst", cfg).cuda().eval()
+    inp = H.make_inputs("bst", cfg, batch, seed=41)
+    inp["seq_length"][:2] = torch.tensor([0, cfg["T"]])
+    d = H.to_device(inp, "cuda")
+    calls = []
+    real = rankops.ops.bst_small_forward
+    monkeypatch.setattr(rankops.ops, "bst_small_forward", lambda *a, **k: calls.append(1) or real(*a, **k))
+    with torch.no_grad():
+        one = H.as_tuple(H.call_model(model, "bst", d))
+        assert calls, "the one-launch path was not taken"
+        monkeypatch.setattr(rankops.common, "FUSED_BST_FWD", False)
+        three = H.as_tuple(H.call_model(model, "bst", d))
+    for a, b in zip(one, three):
+        torch.testing.assert_close(a, b, atol=0, rtol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_small_bst_one_launch_oob_category_index_is_flagged():
+    cfg = {"T": 16, "heads": 4}
+    model = H.build("bst", cfg).cuda().eval()
+    inp = H.to_device(H.make_inputs("bst", cfg, 64, seed=9), "cuda")
+    inp["category"]["userid"][3] = model.embeddings["userid"].num_embeddings + 7
+    rankops.error_flags(reset=True)
+    with torch.no_grad():
+        H.call_model(model, "bst", inp)
+    assert rankops.error_flags(reset=True) & 1
