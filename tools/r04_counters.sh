@@ -26,6 +26,6 @@ if [ -z "$NO_PMC" ]; then
   pmc deepfm_gather65536 --workload deepfm_gather --iters 3 --batch 65536 || { echo "pmc gather 65536 failed"; exit 1; }
 fi
 python3 tools/pmc_counters.py $O din:din_forward_kernel dcn:dcn_fused_kernel deepfm:deepfm_fused_kernel \
-  bst:bst_block_kernel bst:mlp_stream_kernel bst_ref:bst_small_kernel bst_ref:mlp_stream_kernel \
+  bst:bst_block_kernel bst:mlp_stream_kernel bst_ref:bst_small_fwd_kernel \
   deepfm_gather:fm_gather_kernel deepfm_gather65536:fm_gather_kernel > $O/digest.log 2>&1 || { echo "digest failed"; tail $O/digest.log; exit 1; }
 cat $O/digest.log | cut -c1-300
