@@ -74,6 +74,24 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return v;
 }
 
+// Sum / max over the 16 lanes of each DPP row, all on DPP (no LDS round trip).  The pairing is the
+// xor butterfly's (1, 2, then the other quad, then the other half), so the result has exactly the
+// bits of `for x in 1,2,4,8: v += __shfl_xor(v, x)`.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<0xB1>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0x141>(v));
+  v = fmaxf(v, dpp_f32<0x140>(v));
+  return v;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

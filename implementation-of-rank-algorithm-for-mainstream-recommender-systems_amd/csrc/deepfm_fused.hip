@@ -17,6 +17,13 @@
 // fetches its float4s of the row through a cross-lane read of the owning field's address, and lane
 // f the first-order weight (after the ring); (3) the LDS store before the barrier that opens
 // layer 0.
+//
+// Large batches (>= 32 rows per CU): RT = 2 row tiles, 32 rows per workgroup (wave w stages samples
+// m0 + w and m0 + 16 + w), so each CU streams the weight image once per 32 rows; layer 0 writes its
+// output over the input row in place (mlp_stream.h IP0).  Per-row arithmetic and order unchanged:
+// bit-identical to RT = 1 (tests/test_gpu_deepfm_fused.py).
+#include <cstdlib>
+
 #include "mlp_core.h"
 #include "mlp_stream.h"
 
@@ -44,7 +51,7 @@ struct DfArgs {
   uint32_t* flags;
 };
 
-template <class P>
+template <class P, int RT>
 __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -52,94 +59,115 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
   const unsigned long long k_t0 = clock64();
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
 #endif
-  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.M - m0);
+  constexpr int kRows = kMlpRows * RT;
+  const int64_t m0 = (int64_t)blockIdx.x * kRows;
+  const int rows = (int)min<int64_t>(kRows, a.M - m0);
   float* const buf0 = sm;
   float* const buf1 = sm + a.off1;
-  float* const fm_lds = sm + a.off_fm;  // [fm1 x 16][fm2 x 16]
-  const bool live = wave < rows;
-  const int64_t b = live ? m0 + wave : m0;
+  float* const fm_lds = sm + a.off_fm;  // [fm1 x 16 RT][fm2 x 16 RT]
   const int dim = 1 << a.dim_shift, G = dim >> 2;  // float4 quads per field
   const int nq = a.F * G;                            // float4s of the row
   constexpr int kQ = (P::KC0 * 4 + 63) / 64;         // float4s per lane (the padded row)
   const int f_me = lane < a.F ? lane : 0;
 
-  int64_t idx_v = 0;
-  f32x4_t v[kQ];
-  float fw = 0.f;
-  unsigned long long okmask = 0;
+  // per row tile t: the wave's sample m0 + 16 t + wave
+  bool live[RT];
+  int64_t b[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    live[t] = wave + kMlpRows * t < rows;
+    b[t] = live[t] ? m0 + kMlpRows * t + wave : m0;
+  }
+  int64_t idx_v[RT];
+  f32x4_t v[RT][kQ];
+  float fw[RT];
+  unsigned long long okmask[RT];
   // round 1: lane f's index in field f
-  auto st_index = [&]() { idx_v = a.idx[f_me][b * a.istride[f_me]]; };
+  auto st_index = [&]() {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) idx_v[t] = a.idx[f_me][b[t] * a.istride[f_me]];
+  };
   // round 2: the row address in lane f, the row's float4s (quad q of the row = quad q % G of field
   // q / G) and the first-order weight; loads unconditional from valid addresses, masks applied at
   // the store
   auto st_issue = [&]() {
-    const int64_t r = (a.dense_mask >> f_me) & 1u ? b : idx_v;
-    const bool ok = r >= 0 && r < a.rows[f_me];
-    const bool bad = lane < a.F && !ok;
-    if (live && __builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) flag_oob(a.flags);
-    okmask = __builtin_amdgcn_ballot_w64(ok && live && lane < a.F);
-    const float* p = a.src[f_me] + (ok ? r : 0) * a.ld[f_me];
-    const uint64_t pu = reinterpret_cast<uint64_t>(p);
-    const uint32_t plo = (uint32_t)pu, phi = (uint32_t)(pu >> 32);
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) {
-      const int q = lane + 64 * i;
-      const int f = min(q >> (a.dim_shift - 2), a.F - 1);
-      const uint32_t lo = __shfl(plo, f, kWave), hi = __shfl(phi, f, kWave);
-      const float* row = reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
-      v[i] = *reinterpret_cast<const f32x4_t*>(row + 4 * (q & (G - 1)));
+    for (int t = 0; t < RT; ++t) {
+      const int64_t r = (a.dense_mask >> f_me) & 1u ? b[t] : idx_v[t];
+      const bool ok = r >= 0 && r < a.rows[f_me];
+      const bool bad = lane < a.F && !ok;
+      if (live[t] && __builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) flag_oob(a.flags);
+      okmask[t] = __builtin_amdgcn_ballot_w64(ok && live[t] && lane < a.F);
+      const float* p = a.src[f_me] + (ok ? r : 0) * a.ld[f_me];
+      const uint64_t pu = reinterpret_cast<uint64_t>(p);
+      const uint32_t plo = (uint32_t)pu, phi = (uint32_t)(pu >> 32);
+#pragma unroll
+      for (int i = 0; i < kQ; ++i) {
+        const int q = lane + 64 * i;
+        const int f = min(q >> (a.dim_shift - 2), a.F - 1);
+        const uint32_t lo = __shfl(plo, f, kWave), hi = __shfl(phi, f, kWave);
+        const float* row = reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+        v[t][i] = *reinterpret_cast<const f32x4_t*>(row + 4 * (q & (G - 1)));
+      }
+      fw[t] = p[dim];
     }
-    fw = p[dim];
   };
   // round 3: the row into buf0 (zeros for padding quads, out-of-range rows and rows past the batch)
   auto st_store = [&]() {
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) {
-      const int q = lane + 64 * i;
-      if (q < P::KC0 * 4) {
-        const int f = q >> (a.dim_shift - 2);
-        const bool keep = q < nq && ((okmask >> f) & 1ull);
-        *reinterpret_cast<f32x4_t*>(buf0 + wave * a.ld0 + 4 * q) = keep ? v[i] : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < RT; ++t) {
+#pragma unroll
+      for (int i = 0; i < kQ; ++i) {
+        const int q = lane + 64 * i;
+        if (q < P::KC0 * 4) {
+          const int f = q >> (a.dim_shift - 2);
+          const bool keep = q < nq && ((okmask[t] >> f) & 1ull);
+          *reinterpret_cast<f32x4_t*>(buf0 + (kMlpRows * t + wave) * a.ld0 + 4 * q) =
+              keep ? v[t][i] : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        }
       }
     }
   };
-  // beside layer 0's MFMAs (buf0 is read-only until layer 1's epilogue): fm1 = sum_f w1_f, fm2 =
+  // beside layer 0's MFMAs (buf0 is read-only until layer 0's epilogue): fm1 = sum_f w1_f, fm2 =
   // 0.5 sum_d ((sum_f e_fd)^2 - sum_f e_fd^2) over the staged row, as rk_fm_linear_packed
   auto st_fm = [&]() {
-    f32x4_t s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) {
-      const int q = lane + 64 * i;
-      if (q < nq) {
-        const f32x4_t x = *reinterpret_cast<const f32x4_t*>(buf0 + wave * a.ld0 + 4 * q);
-        s += x;
-        sq += x * x;
-      }
-    }
-    float o = ((okmask >> lane) & 1ull) ? fw : 0.f;  // lanes < F
-    // lanes of equal lane % G hold the same dims: sum over lane / G
-    for (int x = G; x < 64; x <<= 1) {
+    for (int t = 0; t < RT; ++t) {
+      const int row = kMlpRows * t + wave;
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[e] += __shfl_xor(s[e], x, kWave);
-        sq[e] += __shfl_xor(sq[e], x, kWave);
+      for (int i = 0; i < kQ; ++i) {
+        const int q = lane + 64 * i;
+        if (q < nq) {
+          const f32x4_t x = *reinterpret_cast<const f32x4_t*>(buf0 + row * a.ld0 + 4 * q);
+          s += x;
+          sq += x * x;
+        }
       }
-    }
-    float part = (s[0] * s[0] - sq[0]) + (s[1] * s[1] - sq[1]) + (s[2] * s[2] - sq[2]) + (s[3] * s[3] - sq[3]);
-    for (int x = G / 2; x > 0; x >>= 1) part += __shfl_xor(part, x, kWave);
-    o = wave_sum(o);
-    if (lane == 0) {
-      const float f2 = 0.5f * part;
-      fm_lds[wave] = o;
-      fm_lds[kMlpRows + wave] = f2;
-      if (live) {
-        a.fm1[b] = o;
-        a.fm2[b] = f2;
+      float o = ((okmask[t] >> lane) & 1ull) ? fw[t] : 0.f;  // lanes < F
+      // lanes of equal lane % G hold the same dims: sum over lane / G
+      for (int x = G; x < 64; x <<= 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[e] += __shfl_xor(s[e], x, kWave);
+          sq[e] += __shfl_xor(sq[e], x, kWave);
+        }
+      }
+      float part = (s[0] * s[0] - sq[0]) + (s[1] * s[1] - sq[1]) + (s[2] * s[2] - sq[2]) + (s[3] * s[3] - sq[3]);
+      for (int x = G / 2; x > 0; x >>= 1) part += __shfl_xor(part, x, kWave);
+      o = wave_sum(o);
+      if (lane == 0) {
+        const float f2 = 0.5f * part;
+        fm_lds[row] = o;
+        fm_lds[kRows + row] = f2;
+        if (live[t]) {
+          a.fm1[b[t]] = o;
+          a.fm2[b[t]] = f2;
+        }
       }
     }
   };
-  mlp_stream_rows<P, RK_STREAM_EPI>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid,
+  mlp_stream_rows<P, RK_STREAM_EPI, RT, (RT > 1)>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid,
                                     side_at<0>(staged(st_index, st_issue, st_store, st_fm)), nullptr, nullptr,
                                     fm_lds);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);
@@ -212,19 +240,39 @@ RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32
   a.F = num_fields;
   a.dim_shift = __builtin_ctz((unsigned)dim);
   a.M = batch;
-  a.ld0 = need0 + kMlpLdPad;
-  a.ld1 = need1 + kMlpLdPad;
-  a.off1 = kMlpRows * a.ld0;
-  a.off_fm = a.off1 + kMlpRows * a.ld1;
   a.fm1 = fm1;
   a.fm2 = fm2;
   a.flags = flags;
-  const size_t shm = (size_t)(a.off_fm + 2 * kMlpRows) * sizeof(float);
-  if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
-  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  // 32-row workgroups once the batch gives every CU at least one (RANKOPS_DEEPFM_ROW_TILES = 1 / 2
+  // forces either); layer 0 in place then: buf0 holds the input and layers 0 and 2, buf1 layer 1
+  int rt = (batch + 2 * kMlpRows - 1) / (2 * kMlpRows) >= num_cus() ? 2 : 1;
+  if (const char* e = getenv("RANKOPS_DEEPFM_ROW_TILES")) rt = atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : rt;
+  const int rows_wg = kMlpRows * rt;
+  int odd = kMlpPad;  // widths of the odd layers (buf1 under IP0)
+  for (int l = 1; l < nlayers; l += 2) odd = std::max(odd, pad64(layers[l].n));
+  a.ld0 = (rt == 2 ? std::max(need0, need1) : need0) + kMlpLdPad;
+  a.ld1 = (rt == 2 ? odd : need1) + kMlpLdPad;
+  a.off1 = rows_wg * a.ld0;
+  a.off_fm = a.off1 + rows_wg * a.ld1;
+  size_t shm = (size_t)(a.off_fm + 2 * rows_wg) * sizeof(float);
+  if (rt == 2 && shm > 160 * 1024 - kStreamStaticLds) {  // (the compiled plan fits; other widths fall back)
+    rt = 1;
+    a.ld0 = need0 + kMlpLdPad;
+    a.ld1 = need1 + kMlpLdPad;
+    a.off1 = kMlpRows * a.ld0;
+    a.off_fm = a.off1 + kMlpRows * a.ld1;
+    shm = (size_t)(a.off_fm + 2 * kMlpRows) * sizeof(float);
+  }
+  if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
+  const int64_t blocks = (batch + kMlpRows * rt - 1) / (kMlpRows * rt);
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: batch too large");
-  raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960>, 160 * 1024);
-  deepfm_fused_kernel<StreamPlanK960><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  if (rt == 2) {
+    raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960, 2>, 160 * 1024);
+    deepfm_fused_kernel<StreamPlanK960, 2><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  } else {
+    raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960, 1>, 160 * 1024);
+    deepfm_fused_kernel<StreamPlanK960, 1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
+  }
   return check_launch("rk_deepfm_forward");
 }

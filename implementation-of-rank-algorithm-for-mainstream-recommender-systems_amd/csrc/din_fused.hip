@@ -579,15 +579,11 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       const bool valid = in_seq && (int64_t)t < len;
       if (a.use_softmax) {
         const float sv = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
-        float mt = sv;
-#pragma unroll
-        for (int x = 1; x < 16; x <<= 1) mt = fmaxf(mt, __shfl_xor(mt, x, kWave));
+        const float mt = row16_max(sv);
         const float m_new = fmaxf(m_run, mt);
         const float scale_old = expf(m_run - m_new);
         const float p = in_seq ? expf(sv - m_new) : 0.f;
-        float ps = p;
-#pragma unroll
-        for (int x = 1; x < 16; x <<= 1) ps += __shfl_xor(ps, x, kWave);
+        const float ps = row16_sum(p);
         l_run = l_run * scale_old + ps;
         m_run = m_new;
 #pragma unroll
@@ -607,9 +603,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     float mine = 0.f;
 #pragma unroll
     for (int e = 0; e < HG; ++e) {
-      float v = o[e];
-#pragma unroll
-      for (int x = 1; x < 16; x <<= 1) v += __shfl_xor(v, x, kWave);
+      const float v = row16_sum(o[e]);
       mine = p16 == e ? v : mine;
     }
     if (p16 < HG) row[a.att_col + HG * g + p16] = a.use_softmax ? mine * inv_l : mine;

@@ -22,6 +22,13 @@
 // Accumulation order, epilogue arithmetic (col_apply) and the head are those of mlp_rows, so the
 // outputs are bit-identical to it (tests/test_gpu_mlp_stream.py).
 //
+// RT = 2 (large batches: DeepFM at 65,536 rows): 32 rows per workgroup, every weight float4 feeds
+// two MFMAs (one per 16-row tile, as mlp_rows' RT), so a CU streams the weight image once per 32
+// rows instead of 16; the accumulation order of a row is unchanged (bit-identical to RT = 1).
+// IP0: layer 0 writes its output over its own input in buf0 after a workgroup barrier (32 rows of
+// a 960-wide input and of the 512-wide layer 0 output do not fit in LDS side by side); the later
+// layers ping-pong buf0 -> buf1 -> buf0.
+//
 // Eval only (no activation stores), no residual layers: everything else stays on mlp_rows.
 #pragma once
 
@@ -227,7 +234,7 @@ constexpr int side_last_pos(int KC, int c) {
 // One wave class W (P::rep(W) == W) of the streamed tail.  `epi` is the LDS parameter image
 // (stored before the barrier that opens layer 0); `stage` as in mlp_rows (issue() before the ring,
 // operator() after it, before that barrier).  EPI: StreamEpiMode.
-template <class P, int W, int EPI, class Stage>
+template <class P, int W, int EPI, int RT, bool IP0, class Stage>
 __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                  float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                  const rk_epilogue& h, int tid, int wave, Stage& stage,
@@ -322,8 +329,10 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   // already), accumulated in order into the accumulators layer 0 continues from — bit-identical
   constexpr int KS = stage_pre_chunks<Stage>::value;
   constexpr int T0 = P::tpw(0, W);
-  static_assert(KS == 0 || (KS < kMlpSyncChunks && KS < P::kc(0) && kSideL != 0 && !(RK_STREAM_SPLITACC && T0 == 1)),
+  static_assert(KS == 0 || (KS < kMlpSyncChunks && KS < P::kc(0) && kSideL != 0 && !(RK_STREAM_SPLITACC && T0 == 1) &&
+                            RT == 1 && !IP0),
                 "pre-barrier chunks: no lockstep barrier or side work among them");
+  static_assert(RT == 1 || RT == 2, "one or two 16-row tiles");
   f32x4_t acc0[T0 > 0 ? T0 : 1];
   if constexpr (KS > 0 && T0 > 0) {
 #pragma unroll
@@ -366,9 +375,12 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
     // lockstep barriers, except in a layer the stage chose for side work that leaves waves without
     // a tile: those waves do the side work instead, and a barrier would make the others wait for it
     constexpr bool kSync = !(stage_side_layer<Stage>::value == l && P::nt(l) < kMlpWaves);
-    const float* in = (l & 1) ? buf1 : buf0;
-    float* out = (l & 1) ? buf0 : buf1;
-    const int ldin = (l & 1) ? ld1 : ld0, ldout = (l & 1) ? ld0 : ld1;
+    // IP0: layer 0 in place in buf0, then the ping-pong one step behind
+    constexpr bool kIn1 = IP0 ? (l > 0 && !(l & 1)) : (l & 1);
+    constexpr bool kOut1 = IP0 ? (l & 1) : !(l & 1);
+    const float* in = kIn1 ? buf1 : buf0;
+    float* out = kOut1 ? buf1 : buf0;
+    const int ldin = kIn1 ? ld1 : ld0, ldout = kOut1 ? ld1 : ld0;
     if constexpr (T == 0) {
       if constexpr (l == kSideL) stage.side();  // (no tile here: the side work all the same)
 #if RK_MLP_SYNC
@@ -376,17 +388,21 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
       if constexpr (kSync)
         static_for<0, (KC - 1) / kMlpSyncChunks>([&](auto) { mlp_sync_barrier(); });
 #endif
+      if constexpr (IP0 && l == 0) mlp_lds_barrier();
     } else {
       constexpr int CB = l == 0 ? KS : 0;  // first chunk of this section (layer 0: after the pre-chunks)
-      f32x4_t acc[T];
+      f32x4_t acc[T][RT];
 #pragma unroll
       for (int j = 0; j < T; ++j) {
-        if constexpr (CB > 0)
-          acc[j] = acc0[j];
-        else
-          acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          if constexpr (CB > 0)
+            acc[j][t] = acc0[j];
+          else
+            acc[j][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        }
       }
-      constexpr bool kSplit = RK_STREAM_SPLITACC && T == 1;
+      constexpr bool kSplit = RK_STREAM_SPLITACC && T == 1 && RT == 1;
       f32x4_t acc_odd = {0.f, 0.f, 0.f, 0.f};
       const float* arow = in + li * ldin + kq;
       // layer l > 0, flag hand-off: K-chunk c is layer l-1's output tile c; `ready` caches the bits
@@ -406,24 +422,30 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
 #endif
       };
       // A float4s one chunk ahead in two register sets (see mlp_layer)
-      f32x4_t ab[2];
+      f32x4_t ab[2][RT];
       wait_chunk(CB);
-      ab[CB & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * CB);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) ab[CB & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin + 16 * CB);
       static_for<CB, KC>([&](auto CI) {
         constexpr int c = CI;
         if constexpr (c + 1 < KC) {
           wait_chunk(c + 1);
-          ab[(c + 1) & 1] = *reinterpret_cast<const f32x4_t*>(arow + 16 * (c + 1));
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+            ab[(c + 1) & 1][t] = *reinterpret_cast<const f32x4_t*>(arow + 16 * t * ldin + 16 * (c + 1));
         }
         __builtin_amdgcn_sched_barrier(0);  // the read goes out before this chunk's MFMAs
         static_for<0, 4>([&](auto EI) {
           constexpr int e = EI;
           static_for<0, T>([&](auto JI) {
             constexpr int j = JI;
-            if constexpr (kSplit && (e & 1))
-              acc_odd = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc_odd);
-            else
-              acc[j] = mfma16(ab[c & 1][e], ring[(B0 + c * T + j) % R][e], acc[j]);
+            static_for<0, RT>([&](auto TI) {
+              constexpr int t = TI;
+              if constexpr (kSplit && (e & 1))
+                acc_odd = mfma16(ab[c & 1][t][e], ring[(B0 + c * T + j) % R][e], acc_odd);
+              else
+                acc[j][t] = mfma16(ab[c & 1][t][e], ring[(B0 + c * T + j) % R][e], acc[j][t]);
+            });
           });
         });
         // refill the slots just read with the stream's next loads (past this layer: the next
@@ -450,7 +472,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
         if constexpr (kSync && (c + 1) % kMlpSyncChunks == 0 && c + 1 < KC) mlp_sync_barrier();
 #endif
       });
-      if constexpr (kSplit) acc[0] += acc_odd;
+      if constexpr (kSplit) acc[0][0] += acc_odd;
+      if constexpr (IP0 && l == 0) mlp_lds_barrier();  // every wave's layer-0 reads of buf0 are done
       MLP_MARK(4 * l, t0);
 #ifdef RK_MLP_PHASES
       if (lane == 0 && l < 4) s_mlp_wave_marks[l][wave][0] = (unsigned)(clock64() - t0);
@@ -480,10 +503,13 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
             e.post_b = p1[3];
           }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = (lane >> 4) * 4 + r;
-            const float z = apply_epi<decltype(DICE)::value>(e, acc[j][r]);
-            out[row * ldout + n] = real ? z : 0.f;  // padded columns: the next layer's zero K pad
+          for (int t = 0; t < RT; ++t) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * t + (lane >> 4) * 4 + r;
+              const float z = apply_epi<decltype(DICE)::value>(e, acc[j][t][r]);
+              out[row * ldout + n] = real ? z : 0.f;  // padded columns: the next layer's zero K pad
+            }
           }
         }
       };
@@ -519,8 +545,9 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   });
 
   // head: one wave per row, as mlp_rows
-  const float* fin = (NL & 1) ? buf1 : buf0;
-  const int ldf = (NL & 1) ? ld1 : ld0;
+  constexpr bool kFin1 = IP0 ? ((NL - 1) & 1) : (NL & 1);
+  const float* fin = kFin1 ? buf1 : buf0;
+  const int ldf = kFin1 ? ld1 : ld0;
   const int K = Kh;
   if (h.head_w) {
     for (int r = wave; r < rows; r += kMlpWaves) {
@@ -543,7 +570,7 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           logit = (pre ? hp : h.head_partial[m]) + logit;
         if (h.fm1) {
           if (h.head_aux) h.head_aux[m] = logit;
-          const float f1 = lds_fm ? lds_fm[r] : h.fm1[m], f2 = lds_fm ? lds_fm[kMlpRows + r] : h.fm2[m];
+          const float f1 = lds_fm ? lds_fm[r] : h.fm1[m], f2 = lds_fm ? lds_fm[kMlpRows * RT + r] : h.fm2[m];
           logit = f1 * h.final_w[0] + f2 * h.final_w[1] + logit * h.final_w[2] + h.final_b[0];
         }
         if (h.head_logit) h.head_logit[m] = logit;
@@ -554,8 +581,9 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
 }
 
 // Entry point: dispatches the calling wave to its class's unrolled body.  Must be called by all
-// kMlpThreads threads.  `epi`: P::epi_floats() floats of LDS (16-B aligned).
-template <class P, int EPI = kEpiRegs, class Stage = NoStage>
+// kMlpThreads threads.  `epi`: P::epi_floats() floats of LDS (16-B aligned).  RT row tiles of 16
+// (rows <= 16 RT; lds_fm: [fm1 x 16 RT][fm2 x 16 RT]); IP0: layer 0 in place (see the top).
+template <class P, int EPI = kEpiRegs, int RT = 1, bool IP0 = false, class Stage = NoStage>
 __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__ layers, float* buf0, int ld0,
                                                 float* buf1, int ld1, float* epi, int64_t m0, int rows,
                                                 const rk_epilogue& h, int tid, Stage stage = Stage(),
@@ -569,7 +597,7 @@ __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__
 #pragma unroll
       for (int l = 0; l < P::NL; ++l) mine = mine && P::tpw(l, wave) == P::tpw(l, w);
       if (mine)
-        mlp_stream_class<P, w, EPI>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
+        mlp_stream_class<P, w, EPI, RT, IP0>(layers, buf0, ld0, buf1, ld1, epi, m0, rows, h, tid, wave, stage,
                                          lds_partial, row_ids, lds_fm);
     }
   });

@@ -3,7 +3,8 @@ packed-table gather, FM sums, the three deep layers on one weight stream and the
 tile; deepfm.py:121-151) — through rankops.DeepFM at configs[1]'s shape (30 fields x 32, hidden
 [512, 256, 128]) against the CPU oracle and against the two-launch path (rk_fm_linear_packed +
 rk_mlp_forward), and directly: out-of-range indices, dense blocks of packed rows (the ShardedDeepFM
-receive layout), hipGraph replay, and the shapes without a compiled plan.
+receive layout), hipGraph replay, the shapes without a compiled plan, and the 32-row workgroups of
+large batches (RT = 2, layer 0 in place) bit-identical to the 16-row ones.
 Tolerance as every forward test: atol = rtol = 1e-4 (fp32)."""
 import pytest
 import torch
@@ -198,3 +199,36 @@ def test_deepfm_prepare_equals_forward():
         ref = model(e["category"])
     for x, y in zip(b, ref):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,oob,dense", [(1, False, False), (33, True, False), (1000, False, True),
+                                         (8200, True, False), (16384, False, False)])
+def test_deepfm_forward_32_row_tiles_bit_identical(M, oob, dense, monkeypatch):
+    """RANKOPS_DEEPFM_ROW_TILES=2 (32 rows per workgroup: each weight float4 feeds both 16-row tiles,
+    layer 0 written over its input in LDS) against =1: every output equal bit for bit, ragged last
+    workgroups included (rows past the batch), with out-of-range indices and with dense blocks; and
+    against the float64 restatement.  The default picks 2 once the batch gives every CU a 32-row
+    workgroup (16384 here), 1 below."""
+    tables, idx, mls, ws, head, keep = _direct_case(M, seed=13, oob=oob)
+    if dense:
+        segs, blocks = [], [t[i].contiguous() for t, i in zip(tables, idx)]  # (kept alive: segments hold raw pointers)
+        for f, (blk, i) in enumerate(zip(blocks, idx)):
+            s = ops.packed_segment(blk, i, 32, f * 32)
+            s.idx, s.idx_stride = None, 0
+            segs.append(s)
+    else:
+        segs = [ops.packed_segment(t, i, 32, f * 32) for f, (t, i) in enumerate(zip(tables, idx))]
+    got = {}
+    for rt in ("1", "2", None):
+        if rt is None:
+            monkeypatch.delenv("RANKOPS_DEEPFM_ROW_TILES", raising=False)
+        else:
+            monkeypatch.setenv("RANKOPS_DEEPFM_ROW_TILES", rt)
+        rankops.error_flags(reset=True)
+        got[rt] = _run_direct(segs, M, mls, head)
+        assert bool(rankops.error_flags(reset=True) & 1) == oob
+    for a, b, c in zip(got["1"], got["2"], got[None]):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    for i, (o, r) in enumerate(zip(got["2"], _reference(tables, idx, ws, head))):
+        torch.testing.assert_close(o, r.float(), atol=ATOL, rtol=RTOL, msg=lambda m: f"output {i}: {m}")
