@@ -30,6 +30,10 @@ namespace rk {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
+#ifndef RK_DIN_HOIST  // experiment (phase A's layer-1 operand per sample): see the tile loop
+#define RK_DIN_HOIST 0
+#endif
+
 constexpr int kDinSegs = 32;
 constexpr int kDinSegLdsOff = 528;  // bytes past the column map: 256 + 256 map bytes, l2_last int, pad to 16
 struct DinSegs {
@@ -521,9 +525,22 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     float o[HG];
 #pragma unroll
     for (int e = 0; e < HG; ++e) o[e] = 0.f;
+    // RK_DIN_HOIST (experiment, off): layer 1's A operand Weff built once per sample in 32 VGPRs
+    // instead of per tile from LDS (118 VGPRs, no spill; half the tile's LDS reads and 32 fewer FMAs
+    // per tile) measured flat (42.0 / 42.7 us against 41.8 / 42.7 us per launch,
+    // profiles/r04/ab_hoist*.json): phase A is not bound by the operand's LDS reads
+#if RK_DIN_HOIST
+    float weff[4][HG];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      const float* wk = sm + Ly::WK + (16 * jt + p16) * Ly::LDH + HG * g;
+      const float* wqk = sm + Ly::WQK + (16 * jt + p16) * Ly::LDH + HG * g;
+#pragma unroll
+      for (int e = 0; e < HG; ++e) weff[jt][e] = fmaf(wqk[e], qv[e], wk[e]);
+    }
+#endif
     for (int tt = 0; tt < ntiles; ++tt) {
-      // the weight LDS reads below are loop-invariant; hoisted out of the tile loop (32 more VGPRs
-      // for the layer-1 A operand alone) they spill at the 128-register budget
+      // the weight LDS reads below are loop-invariant (kept in the loop: see RK_DIN_HOIST above)
       asm volatile("" ::: "memory");
       const int t = 16 * tt + p16;
       const bool in_seq = t < a.T;
@@ -535,6 +552,13 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) acc1[jt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       // layer 1's A operand, Weff[16 jt + p16][HG g + e] = Wk + Wqk q (rows of the LDS image)
+#if RK_DIN_HOIST
+#pragma unroll
+      for (int e = 0; e < HG; ++e) {
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) acc1[jt] = mfma16(weff[jt][e], kk[e], acc1[jt]);
+      }
+#else
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) {
         const float* wk = sm + Ly::WK + (16 * jt + p16) * Ly::LDH + HG * g;
@@ -542,6 +566,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
 #pragma unroll
         for (int e = 0; e < HG; ++e) acc1[jt] = mfma16(fmaf(wqk[e], qv[e], wk[e]), kk[e], acc1[jt]);
       }
+#endif
       // ReLU(layer 1 + u) in place, then layer 2 with the accumulators as its B operands
       f32x4_t acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
