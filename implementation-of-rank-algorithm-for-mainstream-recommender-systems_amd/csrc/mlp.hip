@@ -69,26 +69,28 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
 }
 
 // The same tail on a compiled layer plan (mlp_stream.h): one weight stream across the layers.
-template <class P>
+// RT = 2 (large batches): 32 rows per workgroup, each weight float4 feeding both 16-row tiles.
+template <class P, int RT>
 __global__ __launch_bounds__(kMlpThreads) void mlp_stream_kernel(MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int kRows = kMlpRows * RT;
   const int tid = threadIdx.x;
-  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.M - m0);
+  const int64_t m0 = (int64_t)blockIdx.x * kRows;
+  const int rows = (int)min<int64_t>(kRows, a.M - m0);
   float* const buf0 = sm;
   float* const buf1 = sm + a.off1;
   const int K0p = P::KC0 * 16;
   auto stage = [&]() {
     if (a.x_vec) {
       const int q = K0p / 4;
-      for (int i = tid; i < kMlpRows * q; i += kMlpThreads) {
+      for (int i = tid; i < kRows * q; i += kMlpThreads) {
         const int r = i / q, c = (i % q) * 4;
         f32x4_t v = {0.f, 0.f, 0.f, 0.f};
         if (r < rows && c < a.K0) v = *reinterpret_cast<const f32x4_t*>(a.x + (m0 + r) * a.ldx + c);
         *reinterpret_cast<f32x4_t*>(buf0 + r * a.ld0 + c) = v;
       }
     } else {
-      for (int i = tid; i < kMlpRows * K0p; i += kMlpThreads) {
+      for (int i = tid; i < kRows * K0p; i += kMlpThreads) {
         const int r = i / K0p, c = i % K0p;
         buf0[r * a.ld0 + c] = (r < rows && c < a.K0) ? a.x[(m0 + r) * a.ldx + c] : 0.f;
       }
@@ -98,7 +100,8 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_stream_kernel(MlpArgs a) {
   const unsigned long long k_t0 = clock64();
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
 #endif
-  mlp_stream_rows<P, RK_STREAM_EPI>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.off_epi, m0, rows, a.head, tid, finish_only(stage));
+  mlp_stream_rows<P, RK_STREAM_EPI, RT>(a.L, buf0, a.ld0, buf1, a.ld1, sm + a.off_epi, m0, rows, a.head, tid,
+                                        finish_only(stage));
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
   MLP_FLUSH(tid);
@@ -497,10 +500,15 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   a.ld1 = need1 + kMlpLdPad;
   // rows per workgroup: 16.  32 (two row tiles per wave: half the L2 weight traffic per row)
   // measured slower at batch 4096 — DCN 46.6 vs 52.6 us: half the workgroups, same per-workgroup
-  // latency — and is kept as an option (RANKOPS_MLP_ROWS=32) where the buffers fit in LDS.
+  // latency — so a compiled plan (the streamed tail) takes 32 only once the batch gives every CU a
+  // 32-row workgroup, and mlp_kernel only on request.  RANKOPS_MLP_ROWS=16 / 32 forces either where
+  // the buffers fit in LDS.
   const size_t row_bytes = (size_t)(a.ld0 + a.ld1) * sizeof(float);
-  int rt = 1;
-  if (const char* e = getenv("RANKOPS_MLP_ROWS")) rt = (atoi(e) == 32 && 32 * row_bytes <= 160 * 1024) ? 2 : 1;
+  const int plan0 = stream_plan_for(layers, nlayers, K0);
+  const size_t epi_bytes = plan0 != kStreamNone ? sizeof(float) * stream_plan_epi_floats(plan0) : 0;
+  const bool fits32 = 2 * kMlpRows * row_bytes + epi_bytes <= 160 * 1024 - kStreamStaticLds;
+  int rt = plan0 != kStreamNone && fits32 && (M + 2 * kMlpRows - 1) / (2 * kMlpRows) >= num_cus() ? 2 : 1;
+  if (const char* e = getenv("RANKOPS_MLP_ROWS")) rt = (atoi(e) == 32 && fits32) ? 2 : atoi(e) == 16 ? 1 : rt;
   const int rows_per_wg = kMlpRows * rt;
   a.off1 = rows_per_wg * a.ld0;
   const size_t shm = rows_per_wg * row_bytes;
@@ -522,18 +530,25 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
     kern<<<(unsigned)blocks, kMlpThreads, bytes, (hipStream_t)stream>>>(a);
   };
   // a compiled layer plan: the streamed tail (mlp_stream.h), its epilogue image after the buffers
-  const int plan = rt == 1 ? stream_plan_for(layers, nlayers, K0) : kStreamNone;
+  const int plan = plan0;
   if (plan != kStreamNone) {
     a.off_epi = (int)(shm / sizeof(float));
     const size_t bytes = shm + sizeof(float) * stream_plan_epi_floats(plan);
     if (bytes <= 160 * 1024 - kStreamStaticLds) {
-      switch (plan) {
-        case kStreamK64: go(mlp_stream_kernel<StreamPlanK64>, bytes); break;
-        case kStreamK128: go(mlp_stream_kernel<StreamPlanK128>, bytes); break;
-        case kStreamK192: go(mlp_stream_kernel<StreamPlanK192>, bytes); break;
-        case kStreamK256: go(mlp_stream_kernel<StreamPlanK256>, bytes); break;
-        default: go(mlp_stream_kernel<StreamPlanTail512>, bytes); break;
-      }
+      auto launch = [&](auto RTI) {
+        constexpr int R = decltype(RTI)::value;
+        switch (plan) {
+          case kStreamK64: go(mlp_stream_kernel<StreamPlanK64, R>, bytes); break;
+          case kStreamK128: go(mlp_stream_kernel<StreamPlanK128, R>, bytes); break;
+          case kStreamK192: go(mlp_stream_kernel<StreamPlanK192, R>, bytes); break;
+          case kStreamK256: go(mlp_stream_kernel<StreamPlanK256, R>, bytes); break;
+          default: go(mlp_stream_kernel<StreamPlanTail512, R>, bytes); break;
+        }
+      };
+      if (rt == 2)
+        launch(std::integral_constant<int, 2>{});
+      else
+        launch(std::integral_constant<int, 1>{});
       return check_launch("rk_mlp_forward");
     }
   }

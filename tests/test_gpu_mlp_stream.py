@@ -4,7 +4,8 @@ the same — and against a float64 restatement of the layer stack.
 
 Covered: every compiled plan (K0 chunks 4/8/12/16 over [512, 256, 128], and [256, 128] over K0 512),
 every activation (none, ReLU, LeakyReLU, PReLU with one or per-channel alpha, Dice), with and without
-bias and pre-/post-BatchNorm affines, ragged batches (1, 15, 17, 1000), and the model forwards that
+bias and pre-/post-BatchNorm affines, ragged batches (1, 15, 17, 1000), 32-row workgroups
+(RANKOPS_MLP_ROWS, the default at large batches) bit-identical to 16-row ones, and the model forwards that
 run it: DCN (dcn_fused_kernel), DIN (phase B of din_forward_kernel, contiguous and balanced
 assignment, softmax and PReLU variants), DeepFM (tail after the tiled first layer), BST (DNN tail).
 Reference rows: dcn.py:144-152,175-180; din.py:272-285,312-316; deepfm.py:100-112,143-151;
@@ -127,6 +128,32 @@ def test_stream_mlp_equals_generic_and_float64(K0, widths, act, bias, pre, post)
         assert torch.equal(ps, pg)
         ref = _ref64(x.cpu(), [({k: v.cpu() for k, v in d.items()}, a) for d, a in spec], hw.cpu(), hb.cpu())
         torch.testing.assert_close(ls.cpu().double(), ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K0,widths", PLANS)
+def test_stream_mlp_32_row_workgroups_bit_identical(K0, widths, monkeypatch):
+    """RANKOPS_MLP_ROWS=32 (two 16-row tiles per workgroup, each weight float4 feeding both) against
+    =16 on every compiled plan: equal bit for bit at ragged batches; the default takes 32 once the
+    batch gives every CU a 32-row workgroup (8197 here) and equals both."""
+    dev = torch.device("cuda")
+    spec, mls, keep = _layers(K0, widths, "prelu", True, True, True, seed=K0 + 5, dev=dev)
+    g = torch.Generator().manual_seed(9)
+    hw = ((torch.rand(widths[-1], generator=g) - 0.5) * 0.2).to(dev)
+    hb = torch.tensor([0.05], device=dev)
+    for B in (1, 33, 1000, 8197):
+        x = (torch.rand(B, K0, generator=g) * 2 - 1).to(dev)
+        got = []
+        for rows in ("16", "32", None):
+            if rows is None:
+                monkeypatch.delenv("RANKOPS_MLP_ROWS", raising=False)
+            else:
+                monkeypatch.setenv("RANKOPS_MLP_ROWS", rows)
+            got.append(_run_mlp(x, mls, hw, hb, True))
+        for o in got[1:]:
+            assert torch.equal(o[0], got[0][0]) and torch.equal(o[1], got[0][1]), B
+    ref = _ref64(x.cpu(), [({k: v.cpu() for k, v in d.items()}, a) for d, a in spec], hw.cpu(), hb.cpu())
+    torch.testing.assert_close(got[1][0].cpu().double(), ref, atol=ATOL, rtol=RTOL)
 
 
 @pytest.mark.gpu
