@@ -348,20 +348,24 @@ def bench_sharded(world, rank, steps, warmup):
         g0, _ = graph_of(lambda: model.run_steps(cat))
         step = g0.replay
     else:
-        # the exchange pipeline of ShardedDeepFM.run_steps with each chunk's local segments
-        # (index pack, gather, FM + tail) captured as hipGraphs and the RCCL all-to-alls issued
-        # asynchronously between them: chunk c's rows travel while chunk c+1 gathers
-        step = model.capture_pipeline(cat).step
+        # the cross-batch exchange pipeline (ShardedDeepFM.pipeline, captured): per step the index
+        # all-to-all of batch i, the gather + row all-to-all of batch i-1 (side stream, RCCL async)
+        # and the one-launch forward of batch i-2 (compute stream); three local batches bound to
+        # the pipeline's slots.  Warm-up fills the pipeline; every timed step completes one batch.
+        cats = [cat] + [{f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l, dtype=np.int64)).to(dev)
+                         for f in fields} for _ in range(2)]
+        step = model.pipeline(B_l, capture=cats).step
 
-    t = max_over_ranks(world, time_replays(step, steps, warmup, world))
+    t = max_over_ranks(world, time_replays(step, steps, max(warmup, 3), world))
     wire = B_l * SHARDED_FIELDS * (model.index_dtype.itemsize + 4 * row_stride(32)) * (world - 1) / world
     return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
             "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
             "scaling": "strong",
             "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
-                     f"{len(model.chunk_bounds(B_l))}-chunk pipeline: per chunk 3 hipGraph segments + async RCCL "
-                     "all_to_all_single (row exchange of chunk c overlaps the gather of c+1)")}
+                     "cross-batch pipeline (ShardedDeepFM.pipeline): per step pack + index all_to_all_single of "
+                     "batch i, gather + row all_to_all_single of batch i-1 on a side stream, the one-launch "
+                     "forward of batch i-2; local segments as hipGraphs, RCCL async between them")}
 
 
 XGMI_LINK_BPS = 153e9   # MI355X: 7 xGMI links x ~153 GB/s per GPU, point to point (fully connected node)
@@ -371,12 +375,18 @@ A2A_LATENCY_S = 20e-6   # assumed fixed cost per RCCL all_to_all_single call (no
 def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
     """A MODEL, not a measurement, of the 1 -> 8 GPU strong-scaling curve of configs[4] (global
     batch 65536, 1e8 rows), built from what one GPU can time: rank 0's local device work at P
-    ranks — gather_rows over its fields for the P x B_c rows it serves per chunk and fm_and_tail
-    for its B_c samples, both captured as hipGraphs and timed here — plus the wire time of the two
-    all-to-alls from their per-link bytes at XGMI_LINK_BPS (each peer pair has its own link) and an
-    assumed A2A_LATENCY_S per collective.  Two bounds: serial (compute + wire) and the chunked
-    pipeline's overlap (the row exchange of chunk c hidden behind chunk c+1's compute, first
-    chunk's exchange exposed)."""
+    ranks, captured as hipGraphs and timed here, plus the wire time of the two all-to-alls from
+    their per-link bytes at XGMI_LINK_BPS (each peer pair has its own link) and an assumed
+    A2A_LATENCY_S per collective.  Three columns:
+      serial      the chunked run_steps (pack, per chunk: gather + row exchange + forward), all summed;
+      overlapped  the same with chunk c's row exchange hidden behind chunk c+1's gather and chunk
+                  c-1's forward (round 4's design);
+      pipelined   ShardedDeepFM.pipeline (round 5): the index and row exchanges of batches i and
+                  i-1 run under batch i-2's forward, so a step costs max(local device work, wire +
+                  per-call latency); the local device work is pack + ONE gather over all P x B_l
+                  rows + ONE forward launch over B_l, timed back to back as one hipGraph, plus the
+                  measured slowdown of the forward while a side-stream copy of the row exchange's
+                  bytes runs beside it (a stand-in for RCCL's copy kernels taking CUs)."""
     import helpers as H
     from rankops.sharded import ShardedDeepFM, row_stride
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -398,14 +408,36 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         recv_idx = torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, P * B_l * F_me)).to(
             dev, model.index_dtype)
         recv_rows = torch.randn(B_c * SHARDED_FIELDS * RS, device=dev)
+        recv_full = torch.randn(B_l * SHARDED_FIELDS * RS, device=dev)
         cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l)).to(dev) for f in fields}
         with torch.no_grad():
             g_pack, _ = graph_of(lambda: model.pack_indices(cat))
             g_gather, _ = graph_of(lambda: model.gather_rows(recv_idx, B_l, 0, B_c))
             g_fm, _ = graph_of(lambda: model.fm_and_tail(recv_rows, B_c))
+            g_gather1, rows1 = graph_of(lambda: model.gather_rows(recv_idx, B_l, 0, B_l))
+            g_fm1, _ = graph_of(lambda: model.fm_and_tail(recv_full, B_l))
+            g_seq, _ = graph_of(lambda: (model.pack_indices(cat), model.gather_rows(recv_idx, B_l, 0, B_l),
+                                         model.fm_and_tail(recv_full, B_l)))
         t_pack = kernel_avg_ms(g_pack.replay, iters)
         t_gather = kernel_avg_ms(g_gather.replay, iters) * C
         t_fm = kernel_avg_ms(g_fm.replay, iters) * C
+        t_gather1 = kernel_avg_ms(g_gather1.replay, iters)
+        t_fm1 = kernel_avg_ms(g_fm1.replay, iters)
+        t_seq = kernel_avg_ms(g_seq.replay, iters)
+        # contention proxy: the forward with a copy of the row exchange's bytes (what this rank's
+        # RCCL kernels move: (P-1)/P of its send rows out, as much in) on a second stream
+        xfer = int(B_l * SHARDED_FIELDS * RS * (P - 1) / P)
+        src, dst = torch.empty(2 * xfer, device=dev), torch.empty(2 * xfer, device=dev)
+        side = torch.cuda.Stream()
+
+        def fwd_with_copy():
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                dst.copy_(src)
+            g_fm1.replay()
+            torch.cuda.current_stream().wait_stream(side)
+        t_fm1_copy = kernel_avg_ms(fwd_with_copy, iters)
+        contention = max(0.0, t_fm1_copy - t_fm1)
         t_comp = t_pack + t_gather + t_fm
         # per link: this rank's bytes to one peer (F / P fields of its B_l samples, each way)
         f_peer = SHARDED_FIELDS / P
@@ -414,26 +446,41 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         t_idx = 1e3 * (idx_link / XGMI_LINK_BPS + A2A_LATENCY_S)  # one index exchange per step
         t_rows = 1e3 * (rows_link / XGMI_LINK_BPS + C * A2A_LATENCY_S)
         serial = t_comp + t_idx + t_rows
-        # pipeline: pack + index exchange, then chunk c's rows travel behind chunk c+1's gather and
+        # chunked pipeline: pack + index exchange, then chunk c's rows travel behind chunk c+1's gather and
         # chunk c-1's FM + tail; the first chunk's gather and the last chunk's exchange stay exposed
         overlap = t_pack + t_idx + max(t_gather + t_fm, t_rows) + (t_gather + t_rows) / C
+        # cross-batch pipeline: one row exchange per step (one call), hidden behind the forward
+        wire1 = 1e3 * ((idx_link + rows_link) / XGMI_LINK_BPS + 2 * A2A_LATENCY_S)
+        local1 = t_seq + contention
+        piped = max(local1, wire1)
         curve[str(P)] = {
             "kind": "model, not a measurement",
             "B_local": B_l, "fields_rank0": F_me, "chunks": C,
             "compute_ms": {"pack": round(t_pack, 4), "gather_local": round(t_gather, 4),
                            "fm_and_tail": round(t_fm, 4)},
-            "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4)},
+            "pipelined_compute_ms": {"pack": round(t_pack, 4), "gather_one_launch": round(t_gather1, 4),
+                                     "forward_one_launch": round(t_fm1, 4),
+                                     "pack_gather_forward_one_graph": round(t_seq, 4),
+                                     "forward_with_copy_beside": round(t_fm1_copy, 4),
+                                     "contention": round(contention, 4), "copy_bytes": 8 * xfer},
+            "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4), "pipelined_per_step": round(wire1, 4)},
             "bytes_per_link": {"index": int(idx_link), "rows": int(rows_link)},
-            "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4)},
+            "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4), "pipelined": round(piped, 4)},
             "samples_per_s": {"serial": round(SHARDED_GLOBAL_BATCH / (serial * 1e-3), 1),
-                              "overlapped": round(SHARDED_GLOBAL_BATCH / (overlap * 1e-3), 1)},
-            "speedup_vs_p1": {"serial": round(p1_ms / serial, 2), "overlapped": round(p1_ms / overlap, 2)},
+                              "overlapped": round(SHARDED_GLOBAL_BATCH / (overlap * 1e-3), 1),
+                              "pipelined": round(SHARDED_GLOBAL_BATCH / (piped * 1e-3), 1)},
+            "speedup_vs_p1": {"serial": round(p1_ms / serial, 2), "overlapped": round(p1_ms / overlap, 2),
+                              "pipelined": round(p1_ms / piped, 2)},
+            "pipelined_bound": "device" if local1 >= wire1 else "wire",
         }
-        del model, g_pack, g_gather, g_fm
+        del model, g_pack, g_gather, g_fm, g_gather1, g_fm1, g_seq, rows1, src, dst
         torch.cuda.empty_cache()
-    return {"assumptions": f"up to {chunks} chunks of >= 4096 samples; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
+    return {"assumptions": f"up to {chunks} chunks of >= 4096 samples (serial / overlapped); pipelined: one gather "
+                           f"and one forward launch per step, exchanges of the two younger batches under the "
+                           f"oldest one's forward; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
                            f"peer pair; {A2A_LATENCY_S * 1e6:.0f} us per all_to_all_single call (assumed); "
-                           "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter",
+                           "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter; RCCL's "
+                           "CU use stood in by a same-size local copy on a second stream",
             "curve": curve}
 
 

@@ -9,8 +9,8 @@
 //  rk_shard_gather_rows   the row all-to-all's send buffer for one chunk of samples: for every
 //                         source rank s and sample b of [b0, b0 + bc), the packed rows
 //                         (rk_fm_pack_table layout, RS floats) of this rank's F_me fields at the
-//                         int32 indices the source sent, [s][b'][j][RS].  One wave per output row
-//                         (F_me * RS / 4 float4s), indices read once per lane.
+//                         int32 indices the source sent, [s][b'][j][RS], flattened over the
+//                         output's float4s (kShardU loads in flight per lane).
 //
 // Both are HBM-bound byte movers: pack 12 B per (sample, field); gather 4 B of index + 2 x RS * 4 B
 // per (row, field) (read the packed row, write it to the send buffer).
@@ -34,7 +34,10 @@ __global__ __launch_bounds__(256) void shard_pack_indices_kernel(ShardPackArgs a
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t b = i / a.F;
     const int q = (int)(i - b * a.F);
-    a.out[a.base[q] + b * a.stride[q]] = (int32_t)a.idx[q][b];
+    // an index outside [0, 2^31) would wrap to a valid row when narrowed: it goes out as -1,
+    // which the owner's gather reads as a zero row and flags (RK_FLAG_INDEX_OOB)
+    const int64_t v = a.idx[q][b];
+    a.out[a.base[q] + b * a.stride[q]] = (v >= 0 && v <= (int64_t)INT32_MAX) ? (int32_t)v : -1;
   }
 }
 
@@ -50,25 +53,47 @@ struct ShardGatherArgs {
   uint32_t* flags;
 };
 
+// Flattened over the output's float4s: thread i moves float4s i, i + n/U-stride, ... (kShardU of
+// them, all loads issued before any store, so each lane keeps kShardU row reads in flight).  A
+// float4 t of the output is (row r = t / per, field j, quad q); its index sits at
+// idx[(s * B_l + b0 + r % bc) * F + j] with s = r / bc.  Every lane of a wave works (the old one-
+// wave-per-row form left 28 of 64 lanes idle at 4 fields x 9 quads).
+constexpr int kShardU = 4;
+
 __global__ __launch_bounds__(256) void shard_gather_rows_kernel(ShardGatherArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nrows = (int64_t)a.P * a.bc;
   const int per = a.F * a.RS4;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nrows; r += (int64_t)gridDim.x * 4) {
-    const int64_t s = r / a.bc, bp = r - s * a.bc;
-    const int32_t* ip = a.idx + (s * a.B_l + a.b0 + bp) * a.F;
-    f32x4* dst = reinterpret_cast<f32x4*>(a.out + r * a.F * a.RS4 * 4);
-    bool oob = false;
-    for (int t = lane; t < per; t += 64) {
-      const int j = t / a.RS4, q = t - j * a.RS4;
-      const int64_t row = ip[j];
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row >= 0 && row < a.rows[j])
-        v = *reinterpret_cast<const f32x4*>(a.src[j] + row * a.src_ld[j] + 4 * q);
-      else
-        oob = true;
-      dst[t] = v;
+  const int64_t n4 = (int64_t)a.P * a.bc * per;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  f32x4* const out4 = reinterpret_cast<f32x4*>(a.out);
+  for (; t0 < n4; t0 += stride * kShardU) {
+    int64_t row[kShardU];
+    int jj[kShardU], qq[kShardU];
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u) {
+      const int64_t t = t0 + u * stride;
+      const int64_t tt = t < n4 ? t : 0;
+      const int64_t r = tt / per;
+      const int rem = (int)(tt - r * per);
+      const int j = rem / a.RS4;
+      const int64_t s = r / a.bc, bp = r - s * a.bc;
+      jj[u] = j;
+      qq[u] = rem - j * a.RS4;
+      row[u] = a.idx[(s * a.B_l + a.b0 + bp) * a.F + j];
     }
+    f32x4 v[kShardU];
+    bool oob = false;
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u) {
+      const int j = jj[u];
+      const bool ok = row[u] >= 0 && row[u] < a.rows[j];
+      oob |= !ok && t0 + u * stride < n4;
+      v[u] = *reinterpret_cast<const f32x4*>(a.src[j] + (ok ? row[u] : 0) * a.src_ld[j] + 4 * qq[u]);
+      if (!ok) v[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u)
+      if (t0 + u * stride < n4) out4[t0 + u * stride] = v[u];
     if (oob) flag_oob(a.flags);
   }
 }
@@ -130,7 +155,8 @@ RK_API int rk_shard_gather_rows(const rk_segment* tables, int32_t num_fields, in
   if (!a.flags) return fail(RK_ERR_RUNTIME, "rk_shard_gather_rows: device not initialised (rk_init)");
   const int64_t nrows = (int64_t)num_sources * bc;
   if (nrows == 0) return RK_OK;
-  const unsigned blocks = (unsigned)std::min<int64_t>((nrows + 3) / 4, (int64_t)num_cus() * 16);
+  const int64_t n4 = nrows * num_fields * a.RS4;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n4 + 256 * kShardU - 1) / (256 * kShardU), (int64_t)num_cus() * 32);
   shard_gather_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(a);
   return check_launch("rk_shard_gather_rows");
 }

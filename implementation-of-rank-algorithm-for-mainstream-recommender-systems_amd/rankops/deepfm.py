@@ -201,14 +201,21 @@ class DeepFM(EngineModule):
                                              None, None, None]]
             # keep-alive: what the argument blocks point into (not the caller's index tensors: the
             # cache key's address / shape / stride check makes those pointers valid on a hit)
-            return [front] + tl, (7, 8), ep, B, (keep, arr, packed, w0, ml0, y)
+            return [front] + tl, (7, 8), ep, B, (keep, arr, self._images(names), w0, ml0, y)
         tail = common.tail_launches(deep_in, self._tail, self.deep_output_layer, head_kwargs)
         if tail is None:
             return None
         tl, ep, keep = tail
         gather = ["rk_fm_gather_packed", [arr, len(second), D, B, deep_in.data_ptr(), deep_in.stride(0), None, None,
                                           None]]
-        return [gather] + tl, (6, 7), ep, B, (keep, arr, packed, deep_in)
+        return [gather] + tl, (6, 7), ep, B, (keep, arr, self._images(names), deep_in)
+
+    def _images(self, names):
+        """The device tensors a marshalled launch points into beyond its arguments: the packed FM
+        tables and the folded BatchNorm affines.  A cache rebuild (a later .eval()/.train() or a
+        weight change) replaces them, so a prepared run() must keep its own references."""
+        return ([self.packed_table(n) for n in names],
+                [l.epilogue_kwargs() for l in self._tail])
 
     def _whole_build(self, names, category, head_kwargs):
         """rk_deepfm_forward's launch (gather, FM, deep layers, head in one): the _eager_build tuple,
@@ -221,12 +228,13 @@ class DeepFM(EngineModule):
         ops._lib.ensure_device(dev)
         arr = ops._seg_array(second)
         weights = [common.PACKED(l.linear.weight) for l in self._tail]
-        mls = [ops.make_mlp_layer(l.linear.weight, w, **l.epilogue_kwargs()) for l, w in zip(self._tail, weights)]
+        kws = [l.epilogue_kwargs() for l in self._tail]
+        mls = [ops.make_mlp_layer(l.linear.weight, w, **kw) for l, w, kw in zip(self._tail, weights, kws)]
         la = (ops._lib.MlpLayer * len(mls))(*mls)
         ep = ops.make_epilogue(head_w=self.deep_output_layer.weight, head_b=self.deep_output_layer.bias,
                                **head_kwargs)
         launch = ["rk_deepfm_forward", [arr, len(second), D, B, la, len(mls), ops.ctypes.byref(ep), None, None, None]]
-        return [launch], (7, 8), ep, B, (arr, packed, weights, mls, la)
+        return [launch], (7, 8), ep, B, (arr, self._images(names), weights, kws, mls, la)
 
     def prepare(self, category):
         """An eval forward bound to these input tensors (as DIN.prepare: the single-kernel analogue of

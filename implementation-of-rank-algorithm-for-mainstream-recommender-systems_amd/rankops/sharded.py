@@ -166,7 +166,10 @@ class ShardedDeepFM(EngineModule):
                 blocks.append(torch.stack([category[f] for f in fr], 1).reshape(-1))
         if not blocks:
             return torch.empty(0, dtype=self.index_dtype, device=self._device())
-        return torch.cat(blocks).to(self.index_dtype)
+        idx = torch.cat(blocks)
+        if self.index_dtype == torch.int32:  # as rk_shard_pack_indices: never wrap to a valid row
+            idx = torch.where((idx >= 0) & (idx <= 2 ** 31 - 1), idx, torch.full_like(idx, -1))
+        return idx.to(self.index_dtype)
 
     def _pack_indices_kernel(self, category: dict, B: int) -> torch.Tensor:
         import ctypes
@@ -237,7 +240,7 @@ class ShardedDeepFM(EngineModule):
         return self._exchange(recv, rows.reshape(-1), out_s, in_s, async_op)
 
     def _front_ok(self, B_l: int) -> bool:
-        D, l0 = self.embedding_dim, self._tail[0]
+        D = self.embedding_dim
         return (self.fused_front and B_l > 0 and len(self._tail) >= 2 and len(self.fields) <= 32
                 and 4 <= D <= 256 and D & (D - 1) == 0)
 
@@ -369,6 +372,13 @@ class ShardedDeepFM(EngineModule):
             return outs[0]
         return tuple(torch.cat([o[i] for o in outs], 0) for i in range(len(outs[0])))
 
+    def pipeline(self, batch: int, *, side_stream: bool = True, capture=None) -> "ExchangePipeline":
+        """The cross-batch exchange pipeline (P > 1) for local batches of `batch` samples: push()
+        batch i, get back batch i - 2's outputs; the exchanges of the two younger batches run under
+        the older one's forward (ExchangePipeline).  capture=[3 device batches]: the local segments
+        as hipGraphs bound to those batches (bench.py)."""
+        return ExchangePipeline(self, batch, side_stream=side_stream, capture=capture)
+
     def capture_pipeline(self, cat: dict, chunks: int = None) -> "CapturedPipeline":
         """run_steps with each chunk's three local segments (index pack, gather, FM + tail)
         captured as hipGraphs; the all-to-alls stay outside the graphs (RCCL collectives are
@@ -440,3 +450,193 @@ class CapturedPipeline:
 def _lib_dense(buf: torch.Tensor, offset: int, ld: int, dim: int, out_col: int):
     from ._lib import Segment
     return Segment(buf.data_ptr() + offset * 4, None, 0, ld, 0, dim, out_col)
+
+
+class _Ring:
+    """One pipeline slot's device buffers (index send/receive, row send/receive)."""
+
+    def __init__(self, model: "ShardedDeepFM", B_l: int, dev):
+        out_i, in_i = model.index_splits(B_l)
+        out_r, in_r = model.row_splits(B_l)
+        self.send_idx = torch.zeros(sum(in_i), dtype=model.index_dtype, device=dev)
+        self.recv_idx = torch.zeros(sum(out_i), dtype=model.index_dtype, device=dev)
+        self.recv_rows = torch.zeros(sum(out_r), dtype=torch.float32, device=dev)
+        self.send_rows = None  # gather output (allocated by the gather; captured: fixed)
+        self.idx_work = self.row_work = None
+        self.fwd_done = None  # event after the forward that last read recv_rows
+
+
+class ExchangePipeline:
+    """ShardedDeepFM's P > 1 step as a cross-batch software pipeline.
+
+    Batch i moves through three stages on three consecutive push() calls:
+
+      A(i)    pack(i)   -> index all_to_all_single(i), async          [side stream]
+      B(i)    wait index(i) -> gather_rows(i) -> row all_to_all(i), async  [side stream]
+      C(i)    wait rows(i)  -> the one-launch forward over the received rows [compute stream]
+
+    push(batch i) issues B(i-1), A(i), C(i-2) and returns batch i-2's outputs, so the index and row
+    exchanges of the two younger batches are in flight (RCCL on the process group's stream) while
+    the oldest one's forward runs: a step costs max(local device work, wire) instead of their sum,
+    and the forward covers the whole local batch in one rk_deepfm_forward launch (32-row workgroups
+    from 8,192 rows) — no chunking.  Three buffer slots rotate (batch i uses slot i % 3); every reuse
+    is stream-ordered behind the last reader of the slot:
+      send_idx   rewritten by pack(i+3) on the side stream, which waited for index(i) at B(i);
+      recv_idx   rewritten by index(i+3), issued from the side stream after B(i)'s gather;
+      send rows  rewritten by gather(i+3), which waits for index(i+3), queued behind row(i)
+                 on the collective stream (one stream per process group);
+      recv_rows  rewritten by row(i+3), issued after the side stream waited for C(i)'s event.
+    Collectives are issued in the same order on every rank (B(i-1)'s rows, then A(i)'s indices).
+    flush() drains the two batches still in flight.  Every sample's arithmetic is that of
+    ShardedDeepFM.run_steps: outputs are identical to the unpipelined forward.
+
+    CPU tensors (gloo): no streams; async work handles are waited on the host."""
+
+    DEPTH = 3
+
+    def __init__(self, model: "ShardedDeepFM", batch: int, *, side_stream: bool = True, capture=None):
+        if model.world == 1:
+            raise ValueError("ExchangePipeline: P = 1 has no exchange (use the model's forward)")
+        check_eval(model)
+        self.model, self.B = model, int(batch)
+        dev = model._device()
+        self.cuda = dev.type == "cuda"
+        self.main = torch.cuda.current_stream(dev) if self.cuda else None
+        self.side = (torch.cuda.Stream(dev) if side_stream else self.main) if self.cuda else None
+        self.slots = [_Ring(model, self.B, dev) for _ in range(self.DEPTH)]
+        self.n_in = 0    # batches pushed
+        self.n_out = 0   # batches whose forward has been issued
+        self.cats = [None] * self.DEPTH
+        self.graphs = None
+        if capture is not None:
+            self._capture(capture)
+
+    def _capture(self, cats):
+        """Captured mode (bench.py's P > 1 step): slot k's pack (bound to the index tensors cats[k]),
+        gather and forward as three hipGraphs, replayed by the stages on the same streams; the
+        collectives stay outside the graphs.  push() then takes the slot's bound batch (its
+        contents may change between pushes) and returns the slot's fixed output tensors, valid
+        until the slot's next forward (three pushes later)."""
+        if not self.cuda or len(cats) != self.DEPTH:
+            raise ValueError(f"ExchangePipeline capture: {self.DEPTH} device batches needed")
+        m = self.model
+        graphs = []
+        for k, cat in enumerate(cats):
+            cat = {f: ops.as_index(cat[f], f"category[{f!r}]") for f in m.fields}
+            sl = self.slots[k]
+            g_pack, sl.send_idx = _graph_of(lambda c=cat: m.pack_indices(c))
+            g_gather, sl.send_rows = _graph_of(lambda sl=sl: m.gather_rows(sl.recv_idx, self.B, 0, self.B))
+            g_fwd, outs = _graph_of(lambda sl=sl: m.fm_and_tail(sl.recv_rows, self.B))
+            graphs.append({"pack": g_pack, "gather": g_gather, "forward": g_fwd, "outs": outs, "cat": cat})
+            self.cats[k] = cat
+        self.graphs = graphs
+
+    def step(self):
+        """Captured mode: one pipeline step on the slots' bound batches (push without the checks)."""
+        i = self.n_in
+        if i >= 1:
+            self._stage_b(i - 1)
+        self._stage_a(i, None)
+        self.n_in += 1
+        if i >= 2:
+            self.n_out += 1
+            return self._stage_c(i - 2)
+        return None
+
+    # -- stream helpers
+    def _on(self, st):
+        import contextlib
+        return torch.cuda.stream(st) if self.cuda else contextlib.nullcontext()
+
+    @staticmethod
+    def _wait(work):
+        if work is not None:
+            work.wait()  # stream-ordered on CUDA (the current stream waits), host-blocking on gloo
+
+    # -- stages
+    def _stage_a(self, i: int, cat: dict):
+        m, sl = self.model, self.slots[i % self.DEPTH]
+        if self.cuda and self.side is not self.main:
+            self.side.wait_stream(self.main)  # the caller's index tensors were written on the compute stream
+        with self._on(self.side):
+            if self.graphs:
+                self.graphs[i % self.DEPTH]["pack"].replay()
+                send = sl.send_idx
+            else:
+                send = sl.send_idx = m.pack_indices(cat)
+            out_s, in_s = m.index_splits(self.B)
+            sl.idx_work = m._exchange(sl.recv_idx, send, out_s, in_s, async_op=True)[1]
+
+    def _stage_b(self, i: int):
+        m, sl = self.model, self.slots[i % self.DEPTH]
+        with self._on(self.side):
+            self._wait(sl.idx_work)
+            sl.idx_work = None
+            if self.graphs:
+                self.graphs[i % self.DEPTH]["gather"].replay()
+            else:
+                sl.send_rows = m.gather_rows(sl.recv_idx, self.B, 0, self.B)
+            if sl.fwd_done is not None:  # C(i-3) read recv_rows: the row exchange may overwrite it now
+                self.side.wait_event(sl.fwd_done)
+            out_s, in_s = m.row_splits(self.B)
+            sl.row_work = m._exchange(sl.recv_rows, sl.send_rows.reshape(-1), out_s, in_s, async_op=True)[1]
+
+    def _stage_c(self, i: int):
+        m, sl = self.model, self.slots[i % self.DEPTH]
+        with self._on(self.main):
+            self._wait(sl.row_work)
+            sl.row_work = None
+            if self.graphs:
+                self.graphs[i % self.DEPTH]["forward"].replay()
+                out = self.graphs[i % self.DEPTH]["outs"]
+            else:
+                out = m.fm_and_tail(sl.recv_rows, self.B)
+            if self.cuda:
+                sl.fwd_done = torch.cuda.Event()
+                sl.fwd_done.record(self.main)
+        return out
+
+    # -- driver
+    def push(self, category: dict):
+        """Feed one local batch ({field: [batch] int64}); returns the outputs (prob, total_logit,
+        fm1, fm2, deep_logit) of the batch pushed two calls earlier, or None while the pipeline fills."""
+        m = self.model
+        if self.graphs:
+            return self.step()
+        missing = [f for f in m.fields if f not in category]
+        if missing:
+            raise KeyError(f"ExchangePipeline.push: category features missing: {missing}")
+        # (device checks on the GPU path; the gloo tests drive CPU stand-ins of the device steps)
+        cat = ({f: ops.as_index(category[f], f"category[{f!r}]") for f in m.fields} if self.cuda
+               else {f: category[f] for f in m.fields})
+        if cat[m.fields[0]].shape[0] != self.B:
+            raise ValueError(f"ExchangePipeline.push: batch {cat[m.fields[0]].shape[0]} != {self.B}")
+        i = self.n_in
+        if i >= 1:
+            self._stage_b(i - 1)
+        self._stage_a(i, cat)
+        self.cats[i % self.DEPTH] = cat  # the index tensors stay alive until pack(i) has read them
+        self.n_in += 1
+        if i >= 2:
+            self.n_out += 1
+            return self._stage_c(i - 2)
+        return None
+
+    def flush(self):
+        """Outputs of the batches still in flight, oldest first (the pipeline is empty afterwards)."""
+        outs = []
+        i = self.n_in
+        # C of the older batch in flight, B of the newest (its A ran in the last push), then its C
+        if i >= 2 and self.n_out == i - 2:
+            outs.append(self._stage_c(i - 2))
+            self.n_out += 1
+        if i >= 1:
+            self._stage_b(i - 1)
+        while self.n_out < i:
+            outs.append(self._stage_c(self.n_out))
+            self.n_out += 1
+        self.n_in = self.n_out = 0
+        if not self.graphs:
+            for sl in self.slots:
+                sl.send_rows = None
+        return outs

@@ -429,7 +429,8 @@ int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim,
  * reference's DeepFM.forward, deepfm.py:121-151, runs on one device) ---- */
 /* The index all-to-all's send buffer in one launch: slot q (fields in owner-major order) copies
  * idx[q][0..batch) as int32 to out[base[q] + b * stride[q]] (base = batch * start_r + j,
- * stride = F_r: blocks [r][b][f_r]).  Indices must fit int32 (the caller checks table rows). */
+ * stride = F_r: blocks [r][b][f_r]).  An index outside [0, 2^31) is sent as -1, so the owner's
+ * rk_shard_gather_rows writes a zero row and raises RK_FLAG_INDEX_OOB instead of wrapping. */
 int rk_shard_pack_indices(const int64_t* const* idx, const int64_t* base, const int32_t* stride,
                           int32_t num_fields, int64_t batch, int32_t* out, void* stream);
 /* The row all-to-all's send buffer for samples [b0, b0 + bc) of every source: out[s][b'][j][0..row_floats)

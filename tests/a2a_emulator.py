@@ -6,7 +6,7 @@ P ShardedDeepFM shards live in one process, each driven by its own Python thread
 send buffer, meet at a barrier, each copies the pieces addressed to it (source order, the split
 sizes checked against each other), and meet again before anyone may reuse a buffer.  On a GPU the
 copies are stream-ordered after the producers (all threads enqueue on the device's default
-stream, and every producer was enqueued before its rank reached the first barrier), so every
+stream after an event wait on every rank's producers, whatever streams the ranks use), so every
 device step of the shards stays real and only the RCCL transport is replaced."""
 from __future__ import annotations
 
@@ -14,9 +14,17 @@ import threading
 
 
 class _Done:
-    """Work handle of an already-completed exchange (the copies are enqueued at issue time)."""
+    """Work handle of an exchange whose copies were enqueued at issue time: wait() orders the
+    caller's current stream after them (a no-op for CPU tensors), as a ProcessGroupNCCL work's
+    wait() does."""
+
+    def __init__(self, event=None):
+        self.event = event
 
     def wait(self):
+        if self.event is not None:
+            import torch
+            torch.cuda.current_stream().wait_event(self.event)
         return True
 
 
@@ -25,22 +33,37 @@ class InProcessAllToAll:
         self.world = world
         self.barrier = threading.Barrier(world, timeout=timeout)
         self.slots = [None] * world
+        self.events = [None] * world
         self.calls = 0
 
     def bind(self, rank: int):
         def exchange(out, inp, out_splits, in_splits, async_op=False):
-            self._exchange(rank, out, inp, list(out_splits), list(in_splits))
-            return (out, _Done()) if async_op else out
+            ev = self._exchange(rank, out, inp, list(out_splits), list(in_splits))
+            return (out, _Done(ev)) if async_op else out
         return exchange
 
     def _exchange(self, rank, out, inp, out_splits, in_splits):
+        """Stream-ordered on a GPU: each rank's copies run on its current stream after every
+        rank's producers (an event per rank recorded at deposit), and every rank's stream then
+        waits for every rank's copies (so no send buffer is reused while a peer still reads it).
+        Returns the event after this rank's copies (None on CPU)."""
+        import torch
         if len(out_splits) != self.world or len(in_splits) != self.world:
             raise ValueError("split lists must have one entry per rank")
         if sum(in_splits) != inp.numel() or sum(out_splits) != out.numel():
             raise ValueError(f"rank {rank}: split sums {sum(in_splits)}/{sum(out_splits)} != "
                              f"buffer sizes {inp.numel()}/{out.numel()}")
+        cuda = out.is_cuda
         self.slots[rank] = (inp.reshape(-1), in_splits)
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self.events[rank] = ev
         self.barrier.wait()
+        if cuda:
+            st = torch.cuda.current_stream()
+            for e in list(self.events):
+                st.wait_event(e)
         flat = out.reshape(-1)
         o = 0
         for s in range(self.world):
@@ -53,7 +76,19 @@ class InProcessAllToAll:
             o += n
         if rank == 0:
             self.calls += 1
+        done = None
+        self.barrier.wait()  # every rank has read the deposit events
+        if cuda:
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream())
+            self.events[rank] = done
         self.barrier.wait()
+        if cuda:
+            st = torch.cuda.current_stream()
+            for e in list(self.events):
+                st.wait_event(e)
+        self.barrier.wait()  # every rank has read the copy events before the next call replaces them
+        return done
 
     def abort(self):
         self.barrier.abort()

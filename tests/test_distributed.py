@@ -100,6 +100,69 @@ def _worker(rank, world, port, B, q, chunks=1):
             dist.destroy_process_group()
 
 
+def _pipe_worker(rank, world, port, B, q, nbatch):
+    """ShardedDeepFM.pipeline (the cross-batch exchange pipeline) over `nbatch` consecutive local
+    batches: push() returns batch i - 2's outputs, flush() the last two; all against the oracle."""
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        full = H.build("deepfm", CFG, seed=42)
+        sh = CpuStepsSharded(dict((f, e.num_embeddings) for f, e in full.second_order_embeddings.items()),
+                             CFG["dim"], CFG["hidden"], rank=rank, world_size=world)
+        sd = {k: v for k, v in full.state_dict().items()
+              if not k.startswith(("first_order", "second_order")) or k.split(".")[1] in sh.local_fields}
+        sh.load_state_dict(sd, strict=True)
+        sh.eval()
+        batches, expects = [], []
+        for i in range(nbatch):
+            inp = H.make_inputs("deepfm", CFG, B * world, seed=900 + i)
+            with torch.no_grad():
+                expects.append(ref.deepfm_forward(H.cpu_params(full), inp["category"], list(FIELDS),
+                                                  len(CFG["hidden"])))
+            batches.append({f: v[rank * B:(rank + 1) * B].contiguous() for f, v in inp["category"].items()})
+        pipe = sh.pipeline(B)
+        got = []
+        with torch.no_grad():
+            for i, cat in enumerate(batches):
+                out = pipe.push(cat)
+                assert (out is None) == (i < 2)
+                if out is not None:
+                    got.append(out)
+            got.extend(pipe.flush())
+        assert len(got) == nbatch
+        for g, e in zip(got, expects):
+            for x, y in zip(g, e):
+                torch.testing.assert_close(x, y[rank * B:(rank + 1) * B], atol=1e-5, rtol=1e-5)
+        q.put((rank, "ok"))
+    except Exception as exc:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(exc)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(target, world, B, extra):
+    """Runs target(rank, world, port, B, queue, extra) on `world` spawned processes; the failures."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, B, q, extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    return [r for r in results if r[1] != "ok"]
+
+
+@pytest.mark.parametrize("world,nbatch", [(2, 2), (2, 5), (3, 1), (3, 4)])
+def test_sharded_deepfm_cross_batch_pipeline_gloo(world, nbatch):
+    """The cross-batch pipeline at world 2 / 3 with real gloo all-to-alls, 1-5 batches (fill, steady
+    state and drain): every batch's outputs equal the single-process oracle's."""
+    bad = _spawn(_pipe_worker, world, 16, nbatch)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 3), (3, 4)])
 def test_sharded_deepfm_exchange_gloo(world, chunks):
     """Exchange routing at world 2 / 3, unpipelined and with the batch split into 3-4 chunks whose

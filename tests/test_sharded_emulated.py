@@ -246,3 +246,126 @@ def test_shard_pack_and_gather_kernels(world):
             exp = tab[idx.clamp(max=tab.shape[0] - 1)] * ok[..., None]
             assert torch.equal(rows[:, :, j, :], exp[:, :, :RS])
     assert rankops.error_flags(reset=True) & 1
+
+
+def _pipe_run(shards, emu, batches, B_l, capture=False):
+    """Each emulated rank drives ShardedDeepFM.pipeline over `batches` (per batch: the global
+    category dict); returns per rank the list of per-batch outputs (CPU)."""
+    world = len(shards)
+
+    def rank_fn(r):
+        sh = shards[r]
+        mine = [{f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in cat.items()} for cat in batches]
+        outs = []
+        with torch.no_grad():
+            if capture:
+                pipe = sh.pipeline(B_l, capture=mine[:3])
+                for i in range(len(batches)):
+                    o = pipe.step()
+                    if o is not None:
+                        torch.cuda.synchronize()
+                        outs.append(tuple(x.cpu() for x in o))
+                for o in pipe.flush():
+                    torch.cuda.synchronize()
+                    outs.append(tuple(x.cpu() for x in o))
+            else:
+                pipe = sh.pipeline(B_l)
+                for cat in mine:
+                    o = pipe.push(cat)
+                    if o is not None:
+                        outs.append(o)
+                outs.extend(pipe.flush())
+                if outs and outs[0][0].is_cuda:
+                    torch.cuda.synchronize()
+                outs = [tuple(x.cpu() for x in o) for o in outs]
+        return outs
+
+    return run_ranks(world, rank_fn, on_error=emu.abort)
+
+
+@pytest.mark.parametrize("world,nbatch", [(2, 4), (8, 3)])
+def test_emulator_cross_batch_pipeline_cpu(world, nbatch):
+    """CPU: the cross-batch pipeline through the emulator under the CPU stand-in device steps."""
+    from test_distributed import CFG, CpuStepsSharded
+    full = H.build("deepfm", CFG, seed=42)
+    B = 12
+    batches = [H.make_inputs("deepfm", CFG, B * world, seed=300 + i)["category"] for i in range(nbatch)]
+    shards, emu = _shards(full, world, cls=CpuStepsSharded)
+    outs = _pipe_run(shards, emu, batches, B)
+    for i, cat in enumerate(batches):
+        expect = _oracle(full, CFG, cat)
+        for r in range(world):
+            _check(outs[r][i], expect, r * B, (r + 1) * B, 1e-5)
+    assert emu.calls == 2 * nbatch  # one index and one row exchange per batch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cross_batch_pipeline_emulated_on_gpu(world):
+    """ShardedDeepFM.pipeline (eager) at P = 2 / 4 / 8 on one GPU: 5 batches through the three-stage
+    pipeline (index exchange, gather + row exchange on the side stream, the one-launch forward on the
+    compute stream), each against the oracle; ragged local batch."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 520
+    batches = [H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=7000 + 31 * i + world), "cuda")["category"]
+               for i in range(5)]
+    shards, emu = _shards(full, world)
+    outs = _pipe_run(shards, emu, batches, B_l)
+    for i, cat in enumerate(batches):
+        expect = _oracle(full, CFG30, cat)
+        for r in range(world):
+            _check(outs[r][i], expect, r * B_l, (r + 1) * B_l, 1e-4)
+    assert emu.calls == 2 * len(batches)
+    import rankops
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_captured_cross_batch_pipeline_emulated_on_gpu(world):
+    """bench.py's P > 1 step: the pipeline with pack / gather / forward captured per slot, 5 steps +
+    flush over the three bound batches (slot i % 3), each batch's outputs against the oracle."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 1000
+    batches = [H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=8100 + i), "cuda")["category"]
+               for i in range(3)]
+    shards, emu = _shards(full, world)
+    order = [batches[i % 3] for i in range(5)]
+    outs = _pipe_run(shards, emu, order, B_l, capture=True)
+    for i, cat in enumerate(order):
+        expect = _oracle(full, CFG30, cat)
+        for r in range(world):
+            _check(outs[r][i], expect, r * B_l, (r + 1) * B_l, 1e-4)
+    import rankops
+    assert rankops.error_flags() == 0
+
+
+@pytest.mark.gpu
+def test_cross_batch_pipeline_full_local_batch_p8():
+    """P = 8 at configs[4]'s local batch (8,192 samples: the forward's 32-row workgroups, one per CU)
+    over 30 x 200k-row tables: pipelined outputs bit-equal to the unpipelined run_steps (chunks=1),
+    and the first 300 samples of every rank against the oracle."""
+    cfg = {"dim": 32, "fields": {f"field_{i:02d}": 200_000 + i for i in range(30)}, "hidden": [512, 256, 128]}
+    full = H.build("deepfm", cfg, seed=42).cuda()
+    world, B_l = 8, 8192
+    batches = [H.to_device(H.make_inputs("deepfm", cfg, B_l * world, seed=9100 + i), "cuda")["category"]
+               for i in range(2)]
+    shards, emu = _shards(full, world)
+    outs = _pipe_run(shards, emu, batches, B_l)
+
+    def plain(r):
+        with torch.no_grad():
+            o = shards[r].run_steps({f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in batches[1].items()}, chunks=1)
+        torch.cuda.synchronize()
+        return tuple(x.cpu() for x in o)
+
+    ref_outs = run_ranks(world, plain, on_error=emu.abort)
+    for r in range(world):
+        for a, b in zip(outs[r][1], ref_outs[r]):
+            assert torch.equal(a, b)
+    for i, cat in enumerate(batches):
+        sub = {f: torch.cat([v[r * B_l:r * B_l + 300] for r in range(world)]) for f, v in cat.items()}
+        expect = _oracle(full, cfg, sub)
+        for r in range(world):
+            got = tuple(x[:300] for x in outs[r][i])
+            _check(got, expect, r * 300, (r + 1) * 300, 1e-4)

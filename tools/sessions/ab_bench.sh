@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library builds on the headline legs: for each .so given, the bench's forward legs with
-# RANKOPS_LIB pointing at it.  Usage (on the box): bash tools/ab_bench.sh <tag> <lib.so>...
+# RANKOPS_LIB pointing at it.  Usage (on the box): bash tools/sessions/ab_bench.sh <tag> <lib.so>...
 set -o pipefail
 T=$1; shift; O=${ABDIR:-gpurun_out/r03}; mkdir -p $O
 for L in "$@"; do

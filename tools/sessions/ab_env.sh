@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of one environment switch on the bench's forward legs (one library build): for each value,
 # the headline + DCN / DeepFM / BST legs with VAR=value.  Usage (on the box):
-#   bash tools/ab_env.sh <tag> <VAR> <value>...
+#   bash tools/sessions/ab_env.sh <tag> <VAR> <value>...
 set -o pipefail
 T=$1; V=$2; shift 2; O=gpurun_out/r04; mkdir -p $O
 for X in "$@"; do

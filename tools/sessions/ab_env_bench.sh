@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an environment switch on the bench's forward legs, twice interleaved:
-# bash tools/ab_env_bench.sh <tag> <VAR> <value>...   (run on the box)
+# bash tools/sessions/ab_env_bench.sh <tag> <VAR> <value>...   (run on the box)
 set -o pipefail
 T=$1; V=$2; shift 2; O=gpurun_out/r04; export TMPDIR=/tmp; mkdir -p $O
 for r in 1 2; do for v in "$@"; do

@@ -2,7 +2,7 @@
 # Round-4 counter session on the GPU box: per workload two SQ passes (MFMA busy, waits, LDS) and a
 # kernel trace of the forward; FETCH_SIZE / WRITE_SIZE passes for the headline kernel and the
 # standalone gather; then tools/pmc_counters.py digests it into <session>/counters.json.
-# Usage (on the box): bash tools/r04_counters.sh <tag> [workloads...]
+# Usage (on the box): bash tools/sessions/r04_counters.sh <tag> [workloads...]
 set -o pipefail
 T=${1:-base}; shift
 WL=${@:-din dcn deepfm bst bst_ref}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # DIN kernel split by timing builds (RK_DIN_SKIP_A: phase B on zero rows; RK_DIN_SKIP_B: phase A
 # only; RK_DIN_NO_GATHER: keys from 16 cache-resident rows) at the bench workload.
-# Usage (on the box): bash tools/r04_din_split.sh <tag> [lib names...]
+# Usage (on the box): bash tools/sessions/r04_din_split.sh <tag> [lib names...]
 set -o pipefail
 T=${1:-split}; shift; O=gpurun_out/r04; mkdir -p $O
 P=implementation-of-rank-algorithm-for-mainstream-recommender-systems_amd/rankops

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session: the GPU suite, smoke, the bench under rocprofv3 (tools/bench_final.sh), then
 # optional extra steps.  A test failure (pytest exit 1) does not stop the measurement; a timeout,
-# crash or abort does.  Usage (on the box): bash tools/r04_session.sh <tag> [extra command]
+# crash or abort does.  Usage (on the box): bash tools/sessions/r04_session.sh <tag> [extra command]
 set -o pipefail
 T=${1:-s1}; shift; O=gpurun_out/$T; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1

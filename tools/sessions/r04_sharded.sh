@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU step: sharded DeepFM tests (fused front end, int32 wire) and the sharded leg with its
-# modelled 1->8 curve.  Usage (on the box): bash tools/r04_sharded.sh <tag>
+# modelled 1->8 curve.  Usage (on the box): bash tools/sessions/r04_sharded.sh <tag>
 set -o pipefail
 T=${1:-sh1}; O=gpurun_out/r04; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_sharded_emulated.py tests/test_gpu_fm_linear.py -x -q --timeout 150 --timeout-method thread > $O/test_sharded_$T.log 2>&1 || { echo "sharded tests failed"; tail -40 $O/test_sharded_$T.log; exit 1; }

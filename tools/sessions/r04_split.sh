@@ -3,4 +3,4 @@
 set -o pipefail
 export ABDIR=gpurun_out/r04
 P=implementation-of-rank-algorithm-for-mainstream-recommender-systems_amd/rankops
-bash tools/ab_bench.sh split $P/librankops.so $P/librankops_split.so && bash tools/ab_bench.sh split2 $P/librankops.so $P/librankops_split.so
+bash tools/sessions/ab_bench.sh split $P/librankops.so $P/librankops_split.so && bash tools/sessions/ab_bench.sh split2 $P/librankops.so $P/librankops_split.so

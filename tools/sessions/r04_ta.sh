@@ -1,6 +1,6 @@
 #!/bin/bash
 # Memory-pipe counters of the DIN / DCN / DeepFM forward kernels (one --pmc pass per block group):
-# TA busy / stalls, TCP stalls and L2 requests, L2 hit/miss.  bash tools/r04_ta.sh <tag>  (on the box)
+# TA busy / stalls, TCP stalls and L2 requests, L2 hit/miss.  bash tools/sessions/r04_ta.sh <tag>  (on the box)
 set -o pipefail
 T=${1:-ta}; O=gpurun_out/r04/$T; mkdir -p $O; export TMPDIR=/tmp
 pass() {  # <name> <workload> <counters...>
