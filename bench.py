@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--no-sharded", action="store_true", help="skip the table-sharded DeepFM (configs[4])")
     ap.add_argument("--no-model-curve", action="store_true", help="skip the modelled 1->8 GPU curve of configs[4]")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,bst_ref,fwfm,din_per_call,din_zipf,"
-                                        "dcn_eager,din_eager,deepfm_eager,bst_eager")
+    ap.add_argument("--models", default="dcn,dcn_per_call,dcn_256_per_call,deepfm,bst,bst_ref,fwfm,afm,deepcrossing,"
+                                        "din_per_call,din_zipf,dcn_eager,din_eager,deepfm_eager,bst_eager")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step legs")
     return ap.parse_args()
@@ -130,6 +130,12 @@ def workload(name: str, batch: int, seed: int, zipf: float = None):
     elif name == "fwfm":
         cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8}
         model_name = "fwfm"
+    elif name == "afm":  # afm.py:241-242 defaults: embedding_dim 8, attention_factor 128
+        cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8, "att": 128}
+        model_name = "afm"
+    elif name == "deepcrossing":  # deepcrossing.py:319-320 defaults: residual_internal_dim 128, 1 unit
+        cfg = {"vocab": H.WECHAT_VOCAB, "internal": 128, "units": 1, "interaction_weights": "frozen"}
+        model_name = "deepcrossing"
     else:
         raise ValueError(name)
     with torch.device(dev):
@@ -424,10 +430,11 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         t_gather1 = kernel_avg_ms(g_gather1.replay, iters)
         t_fm1 = kernel_avg_ms(g_fm1.replay, iters)
         t_seq = kernel_avg_ms(g_seq.replay, iters)
-        # contention proxy: the forward with a copy of the row exchange's bytes (what this rank's
-        # RCCL kernels move: (P-1)/P of its send rows out, as much in) on a second stream
+        # contention proxy: the forward with a copy of the bytes this rank's RCCL kernels move
+        # (P2P writes: (P-1)/P of its send rows out to the peers; the peers' kernels push its
+        # receive rows) on a second stream, which takes CUs from the forward as RCCL's would
         xfer = int(B_l * SHARDED_FIELDS * RS * (P - 1) / P)
-        src, dst = torch.empty(2 * xfer, device=dev), torch.empty(2 * xfer, device=dev)
+        src, dst = torch.empty(xfer, device=dev), torch.empty(xfer, device=dev)
         side = torch.cuda.Stream()
 
         def fwd_with_copy():
@@ -453,6 +460,7 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         wire1 = 1e3 * ((idx_link + rows_link) / XGMI_LINK_BPS + 2 * A2A_LATENCY_S)
         local1 = t_seq + contention
         piped = max(local1, wire1)
+        piped_free = max(t_seq, wire1)  # if RCCL's kernels found idle CUs (no slowdown of the forward)
         curve[str(P)] = {
             "kind": "model, not a measurement",
             "B_local": B_l, "fields_rank0": F_me, "chunks": C,
@@ -462,15 +470,17 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
                                      "forward_one_launch": round(t_fm1, 4),
                                      "pack_gather_forward_one_graph": round(t_seq, 4),
                                      "forward_with_copy_beside": round(t_fm1_copy, 4),
-                                     "contention": round(contention, 4), "copy_bytes": 8 * xfer},
+                                     "contention": round(contention, 4), "copy_bytes": 4 * xfer},
             "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4), "pipelined_per_step": round(wire1, 4)},
             "bytes_per_link": {"index": int(idx_link), "rows": int(rows_link)},
-            "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4), "pipelined": round(piped, 4)},
+            "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4), "pipelined": round(piped, 4),
+                            "pipelined_no_contention": round(piped_free, 4)},
             "samples_per_s": {"serial": round(SHARDED_GLOBAL_BATCH / (serial * 1e-3), 1),
                               "overlapped": round(SHARDED_GLOBAL_BATCH / (overlap * 1e-3), 1),
                               "pipelined": round(SHARDED_GLOBAL_BATCH / (piped * 1e-3), 1)},
             "speedup_vs_p1": {"serial": round(p1_ms / serial, 2), "overlapped": round(p1_ms / overlap, 2),
-                              "pipelined": round(p1_ms / piped, 2)},
+                              "pipelined": round(p1_ms / piped, 2),
+                              "pipelined_no_contention": round(p1_ms / piped_free, 2)},
             "pipelined_bound": "device" if local1 >= wire1 else "wire",
         }
         del model, g_pack, g_gather, g_fm, g_gather1, g_fm1, g_seq, rows1, src, dst
@@ -696,12 +706,16 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
     for b in (batch, big_batch):  # SURVEY §8d cache-sensitivity variant: Zipf(1.1) row popularity
         legs.append((f"zipf_{ZIPF_A}_batch_{b}", b,
                      H.to_device(H.make_inputs("deepfm", dict(cfg, zipf=ZIPF_A), b, seed=4321 + b), dev)["category"]))
+    # the alternative layout: line-aligned [V, 32] second-order rows (one 128-B line
+    # each) and the first-order weights in their own [V, 1] table, i.e. the nn.Embedding weights as
+    # they are (fm_gather_kernel<8, kFmTables>)
+    legs += [(f"tables_batch_{b}", b, c) for (_, b, c) in legs[:2]]
     for key, b, cat in legs:
-        ms = graph_kernel_avg_ms(model.gather_launcher(cat))
+        ms = graph_kernel_avg_ms(model.gather_launcher(cat, packed=not key.startswith("tables")))
         achieved = DEEPFM_GATHER_BYTES * b / (ms * 1e-3)
         # (tools/r04_counters.sh: workloads deepfm_gather at the config's batch, deepfm_gather65536)
-        tr = load_traffic("fm_gather_kernel", "deepfm_gather" if b == batch else f"deepfm_gather{b}") \
-            if not key.startswith("zipf") else None
+        wl = ("deepfm_gather_tables" if key.startswith("tables") else "deepfm_gather") + ("" if b == batch else str(b))
+        tr = load_traffic("fm_gather_kernel", wl) if not key.startswith("zipf") else None
         out[key] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
                     "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
         if tr:  # PMC-measured HBM bytes at the same launch time
@@ -758,22 +772,31 @@ def deepfm_roofline(model, inp, batch):
 
 
 def bst_small_roofline(model, inp, batch, cfg):
-    """bst_small_kernel (every block + pooling of BST at the reference's own shape, d_model 16, one
-    launch) timed alone: back-to-back launches, HIP events on the stream they run on.  VALU-bound:
-    priced against the FP32 vector peak (157.3 TF needs packed FMAs; the kernel's scalar fmaf chain
-    tops out at half of it)."""
+    """The blocks + pooling of BST at the reference's own shape (d_model 16, one launch) timed alone:
+    back-to-back launches, HIP events on the stream they run on.  4 heads: bst_mfma_kernel (round 5:
+    projections on v_mfma_f32_16x16x4_f32, QK^T and P V on v_mfma_f32_4x4x1f32, key tiles past each
+    sample's length skipped), priced against the FP32 MFMA peak; other head counts: the VALU kernel
+    bst_small_kernel.  The flop basis is the reference formulation's (every key position counted)."""
     launch = model.blocks_kernel_launcher(inp["seq_feedid"], inp["seq_length"])
     ms = kernel_avg_ms(launch, 20)
     T, d = cfg["max_len"], cfg["dim"]
     per = 8 * T * d * d + 4 * T * T * d + 4 * T * d * d  # projections, QK^T + AV, FFN (as BST_BLOCK_FLOP)
     nb = len(getattr(model, "transformer_blocks", [None]))
     flop = per * nb * batch
-    r = {"kernel": "bst_small_kernel", "bound": "valu", "unit": "TFLOP/s", "peak": PEAK_FP32_MFMA / 1e12,
+    mfma = cfg.get("heads", 4) == 4 and os.environ.get("RANKOPS_BST_MFMA", "1") != "0"
+    r = {"kernel": "bst_mfma_kernel" if mfma else "bst_small_kernel", "bound": "mfma" if mfma else "valu",
+         "unit": "TFLOP/s", "peak": PEAK_FP32_MFMA / 1e12,
          "avg_launch_ms": round(ms, 5), "flop_per_launch": flop,
          "flop_basis": f"{per:,} per sample per block (T = {T}, d_model {d}) x {nb} block(s)",
          "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4),
-         "frac_of_unpacked_fma_peak": round(2 * flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
-    r.update(counter_fields("bst_small_kernel", "bst_ref", flop))
+         "frac_of_one_wave_valu_issue_peak": round(2 * flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
+    if mfma:
+        r.update(counter_fields("bst_mfma_kernel", "bst_ref_blocks", flop))
+        whole = counter_fields("bst_mfma_fwd_kernel", "bst_ref")
+        r["whole_forward_counters"] = {"kernel": "bst_mfma_fwd_kernel", "mfma_busy_frac": whole.get("mfma_busy_frac"),
+                                       "counters": whole.get("counters")}
+    else:
+        r.update(counter_fields("bst_small_kernel", "bst_ref", flop))
     return r
 
 
@@ -790,6 +813,44 @@ def bst_roofline(model, inp, batch):
          "achieved": round(flop / (ms * 1e-3) / 1e12, 3), "frac": round(flop / (ms * 1e-3) / PEAK_FP32_MFMA, 4)}
     r.update(counter_fields("bst_block_kernel", "bst", flop))
     return r
+
+
+# AFM forward (afm.py:92-119, D 8, A 128, 7 fields = 21 pairs): per pair the Hadamard product, the
+# attention MLP 8 -> 128 (ReLU) -> 1, the softmax-weighted sum; then p (8 -> 1) and the dense term
+AFM_FLOP = 21 * (8 + 2 * 8 * 128 + 128 + 2 * 128 + 1) + 21 * 8 * 2 + (2 * 8 + 1) + (2 * 16 + 1)  # 51,647
+AFM_BYTES = 7 * (8 + 8 * 4) + 16 * 4 + 2 * 4  # indices + 32-B rows, 16 dense floats, prob + logit: 352
+# DeepCrossing forward (deepcrossing.py:146-163, one residual unit 50 -> 128 -> 50, output 50 -> 1)
+DEEPCROSSING_FLOP = 2 * 50 * 128 + 128 + 2 * 128 * 50 + 50 + 50 + 2 * 50 + 1  # 25,929
+DEEPCROSSING_BYTES = 16 * 4 + 6 * 8 + (16 + 2 + 4 * 4) * 4 + 2 * 4  # dense, 6 indices, 34 embedding floats, outputs: 256
+
+
+def small_forward_roofline(model, name, inp, batch, flop_per_sample, bytes_per_sample, kernels, big_batch=65536):
+    """AFM / DeepCrossing forward legs: the whole eval forward (AFM: one rk_afm_forward
+    launch; DeepCrossing: rk_concat_gather + the one-launch residual MLP) timed as 20 back-to-back
+    forwards in one hipGraph (HIP events on the replay stream), at the bench batch and at 65,536 rows
+    (launch ramp amortised).  Both roofs are reported: FP32 matrix/vector peak for the flops, HBM for
+    the bytes; at these per-sample sizes neither is close — the forwards are launch- and latency-bound."""
+    import helpers as H
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = {"kernels": kernels, "flop_per_sample": flop_per_sample, "bytes_per_sample": bytes_per_sample,
+           "peak_tflops": PEAK_FP32_MFMA / 1e12, "peak_hbm_gbs": PEAK_HBM / 1e9}
+    cfg = workload_cfg(name)
+    for b in (batch, big_batch):
+        x = inp if b == batch else H.to_device(H.make_inputs(name, cfg, b, seed=4242), dev)
+        ms = graph_kernel_avg_ms(lambda x=x: H.call_model(model, name, x))
+        out[f"batch_{b}"] = {"avg_forward_ms": round(ms, 5), "samples_per_s": round(b / (ms * 1e-3), 1),
+                             "tflops": round(flop_per_sample * b / (ms * 1e-3) / 1e12, 3),
+                             "frac_flop": round(flop_per_sample * b / (ms * 1e-3) / PEAK_FP32_MFMA, 4),
+                             "gb_per_s": round(bytes_per_sample * b / (ms * 1e-3) / 1e9, 1),
+                             "frac_hbm": round(bytes_per_sample * b / (ms * 1e-3) / PEAK_HBM, 4)}
+    return out
+
+
+def workload_cfg(name):
+    import helpers as H
+    return {"afm": {"vocab": H.WECHAT_VOCAB, "dim": 8, "att": 128},
+            "deepcrossing": {"vocab": H.WECHAT_VOCAB, "internal": 128, "units": 1,
+                             "interaction_weights": "frozen"}}[name]
 
 
 # ------------------------------------------------------------------ main
@@ -935,6 +996,13 @@ def main():
                 r["roofline"] = deepfm_roofline(m2, inp2, batch)
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
+            if name == "afm":
+                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_kernel<8,128>"])
+                r["roofline"].update(counter_fields("afm_kernel", "afm"))
+            if name == "deepcrossing":
+                r["roofline"] = small_forward_roofline(m2, "deepcrossing", inp2, batch, DEEPCROSSING_FLOP,
+                                                       DEEPCROSSING_BYTES, ["concat_gather_kernel", "mlp_stream_kernel"])
+                r["roofline"].update(counter_fields("mlp", "deepcrossing"))
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob
                 r["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * r["samples_per_s"] / 1e9, 1)
                 r["bytes_per_sample"] = FWFM_BYTES_PER_SAMPLE

@@ -17,6 +17,8 @@
 //
 // Work split: 256-thread workgroups (4 waves), persistent — each wave walks samples
 // b = (blockIdx.x * 4 + wave) + k * gridDim.x * 4.
+#include <cstdlib>
+
 #include "common.h"
 #include "mlp_stream.h"
 
@@ -237,6 +239,255 @@ __device__ __forceinline__ float bst_small_sample(const BstSmallArgs& a, int64_t
   return a.pool_mean ? pooled / (float)len : pooled;
 }
 
+// ---------------------------------------------------------------------------------------------
+// 4 heads (d_h = 4) on the matrix cores (round 5).  One wave per sample, the sequence in 16-position
+// tiles; every activation stays in registers in one layout, L0: lane (p16 = lane & 15, grp = lane >> 4)
+// holds features 4 grp .. 4 grp + 3 of position 16 pt + p16 (4 VGPRs per tile) — so head h's four
+// dimensions are lane group h, register e.
+//  * projections Y = X W^T + b as Y^T = W X^T on v_mfma_f32_16x16x4_f32: the weights are the A
+//    operand (lane l: W[l % 16][4 (l / 16) + s] for K-step s, one float4), the activation tile the B
+//    operand as it stands (K-step s contracts features {4 g + s}), the bias the initial accumulator;
+//    the result is again in L0.  16 MFMAs per projection over 64 positions.
+//  * scores S^T_h = K_h Q_h^T on v_mfma_f32_4x4x1f32, 16 blocks = 4 heads x 4 query quads: the B
+//    operand is Q's register e (lane (4 qg + j, h)), the A operand K's register e broadcast from block
+//    ABID = kg of each 4-block group (CBSZ 2: lanes 16 h + 4 kg + i = keys 4 kg + i of head h), so 16
+//    instructions give lane (q, h) the 16 scores of its query and head over a key tile: softmax runs
+//    in-lane (online over key tiles, exp2), no cross-lane reduction.
+//  * P V on the same instruction: B = the probabilities as they stand (register (kg, i) = key
+//    4 kg + i), A = V transposed within each lane quad (DPP quad_perm) and broadcast with ABID = kg;
+//    the context lands in L0, ready for W_o.
+//  * key tiles past the sample's length are skipped (their keys are masked: exactly zero weight);
+//    LayerNorm reduces over the 4 lane groups by two lane shuffles.
+// Parameters of every block (the six 16 x 16 weights, biases, LayerNorm affines, position rows) are
+// staged once per workgroup in LDS: kBmBlockFloats per block.
+constexpr int kBmW = 0, kBmB = 6 * 256, kBmLN = kBmB + 6 * 16, kBmSc = kBmLN + 4 * 16, kBmPos = kBmSc + 4;
+constexpr int kBmBlockFloats = kBmPos + kST * kSD;  // 2724: ..., eps1 eps2 slope pad, pos
+
+__device__ __forceinline__ f32x4_t bm_proj(const float* W, const float* bias, f32x4_t x, int lane) {
+  const f32x4_t w = *reinterpret_cast<const f32x4_t*>(W + (lane & 15) * kSD + 4 * (lane >> 4));
+  f32x4_t acc = *reinterpret_cast<const f32x4_t*>(bias + 4 * (lane >> 4));
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = mfma16(w[s], x[s], acc);
+  return acc;
+}
+
+template <int ABID>
+__device__ __forceinline__ f32x4_t mfma4b(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 2, ABID, 0);
+}
+
+// out[i][e] = in[e][i] within each lane quad (i = lane & 3, e = register)
+__device__ __forceinline__ f32x4_t quad_transpose(f32x4_t m, int lane) {
+  const bool b0 = lane & 1, b1 = (lane >> 1) & 1;
+  float r0 = dpp_f32<0xB1>(b0 ? m[0] : m[1]);
+  float r1 = dpp_f32<0xB1>(b0 ? m[2] : m[3]);
+  f32x4_t m1;
+  m1[0] = b0 ? r0 : m[0];
+  m1[1] = b0 ? m[1] : r0;
+  m1[2] = b0 ? r1 : m[2];
+  m1[3] = b0 ? m[3] : r1;
+  r0 = dpp_f32<0x4E>(b1 ? m1[0] : m1[2]);
+  r1 = dpp_f32<0x4E>(b1 ? m1[1] : m1[3]);
+  f32x4_t m2;
+  m2[0] = b1 ? r0 : m1[0];
+  m2[1] = b1 ? r1 : m1[1];
+  m2[2] = b1 ? m1[2] : r0;
+  m2[3] = b1 ? m1[3] : r1;
+  return m2;
+}
+
+// LayerNorm of each position over its 16 features (4 in-lane x the 4 lane groups), biased variance
+__device__ __forceinline__ f32x4_t bm_layernorm(f32x4_t x, const float* g, const float* be, float eps, int lane) {
+  float s = (x[0] + x[1]) + (x[2] + x[3]);
+  s += __shfl_xor(s, 16, kWave);
+  s += __shfl_xor(s, 32, kWave);
+  const float m = s / (float)kSD;
+  f32x4_t d;
+  float v = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    d[r] = x[r] - m;
+    v = fmaf(d[r], d[r], v);
+  }
+  v += __shfl_xor(v, 16, kWave);
+  v += __shfl_xor(v, 32, kWave);
+  const float rs = 1.0f / sqrtf(v / (float)kSD + eps);
+  const f32x4_t gg = *reinterpret_cast<const f32x4_t*>(g + 4 * (lane >> 4));
+  const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(be + 4 * (lane >> 4));
+  f32x4_t y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) y[r] = d[r] * rs * gg[r] + bb[r];
+  return y;
+}
+
+// One sample (4 heads) by one wave: blocks + pooling.  prm: the LDS parameter image of all blocks.
+// Returns the pooled value of feature 4 (lane >> 4) + ((lane & 15) >> 2) in lanes with lane % 4 == 0.
+__device__ __forceinline__ float bst_mfma_sample(const BstSmallArgs& a, const float* prm, int64_t b, int lane) {
+  const int p16 = lane & 15, grp = lane >> 4;
+  const int T = a.T;
+  const int64_t len = a.seq_len[b];
+  const int lc = len <= 0 ? 0 : (len >= T ? T : (int)len);  // unmasked keys (bst.py:229)
+  const int NT = (T + 15) >> 4, NKT = (lc + 15) >> 4;
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float qscale = kLog2e / 2.0f;  // log2(e) / sqrt(d_h), d_h = 4
+  f32x4_t x[4];
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    x[pt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int p = 16 * pt + p16;
+    if (pt < NT && p < T) {
+      const int64_t r = a.seq[b * a.ld_seq + p];
+      if (r >= 0 && r < a.rows)
+        x[pt] = *reinterpret_cast<const f32x4_t*>(a.table + r * a.ld + 4 * grp);
+      else
+        flag_oob(a.flags);
+    }
+  }
+  for (int blk = 0; blk < a.nblocks; ++blk) {
+    const float* P = prm + blk * kBmBlockFloats;
+    const float* Wq = P + kBmW;
+    const float* Wk = Wq + 256;
+    const float* Wv = Wk + 256;
+    const float* Wo = Wv + 256;
+    const float* W1 = Wo + 256;
+    const float* W2 = W1 + 256;
+    const float* B = P + kBmB;
+    const float* LN = P + kBmLN;
+    // queries / keys get the position embedding, values do not (bst.py:69-71); formed where used
+    // (a tile's x is overwritten only after its last use in this block)
+    auto qin = [&](int pt) {
+      f32x4_t v = x[pt];
+      const int p = 16 * pt + p16;
+      if (p < T) v += *reinterpret_cast<const f32x4_t*>(P + kBmPos + p * kSD + 4 * grp);
+      return v;
+    };
+    f32x4_t K[4], Vq[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      if (kt < NKT) {
+        K[kt] = bm_proj(Wk, B + 16, qin(kt), lane);
+        Vq[kt] = quad_transpose(bm_proj(Wv, B + 32, x[kt], lane), lane);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      if (qt >= NT) break;
+      // the parameter loads stay inside the tile (hoisted, the 4 projections' weights, biases and
+      // LayerNorm affines would hold 48 VGPRs across the tile loop and spill)
+      asm volatile("" ::: "memory");
+      const f32x4_t q = bm_proj(Wq, B, qin(qt), lane);
+      float m_run = -INFINITY, l_run = 0.f;
+      f32x4_t o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        if (kt >= NKT) break;
+        f32x4_t sc[4];
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg) sc[kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sc[0] = mfma4b<0>(K[kt][e], q[e], sc[0]);
+          sc[1] = mfma4b<1>(K[kt][e], q[e], sc[1]);
+          sc[2] = mfma4b<2>(K[kt][e], q[e], sc[2]);
+          sc[3] = mfma4b<3>(K[kt][e], q[e], sc[3]);
+        }
+        // lane (q, h) register (kg, i): key 16 kt + 4 kg + i; masked keys -inf (bst.py:80)
+        float mt = -INFINITY;
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = 16 * kt + 4 * kg + i;
+            sc[kg][i] = key < lc ? sc[kg][i] * qscale : -INFINITY;
+            mt = fmaxf(mt, sc[kg][i]);
+          }
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        float ls = 0.f;
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            sc[kg][i] = __builtin_amdgcn_exp2f(sc[kg][i] - m_new);
+            ls += sc[kg][i];
+          }
+        l_run = fmaf(l_run, alpha, ls);
+        m_run = m_new;
+        o *= alpha;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o = mfma4b<0>(Vq[kt][i], sc[0][i], o);
+          o = mfma4b<1>(Vq[kt][i], sc[1][i], o);
+          o = mfma4b<2>(Vq[kt][i], sc[2][i], o);
+          o = mfma4b<3>(Vq[kt][i], sc[3][i], o);
+        }
+      }
+      // context (an all-masked row gives 0 * inf = NaN, as torch's softmax over -inf)
+      o *= 1.0f / l_run;
+      // out1 = norm1(queries + W_o ctx); out = norm2(out1 + W2 LeakyReLU(W1 out1)) (bst.py:85-90)
+      f32x4_t o1 = bm_proj(Wo, B + 48, o, lane) + qin(qt);
+      o1 = bm_layernorm(o1, LN, LN + 16, P[kBmSc], lane);
+      f32x4_t f = bm_proj(W1, B + 64, o1, lane);
+      const float slope = P[kBmSc + 2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f[r] = f[r] >= 0.f ? f[r] : f[r] * slope;
+      f = bm_proj(W2, B + 80, f, lane) + o1;
+      x[qt] = bm_layernorm(f, LN + 32, LN + 48, P[kBmSc + 1], lane);
+    }
+  }
+  // pooling over the T positions (bst.py:236-241: the padded positions' outputs included)
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const bool on = pt < NT && 16 * pt + p16 < T;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += on ? x[pt][r] : 0.f;
+  }
+  const float pooled = row16_transpose_sum<4>(v, p16);
+  return a.pool_mean ? pooled / (float)len : pooled;
+}
+
+// stage every block's parameters into the LDS image (all threads of the workgroup); static
+// indexing of the argument block (a runtime-indexed kernel-argument array is copied out whole)
+__device__ __forceinline__ void bst_mfma_stage(const BstSmallArgs& a, float* prm, int tid, int nthreads) {
+  // image order: wq wk wv wo w1 w2 | bq bk bv bo b1 b2 | g1 be1 g2 be2 | pos[T][16]
+  constexpr int kSrc[16] = {1, 3, 5, 7, 9, 11, 2, 4, 6, 8, 10, 12, 13, 14, 15, 16};
+  const int npos = a.T * kSD;
+#pragma unroll
+  for (int blk = 0; blk < kSMaxBlocks; ++blk) {
+    if (blk < a.nblocks) {
+      float* dst = prm + blk * kBmBlockFloats;
+      static_for<0, 16>([&](auto KI) {
+        constexpr int k = KI;
+        constexpr int n = k < 6 ? 256 : 16;
+        constexpr int off = k < 6 ? 256 * k : kBmB + 16 * (k - 6);
+        const float* src = a.blk[blk].p[kSrc[k]];
+        for (int i = tid; i < n; i += nthreads) dst[off + i] = src[i];
+      });
+      const float* pos = a.blk[blk].p[0];
+      for (int i = tid; i < npos; i += nthreads) dst[kBmPos + i] = pos[i];
+      if (tid == 0) {
+        dst[kBmSc] = a.blk[blk].eps1;
+        dst[kBmSc + 1] = a.blk[blk].eps2;
+        dst[kBmSc + 2] = a.blk[blk].slope;
+      }
+    }
+  }
+}
+
+// rk_bst_forward_blocks at d 16, 4 heads: the blocks + pooling only (bench roofline launch), 4 waves
+// per workgroup, persistent over the samples
+__global__ __launch_bounds__(kSWaves * 64, 4) void bst_mfma_kernel(BstSmallArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bst_mfma_stage(a, sm, tid, kSWaves * 64);
+  __syncthreads();
+  for (int64_t b = (int64_t)blockIdx.x * kSWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kSWaves) {
+    const float v = bst_mfma_sample(a, sm, b, lane);
+    if ((lane & 3) == 0) a.pool_out[b * a.ld_pool + 4 * (lane >> 4) + ((lane & 15) >> 2)] = v;
+  }
+}
+
 template <int NH>
 __global__ __launch_bounds__(kSWaves * 64, 4) void bst_small_kernel(BstSmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -266,6 +517,7 @@ struct BstFwdArgs {
   rk_mlp_layer L[RK_MLP_MAX_LAYERS];
   rk_epilogue head;
   int ld0, ld1, off1;  // LDS (floats): buf0 [16][ld0]; at off1 buf1 [16][ld1] / the K, V slices
+  int off_p;           // 4 heads on MFMA: the blocks' parameter image (kBmBlockFloats per block)
 };
 static_assert(sizeof(BstFwdArgs) <= 4096, "kernel arguments beyond 4 KiB");
 
@@ -304,6 +556,55 @@ __global__ __launch_bounds__(kMlpThreads) void bst_small_fwd_kernel(BstFwdArgs a
   const float pooled = live ? bst_small_sample<NH>(a.s, b, kv, kv + kST * kSD, lane) : 0.f;
   if (lane < kSD) row[a.width + lane] = pooled;
   mlp_stream_rows<StreamPlanK128, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
+}
+
+// The same forward with 4 heads on the matrix cores (bst_mfma_sample): no K / V slices in LDS; the
+// blocks' parameter image after buf1.
+__global__ __launch_bounds__(kMlpThreads) void bst_mfma_fwd_kernel(BstFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.s.batch - m0);
+  const int64_t b = m0 + wave;
+  const bool live = wave < rows;
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.off1;
+  float* const prm = sm + a.off_p;
+  float* const row = buf0 + wave * a.ld0;
+  bst_mfma_stage(a.s, prm, tid, kMlpThreads);
+#pragma unroll
+  for (int i = 0; i < kBfCols / 64; ++i) {
+    const int c = lane + 64 * i;
+    float v = 0.f;
+    const int sg = live && c < a.width ? a.col_seg[c] : 255;
+    if (sg != 255) {
+      const rk_segment& g = a.segs[sg];
+      int64_t r = b;
+      if (g.idx) {
+        r = g.idx[b * g.idx_stride];
+        if (r < 0 || r >= g.rows) {
+          flag_oob(a.s.flags);
+          r = -1;
+        }
+      }
+      if (r >= 0) v = g.src[r * g.src_ld + a.col_off[c]];
+    }
+    row[c] = v;
+  }
+  __syncthreads();  // the parameter image
+  if (live) {
+    const float pooled = bst_mfma_sample(a.s, prm, b, lane);
+    if ((lane & 3) == 0) row[a.width + 4 * (lane >> 4) + ((lane & 15) >> 2)] = pooled;
+  } else if (lane < kSD) {
+    row[a.width + lane] = 0.f;
+  }
+  mlp_stream_rows<StreamPlanK128, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
+}
+
+static bool bst_use_mfma(int heads) {
+  if (heads != 4) return false;
+  const char* e = getenv("RANKOPS_BST_MFMA");  // 0: the VALU kernels (A/B timing)
+  return !(e && e[0] == '0');
 }
 
 RK_API int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_t width, const float* table,
@@ -370,8 +671,15 @@ RK_API int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_
   a.ld0 = need0 + kMlpLdPad;
   a.ld1 = need1 + kMlpLdPad;
   a.off1 = kMlpRows * a.ld0;
-  const size_t region = std::max<size_t>((size_t)kMlpWaves * 2 * kST * kSD, (size_t)kMlpRows * a.ld1);
-  const size_t shm = ((size_t)a.off1 + region) * sizeof(float);
+  const bool mfma = bst_use_mfma(heads);
+  size_t shm;
+  if (mfma) {
+    a.off_p = (a.off1 + kMlpRows * a.ld1 + 3) / 4 * 4;
+    shm = ((size_t)a.off_p + (size_t)nblocks * kBmBlockFloats) * sizeof(float);
+  } else {
+    const size_t region = std::max<size_t>((size_t)kMlpWaves * 2 * kST * kSD, (size_t)kMlpRows * a.ld1);
+    shm = ((size_t)a.off1 + region) * sizeof(float);
+  }
   if (shm > 160 * 1024 - kStreamStaticLds)
     return fail(RK_ERR_UNSUPPORTED, "rk_bst_small_forward: %zu B of LDS needed", shm);
   if (batch == 0) return RK_OK;
@@ -381,6 +689,10 @@ RK_API int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   };
+  if (mfma) {
+    go(bst_mfma_fwd_kernel);
+    return check_launch("rk_bst_small_forward");
+  }
   switch (heads) {
     case 1: go(bst_small_fwd_kernel<1>); break;
     case 2: go(bst_small_fwd_kernel<2>); break;
@@ -428,6 +740,14 @@ int bst_small_forward(const float* table, int64_t table_rows, int64_t ld_table, 
   a.pool_mean = pool_mean;
   a.flags = device_flags();
   if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_bst_forward_blocks: negative batch");
+  if (bst_use_mfma(heads)) {
+    const size_t pshm = (size_t)nblocks * kBmBlockFloats * sizeof(float);
+    const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024) / pshm)));
+    const int64_t need = (batch + kSWaves - 1) / kSWaves;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)num_cus() * per_cu));
+    bst_mfma_kernel<<<grid, kSWaves * 64, pshm, st>>>(a);
+    return check_launch("rk_bst_forward_blocks (d_model 16, MFMA)");
+  }
   const size_t shm = (size_t)(kSWaves * 2 * kST * kSD) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / shm)));
   const int64_t need = (batch + kSWaves - 1) / kSWaves;

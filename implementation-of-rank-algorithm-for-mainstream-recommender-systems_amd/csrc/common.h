@@ -92,6 +92,35 @@ __device__ __forceinline__ float row16_max(float v) {
   return v;
 }
 
+// Sums of N values over the 16 lanes of each DPP row, transposed: each step pairs lanes across one
+// lane bit (row_mirror: bit 3, row_half_mirror: bit 2, quad_perm [2,3,0,1]: bit 1, [1,0,3,2]: bit 0)
+// and, while a lane still holds more than one value, keeps one half (the upper half where its bit is
+// set) and adds the partner's copy of it — N - 1 + log2(16 / N) DPP moves instead of 4 N.  Lane p16
+// returns the row sum of element e = (N/2) bit3 + (N/4) bit2 + (N/8) bit1, i.e. e = p16 / (16 / N);
+// v is clobbered.  Deterministic (fixed pairing), not bit-equal to N row16_sum calls.
+template <int CTRL, int BIT, int N>
+__device__ __forceinline__ void row16_split_step(float* v, int p16) {
+  const bool hi = (p16 >> BIT) & 1;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const float keep = hi ? v[i + N / 2] : v[i];
+    const float send = hi ? v[i] : v[i + N / 2];
+    v[i] = keep + dpp_f32<CTRL>(send);
+  }
+}
+template <int N>
+__device__ __forceinline__ float row16_transpose_sum(float (&v)[N], int p16) {
+  static_assert(N == 1 || N == 2 || N == 4 || N == 8, "1, 2, 4 or 8 values");
+  if constexpr (N >= 2) row16_split_step<0x140, 3, N>(v, p16);
+  else v[0] += dpp_f32<0x140>(v[0]);
+  if constexpr (N >= 4) row16_split_step<0x141, 2, N / 2>(v, p16);
+  else v[0] += dpp_f32<0x141>(v[0]);
+  if constexpr (N >= 8) row16_split_step<0x4E, 1, N / 4>(v, p16);
+  else v[0] += dpp_f32<0x4E>(v[0]);
+  v[0] += dpp_f32<0xB1>(v[0]);
+  return v[0];
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

@@ -142,21 +142,26 @@ struct DcnArgs {
   uint32_t* flags;
 };
 
-// NJ = column groups of 64 per lane (1: width <= 64, the DCN wechat row of 50; 4: width <= 256)
-template <int NJ, class P>
+// NJ = column groups of 64 per lane (1: width <= 64, the DCN wechat row of 50; 4: width <= 256).
+// RT = 2 (streamed plan, large batches): 32 rows per workgroup — wave w stages rows m0 + w and
+// m0 + 16 + w, each weight-ring slot feeds both 16-row tiles (mlp_stream.h RT), and the side waves
+// 8..15 take four cross rows each.  Per-row arithmetic unchanged: bit-identical to RT = 1.
+template <int NJ, class P, int RT = 1>
 __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
+  static_assert(RT == 1 || (NJ == 1 && !std::is_void_v<P>), "32-row workgroups: streamed plan, width <= 64");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
 #ifdef RK_MLP_PHASES
   const unsigned long long k_t0 = clock64();
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 2);
 #endif
-  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
-  const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
+  constexpr int kRows = kMlpRows * RT;
+  const int64_t m0 = (int64_t)blockIdx.x * kRows;
+  const int rows = (int)min<int64_t>(kRows, a.m.M - m0);
   float* const buf0 = sm;
   float* const buf1 = sm + a.m.off1;
-  float* const part = buf1 + kMlpRows * a.m.ld1;
-  float* const x0s = part + kMlpRows;  // streamed path: the staged rows [16][64], for the side work
+  float* const part = buf1 + kRows * a.m.ld1;
+  float* const x0s = part + kRows;  // streamed path: the staged rows [16 RT][64], for the side work
   const int width = a.m.K0;
   // Two memory round trips per row instead of one dependent index -> row chain per column: (1) the
   // sample's row index in every segment (wave-uniform loads), (2) the row values of the lane's
@@ -164,49 +169,49 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   // Out-of-range indices read row 0 with the value forced to zero and raise RK_FLAG_INDEX_OOB.
   // stage state carried from issue() (before layer 0's weight prefetch) to the finish
   const int nl = a.num_layers;
-  float x0[NJ], xl[NJ], cw[kDcnPreLayers][NJ], cb[kDcnPreLayers][NJ], hw[NJ];
-  const int64_t b = m0 + wave;
-  const bool live = wave < rows;
-  const int64_t bb = live ? b : m0;
+  float x0[RT][NJ], xl[NJ], cw[kDcnPreLayers][NJ], cb[kDcnPreLayers][NJ], hw[NJ];
+  bool live[RT];
+  int64_t bb[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    live[t] = wave + kMlpRows * t < rows;
+    bb[t] = live[t] ? m0 + kMlpRows * t + wave : m0;
+  }
   // round trip 1: the sample's row in every segment — lane t loads segment t's index (one vector
   // load per wave; 8 scalar loads measured ~2.4 us at kernel start), then every lane reads them
   // back (wave-uniform).  The streamed tail issues it ahead of its weight ring (stage.early()).
-  int64_t mine = 0;
+  int64_t mine[RT];
   auto stage_index = [&]() {
     const int64_t* ip = a.segs[0].idx;
     int64_t st = a.segs[0].idx_stride;
 #pragma unroll
     for (int t = 1; t < kDcnSegs; ++t)
       if (lane == t) ip = a.segs[t].idx, st = a.segs[t].idx_stride;
-    mine = ip[bb * st];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) mine[t] = ip[bb[t] * st];
   };
   auto stage_issue = [&]() {
-    int64_t rix[kDcnSegs];
-    {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      int64_t rix[kDcnSegs];
 #pragma unroll
       for (int t = 0; t < kDcnSegs; ++t) {
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, t);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)mine >> 32), t);
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine[rt], t);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)mine[rt] >> 32), t);
         rix[t] = (int64_t)(((uint64_t)hi << 32) | lo);
       }
-    }
-    bool bad = false;
+      bool bad = false;
 #pragma unroll
-    for (int t = 0; t < kDcnSegs; ++t) {
-      if (a.segs[t].dense) rix[t] = bb;
-      const bool okt = rix[t] >= 0 && rix[t] < a.segs[t].rows;
-      bad = bad || !okt;
-      rix[t] = okt ? rix[t] : -1;  // -1: zero row (read row 0, value dropped)
-    }
-    if (bad && live && lane == 0) flag_oob(a.flags);
-    // round trip 2: the lane's row values, the cross weights / biases of the first layers and the
-    // cross half of output_layer
+      for (int t = 0; t < kDcnSegs; ++t) {
+        if (a.segs[t].dense) rix[t] = bb[rt];
+        const bool okt = rix[t] >= 0 && rix[t] < a.segs[t].rows;
+        bad = bad || !okt;
+        rix[t] = okt ? rix[t] : -1;  // -1: zero row (read row 0, value dropped)
+      }
+      if (bad && live[rt] && lane == 0) flag_oob(a.flags);
+      // round trip 2: the lane's row values
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      x0[j] = hw[j] = 0.f;
-#pragma unroll
-      for (int l = 0; l < kDcnPreLayers; ++l) cw[l][j] = cb[l][j] = 0.f;
-      {
+      for (int j = 0; j < NJ; ++j) {
         const int c = lane + 64 * j;
         const int cc = min(c, width - 1);
         const float* src = a.segs[0].src;
@@ -221,30 +226,38 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
           col = sel ? cc - a.segs[t].out_col : col;
         }
         const float v = src[(r < 0 ? 0 : r) * ld + col];
-        x0[j] = (live && c < width && r >= 0) ? v : 0.f;
-        // unconditional loads (a clamped layer; with no cross layer, any valid vector): loads under
-        // `if (l < nl)` were placed after layer 0's weight ring, and waiting for them drained it
-        const float* cwp = nl > 0 ? a.cross_w : a.cross_head_w;
-        const float* cbp = nl > 0 ? a.cross_b : a.cross_head_w;
-#pragma unroll
-        for (int l = 0; l < kDcnPreLayers; ++l) {
-          const int64_t o = (int64_t)min(l, max(nl - 1, 0)) * width + cc;
-          cw[l][j] = cwp[o];
-          cb[l][j] = cbp[o];
-        }
-        hw[j] = a.cross_head_w[cc];
+        x0[rt][j] = (live[rt] && c < width && r >= 0) ? v : 0.f;
       }
+    }
+    // ... with the cross weights / biases of the first layers and the cross half of output_layer
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cc = min(lane + 64 * j, width - 1);
+      // unconditional loads (a clamped layer; with no cross layer, any valid vector): loads under
+      // `if (l < nl)` were placed after layer 0's weight ring, and waiting for them drained it
+      const float* cwp = nl > 0 ? a.cross_w : a.cross_head_w;
+      const float* cbp = nl > 0 ? a.cross_b : a.cross_head_w;
+#pragma unroll
+      for (int l = 0; l < kDcnPreLayers; ++l) {
+        const int64_t o = (int64_t)min(l, max(nl - 1, 0)) * width + cc;
+        cw[l][j] = cwp[o];
+        cb[l][j] = cbp[o];
+      }
+      hw[j] = a.cross_head_w[cc];
     }
   };
   auto stage_store = [&]() {
     const int K0p = pad64(width);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      xl[j] = x0[j];
-      if (c < K0p) buf0[wave * a.m.ld0 + c] = x0[j];
+    for (int t = 0; t < RT; ++t) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        if (t == 0) xl[j] = x0[0][j];
+        if (c < K0p) buf0[(kMlpRows * t + wave) * a.m.ld0 + c] = x0[t][j];
+      }
+      if constexpr (!std::is_void_v<P>) x0s[(kMlpRows * t + wave) * 64 + lane] = x0[t][0];
     }
-    if constexpr (!std::is_void_v<P>) x0s[wave * 64 + lane] = x0[0];
   };
   // the cross stack and the cross half of output_layer (generic path, after the stage; the
   // streamed path runs cross_row below as side work instead)
@@ -258,9 +271,9 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         if (lane + 64 * j < width) {
-          float t = x0[j] * d;   // torch.mul(x0, xl_wl)
-          t = t + bl[j];         // + bl.t()
-          xl[j] = t + xl[j];     // + xl
+          float t = x0[0][j] * d;  // torch.mul(x0, xl_wl)
+          t = t + bl[j];           // + bl.t()
+          xl[j] = t + xl[j];       // + xl
         }
     };
     // the first kDcnPreLayers layers straight-line from registers (a runtime loop with loads in it
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   };
   // streamed path (NJ = 1): the cross stack of staged row s, by any wave (the same arithmetic as
   // stage_cross); the side work of the third layer, whose 8 column tiles leave waves 8..15 idle:
-  // wave w takes rows w - 8 and w, off the second layer's critical path
+  // wave w takes rows w - 8 and w (and, at RT = 2, those plus 16), off the second layer's critical path
   auto cross_row = [&](int r) {
     const float x0v = x0s[r * 64 + lane];
     float xlv = x0v;
@@ -316,8 +329,11 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
   };
   auto side_cross = [&]() {
     if (wave >= kMlpWaves / 2) {
-      cross_row(wave - kMlpWaves / 2);
-      cross_row(wave);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        cross_row(kMlpRows * t + wave - kMlpWaves / 2);
+        cross_row(kMlpRows * t + wave);
+      }
     }
   };
   if constexpr (std::is_void_v<P>)
@@ -333,8 +349,9 @@ __global__ __launch_bounds__(kMlpThreads) void dcn_fused_kernel(DcnArgs a) {
                  }),
              part);
   else
-    mlp_stream_rows<P, RK_STREAM_EPI>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head, tid,
-                                      side_at<2>(staged(stage_index, stage_issue, stage_store, side_cross)), part);
+    mlp_stream_rows<P, RK_STREAM_EPI, RT>(a.m.L, buf0, a.m.ld0, buf1, a.m.ld1, sm + a.m.off_epi, m0, rows, a.m.head,
+                                          tid, side_at<2>(staged(stage_index, stage_issue, stage_store, side_cross)),
+                                          part);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);  // whole workgroup (incl. stage and head)
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);
   MLP_FLUSH(tid);
@@ -618,7 +635,6 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   a.m.nl = nlayers;
   a.m.ld0 = need0 + kMlpLdPad;
   a.m.ld1 = need1 + kMlpLdPad;
-  a.m.off1 = kMlpRows * a.m.ld0;
   a.m.M = batch;
   a.m.K0 = width;
   a.nseg = nseg;
@@ -629,16 +645,23 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
   a.num_layers = num_layers;
   a.cross_head_w = cross_head_w;
   a.flags = flags;
-  size_t shm = (size_t)kMlpRows * (a.m.ld0 + a.m.ld1) * sizeof(float) + kMlpRows * sizeof(float);
-  const size_t x0_bytes = (size_t)kMlpRows * 64 * sizeof(float);  // streamed path: x0s
-  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
   if (batch == 0) return RK_OK;
-  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
-  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
   // the wechat row (width <= 64) on a compiled layer plan: the streamed tail, its epilogue image
   // after the cross partials
   int plan = width <= 64 ? stream_plan_for(layers, nlayers, width) : kStreamNone;
   if (plan != kStreamNone && plan != kStreamK64) plan = kStreamNone;
+  // 32-row workgroups (streamed plan) once the batch gives every CU one (RANKOPS_DCN_ROW_TILES =
+  // 1 / 2 forces either)
+  int rt = plan == kStreamK64 && (batch + 2 * kMlpRows - 1) / (2 * kMlpRows) >= num_cus() ? 2 : 1;
+  if (const char* e = getenv("RANKOPS_DCN_ROW_TILES"))
+    rt = plan == kStreamK64 && atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : rt;
+  const int rows_wg = kMlpRows * rt;
+  a.m.off1 = rows_wg * a.m.ld0;
+  size_t shm = (size_t)rows_wg * (a.m.ld0 + a.m.ld1) * sizeof(float) + rows_wg * sizeof(float);
+  const size_t x0_bytes = (size_t)rows_wg * 64 * sizeof(float);  // streamed path: x0s
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: widths need %zu B of LDS", shm);
+  const int64_t blocks = (batch + rows_wg - 1) / rows_wg;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_dcn_forward: batch too large");
   if (plan != kStreamNone) {
     a.m.off_epi = (int)((shm + x0_bytes) / sizeof(float));
     if (shm + x0_bytes + sizeof(float) * stream_plan_epi_floats(plan) <= 160 * 1024 - kStreamStaticLds)
@@ -650,7 +673,9 @@ RK_API int rk_dcn_forward(const rk_segment* segs, int32_t nseg, int64_t batch, i
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   };
-  if (plan == kStreamK64)
+  if (plan == kStreamK64 && rt == 2)
+    go(dcn_fused_kernel<1, StreamPlanK64, 2>);
+  else if (plan == kStreamK64)
     go(dcn_fused_kernel<1, StreamPlanK64>);
   else
     width <= 64 ? go(dcn_fused_kernel<1, void>) : go(dcn_fused_kernel<kDcnPerLane, void>);

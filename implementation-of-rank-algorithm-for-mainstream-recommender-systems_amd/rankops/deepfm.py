@@ -87,11 +87,12 @@ class DeepFM(EngineModule):
             pk = self._fm_packs[name] = PackedFMTable()
         return pk(self.second_order_embeddings[name].weight, self.first_order_embeddings[name].weight)
 
-    def _gather_plan(self, names, category, deep=True):
+    def _gather_plan(self, names, category, deep=True, packed=None):
         D = self.embedding_dim
         first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
         B, dev = first.shape[0], first.device
-        packed = PACKED_TABLES and D % 4 == 0 and (D // 4) & (D // 4 - 1) == 0 and D <= 256
+        fits = D % 4 == 0 and (D // 4) & (D // 4 - 1) == 0 and D <= 256
+        packed = (PACKED_TABLES if packed is None else packed) and fits
         second_segs, first_segs = [], []
         for f, name in enumerate(names):
             idx = ops.as_index(category[name], f"category[{name!r}]")
@@ -123,11 +124,12 @@ class DeepFM(EngineModule):
         self._launch(plan)
         return plan[5], plan[6], plan[7]
 
-    def gather_launcher(self, category):
+    def gather_launcher(self, category, packed=None):
         """Zero-argument re-launch of this forward's FM gather kernel, for kernel-level timing
-        (bench.py gather roofline)."""
+        (bench.py gather roofline).  packed=False: the two nn.Embedding weights as they are — the
+        [V, D] second-order rows (128 B = one line at D = 32) and the [V, 1] first-order table."""
         names = [c for c in self.second_order_embeddings if c in category]
-        plan = self._gather_plan(names, category)
+        plan = self._gather_plan(names, category, packed=packed)
         return lambda: self._launch(plan)
 
     def _eager_eval(self, category):

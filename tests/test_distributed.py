@@ -200,3 +200,9 @@ def test_sharded_single_rank_equals_deepfm_on_gpu():
         b = sh(inp["category"])
     for x, y in zip(a, b):
         torch.testing.assert_close(x, y, atol=1e-5, rtol=1e-5)
+
+
+def test_front_ok_without_hidden_layers():
+    """with hidden_units=[] the fused front end is off (no IndexError on the empty tail)."""
+    sh = sharded.ShardedDeepFM({"a": 10, "b": 12}, 8, [], rank=0, world_size=1)
+    assert sh._front_ok(64) is False

@@ -99,3 +99,25 @@ def test_small_bst_one_launch_oob_category_index_is_flagged():
     with torch.no_grad():
         H.call_model(model, "bst", inp)
     assert rankops.error_flags(reset=True) & 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{"T": 50, "heads": 4, "vocab": H.WECHAT_VOCAB},
+                                 {"T": 64, "heads": 4, "max_len": 64, "pooling": "mean", "blocks": 2},
+                                 {"T": 7, "heads": 4, "max_len": 8}])
+def test_small_bst_mfma_equals_valu_kernel(monkeypatch, cfg):
+    """4 heads run on the matrix cores (bst_mfma_sample); RANKOPS_BST_MFMA=0 selects the VALU kernel:
+    the two agree within the fp32 tolerance on the whole forward and on the blocks-only launch."""
+    model = H.build("bst", cfg).cuda()
+    inp = H.to_device(H.make_inputs("bst", cfg, 1000, seed=13), "cuda")
+    inp["seq_length"][:4] = torch.tensor([1, cfg["T"], cfg["T"] + 3, 2], device="cuda")
+    with torch.no_grad():
+        mf = H.as_tuple(H.call_model(model, "bst", inp))
+        launch = model.blocks_kernel_launcher(inp["seq_feedid"], inp["seq_length"])
+        pm = launch()
+        pm = pm.clone() if isinstance(pm, torch.Tensor) else None
+        monkeypatch.setenv("RANKOPS_BST_MFMA", "0")
+        va = H.as_tuple(H.call_model(model, "bst", inp))
+    torch.cuda.synchronize()
+    for a, b in zip(mf, va):
+        torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL, equal_nan=True)

@@ -232,3 +232,27 @@ def test_deepfm_forward_32_row_tiles_bit_identical(M, oob, dense, monkeypatch):
         assert torch.equal(a, b) and torch.equal(a, c)
     for i, (o, r) in enumerate(zip(got["2"], _reference(tables, idx, ws, head))):
         torch.testing.assert_close(o, r.float(), atol=ATOL, rtol=RTOL, msg=lambda m: f"output {i}: {m}")
+
+
+@pytest.mark.gpu
+def test_prepared_run_survives_cache_rebuilds():
+    """DeepFM.prepare()'s run() binds raw pointers to the packed FM tables and the folded
+    BatchNorm affines.  A later .eval() (generation bump) plus a normal forward rebuilds both caches;
+    run() must still read live images and reproduce its first outputs bit for bit."""
+    cfg = {"dim": 32, "fields": FIELDS30}
+    model = H.build("deepfm", cfg)
+    H.randomize_eval_stats(model, 9)
+    model = model.cuda().eval()
+    d = H.to_device(H.make_inputs("deepfm", cfg, 700, seed=3), "cuda")
+    run = model.prepare(d["category"])
+    with torch.no_grad():
+        first = tuple(o.clone() for o in run())
+    model.eval()  # bumps the generation: the next forward repacks tables and refolds BatchNorm
+    with torch.no_grad():
+        model(d["category"])
+        scratch = [torch.randn(1 << 20, device="cuda") for _ in range(64)]  # reuse freed blocks
+        again = run()
+    torch.cuda.synchronize()
+    for a, b in zip(first, again):
+        assert torch.equal(a, b)
+    del scratch

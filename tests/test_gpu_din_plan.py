@@ -214,7 +214,8 @@ def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch, b
         monkeypatch.setenv("RANKOPS_DIN_EPI_DMA", "1")
         run = model.prepare(*args)
         assert run.plan._epi is not None  # the image is bound
-        dma = [t.clone() for t in H.as_tuple(run())[:2]]
+        dma_all = [t.clone() for t in H.as_tuple(run())]
+        dma = dma_all[:2]
         monkeypatch.setenv("RANKOPS_DIN_EPI_DMA", "0")
         run0 = model.prepare(*args)
         assert run0.plan._epi is None
@@ -232,7 +233,10 @@ def test_plan_epilogue_image_by_lds_dma_bit_identical(monkeypatch, dim, batch, b
     torch.manual_seed(5)
     with torch.no_grad():
         ref = H.as_tuple(H.call_oracle("din", cfg, p, inp))
-    torch.testing.assert_close(dma[0].cpu(), ref[0], atol=ATOL, rtol=RTOL)
+    # prob, logit and the l2 term of the prepared LDS-DMA launch against the oracle
+    assert len(dma_all) == len(ref) == 3
+    for i, (g, r) in enumerate(zip(dma_all, ref)):
+        torch.testing.assert_close(g.cpu().reshape(r.shape), r, atol=ATOL, rtol=RTOL, msg=lambda m: f"output {i}: {m}")
 
 
 @pytest.mark.gpu

@@ -246,20 +246,40 @@ def test_shard_pack_and_gather_kernels(world):
             exp = tab[idx.clamp(max=tab.shape[0] - 1)] * ok[..., None]
             assert torch.equal(rows[:, :, j, :], exp[:, :, :RS])
     assert rankops.error_flags(reset=True) & 1
+    # ids outside [0, 2^31) go out as -1: never narrowed into a valid row
+    bad = dict(cat)
+    f0 = sh.fields[0]
+    bad[f0] = cat[f0].clone()
+    bad[f0][3] = 2 ** 32 + 5
+    bad[f0][4] = -2 ** 32 + 1
+    got = sh.pack_indices(bad).cpu()
+    pos = [q for q, f in enumerate([f for fr in sh.fields_of for f in fr]) if f == f0][0]
+    o = sh.owner[0]
+    start = sum(len(sh.fields_of[r]) for r in range(o))
+    j = sh.fields_of[o].index(f0)
+    Fr = len(sh.fields_of[o])
+    assert got[B * start + 3 * Fr + j] == -1 and got[B * start + 4 * Fr + j] == -1
+    assert pos >= 0
 
 
 def _pipe_run(shards, emu, batches, B_l, capture=False):
     """Each emulated rank drives ShardedDeepFM.pipeline over `batches` (per batch: the global
     category dict); returns per rank the list of per-batch outputs (CPU)."""
     world = len(shards)
+    mines = [[{f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in cat.items()} for cat in batches]
+             for r in range(world)]
+    pipes = []
+    if capture:  # capture is process-global: serially, here (no collective inside the graphs)
+        with torch.no_grad():
+            pipes = [shards[r].pipeline(B_l, capture=mines[r][:3]) for r in range(world)]
 
     def rank_fn(r):
         sh = shards[r]
-        mine = [{f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in cat.items()} for cat in batches]
+        mine = mines[r]
         outs = []
         with torch.no_grad():
             if capture:
-                pipe = sh.pipeline(B_l, capture=mine[:3])
+                pipe = pipes[r]
                 for i in range(len(batches)):
                     o = pipe.step()
                     if o is not None:

@@ -27,10 +27,17 @@ def main():
     import rankops
     rankops.load_library()
     batch = args.batch or (2048 if args.workload == "bst" else 4096)
-    gather = args.workload == "deepfm_gather"  # rk_fm_gather_packed alone (bench.py gather_roofline)
-    model, inp, fn, cfg, name = bench.workload("deepfm" if gather else args.workload, batch, 0)
+    # rk_fm_gather alone (bench.py gather_roofline): packed [V, 36] tables, or (_tables) the
+    # line-aligned [V, 32] second-order rows with the first-order weights in their own [V, 1] table
+    gather = args.workload in ("deepfm_gather", "deepfm_gather_tables")
+    blocks = args.workload == "bst_ref_blocks"  # the d-16 blocks + pooling launch alone (bench roofline)
+    model, inp, fn, cfg, name = bench.workload("deepfm" if gather else "bst_ref" if blocks else args.workload,
+                                               batch, 0)
+    if blocks:
+        bl = model.blocks_kernel_launcher(inp["seq_feedid"], inp["seq_length"])
+        fn = lambda: [bl() for _ in range(20)]  # noqa: E731
     if gather:
-        launch = model.gather_launcher(inp["category"])
+        launch = model.gather_launcher(inp["category"], packed=args.workload == "deepfm_gather")
         fn = lambda: [launch() for _ in range(20)]  # noqa: E731
     torch.cuda.synchronize()
     if args.eager:
