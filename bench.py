@@ -363,10 +363,12 @@ def bench_sharded(world, rank, steps, warmup):
         step = model.pipeline(B_l, capture=cats).step
 
     t = max_over_ranks(world, time_replays(step, steps, max(warmup, 3), world))
-    wire = B_l * SHARDED_FIELDS * (model.index_dtype.itemsize + 4 * row_stride(32)) * (world - 1) / world
+    # bytes this rank sends per step (indices + rows), (P-1)/P of them to peers
+    wire = (B_l * SHARDED_FIELDS * model.index_dtype.itemsize + sum(model.row_splits(B_l)[0]) * 4) * (world - 1) / world
     return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
             "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),
+            "wire_format": "split" if model.split_wire() else "packed",
             "scaling": "strong",
             "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
                      "cross-batch pipeline (ShardedDeepFM.pipeline): per step pack + index all_to_all_single of "
@@ -413,8 +415,8 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         rng = np.random.default_rng(77 + P)
         recv_idx = torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, P * B_l * F_me)).to(
             dev, model.index_dtype)
-        recv_rows = torch.randn(B_c * SHARDED_FIELDS * RS, device=dev)
-        recv_full = torch.randn(B_l * SHARDED_FIELDS * RS, device=dev)
+        recv_rows = torch.randn(sum(model.row_splits(B_c)[0]), device=dev)
+        recv_full = torch.randn(sum(model.row_splits(B_l)[0]), device=dev)
         cat = {f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l)).to(dev) for f in fields}
         with torch.no_grad():
             g_pack, _ = graph_of(lambda: model.pack_indices(cat))
@@ -433,7 +435,7 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         # contention proxy: the forward with a copy of the bytes this rank's RCCL kernels move
         # (P2P writes: (P-1)/P of its send rows out to the peers; the peers' kernels push its
         # receive rows) on a second stream, which takes CUs from the forward as RCCL's would
-        xfer = int(B_l * SHARDED_FIELDS * RS * (P - 1) / P)
+        xfer = int(sum(model.row_splits(B_l)[1]) * (P - 1) / P)
         src, dst = torch.empty(xfer, device=dev), torch.empty(xfer, device=dev)
         side = torch.cuda.Stream()
 
@@ -445,11 +447,25 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
             torch.cuda.current_stream().wait_stream(side)
         t_fm1_copy = kernel_avg_ms(fwd_with_copy, iters)
         contention = max(0.0, t_fm1_copy - t_fm1)
+
+        # one steady-state step of the cross-batch pipeline on one GPU: the forward of batch i-2 on
+        # the compute stream while the side stream packs batch i, gathers batch i-1 and then moves
+        # that rank's row-exchange bytes (the stand-in for RCCL's copy kernels); the side work takes
+        # CUs as the forward's workgroups retire
+        def step_stand_in():
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                g_pack.replay()
+                g_gather1.replay()
+                dst.copy_(src)
+            g_fm1.replay()
+            torch.cuda.current_stream().wait_stream(side)
+        t_step = kernel_avg_ms(step_stand_in, iters)
         t_comp = t_pack + t_gather + t_fm
         # per link: this rank's bytes to one peer (F / P fields of its B_l samples, each way)
         f_peer = SHARDED_FIELDS / P
         idx_link = B_l * f_peer * model.index_dtype.itemsize
-        rows_link = B_l * f_peer * RS * 4
+        rows_link = sum(model.row_splits(B_l)[0]) * 4 / P  # one owner's block per peer link
         t_idx = 1e3 * (idx_link / XGMI_LINK_BPS + A2A_LATENCY_S)  # one index exchange per step
         t_rows = 1e3 * (rows_link / XGMI_LINK_BPS + C * A2A_LATENCY_S)
         serial = t_comp + t_idx + t_rows
@@ -458,9 +474,9 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         overlap = t_pack + t_idx + max(t_gather + t_fm, t_rows) + (t_gather + t_rows) / C
         # cross-batch pipeline: one row exchange per step (one call), hidden behind the forward
         wire1 = 1e3 * ((idx_link + rows_link) / XGMI_LINK_BPS + 2 * A2A_LATENCY_S)
-        local1 = t_seq + contention
+        local1 = t_step  # measured: forward || (pack, gather, exchange-bytes copy) on two streams
         piped = max(local1, wire1)
-        piped_free = max(t_seq, wire1)  # if RCCL's kernels found idle CUs (no slowdown of the forward)
+        piped_free = max(t_seq, wire1)  # serial local work, RCCL's kernels on idle CUs (no contention)
         curve[str(P)] = {
             "kind": "model, not a measurement",
             "B_local": B_l, "fields_rank0": F_me, "chunks": C,
@@ -470,9 +486,11 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
                                      "forward_one_launch": round(t_fm1, 4),
                                      "pack_gather_forward_one_graph": round(t_seq, 4),
                                      "forward_with_copy_beside": round(t_fm1_copy, 4),
-                                     "contention": round(contention, 4), "copy_bytes": 4 * xfer},
+                                     "contention": round(contention, 4), "copy_bytes": 4 * xfer,
+                                     "step_two_streams": round(t_step, 4)},
             "wire_ms": {"index": round(t_idx, 4), "rows": round(t_rows, 4), "pipelined_per_step": round(wire1, 4)},
             "bytes_per_link": {"index": int(idx_link), "rows": int(rows_link)},
+            "wire_format": "split" if model.split_wire() else "packed",
             "ms_per_step": {"serial": round(serial, 4), "overlapped": round(overlap, 4), "pipelined": round(piped, 4),
                             "pipelined_no_contention": round(piped_free, 4)},
             "samples_per_s": {"serial": round(SHARDED_GLOBAL_BATCH / (serial * 1e-3), 1),
@@ -483,14 +501,16 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
                               "pipelined_no_contention": round(p1_ms / piped_free, 2)},
             "pipelined_bound": "device" if local1 >= wire1 else "wire",
         }
-        del model, g_pack, g_gather, g_fm, g_gather1, g_fm1, g_seq, rows1, src, dst
+        del model, g_pack, g_gather, g_fm, g_gather1, g_fm1, g_seq, rows1, src, dst, step_stand_in, fwd_with_copy
         torch.cuda.empty_cache()
     return {"assumptions": f"up to {chunks} chunks of >= 4096 samples (serial / overlapped); pipelined: one gather "
                            f"and one forward launch per step, exchanges of the two younger batches under the "
                            f"oldest one's forward; {XGMI_LINK_BPS / 1e9:.0f} GB/s per xGMI link, one link per "
                            f"peer pair; {A2A_LATENCY_S * 1e6:.0f} us per all_to_all_single call (assumed); "
-                           "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter; RCCL's "
-                           "CU use stood in by a same-size local copy on a second stream",
+                           "rank 0 (the most fields) timed; kernels of the other ranks equal or shorter; pipelined "
+                           "= max(wire + 2 calls, one measured steady-state step: the forward on the compute "
+                           "stream while a second stream packs, gathers and copies the rank's row-exchange "
+                           "bytes, a stand-in for RCCL's copy kernels taking CUs)",
             "curve": curve}
 
 

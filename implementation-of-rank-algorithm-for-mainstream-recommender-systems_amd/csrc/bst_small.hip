@@ -311,7 +311,7 @@ __device__ __forceinline__ f32x4_t bm_layernorm(f32x4_t x, const float* g, const
   }
   v += __shfl_xor(v, 16, kWave);
   v += __shfl_xor(v, 32, kWave);
-  const float rs = 1.0f / sqrtf(v / (float)kSD + eps);
+  const float rs = __builtin_amdgcn_rsqf(v / (float)kSD + eps);  // v_rsq_f32 (1 ulp), not div + sqrt
   const f32x4_t gg = *reinterpret_cast<const f32x4_t*>(g + 4 * (lane >> 4));
   const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(be + 4 * (lane >> 4));
   f32x4_t y;
@@ -423,7 +423,7 @@ __device__ __forceinline__ float bst_mfma_sample(const BstSmallArgs& a, const fl
         }
       }
       // context (an all-masked row gives 0 * inf = NaN, as torch's softmax over -inf)
-      o *= 1.0f / l_run;
+      o *= __builtin_amdgcn_rcpf(l_run);  // v_rcp_f32 (1 ulp); rcp(0) = inf keeps the NaN
       // out1 = norm1(queries + W_o ctx); out = norm2(out1 + W2 LeakyReLU(W1 out1)) (bst.py:85-90)
       f32x4_t o1 = bm_proj(Wo, B + 48, o, lane) + qin(qt);
       o1 = bm_layernorm(o1, LN, LN + 16, P[kBmSc], lane);

@@ -42,6 +42,11 @@ struct DfArgs {
   int64_t istride[kDfMaxFields];
   int64_t ld[kDfMaxFields];
   int64_t rows[kDfMaxFields];
+  // first-order weight of field f for row index r: fo[f][r * fo_ld[f]] (packed tables: the row's
+  // float at column dim; split wire rows: the owner's per-sample partial sum on its first field,
+  // nullptr on the others)
+  const float* fo[kDfMaxFields];
+  int64_t fo_ld[kDfMaxFields];
   uint32_t dense_mask;
   int F, dim_shift;
   int64_t M;
@@ -98,7 +103,8 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
       const bool bad = lane < a.F && !ok;
       if (live[t] && __builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) flag_oob(a.flags);
       okmask[t] = __builtin_amdgcn_ballot_w64(ok && live[t] && lane < a.F);
-      const float* p = a.src[f_me] + (ok ? r : 0) * a.ld[f_me];
+      const int64_t rr = ok ? r : 0;
+      const float* p = a.src[f_me] + rr * a.ld[f_me];
       const uint64_t pu = reinterpret_cast<uint64_t>(p);
       const uint32_t plo = (uint32_t)pu, phi = (uint32_t)(pu >> 32);
 #pragma unroll
@@ -109,7 +115,8 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
         const float* row = reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
         v[t][i] = *reinterpret_cast<const f32x4_t*>(row + 4 * (q & (G - 1)));
       }
-      fw[t] = p[dim];
+      const float* fop = a.fo[f_me];
+      fw[t] = fop ? fop[rr * a.fo_ld[f_me]] : 0.f;
     }
   };
   // round 3: the row into buf0 (zeros for padding quads, out-of-range rows and rows past the batch)
@@ -191,9 +198,9 @@ RK_API int rk_debug_deepfm_phases(unsigned long long* marks, int32_t nwg, unsign
 }
 #endif
 
-RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
-                             const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, float* fm1,
-                             float* fm2, void* stream) {
+static int deepfm_forward_impl(const rk_segment* fields, const float* const* first, const int64_t* first_ld,
+                               int32_t num_fields, int32_t dim, int64_t batch, const rk_mlp_layer* layers,
+                               int32_t nlayers, const rk_epilogue* head, float* fm1, float* fm2, void* stream) {
   if (!fields || num_fields <= 0 || num_fields > kDfMaxFields)
     return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: %d fields (max %d)", num_fields, kDfMaxFields);
   if (dim < 4 || dim > 256 || (dim & (dim - 1)))
@@ -217,14 +224,24 @@ RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32
   if (!flags) return fail(RK_ERR_RUNTIME, "rk_deepfm_forward: device not initialised (rk_init)");
   for (int f = 0; f < num_fields; ++f) {
     const rk_segment& s = fields[f];
-    if (!s.src || (s.idx && (s.rows <= 0 || s.idx_stride != 1)) || s.dim != dim || s.src_ld < dim + 1 ||
-        s.src_ld % 4 || !aligned16(s.src) || s.out_col != f * dim)
+    if (!s.src || (s.idx && (s.rows <= 0 || s.idx_stride != 1)) || s.dim != dim ||
+        s.src_ld < (first ? dim : dim + 1) || s.src_ld % 4 || !aligned16(s.src) || s.out_col != f * dim)
       return fail(RK_ERR_INVALID,
                   "rk_deepfm_forward: field %d is not a packed [rows, >= dim+1] table (unit-stride indices, or "
-                  "none: a dense block of packed rows) at column f*dim",
+                  "none: a dense block of packed rows; with separate first-order sources, rows of >= dim) at "
+                  "column f*dim",
                   f);
     a.src[f] = s.src;
     a.ld[f] = s.src_ld;
+    if (first) {
+      if (first[f] && (!first_ld || first_ld[f] < 0))
+        return fail(RK_ERR_INVALID, "rk_deepfm_forward_fo: field %d first-order stride", f);
+      a.fo[f] = first[f];
+      a.fo_ld[f] = first[f] ? first_ld[f] : 0;
+    } else {
+      a.fo[f] = s.src + dim;  // packed layout: the weight follows the row's dim floats
+      a.fo_ld[f] = s.src_ld;
+    }
     if (s.idx) {
       a.idx[f] = s.idx;
       a.istride[f] = 1;
@@ -275,4 +292,18 @@ RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32
     deepfm_fused_kernel<StreamPlanK960, 1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   }
   return check_launch("rk_deepfm_forward");
+}
+
+RK_API int rk_deepfm_forward(const rk_segment* fields, int32_t num_fields, int32_t dim, int64_t batch,
+                             const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, float* fm1,
+                             float* fm2, void* stream) {
+  return deepfm_forward_impl(fields, nullptr, nullptr, num_fields, dim, batch, layers, nlayers, head, fm1, fm2,
+                             stream);
+}
+
+RK_API int rk_deepfm_forward_fo(const rk_segment* fields, const float* const* first, const int64_t* first_ld,
+                                int32_t num_fields, int32_t dim, int64_t batch, const rk_mlp_layer* layers,
+                                int32_t nlayers, const rk_epilogue* head, float* fm1, float* fm2, void* stream) {
+  if (!first) return fail(RK_ERR_INVALID, "rk_deepfm_forward_fo: null first-order source array");
+  return deepfm_forward_impl(fields, first, first_ld, num_fields, dim, batch, layers, nlayers, head, fm1, fm2, stream);
 }

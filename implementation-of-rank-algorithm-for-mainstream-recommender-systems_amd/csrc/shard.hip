@@ -98,9 +98,99 @@ __global__ __launch_bounds__(256) void shard_gather_rows_kernel(ShardGatherArgs 
   }
 }
 
+// The split wire format (round 5): the row exchange carries each field's D second-order floats as
+// they are in the nn.Embedding weight ([V, D]: one 128-B line at D = 32, no packed copy of the
+// table) and, per (source, sample), ONE first-order value: the sum of this owner's fields' weights
+// in field order.  Send block of source s: [b'][j][D] rows, then pad4(bc) partial sums.  One wave
+// per (source, sample): its F x D / 4 float4s, then the F first-order weights summed in field order.
+struct ShardSplitArgs {
+  const float* src2[kShardMaxFields];
+  const float* src1[kShardMaxFields];
+  int64_t ld2[kShardMaxFields], ld1[kShardMaxFields], rows[kShardMaxFields];
+  int F, G;            // this rank's fields; float4 quads per row (D / 4)
+  const int32_t* idx;  // [P][B_l][F] as received
+  int64_t B_l, b0, bc;
+  int P;
+  float* out;  // per source: [bc][F][D] then pad4(bc) partials
+  uint32_t* flags;
+};
+
+__global__ __launch_bounds__(256) void shard_gather_split_kernel(ShardSplitArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int D = 4 * a.G;
+  const int64_t blk = a.bc * a.F * D + ((a.bc + 3) & ~(int64_t)3);  // floats per source block
+  const int64_t nrows = (int64_t)a.P * a.bc;                         // (source, sample) rows
+  // one wave per (source, sample): lane t moves quad t % G of field t / G (t += 64 past one
+  // instruction), then lane j < F fetches field j's first-order weight
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nrows; r += (int64_t)gridDim.x * 4) {
+    const int64_t s = r / a.bc, bp = r - s * a.bc;
+    const int32_t* ip = a.idx + (s * a.B_l + a.b0 + bp) * a.F;
+    float* const base = a.out + s * blk;
+    const int per = a.F * a.G;
+    bool oob = false;
+    for (int t = lane; t < per; t += 64) {
+      const int j = t / a.G, q = t - j * a.G;
+      const int64_t row = ip[j];
+      const bool ok = row >= 0 && row < a.rows[j];
+      oob |= !ok;
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.src2[j] + (ok ? row : 0) * a.ld2[j] + 4 * q);
+      if (!ok) v = (f32x4){0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(base + (bp * a.F + j) * D + 4 * q) = v;
+    }
+    float w1 = 0.f;
+    if (lane < a.F) {
+      const int64_t row = ip[lane];
+      if (row >= 0 && row < a.rows[lane]) w1 = a.src1[lane][row * a.ld1[lane]];
+    }
+    // the partial sum over this owner's fields, in field order
+    float acc = 0.f;
+    for (int j = 0; j < a.F; ++j) acc += __shfl(w1, j, kWave);
+    if (lane == 0) base[a.bc * a.F * D + bp] = acc;
+    if (oob) flag_oob(a.flags);
+  }
+}
+
 }  // namespace rk
 
 using namespace rk;
+
+RK_API int rk_shard_gather_rows_split(const rk_segment* second, const rk_segment* first, int32_t num_fields,
+                                      int32_t dim, const int32_t* idx, int32_t num_sources, int64_t source_batch,
+                                      int64_t b0, int64_t bc, float* out, void* stream) {
+  if (!second || !first || num_fields <= 0 || num_fields > kShardMaxFields || dim < 4 || dim % 4 || !idx || !out ||
+      num_sources <= 0 || source_batch < 0 || b0 < 0 || bc < 0 || b0 + bc > source_batch || !aligned16(out))
+    return fail(RK_ERR_INVALID, "rk_shard_gather_rows_split: bad arguments (fields %d <= %d, dim %d %% 4 == 0)",
+                num_fields, kShardMaxFields, dim);
+  ShardSplitArgs a = {};
+  for (int j = 0; j < num_fields; ++j) {
+    const rk_segment& t2 = second[j];
+    const rk_segment& t1 = first[j];
+    if (!t2.src || t2.rows <= 0 || t2.src_ld < dim || t2.src_ld % 4 || !aligned16(t2.src) || !t1.src ||
+        t1.rows < t2.rows || t1.src_ld < 1)
+      return fail(RK_ERR_INVALID, "rk_shard_gather_rows_split: table %d ([rows, >= dim] 16-B aligned, first-order "
+                                  "[rows, 1])", j);
+    a.src2[j] = t2.src;
+    a.ld2[j] = t2.src_ld;
+    a.rows[j] = t2.rows;
+    a.src1[j] = t1.src;
+    a.ld1[j] = t1.src_ld;
+  }
+  a.F = num_fields;
+  a.G = dim / 4;
+  a.idx = idx;
+  a.B_l = source_batch;
+  a.b0 = b0;
+  a.bc = bc;
+  a.P = num_sources;
+  a.out = out;
+  a.flags = device_flags();
+  if (!a.flags) return fail(RK_ERR_RUNTIME, "rk_shard_gather_rows_split: device not initialised (rk_init)");
+  const int64_t nrows = (int64_t)num_sources * bc;
+  if (nrows == 0) return RK_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((nrows + 3) / 4, (int64_t)num_cus() * 32);
+  shard_gather_split_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(a);
+  return check_launch("rk_shard_gather_rows_split");
+}
 
 RK_API int rk_shard_pack_indices(const int64_t* const* idx, const int64_t* base, const int32_t* stride,
                                  int32_t num_fields, int64_t batch, int32_t* out, void* stream) {

@@ -303,6 +303,10 @@ SIGNATURES = {
                                            c_void_p, c_void_p]),
     "rk_deepfm_forward": (ctypes.c_int, [_SEG_P, c_int32, c_int32, c_int64, _MLP_P, c_int32, _EPI_P, c_void_p,
                                          c_void_p, c_void_p]),
+    "rk_deepfm_forward_fo": (ctypes.c_int, [_SEG_P, c_void_p, c_void_p, c_int32, c_int32, c_int64, _MLP_P, c_int32,
+                                            _EPI_P, c_void_p, c_void_p, c_void_p]),
+    "rk_shard_gather_rows_split": (ctypes.c_int, [_SEG_P, _SEG_P, c_int32, c_int32, c_void_p, c_int32, c_int64,
+                                                  c_int64, c_int64, c_void_p, c_void_p]),
     "rk_bn_fold": (
         ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int32, c_void_p, c_void_p, c_void_p]),
     # include/rankops_io.h (host input path)

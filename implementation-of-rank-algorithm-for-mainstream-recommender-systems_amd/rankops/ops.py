@@ -221,6 +221,20 @@ def deepfm_forward(fields, dim, batch, layers, ep, fm1, fm2):
                                 _lib.stream_of(fm1)), "rk_deepfm_forward")
 
 
+def deepfm_forward_fo(fields, first, first_ld, dim, batch, layers, ep, fm1, fm2):
+    """rk_deepfm_forward_fo: rk_deepfm_forward with the first-order weights from their own sources
+    (first[f]: a device address or None, first_ld[f] its row stride in floats)."""
+    lib = _lib.load()
+    _lib.ensure_device(fm1.device)
+    arr = _seg_array(fields)
+    n = len(fields)
+    fp = (ctypes.c_void_p * n)(*[x or None for x in first])
+    fl = (ctypes.c_int64 * n)(*first_ld)
+    la = (_lib.MlpLayer * len(layers))(*layers)
+    check(lib.rk_deepfm_forward_fo(arr, fp, fl, n, dim, batch, la, len(layers), ctypes.byref(ep), ptr(fm1), ptr(fm2),
+                                   _lib.stream_of(fm1)), "rk_deepfm_forward_fo")
+
+
 def din_attention(query_ptr, ld_query, key_table, seq, seq_len, T, H, weights, use_softmax, out_ptr, ld_out,
                   batch, device):
     lib = _lib.load()

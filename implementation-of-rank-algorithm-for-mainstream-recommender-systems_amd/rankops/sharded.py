@@ -26,7 +26,10 @@ issued asynchronously and overlaps the next chunk's gather and the previous chun
 At P = 1 there is nothing to exchange: the forward is rk_deepfm_forward over the packed tables,
 i.e. `DeepFM.forward` on the same weights.
 The exchange volume per rank and step is B_l * F * (4 + 4 * RS) bytes (int32 indices), (P-1)/P of
-it on the wire.  Rows travel at RS = 36 floats (144 B, 132 live): the receiver's fused front end
+it on the wire, with the packed rows; the split wire format (round 5, `wire`, the default where
+the one-launch forward applies) sends D floats per (sample, field) straight from the [V, D]
+nn.Embedding weight plus one first-order partial sum per (sample, owner): B_l * (F * (4 + 4 * D) +
+4 * P) bytes, and the owner reads one 128-B line per row instead of the packed row's two.  Rows travel at RS = 36 floats (144 B, 132 live): the receiver's fused front end
 reads them in place with 16-B loads, which a 132-B stride would misalign for three rows in four,
 and the row exchange overlaps the next chunk's gather.  Reference: DeepFM.forward, deepfm.py:121-151 (the reference is single-device; the
 sharding is the MI355X build's own).
@@ -84,6 +87,12 @@ class ShardedDeepFM(EngineModule):
         # ... and, where a plan is compiled for the shape (960 -> 512 -> 256 -> 128), the whole
         # forward in one rk_deepfm_forward launch (False: rk_fm_linear_packed + the tail)
         self.fused_whole = True
+        # row-exchange wire format (round 5): "split" = each field's D second-order floats read from
+        # the [V, D] nn.Embedding weight as they are (one 128-B line at D = 32) plus ONE first-order
+        # value per (sample, owner) — the sum of the owner's fields' weights — received by
+        # rk_deepfm_forward_fo; "packed" = the rk_fm_pack_table row, pad4(D + 1) floats per field.
+        # split applies where the one-launch forward does (split_wire()); otherwise packed.
+        self.wire = "split"
         self.first_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], 1)
                                                      for f in self.local_fields})
         self.second_order_embeddings = nn.ModuleDict({f: nn.Embedding(self.field_rows[f], embedding_dim)
@@ -142,6 +151,20 @@ class ShardedDeepFM(EngineModule):
         work = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=async_op)
         return (out, work) if async_op else out
 
+    def split_wire(self) -> bool:
+        """Whether the row exchange uses the split format (config only: the same on every rank)."""
+        D = self.embedding_dim
+        widths = [l.linear.out_features for l in self._tail]
+        return (self.wire == "split" and self.world > 1 and self.fused_front and self.fused_whole
+                and self.index_dtype == torch.int32 and len(self._tail) >= 2 and len(self.fields) <= 32
+                and 4 <= D <= 256 and D & (D - 1) == 0 and ops.deepfm_whole_plan(len(self.fields) * D, widths))
+
+    def _block(self, B: int, F_r: int) -> int:
+        """Floats of one owner's row block for B samples of F_r of its fields."""
+        if self.split_wire():
+            return B * F_r * self.embedding_dim + (B + 3) // 4 * 4
+        return B * F_r * row_stride(self.embedding_dim)
+
     def index_splits(self, B_l: int):
         """(output_split_sizes, input_split_sizes) of the index all-to-all, in int64 elements."""
         F_me = len(self.local_fields)
@@ -149,8 +172,8 @@ class ShardedDeepFM(EngineModule):
 
     def row_splits(self, B_l: int):
         """(output_split_sizes, input_split_sizes) of the row all-to-all, in floats."""
-        RS, F_me = row_stride(self.embedding_dim), len(self.local_fields)
-        return [B_l * len(self.fields_of[r]) * RS for r in range(self.world)], [B_l * F_me * RS] * self.world
+        F_me = len(self.local_fields)
+        return [self._block(B_l, len(self.fields_of[r])) for r in range(self.world)], [self._block(B_l, F_me)] * self.world
 
     def pack_indices(self, category: dict) -> torch.Tensor:
         """Send buffer of step 1: [r][b][f_r] index blocks in index_dtype (on the GPU with int32:
@@ -201,6 +224,25 @@ class ShardedDeepFM(EngineModule):
         packed tables at the received indices (recv_idx: [s][B_src][f_me] as exchanged).  int32:
         one rk_shard_gather_rows launch; int64: rk_concat_gather over the chunk's copy."""
         RS, F_me = row_stride(self.embedding_dim), len(self.local_fields)
+        if self.split_wire() and F_me > 0:
+            # [s]: [bc][F_me][D] second-order rows, then pad4(bc) first-order partial sums
+            out = torch.empty(self.world * self._block(bc, F_me), device=recv_idx.device, dtype=torch.float32)
+            if bc == 0:
+                return out
+            from ._lib import Segment
+            second = [Segment(self.second_order_embeddings[f].weight.data_ptr(), None, 0,
+                              self.second_order_embeddings[f].weight.stride(0), self.field_rows[f],
+                              self.embedding_dim, 0) for f in self.local_fields]
+            first = [Segment(self.first_order_embeddings[f].weight.data_ptr(), None, 0,
+                             self.first_order_embeddings[f].weight.stride(0), self.field_rows[f], 1, 0)
+                     for f in self.local_fields]
+            lib = ops._lib.load()
+            ops._lib.ensure_device(out.device)
+            ops.check(lib.rk_shard_gather_rows_split(ops._seg_array(second), ops._seg_array(first), F_me,
+                                                     self.embedding_dim, recv_idx.data_ptr(), self.world, B_src, b0,
+                                                     bc, out.data_ptr(), ops._lib.stream_of(out)),
+                      "rk_shard_gather_rows_split")
+            return out
         if recv_idx.dtype == torch.int32 and F_me > 0:
             out = torch.empty(self.world * bc, F_me * RS, device=recv_idx.device, dtype=torch.float32)
             if bc == 0:
@@ -278,6 +320,32 @@ class ShardedDeepFM(EngineModule):
         """Step 4: FM + deep tail on the received rows (field order restored by out_col)."""
         D, RS = self.embedding_dim, row_stride(self.embedding_dim)
         dev = recv_rows.device
+        if self.split_wire():
+            # owner r's block: [B_l][F_r][D] rows then pad4(B_l) first-order partials; the partials
+            # ride on the owner's first field (the others contribute no first-order term)
+            from ._lib import Segment
+            segs, first, first_ld = [], [], []
+            off, place = 0, {}
+            for r in range(self.world):
+                F_r = len(self.fields_of[r])
+                for j, f in enumerate(self.fields_of[r]):
+                    place[f] = (off + j * D, F_r * D, off + B_l * F_r * D if j == 0 else None)
+                off += self._block(B_l, F_r)
+            base = recv_rows.data_ptr()
+            for i, f in enumerate(self.fields):
+                o, ld, po = place[f]
+                segs.append(Segment(base + 4 * o, None, 0, ld, 0, D, i * D))
+                first.append(base + 4 * po if po is not None else None)
+                first_ld.append(1 if po is not None else 0)
+            mls = [ops.make_mlp_layer(l.linear.weight, common_packed(l.linear.weight), **l.epilogue_kwargs())
+                   for l in self._tail]
+            fm1, fm2, deep, total, prob = (torch.empty(B_l, 1, device=dev, dtype=torch.float32) for _ in range(5))
+            ep = ops.make_epilogue(head_w=self.deep_output_layer.weight, head_b=self.deep_output_layer.bias,
+                                   final_w=self.final_layer.weight, final_b=self.final_layer.bias, head_logit=total,
+                                   head_prob=prob, head_aux=deep)
+            if B_l > 0:
+                ops.deepfm_forward_fo(segs, first, first_ld, D, B_l, mls, ep, fm1, fm2)
+            return prob, total, fm1, fm2, deep
         second, first = [], []
         off = 0
         base = {}
@@ -445,6 +513,11 @@ class CapturedPipeline:
         if len(outs) == 1:
             return outs[0]
         return tuple(torch.cat([o[i] for o in outs], 0) for i in range(len(outs[0])))
+
+
+def common_packed(w):
+    from . import common
+    return common.PACKED(w)
 
 
 def _lib_dense(buf: torch.Tensor, offset: int, ld: int, dim: int, out_col: int):

@@ -441,6 +441,22 @@ int rk_shard_gather_rows(const rk_segment* tables, int32_t num_fields, int32_t r
                          int32_t num_sources, int64_t source_batch, int64_t b0, int64_t bc, float* out,
                          void* stream);
 
+/* The split wire format of the row exchange (round 5): out per source s = [bc][j][dim] second-order
+ * rows straight from second[j] (the [V, dim] nn.Embedding weight, src_ld >= dim, 16-B aligned), then
+ * pad4(bc) floats: per sample the sum over j = 0..num_fields-1 (in order) of the first-order weight
+ * first[j].src[row * first[j].src_ld].  dim % 4 == 0.  Out-of-range indices give zero
+ * rows / weights and raise RK_FLAG_INDEX_OOB. */
+int rk_shard_gather_rows_split(const rk_segment* second, const rk_segment* first, int32_t num_fields,
+                               int32_t dim, const int32_t* idx, int32_t num_sources, int64_t source_batch,
+                               int64_t b0, int64_t bc, float* out, void* stream);
+/* rk_deepfm_forward with the first-order weight of field f read from first[f][r * first_ld[f]]
+ * (r = the field's index, or the sample for a dense block) instead of the packed row's column dim;
+ * first[f] == NULL contributes 0 (ShardedDeepFM's split rows: the owner's partial sum on its first
+ * field).  Rows then need src_ld >= dim only. */
+int rk_deepfm_forward_fo(const rk_segment* fields, const float* const* first, const int64_t* first_ld,
+                         int32_t num_fields, int32_t dim, int64_t batch, const rk_mlp_layer* layers,
+                         int32_t nlayers, const rk_epilogue* head, float* fm1, float* fm2, void* stream);
+
 /* FwFM.forward (fwfm.py:114-139): per sample, logit = sum_f linear[f] row + sum_{i<j} field_weight[p]
  * <embeddings[i] row, embeddings[j] row> + bias[0] (p runs i-major over i < j, fwfm.py:129-136),
  * prob = sigmoid(logit).  embeddings[f]: table segments of width dim (out_col ignored);

@@ -111,15 +111,17 @@ def test_sharded_pipeline_emulated_on_gpu(world, chunks):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 8])
 def test_sharded_step_functions_emulated_on_gpu(world):
-    """The four steps one by one (index exchange, local gather, row exchange, FM + tail):
-    received indices equal the owner's fields of every source, gathered rows equal the packed
-    table rows (second order, then the first-order weight at column D), and the FM + tail equals
-    the oracle."""
+    """The four steps one by one (index exchange, local gather, row exchange, FM + tail) with the
+    packed wire rows: received indices equal the owner's fields of every source, gathered rows
+    equal the packed table rows (second order, then the first-order weight at column D), and the
+    FM + tail equals the oracle."""
     full = H.build("deepfm", CFG30, seed=42).cuda()
     B_l = 96
     inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=11), "cuda")
     expect = _oracle(full, CFG30, inp["category"])
     shards, emu = _shards(full, world)
+    for sh in shards:
+        sh.wire = "packed"
     D, RS = 32, sharded.row_stride(32)
 
     def rank_fn(r):
@@ -228,6 +230,7 @@ def test_shard_pack_and_gather_kernels(world):
     B = 777
     g = torch.Generator().manual_seed(world)
     cat = {f: torch.randint(0, n, (B,), generator=g).cuda() for f, n in FIELDS30.items()}
+    sh.wire = "packed"  # the packed-row gather here; the split one in test_split_wire_gather_rows
     got = sh.pack_indices(cat)
     want = torch.cat([torch.stack([cat[f] for f in fr], 1).reshape(-1) for fr in sh.fields_of if fr]).to(torch.int32)
     assert got.dtype == torch.int32 and torch.equal(got, want)
@@ -389,3 +392,72 @@ def test_cross_batch_pipeline_full_local_batch_p8():
         for r in range(world):
             got = tuple(x[:300] for x in outs[r][i])
             _check(got, expect, r * 300, (r + 1) * 300, 1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_split_wire_gather_rows(world):
+    """rk_shard_gather_rows_split: per source block, the [bc][F_me][D] second-order rows straight from
+    the nn.Embedding weights, then per sample the owner's first-order weights summed in field order;
+    an out-of-range index gives a zero row, adds 0 and raises RK_FLAG_INDEX_OOB."""
+    import rankops
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    shards, _ = _shards(full, world)
+    sh = shards[0]
+    assert sh.split_wire()
+    B, D = 515, 32
+    g = torch.Generator().manual_seed(world)
+    F_me = len(sh.local_fields)
+    recv = torch.stack([torch.randint(0, FIELDS30[f], (world, B), generator=g) for f in sh.local_fields], 2)
+    recv[1, 5, 0] = FIELDS30[sh.local_fields[0]]  # one past the table's last row: OOB
+    recv_d = recv.reshape(-1).to(torch.int32).cuda()
+    rankops.error_flags(reset=True)
+    for b0, bc in ((0, B), (100, 333), (514, 1)):
+        out = sh.gather_rows(recv_d, B, b0, bc).cpu()
+        blk = bc * F_me * D + (bc + 3) // 4 * 4
+        assert out.numel() == world * blk
+        for s_ in range(world):
+            rows = out[s_ * blk:s_ * blk + bc * F_me * D].view(bc, F_me, D)
+            part = out[s_ * blk + bc * F_me * D:s_ * blk + bc * F_me * D + bc]
+            want_p = torch.zeros(bc)
+            for j, f in enumerate(sh.local_fields):
+                w2 = full.second_order_embeddings[f].weight.detach().cpu()
+                w1 = full.first_order_embeddings[f].weight.detach().cpu()[:, 0]
+                idx = recv[s_, b0:b0 + bc, j]
+                ok = idx < w2.shape[0]
+                cl = idx.clamp(max=w2.shape[0] - 1)
+                assert torch.equal(rows[:, j, :], w2[cl] * ok[:, None])
+                want_p = want_p + torch.where(ok, w1[cl], torch.zeros(()))
+            torch.testing.assert_close(part, want_p, atol=1e-6, rtol=1e-6)
+    assert rankops.error_flags(reset=True) & 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_split_and_packed_wire_agree(world):
+    """The split wire format (default) and the packed one give the same forward (within fp32
+    rounding: fm1 is summed per owner first), both against the oracle."""
+    full = H.build("deepfm", CFG30, seed=42).cuda()
+    B_l = 300
+    inp = H.to_device(H.make_inputs("deepfm", CFG30, B_l * world, seed=77 + world), "cuda")
+    expect = _oracle(full, CFG30, inp["category"])
+    outs = {}
+    for wire in ("split", "packed"):
+        shards, emu = _shards(full, world)
+
+        def rank_fn(r, shards=shards, wire=wire):
+            sh = shards[r]
+            sh.wire = wire
+            assert sh.split_wire() == (wire == "split")
+            mine = {f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in inp["category"].items()}
+            with torch.no_grad():
+                out = sh.run_steps(mine, chunks=1)
+            torch.cuda.synchronize()
+            return tuple(o.cpu() for o in out)
+
+        outs[wire] = run_ranks(world, rank_fn, on_error=emu.abort)
+    for r in range(world):
+        _check(outs["split"][r], expect, r * B_l, (r + 1) * B_l, 1e-4)
+        _check(outs["packed"][r], expect, r * B_l, (r + 1) * B_l, 1e-4)
+        for a, b in zip(outs["split"][r], outs["packed"][r]):
+            torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
