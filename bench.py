@@ -360,7 +360,9 @@ def bench_sharded(world, rank, steps, warmup):
         # the pipeline's slots.  Warm-up fills the pipeline; every timed step completes one batch.
         cats = [cat] + [{f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l, dtype=np.int64)).to(dev)
                          for f in fields} for _ in range(2)]
-        step = model.pipeline(B_l, capture=cats).step
+        # side_stream=False: pack and gather in stream order before the forward (a gather beside the
+        # forward displaces its one-per-CU workgroups: sharded_model_curve's step_two_streams)
+        step = model.pipeline(B_l, capture=cats, side_stream=False).step
 
     t = max_over_ranks(world, time_replays(step, steps, max(warmup, 3), world))
     # bytes this rank sends per step (indices + rows), (P-1)/P of them to peers
@@ -474,7 +476,12 @@ def sharded_model_curve(p1_ms: float, ps=(2, 4, 8), chunks=4, iters=20):
         overlap = t_pack + t_idx + max(t_gather + t_fm, t_rows) + (t_gather + t_rows) / C
         # cross-batch pipeline: one row exchange per step (one call), hidden behind the forward
         wire1 = 1e3 * ((idx_link + rows_link) / XGMI_LINK_BPS + 2 * A2A_LATENCY_S)
-        local1 = t_step  # measured: forward || (pack, gather, exchange-bytes copy) on two streams
+        # the pipeline's schedule (ShardedDeepFM.pipeline(side_stream=False), the bench's): pack and
+        # gather in stream order before the forward, only the collectives beside it -> the serial local
+        # work plus the forward's measured slowdown under the exchange's copy traffic; gather and
+        # forward on two streams (step_two_streams) measured slower: the gather's workgroups displace
+        # the forward's one-per-CU workgroups
+        local1 = min(t_seq + contention, t_step)
         piped = max(local1, wire1)
         piped_free = max(t_seq, wire1)  # serial local work, RCCL's kernels on idle CUs (no contention)
         curve[str(P)] = {

@@ -257,18 +257,23 @@ __device__ __forceinline__ float bst_small_sample(const BstSmallArgs& a, int64_t
 //    4 kg + i), A = V transposed within each lane quad (DPP quad_perm) and broadcast with ABID = kg;
 //    the context lands in L0, ready for W_o.
 //  * key tiles past the sample's length are skipped (their keys are masked: exactly zero weight);
-//    LayerNorm reduces over the 4 lane groups by two lane shuffles.
+//    LayerNorm reduces over the 4 lane groups by two cross-row swaps (v_permlane16/32_swap).
 // Parameters of every block (the six 16 x 16 weights, biases, LayerNorm affines, position rows) are
 // staged once per workgroup in LDS: kBmBlockFloats per block.
 constexpr int kBmW = 0, kBmB = 6 * 256, kBmLN = kBmB + 6 * 16, kBmSc = kBmLN + 4 * 16, kBmPos = kBmSc + 4;
 constexpr int kBmBlockFloats = kBmPos + kST * kSD;  // 2724: ..., eps1 eps2 slope pad, pos
 
+// two accumulation chains (K-steps 0, 2 on the bias; 1, 3 from zero), added at the end: the
+// dependent-MFMA latency (40 cycles) paid twice per projection instead of four times
 __device__ __forceinline__ f32x4_t bm_proj(const float* W, const float* bias, f32x4_t x, int lane) {
   const f32x4_t w = *reinterpret_cast<const f32x4_t*>(W + (lane & 15) * kSD + 4 * (lane >> 4));
   f32x4_t acc = *reinterpret_cast<const f32x4_t*>(bias + 4 * (lane >> 4));
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc = mfma16(w[s], x[s], acc);
-  return acc;
+  f32x4_t acc1 = {0.f, 0.f, 0.f, 0.f};
+  acc = mfma16(w[0], x[0], acc);
+  acc1 = mfma16(w[1], x[1], acc1);
+  acc = mfma16(w[2], x[2], acc);
+  acc1 = mfma16(w[3], x[3], acc1);
+  return acc + acc1;
 }
 
 template <int ABID>
@@ -299,8 +304,7 @@ __device__ __forceinline__ f32x4_t quad_transpose(f32x4_t m, int lane) {
 // LayerNorm of each position over its 16 features (4 in-lane x the 4 lane groups), biased variance
 __device__ __forceinline__ f32x4_t bm_layernorm(f32x4_t x, const float* g, const float* be, float eps, int lane) {
   float s = (x[0] + x[1]) + (x[2] + x[3]);
-  s += __shfl_xor(s, 16, kWave);
-  s += __shfl_xor(s, 32, kWave);
+  s = xor32_sum(xor16_sum(s));
   const float m = s / (float)kSD;
   f32x4_t d;
   float v = 0.f;
@@ -309,8 +313,7 @@ __device__ __forceinline__ f32x4_t bm_layernorm(f32x4_t x, const float* g, const
     d[r] = x[r] - m;
     v = fmaf(d[r], d[r], v);
   }
-  v += __shfl_xor(v, 16, kWave);
-  v += __shfl_xor(v, 32, kWave);
+  v = xor32_sum(xor16_sum(v));
   const float rs = __builtin_amdgcn_rsqf(v / (float)kSD + eps);  // v_rsq_f32 (1 ulp), not div + sqrt
   const f32x4_t gg = *reinterpret_cast<const f32x4_t*>(g + 4 * (lane >> 4));
   const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(be + 4 * (lane >> 4));
@@ -326,7 +329,8 @@ __device__ __forceinline__ float bst_mfma_sample(const BstSmallArgs& a, const fl
   const int p16 = lane & 15, grp = lane >> 4;
   const int T = a.T;
   const int64_t len = a.seq_len[b];
-  const int lc = len <= 0 ? 0 : (len >= T ? T : (int)len);  // unmasked keys (bst.py:229)
+  // unmasked keys (bst.py:229), wave-uniform (one sample per wave) and held in an SGPR
+  const int lc = __builtin_amdgcn_readfirstlane(len <= 0 ? 0 : (len >= T ? T : (int)len));
   const int NT = (T + 15) >> 4, NKT = (lc + 15) >> 4;
   constexpr float kLog2e = 1.4426950408889634f;
   const float qscale = kLog2e / 2.0f;  // log2(e) / sqrt(d_h), d_h = 4
@@ -391,14 +395,17 @@ __device__ __forceinline__ float bst_mfma_sample(const BstSmallArgs& a, const fl
           sc[2] = mfma4b<2>(K[kt][e], q[e], sc[2]);
           sc[3] = mfma4b<3>(K[kt][e], q[e], sc[3]);
         }
-        // lane (q, h) register (kg, i): key 16 kt + 4 kg + i; masked keys -inf (bst.py:80)
+        // lane (q, h) register (kg, i): key 16 kt + 4 kg + i; masked keys -inf (bst.py:80).  The
+        // tile's key limit is laundered per tile: hoisted, the 64 compile-time key compares became 64
+        // SGPR-pair masks spilled to VGPR lanes (two v_readlane per score)
+        int klim = lc - 16 * kt;
+        asm volatile("" : "+s"(klim));
         float mt = -INFINITY;
 #pragma unroll
         for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int key = 16 * kt + 4 * kg + i;
-            sc[kg][i] = key < lc ? sc[kg][i] * qscale : -INFINITY;
+            sc[kg][i] = 4 * kg + i < klim ? sc[kg][i] * qscale : -INFINITY;
             mt = fmaxf(mt, sc[kg][i]);
           }
         const float m_new = fmaxf(m_run, mt);
@@ -475,14 +482,15 @@ __device__ __forceinline__ void bst_mfma_stage(const BstSmallArgs& a, float* prm
   }
 }
 
-// rk_bst_forward_blocks at d 16, 4 heads: the blocks + pooling only (bench roofline launch), 4 waves
-// per workgroup, persistent over the samples
-__global__ __launch_bounds__(kSWaves * 64, 4) void bst_mfma_kernel(BstSmallArgs a) {
+// rk_bst_forward_blocks at d 16, 4 heads: the blocks + pooling only (bench roofline launch), 16 waves
+// per workgroup (the parameter image staged once per CU), persistent over the samples
+constexpr int kBmWaves = 16;
+__global__ __launch_bounds__(kBmWaves * 64) void bst_mfma_kernel(BstSmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  bst_mfma_stage(a, sm, tid, kSWaves * 64);
+  bst_mfma_stage(a, sm, tid, kBmWaves * 64);
   __syncthreads();
-  for (int64_t b = (int64_t)blockIdx.x * kSWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kSWaves) {
+  for (int64_t b = (int64_t)blockIdx.x * kBmWaves + wave; b < a.batch; b += (int64_t)gridDim.x * kBmWaves) {
     const float v = bst_mfma_sample(a, sm, b, lane);
     if ((lane & 3) == 0) a.pool_out[b * a.ld_pool + 4 * (lane >> 4) + ((lane & 15) >> 2)] = v;
   }
@@ -742,10 +750,9 @@ int bst_small_forward(const float* table, int64_t table_rows, int64_t ld_table, 
   if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_bst_forward_blocks: negative batch");
   if (bst_use_mfma(heads)) {
     const size_t pshm = (size_t)nblocks * kBmBlockFloats * sizeof(float);
-    const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024) / pshm)));
-    const int64_t need = (batch + kSWaves - 1) / kSWaves;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)num_cus() * per_cu));
-    bst_mfma_kernel<<<grid, kSWaves * 64, pshm, st>>>(a);
+    const int64_t need = (batch + kBmWaves - 1) / kBmWaves;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)num_cus()));
+    bst_mfma_kernel<<<grid, kBmWaves * 64, pshm, st>>>(a);
     return check_launch("rk_bst_forward_blocks (d_model 16, MFMA)");
   }
   const size_t shm = (size_t)(kSWaves * 2 * kST * kSD) * sizeof(float);

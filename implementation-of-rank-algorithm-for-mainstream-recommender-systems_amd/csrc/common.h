@@ -121,6 +121,19 @@ __device__ __forceinline__ float row16_transpose_sum(float (&v)[N], int p16) {
   return v[0];
 }
 
+// Sums across lane bit 4 / bit 5 on the gfx950 cross-row swaps (VALU, no LDS round trip):
+// v_permlane16_swap / v_permlane32_swap with vdst = vsrc = v leave v of the partner row / half in
+// one of the two results and v in the other, in the same (low lane, high lane) order in both lanes
+// of a pair, so r[0] + r[1] is bit-identical to v + __shfl_xor(v, 16 | 32) in every lane.
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

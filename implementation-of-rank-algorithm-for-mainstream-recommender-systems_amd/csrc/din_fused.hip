@@ -30,6 +30,10 @@ namespace rk {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
+#ifndef RK_DIN_HOIST  // experiment (phase A's layer-1 operand per sample): see the tile loop
+#define RK_DIN_HOIST 0
+#endif
+
 constexpr int kDinSegs = 32;
 constexpr int kDinSegLdsOff = 528;  // bytes past the column map: 256 + 256 map bytes, l2_last int, pad to 16
 struct DinSegs {
@@ -444,132 +448,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   //   layer 3  the score of each position: ReLU(acc2 + b2) . w3 over the lane's 8 values, summed over
   //            the 4 lane groups
   // then the masked (online) softmax and the weighted key sum o[h] over the tile's positions.
-  // ---- Phase A.1 on tiles of 16 history positions (v_mfma_f32_16x16x4_f32): lane l holds position
-  // p16 = l & 15 of the tile and the key elements h in [HG g, HG g + HG), g = l >> 4, so a tile's 16
-  // key rows are one 128-B load round per lane group.  Per tile (64 MFMAs, 128 MFMA-cycles per
-  // position as the 32 x 32 form, but a sample pads only to 16 positions: 33 instead of 44
-  // positions per sample at T = 50, lengths U[1, 50]):
-  //   layer 1  acc1[jt] (j = 16 jt + 4 g + r, position p16) = Weff[j][h] . k[h], K = H: the A operand
-  //            Weff = (W1b - W1c) + W1d diag(q) (rows 16 jt + p16, lane group g's h), built per sample
-  //   ReLU(+ u[j])  on the accumulators; they are layer 2's B operands as they stand (K-step (jt, r)
-  //            takes j = 16 jt + 4 g + r from lane group g)
-  //   layer 2  acc2[jt2] (j2 = 16 jt2 + 4 g + r) = W2[j2][j] . h1[j], 16 K-steps
-  //   layer 3  the score of each position: ReLU(acc2 + b2) . w3 over the lane's 8 values, summed over
-  //            the 4 lane groups
-  // then the masked softmax weights and the tile's weighted key sum (A.3).
-  const int p16_ = lane & 15, g_ = lane >> 4;
-  constexpr int HG0 = H / 4;
-  float kk0[HG0];  // this wave's own sample, tile 0 (A.1)
-  auto load_first = [&](int64_t r, int t) {
-    const float* krow = nullptr;
-    if (t < a.T) {
-      if (r >= 0 && r < a.key_rows)
-        krow = a.key_table + r * a.ld_key + HG0 * g_;
-      else
-        flag_oob(flags);
-#ifdef RK_DIN_NO_GATHER
-      krow = a.key_table + (int64_t)p16_ * a.ld_key + HG0 * g_;
-#endif
-    }
-    if constexpr (HG0 >= 4) {
-#pragma unroll
-      for (int c = 0; c < HG0 / 4; ++c) {
-        const f32x4_t v4 = krow ? *reinterpret_cast<const f32x4_t*>(krow + 4 * c) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) kk0[4 * c + e] = v4[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < HG0; ++e) kk0[e] = krow ? krow[e] : 0.f;
-    }
-  };
-#pragma unroll
-  for (int e = 0; e < HG0; ++e) kk0[e] = 0.f;
-  const int64_t* const kslot = kpre0 + 64 * loc;
-  // ---- Phase A.1: the first tile's keys.  NIT == 0: the row and the indices are in LDS already
-  // (gathered before the barrier above).  NIT > 0: the row, the indices and then the keys for the
-  // assigned sample, the row going to LDS while the key rows are still in flight.
-  if constexpr (NIT == 0) {
-    if (live && ntiles > 0) load_first(kslot[p16_], p16_);
-  } else {
-    gather_issue(b, live, ntiles);
-    const uint32_t lo = __shfl((uint32_t)kidx, p16_, kWave), hi = __shfl((uint32_t)((uint64_t)kidx >> 32), p16_, kWave);
-    if (live && ntiles > 0) load_first((int64_t)(((uint64_t)hi << 32) | lo), p16_);
-    gather_store(row, kpre0 + 64 * loc);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  if constexpr (NIT > 0 && KS > 0) {  // this wave's row is in LDS (its stores completed above)
-    if (lane == 0) __hip_atomic_fetch_add(&s_din_rows_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-#ifdef RK_DIN_PHASES
-  if (tid == 0) {  // wave 0: its row in LDS and its first tile's keys landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_din_ts[7] = wall_clock64();
-  }
-#endif
-
-  // ---- Phase A.2: per-sample bias u[j] = b1[j] + q . Wq[j] (lane j) of this wave's own sample,
-  // and the sample's tile count and clamped length, for whichever wave takes its tiles.  The
-  // per-sample table and the tile partials live in buf1 (phase B's layer-1 buffer: free until
-  // phase B's layer 0 writes it, after the barrier that opens phase B).
-  int* const s_nt = reinterpret_cast<int*>(buf1);    // [16] tiles of LDS row s
-  int* const s_lc = s_nt + kMlpRows;                 // [16] min(max(len, 0), T)
-  float* const slots = buf1 + 2 * kMlpRows;          // [16][ntiles_all][SL]: per tile (m, l, o[H])
-  constexpr int SL = H + 2;
-  if (live) {
-    float u = sm[Ly::B1 + lane];
-    const float* wq = sm + Ly::WQ + lane * Ly::LDH;
-    const float* q = row + a.q_col;
-#pragma unroll
-    for (int h = 0; h < H; ++h) u = fmaf(q[h], wq[h], u);
-    sm[Ly::U + loc * 64 + lane] = u;
-  }
-  if (lane == 0) {
-    s_nt[loc] = live ? ntiles : 0;
-    s_lc[loc] = live ? clamp_len(len) : 0;
-  }
-  // every row, history-index slot, u and tile count in LDS (and no wave still reads buf1's previous
-  // launch contents: buf1 is written only here and in phase B)
-  __syncthreads();
-
-  // ---- Phase A.3: the attention tiles, spread over the 16 waves.  Every wave first takes tile 0
-  // of its own sample (its keys are in flight since A.1); the remaining tiles of all 16 samples
-  // (sample-major, E of them) are dealt in contiguous ranges so that each SIMD (waves w, w+4, w+8,
-  // w+12) gets E/4 +- 1: range kw = 4 (w % 4) + w / 4.  With one sample per wave the SIMD holding
-  // the longest samples set phase A's length (tile counts 4+3+2+1 against 3+2+1+1 at T = 50);
-  // now every SIMD carries within one tile of the mean.  Each tile leaves its partial result in
-  // its own slot — plain: o[h] = sum_p w_p k_p[h]; softmax: the tile max m, l = sum_p e^(s_p - m)
-  // and o[h] = sum_p e^(s_p - m) k_p[h] — and the sample's wave merges the slots in tile order
-  // (A.4), so the arithmetic of a sample never depends on which waves took its tiles.
   constexpr int HG = H / 4;
   const int p16 = lane & 15, g = lane >> 4;
-  const int nta = ntiles_all;
-  const int nt_l = lane < kMlpRows ? s_nt[lane] : 0;
-  const int ext_l = nt_l > 1 ? nt_l - 1 : 0;
-  const int cex_l = wave_incl_scan(ext_l) - ext_l;  // exclusive prefix of the extra tiles
-  const int E = __builtin_amdgcn_readlane(cex_l + ext_l, kMlpRows - 1);
-  const int kw = 4 * (wave & 3) + (wave >> 2);
-  const int x_lo = kw * E / kMlpRows, x_hi = (kw + 1) * E / kMlpRows;
-  const bool own0 = live && ntiles > 0;
-  const int n_items = (own0 ? 1 : 0) + (x_hi - x_lo);
-  // item i of this wave -> (LDS row, tile)
-  auto item = [&](int i, int& s_, int& tt_) {
-    if (own0 && i == 0) {
-      s_ = loc;
-      tt_ = 0;
-      return;
-    }
-    const int k = x_lo + i - (own0 ? 1 : 0);
-    const unsigned long long m = __ballot(lane < kMlpRows && ext_l > 0 && cex_l <= k);
-    s_ = 63 - __builtin_clzll(m);
-    tt_ = 1 + k - __builtin_amdgcn_readlane(cex_l, s_);
-  };
-  const int64_t* const kslot0 = kpre0;  // [16][64]: history indices of positions 0..63 per LDS row
-  auto row_b = [&](int s_) -> int64_t {
-    if constexpr (NIT > 0) return s_rows[s_];
-    else return m0 + s_;
-  };
+  const int64_t* const kslot = kpre0 + 64 * loc;  // indices of positions 0..63 (staged with the row)
   float kk[HG];  // keys of the current tile: position p16, elements HG g + e
   // key row of position t (index r) into kv; positions past T read as zeros, out-of-range rows too
   // (flagged)
@@ -596,142 +477,160 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       for (int e = 0; e < HG; ++e) kv[e] = krow ? krow[e] : 0.f;
     }
   };
-  auto index_of = [&](int s_, int t) -> int64_t {
-    return t < 64 ? kslot0[64 * s_ + t] : (t < a.T ? a.seq[row_b(s_) * a.ld_seq + t] : 0);
-  };
-#pragma unroll
-  for (int e = 0; e < HG; ++e) kk[e] = kk0[e];  // own tile 0 (A.1)
-  if (!own0 && n_items > 0) {  // no own tile: the first item's keys now
-    int s1, t1;
-    item(0, s1, t1);
-    load_keys16(index_of(s1, 16 * t1 + p16), 16 * t1 + p16, kk);
+  auto index_of = [&](int t) -> int64_t { return t < 64 ? kslot[t] : (t < a.T ? a.seq[b * a.ld_seq + t] : 0); };
+  // ---- Phase A.1: the first tile's keys.  NIT == 0: the row and the indices are in LDS already
+  // (gathered before the barrier above).  NIT > 0: the row, the indices and then the keys for the
+  // assigned sample, the row going to LDS while the key rows are still in flight.
+  if constexpr (NIT == 0) {
+    if (live && ntiles > 0) load_keys16(kslot[p16], p16, kk);
+  } else {
+    gather_issue(b, live, ntiles);
+    const uint32_t lo = __shfl((uint32_t)kidx, p16, kWave), hi = __shfl((uint32_t)((uint64_t)kidx >> 32), p16, kWave);
+    if (live && ntiles > 0) load_keys16((int64_t)(((uint64_t)hi << 32) | lo), p16, kk);
+    gather_store(row, kpre0 + 64 * loc);
   }
-  const float sqrt_h = (float)__builtin_sqrt((double)H);
-  const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
-  const float b3 = a.b3[0];
-  int cur_s = -1, cur_lc = 0;
-  float qv[HG];  // the query elements of lane group g (sample cur_s)
-  for (int it = 0; it < n_items; ++it) {
-    int s_, tt;
-    item(it, s_, tt);
-    if (s_ != cur_s) {
-      cur_s = s_;
-      const float* rs = buf0 + s_ * a.ld0 + a.q_col + HG * g;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (NIT > 0 && KS > 0) {  // this wave's row is in LDS (its stores completed above)
+    if (lane == 0) __hip_atomic_fetch_add(&s_din_rows_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+#ifdef RK_DIN_PHASES
+  if (tid == 0) {  // wave 0: its row in LDS and its first tile's keys landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_din_ts[7] = wall_clock64();
+  }
+#endif
+
+  float norm_part = 0.f;
+  if (live) {
+    // ---- Phase A.2: per-sample bias u[j] = b1[j] + q . Wq[j]   (lane j)
+    {
+      float u = sm[Ly::B1 + lane];
+      const float* wq = sm + Ly::WQ + lane * Ly::LDH;
+      const float* q = row + a.q_col;
 #pragma unroll
-      for (int e = 0; e < HG; ++e) qv[e] = rs[e];
-      cur_lc = s_lc[s_];
+      for (int h = 0; h < H; ++h) u = fmaf(q[h], wq[h], u);
+      sm[Ly::U + wave * 64 + lane] = u;
     }
-    // the weight LDS reads below are loop-invariant (kept in the loop: see RK_DIN_HOIST, round 4)
-    asm volatile("" ::: "memory");
-    const int t = 16 * tt + p16;
-    const bool in_seq = t < a.T;
-    // the next item's keys go out before this tile's MFMAs
-    float kn[HG];
-    const bool more = it + 1 < n_items;
-    if (more) {
-      int sn, tn;
-      item(it + 1, sn, tn);
-      load_keys16(index_of(sn, 16 * tn + p16), 16 * tn + p16, kn);
-    }
-    f32x4_t acc1[4];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    float qv[HG];  // the query elements of lane group g
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt) acc1[jt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    // layer 1's A operand, Weff[16 jt + p16][HG g + e] = Wk + Wqk q (rows of the LDS image)
+    for (int e = 0; e < HG; ++e) qv[e] = row[a.q_col + HG * g + e];
+
+    const float sqrt_h = (float)__builtin_sqrt((double)H);
+    const float pad = -4294967296.0f;  // (-2**32 + 1) rounded to fp32, din.py:74
+    const float b3 = a.b3[0];
+    float m_run = -INFINITY, l_run = 0.f;
+    float o[HG];
+#pragma unroll
+    for (int e = 0; e < HG; ++e) o[e] = 0.f;
+    // RK_DIN_HOIST (experiment, off): layer 1's A operand Weff built once per sample in 32 VGPRs
+    // instead of per tile from LDS (118 VGPRs, no spill; half the tile's LDS reads and 32 fewer FMAs
+    // per tile) measured flat (42.0 / 42.7 us against 41.8 / 42.7 us per launch,
+    // profiles/r04/ab_hoist*.json): phase A is not bound by the operand's LDS reads
+#if RK_DIN_HOIST
+    float weff[4][HG];
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) {
       const float* wk = sm + Ly::WK + (16 * jt + p16) * Ly::LDH + HG * g;
       const float* wqk = sm + Ly::WQK + (16 * jt + p16) * Ly::LDH + HG * g;
 #pragma unroll
-      for (int e = 0; e < HG; ++e) acc1[jt] = mfma16(fmaf(wqk[e], qv[e], wk[e]), kk[e], acc1[jt]);
+      for (int e = 0; e < HG; ++e) weff[jt][e] = fmaf(wqk[e], qv[e], wk[e]);
     }
-    // ReLU(layer 1 + u) in place, then layer 2 with the accumulators as its B operands
-    f32x4_t acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#endif
+    for (int tt = 0; tt < ntiles; ++tt) {
+      // the weight LDS reads below are loop-invariant (kept in the loop: see RK_DIN_HOIST above)
+      asm volatile("" ::: "memory");
+      const int t = 16 * tt + p16;
+      const bool in_seq = t < a.T;
+      // the next tile's keys go out before this tile's MFMAs
+      float kn[HG];
+      const bool more = tt + 1 < ntiles;
+      if (more) load_keys16(index_of(t + 16), t + 16, kn);
+      f32x4_t acc1[4];
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const f32x4_t uu = *reinterpret_cast<const f32x4_t*>(sm + Ly::U + s_ * 64 + 16 * jt + 4 * g);
-      f32x4_t w2[2];
+      for (int jt = 0; jt < 4; ++jt) acc1[jt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      // layer 1's A operand, Weff[16 jt + p16][HG g + e] = Wk + Wqk q (rows of the LDS image)
+#if RK_DIN_HOIST
 #pragma unroll
-      for (int jt2 = 0; jt2 < 2; ++jt2)
-        w2[jt2] = *reinterpret_cast<const f32x4_t*>(sm + Ly::W2 + (16 * jt2 + p16) * 68 + 16 * jt + 4 * g);
+      for (int e = 0; e < HG; ++e) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = acc1[jt][r] + uu[r];
-        const float h1 = z < 0.f ? 0.f : z;
-#pragma unroll
-        for (int jt2 = 0; jt2 < 2; ++jt2) acc2[jt2] = mfma16(w2[jt2][r], h1, acc2[jt2]);
+        for (int jt = 0; jt < 4; ++jt) acc1[jt] = mfma16(weff[jt][e], kk[e], acc1[jt]);
       }
-    }
-    // layer 3: the position's score
-    float sc = 0.f;
+#else
 #pragma unroll
-    for (int jt2 = 0; jt2 < 2; ++jt2) {
-      const f32x4_t b2v = *reinterpret_cast<const f32x4_t*>(sm + Ly::B2 + 16 * jt2 + 4 * g);
-      const f32x4_t w3v = *reinterpret_cast<const f32x4_t*>(sm + Ly::W3 + 16 * jt2 + 4 * g);
+      for (int jt = 0; jt < 4; ++jt) {
+        const float* wk = sm + Ly::WK + (16 * jt + p16) * Ly::LDH + HG * g;
+        const float* wqk = sm + Ly::WQK + (16 * jt + p16) * Ly::LDH + HG * g;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float z = acc2[jt2][r] + b2v[r];
-        z = z < 0.f ? 0.f : z;
-        sc = fmaf(z, w3v[r], sc);
+        for (int e = 0; e < HG; ++e) acc1[jt] = mfma16(fmaf(wqk[e], qv[e], wk[e]), kk[e], acc1[jt]);
       }
-    }
-    sc += __shfl_xor(sc, 16, kWave);
-    sc += __shfl_xor(sc, 32, kWave);
-    sc = sc + b3;
-
-    const bool valid = in_seq && t < cur_lc;
-    float wgt, mt = 0.f;
-    if (a.use_softmax) {
-      const float sv = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
-      mt = row16_max(sv);
-      wgt = in_seq ? expf(sv - mt) : 0.f;
-    } else {
-      wgt = valid ? sc : 0.f;
-    }
-    // the tile's sums over its 16 positions (the lanes of a DPP row): o[e] by a transposing
-    // butterfly — each step halves the values a lane holds, so HG values take HG - 1 + log2(16 / HG)
-    // DPP moves instead of 4 HG; lane p16 ends with element e = (p16 >> 1) & (HG - 1) (HG = 8)
-    float vals[HG];
+#endif
+      // ReLU(layer 1 + u) in place, then layer 2 with the accumulators as its B operands
+      f32x4_t acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int e = 0; e < HG; ++e) vals[e] = wgt * kk[e];
-    const float o_t = row16_transpose_sum<HG>(vals, p16);
-    float* const slot = slots + (s_ * nta + tt) * SL;
-    if ((p16 & (16 / HG - 1)) == 0) slot[2 + HG * g + p16 / (16 / HG)] = o_t;
-    if (a.use_softmax) {
-      const float l_t = row16_sum(wgt);
-      if (lane == 0) {
-        slot[0] = mt;
-        slot[1] = l_t;
-      }
-    }
-    if (more) {
+      for (int jt = 0; jt < 4; ++jt) {
+        const f32x4_t uu = *reinterpret_cast<const f32x4_t*>(sm + Ly::U + wave * 64 + 16 * jt + 4 * g);
+        f32x4_t w2[2];
 #pragma unroll
-      for (int e = 0; e < HG; ++e) kk[e] = kn[e];
-    }
-  }
-  __syncthreads();  // every tile partial in LDS
-
-  // ---- Phase A.4: the sample's attention output from its tile partials, in tile order, into the
-  // LDS row; then the row's l2 norm (din.py:318-322)
-  float norm_part = 0.f;
-  if (live) {
-    if (lane < H) {
-      float out = 0.f;
-      if (a.use_softmax) {
-        float M = -INFINITY;
-        for (int t2 = 0; t2 < ntiles; ++t2) M = fmaxf(M, slots[(loc * nta + t2) * SL]);
-        float L = 0.f, O = 0.f;
-        for (int t2 = 0; t2 < ntiles; ++t2) {
-          const float* sl = slots + (loc * nta + t2) * SL;
-          const float sc_t = expf(sl[0] - M);
-          L = fmaf(sl[1], sc_t, L);
-          O = fmaf(sl[2 + lane], sc_t, O);
+        for (int jt2 = 0; jt2 < 2; ++jt2)
+          w2[jt2] = *reinterpret_cast<const f32x4_t*>(sm + Ly::W2 + (16 * jt2 + p16) * 68 + 16 * jt + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = acc1[jt][r] + uu[r];
+          const float h1 = z < 0.f ? 0.f : z;
+#pragma unroll
+          for (int jt2 = 0; jt2 < 2; ++jt2) acc2[jt2] = mfma16(w2[jt2][r], h1, acc2[jt2]);
         }
-        out = O * (1.0f / L);
-      } else {
-        for (int t2 = 0; t2 < ntiles; ++t2) out += slots[(loc * nta + t2) * SL + 2 + lane];
       }
-      row[a.att_col + lane] = out;
+      // layer 3: the position's score
+      float sc = 0.f;
+#pragma unroll
+      for (int jt2 = 0; jt2 < 2; ++jt2) {
+        const f32x4_t b2v = *reinterpret_cast<const f32x4_t*>(sm + Ly::B2 + 16 * jt2 + 4 * g);
+        const f32x4_t w3v = *reinterpret_cast<const f32x4_t*>(sm + Ly::W3 + 16 * jt2 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float z = acc2[jt2][r] + b2v[r];
+          z = z < 0.f ? 0.f : z;
+          sc = fmaf(z, w3v[r], sc);
+        }
+      }
+      sc = xor32_sum(xor16_sum(sc));  // bit-identical to the two xor shuffles, no LDS round trip
+      sc = sc + b3;
+
+      const bool valid = in_seq && (int64_t)t < len;
+      if (a.use_softmax) {
+        const float sv = in_seq ? (valid ? sc : pad) / sqrt_h : -INFINITY;
+        const float mt = row16_max(sv);
+        const float m_new = fmaxf(m_run, mt);
+        const float scale_old = expf(m_run - m_new);
+        const float p = in_seq ? expf(sv - m_new) : 0.f;
+        const float ps = row16_sum(p);
+        l_run = l_run * scale_old + ps;
+        m_run = m_new;
+#pragma unroll
+        for (int e = 0; e < HG; ++e) o[e] = o[e] * scale_old + p * kk[e];
+      } else {
+        const float w = valid ? sc : 0.f;
+#pragma unroll
+        for (int e = 0; e < HG; ++e) o[e] = o[e] + w * kk[e];
+      }
+      if (more) {
+#pragma unroll
+        for (int e = 0; e < HG; ++e) kk[e] = kn[e];
+      }
     }
+    // the weighted key sum over the positions (the 16 lanes of a group), into the LDS row
+    const float inv_l = a.use_softmax ? 1.0f / l_run : 1.0f;
+    float mine = 0.f;
+#pragma unroll
+    for (int e = 0; e < HG; ++e) {
+      const float v = row16_sum(o[e]);
+      mine = p16 == e ? v : mine;
+    }
+    if (p16 < HG) row[a.att_col + HG * g + p16] = a.use_softmax ? mine * inv_l : mine;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     if (a.l2_part) {
@@ -951,14 +850,6 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   a.flags = device_flags();
   a.ld0 = need0 + kMlpLdPad;
   a.ld1 = need1 + kMlpLdPad;
-  // phase A's per-sample table and tile partials live in buf1 (16 x ld1 floats, free until phase B's
-  // layer 0): 2 ints + (H + 2) floats per (sample, tile); a wider stride where they need more
-  const int64_t slot_floats = 2 * kMlpRows + (int64_t)kMlpRows * ((T + 15) / 16) * (H + 2);
-  if (slot_floats > (int64_t)kMlpRows * a.ld1) {
-    const int64_t ld = ((slot_floats + kMlpRows - 1) / kMlpRows + 3) / 4 * 4;
-    if (ld > 40 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: T = %d needs too much LDS", T);
-    a.ld1 = (int)ld;
-  }
   static_assert(sizeof(DinArgs) <= 4096, "kernel arguments beyond 4 KiB");
   if (batch < 0) return fail(RK_ERR_INVALID, "rk_din_forward: negative batch");
   plan->blocks = (batch + kMlpRows - 1) / kMlpRows;

@@ -101,8 +101,9 @@ __global__ __launch_bounds__(256) void shard_gather_rows_kernel(ShardGatherArgs 
 // The split wire format (round 5): the row exchange carries each field's D second-order floats as
 // they are in the nn.Embedding weight ([V, D]: one 128-B line at D = 32, no packed copy of the
 // table) and, per (source, sample), ONE first-order value: the sum of this owner's fields' weights
-// in field order.  Send block of source s: [b'][j][D] rows, then pad4(bc) partial sums.  One wave
-// per (source, sample): its F x D / 4 float4s, then the F first-order weights summed in field order.
+// in field order.  Send block of source s: [b'][j][D] rows, then pad4(bc) partial sums.  The rows
+// flattened over float4s (as the packed gather), then one thread per (source, sample) sums the F
+// first-order weights in field order.
 struct ShardSplitArgs {
   const float* src2[kShardMaxFields];
   const float* src1[kShardMaxFields];
@@ -116,38 +117,56 @@ struct ShardSplitArgs {
 };
 
 __global__ __launch_bounds__(256) void shard_gather_split_kernel(ShardSplitArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int D = 4 * a.G;
+  const int D = 4 * a.G, per = a.F * a.G;
   const int64_t blk = a.bc * a.F * D + ((a.bc + 3) & ~(int64_t)3);  // floats per source block
   const int64_t nrows = (int64_t)a.P * a.bc;                         // (source, sample) rows
-  // one wave per (source, sample): lane t moves quad t % G of field t / G (t += 64 past one
-  // instruction), then lane j < F fetches field j's first-order weight
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nrows; r += (int64_t)gridDim.x * 4) {
+  const int64_t n4 = nrows * per;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool oob = false;
+  // the second-order rows, flattened over the output's float4s as the packed gather (kShardU loads
+  // in flight per lane): float4 t = (row r = t / per, field j, quad q)
+  for (int64_t t0 = tid; t0 < n4; t0 += stride * kShardU) {
+    int64_t row[kShardU], dst[kShardU];
+    int jj[kShardU], qq[kShardU];
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u) {
+      const int64_t t = t0 + u * stride;
+      const int64_t tt = t < n4 ? t : 0;
+      const int64_t r = tt / per;
+      const int rem = (int)(tt - r * per);
+      const int j = rem / a.G;
+      const int64_t s = r / a.bc, bp = r - s * a.bc;
+      jj[u] = j;
+      qq[u] = rem - j * a.G;
+      dst[u] = s * blk + (bp * a.F + j) * D + 4 * qq[u];
+      row[u] = a.idx[(s * a.B_l + a.b0 + bp) * a.F + j];
+    }
+    f32x4 v[kShardU];
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u) {
+      const int j = jj[u];
+      const bool ok = row[u] >= 0 && row[u] < a.rows[j];
+      oob |= !ok && t0 + u * stride < n4;
+      v[u] = *reinterpret_cast<const f32x4*>(a.src2[j] + (ok ? row[u] : 0) * a.ld2[j] + 4 * qq[u]);
+      if (!ok) v[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kShardU; ++u)
+      if (t0 + u * stride < n4) *reinterpret_cast<f32x4*>(a.out + dst[u]) = v[u];
+  }
+  // the first-order partial sums: one thread per (source, sample), the owner's fields in order
+  for (int64_t r = tid; r < nrows; r += stride) {
     const int64_t s = r / a.bc, bp = r - s * a.bc;
     const int32_t* ip = a.idx + (s * a.B_l + a.b0 + bp) * a.F;
-    float* const base = a.out + s * blk;
-    const int per = a.F * a.G;
-    bool oob = false;
-    for (int t = lane; t < per; t += 64) {
-      const int j = t / a.G, q = t - j * a.G;
-      const int64_t row = ip[j];
-      const bool ok = row >= 0 && row < a.rows[j];
-      oob |= !ok;
-      f32x4 v = *reinterpret_cast<const f32x4*>(a.src2[j] + (ok ? row : 0) * a.ld2[j] + 4 * q);
-      if (!ok) v = (f32x4){0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(base + (bp * a.F + j) * D + 4 * q) = v;
-    }
-    float w1 = 0.f;
-    if (lane < a.F) {
-      const int64_t row = ip[lane];
-      if (row >= 0 && row < a.rows[lane]) w1 = a.src1[lane][row * a.ld1[lane]];
-    }
-    // the partial sum over this owner's fields, in field order
     float acc = 0.f;
-    for (int j = 0; j < a.F; ++j) acc += __shfl(w1, j, kWave);
-    if (lane == 0) base[a.bc * a.F * D + bp] = acc;
-    if (oob) flag_oob(a.flags);
+    for (int j = 0; j < a.F; ++j) {
+      const int64_t row = ip[j];
+      if (row >= 0 && row < a.rows[j]) acc += a.src1[j][row * a.ld1[j]];
+    }
+    a.out[s * blk + a.bc * a.F * D + bp] = acc;
   }
+  if (oob) flag_oob(a.flags);
 }
 
 }  // namespace rk
@@ -187,7 +206,9 @@ RK_API int rk_shard_gather_rows_split(const rk_segment* second, const rk_segment
   if (!a.flags) return fail(RK_ERR_RUNTIME, "rk_shard_gather_rows_split: device not initialised (rk_init)");
   const int64_t nrows = (int64_t)num_sources * bc;
   if (nrows == 0) return RK_OK;
-  const unsigned blocks = (unsigned)std::min<int64_t>((nrows + 3) / 4, (int64_t)num_cus() * 32);
+  const int64_t n4 = nrows * num_fields * a.G;
+  const unsigned blocks = (unsigned)std::min<int64_t>(
+      std::max<int64_t>((n4 + 256 * kShardU - 1) / (256 * kShardU), (nrows + 255) / 256), (int64_t)num_cus() * 32);
   shard_gather_split_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(a);
   return check_launch("rk_shard_gather_rows_split");
 }

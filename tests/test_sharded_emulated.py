@@ -409,7 +409,7 @@ def test_split_wire_gather_rows(world):
     g = torch.Generator().manual_seed(world)
     F_me = len(sh.local_fields)
     recv = torch.stack([torch.randint(0, FIELDS30[f], (world, B), generator=g) for f in sh.local_fields], 2)
-    recv[1, 5, 0] = FIELDS30[sh.local_fields[0]]  # one past the table's last row: OOB
+    recv[1, 5, 0] = full.second_order_embeddings[sh.local_fields[0]].num_embeddings  # one past the last row: OOB
     recv_d = recv.reshape(-1).to(torch.int32).cuda()
     rankops.error_flags(reset=True)
     for b0, bc in ((0, B), (100, 333), (514, 1)):
