@@ -356,19 +356,21 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   const unsigned long long wave_t0 = clock64();
 #endif
 
-  // ---- balance the attention work over the SIMDs: waves w, w+4, w+8, w+12 share one SIMD, so
-  // wave w takes the sample of rank w in descending tile count (the longest four samples land on
-  // four different SIMDs, and so on).  Every wave computes the same ranking, from scalar reads of
-  // lanes 0..15.  (Balanced launches: the ranks are already in descending tile order, wave j takes
-  // rank j.)
+  // ---- balance the attention work over the SIMDs: waves w, w+4, w+8, w+12 share one SIMD (SIMD
+  // w % 4, position w / 4), and the ranks (descending tile count) are dealt to the SIMDs in snake
+  // order — position 0 takes ranks 0..3 on SIMDs 0..3, position 1 ranks 4..7 on SIMDs 3..0, and so
+  // on: at T = 50 the SIMDs then carry 9/8/9/8 tiles instead of 10/9/8/7 (round 5; rank rho(w)).
+  // Every wave computes the same ranking, from scalar reads of lanes 0..15.  (Balanced launches: the
+  // ranks are already in descending tile order.)  A sample's LDS row is its rank in the workgroup.
+  const int rho = (wave & ~3) | (((wave >> 2) & 1) ? 3 - (wave & 3) : (wave & 3));
   int loc, ntiles;
   int64_t len, b;
   bool live;
   if constexpr (NIT > 0) {
     const int G = gridDim.x, B = (int)a.batch;  // batch <= 8192 here: 32-bit index math
-    const int p = blockIdx.x + G * wave;  // this wave's rank
+    const int p = blockIdx.x + G * rho;  // this wave's rank
     rows = min(kMlpRows, (B - (int)blockIdx.x + G - 1) / G);
-    loc = wave;
+    loc = rho;
     live = p < B;
     int cls = 0;
     b = 0;
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
     int bv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(bv) : "s"((int)b));
     len = live ? a.seq_len[bv] : 0;
-    if (lane == 0) s_rows[wave] = b;
+    if (lane == 0) s_rows[loc] = b;
   } else {
     int rank = 0;
 #pragma unroll
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       const int tj = __builtin_amdgcn_readlane(my_tiles, j);
       rank += (tj > my_tiles) || (tj == my_tiles && j < lane);
     }
-    const unsigned long long pick = __ballot(lane < kMlpRows && rank == wave);
+    const unsigned long long pick = __ballot(lane < kMlpRows && rank == rho);
     // wave-uniform values in scalar registers (readfirstlane): the sample's addresses stay scalar
     loc = __builtin_amdgcn_readfirstlane(pick ? __builtin_ctzll(pick) : wave);  // sample in the WG
     ntiles = __builtin_amdgcn_readfirstlane(max(0, __builtin_amdgcn_readlane(my_tiles, loc)));
