@@ -14,6 +14,8 @@
 //
 // Both are HBM-bound byte movers: pack 12 B per (sample, field); gather 4 B of index + 2 x RS * 4 B
 // per (row, field) (read the packed row, write it to the send buffer).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rk {
@@ -169,6 +171,70 @@ __global__ __launch_bounds__(256) void shard_gather_split_kernel(ShardSplitArgs 
   if (oob) flag_oob(a.flags);
 }
 
+// The same send block with one lane group per (source, sample) (round 5, second form): G = D / 4
+// lanes take the quads of that sample's F rows, all F row loads (and, on the group's first lane, the
+// F first-order weights) in flight together; grid.y = the source, so no 64-bit divisions by runtime
+// sizes.  The first-order sum keeps the field order and skips out-of-range rows, as above.
+constexpr int kShardSplitU = 8;  // fields per pass
+// nontemporal row loads and send-buffer stores (experiment: each row is read once, the send buffer
+// is read next by the collective)
+#ifndef RK_SHARD_NT
+#define RK_SHARD_NT 0
+#endif
+template <int G>
+__global__ __launch_bounds__(256) void shard_gather_split_group_kernel(ShardSplitArgs a) {
+  constexpr int S = 256 / G, D = 4 * G;
+  const int tid = threadIdx.x, q = tid & (G - 1);
+  const int64_t bp = (int64_t)blockIdx.x * S + tid / G;
+  if (bp >= a.bc) return;  // no barrier below
+  const int F = a.F, s = blockIdx.y;
+  const int64_t blk = a.bc * F * D + ((a.bc + 3) & ~(int64_t)3);
+  float* const out = a.out + s * blk;
+  const int32_t* const ip = a.idx + ((int64_t)s * a.B_l + a.b0 + bp) * F;
+  float acc = 0.f;
+  bool oob = false;
+  for (int j0 = 0; j0 < F; j0 += kShardSplitU) {
+    int64_t row[kShardSplitU];
+#pragma unroll
+    for (int u = 0; u < kShardSplitU; ++u) row[u] = j0 + u < F ? ip[j0 + u] : 0;
+    f32x4 v[kShardSplitU];
+    float w[kShardSplitU];
+    bool ok[kShardSplitU];
+#pragma unroll
+    for (int u = 0; u < kShardSplitU; ++u) {
+      const int j = j0 + u;
+      ok[u] = false;
+      w[u] = 0.f;
+      if (j < F) {
+        ok[u] = row[u] >= 0 && row[u] < a.rows[j];
+        oob |= !ok[u];
+        const int64_t r = ok[u] ? row[u] : 0;
+#if RK_SHARD_NT
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.src2[j] + r * a.ld2[j] + 4 * q));
+#else
+        v[u] = *reinterpret_cast<const f32x4*>(a.src2[j] + r * a.ld2[j] + 4 * q);
+#endif
+        if (q == 0) w[u] = a.src1[j][r * a.ld1[j]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kShardSplitU; ++u) {
+      const int j = j0 + u;
+      if (j < F) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#if RK_SHARD_NT
+        __builtin_nontemporal_store(ok[u] ? v[u] : z, reinterpret_cast<f32x4*>(out + (bp * F + j) * D + 4 * q));
+#else
+        *reinterpret_cast<f32x4*>(out + (bp * F + j) * D + 4 * q) = ok[u] ? v[u] : z;
+#endif
+        if (ok[u]) acc += w[u];
+      }
+    }
+  }
+  if (q == 0) out[a.bc * F * D + bp] = acc;
+  if (oob) flag_oob(a.flags);
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -206,6 +272,21 @@ RK_API int rk_shard_gather_rows_split(const rk_segment* second, const rk_segment
   if (!a.flags) return fail(RK_ERR_RUNTIME, "rk_shard_gather_rows_split: device not initialised (rk_init)");
   const int64_t nrows = (int64_t)num_sources * bc;
   if (nrows == 0) return RK_OK;
+  static const bool flat = [] {  // A/B switch: RANKOPS_SHARD_SPLIT_FLAT=1 keeps the flattened form
+    const char* e = getenv("RANKOPS_SHARD_SPLIT_FLAT");
+    return e && e[0] == '1';
+  }();
+  if (!flat && num_sources <= 65535 && (a.G == 4 || a.G == 8 || a.G == 16)) {
+    const int S = 256 / a.G;
+    const dim3 grid((unsigned)((bc + S - 1) / S), (unsigned)num_sources);
+    if (a.G == 8)
+      shard_gather_split_group_kernel<8><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else if (a.G == 4)
+      shard_gather_split_group_kernel<4><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else
+      shard_gather_split_group_kernel<16><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    return check_launch("rk_shard_gather_rows_split");
+  }
   const int64_t n4 = nrows * num_fields * a.G;
   const unsigned blocks = (unsigned)std::min<int64_t>(
       std::max<int64_t>((n4 + 256 * kShardU - 1) / (256 * kShardU), (nrows + 255) / 256), (int64_t)num_cus() * 32);
