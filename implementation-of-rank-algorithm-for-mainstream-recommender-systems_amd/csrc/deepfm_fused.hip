@@ -23,6 +23,7 @@
 // output over the input row in place (mlp_stream.h IP0).  Per-row arithmetic and order unchanged:
 // bit-identical to RT = 1 (tests/test_gpu_deepfm_fused.py).
 #include <cstdlib>
+#include <type_traits>
 
 #include "mlp_core.h"
 #include "mlp_stream.h"
@@ -42,11 +43,6 @@ struct DfArgs {
   int64_t istride[kDfMaxFields];
   int64_t ld[kDfMaxFields];
   int64_t rows[kDfMaxFields];
-  // first-order weight of field f for row index r: fo[f][r * fo_ld[f]] (packed tables: the row's
-  // float at column dim; split wire rows: the owner's per-sample partial sum on its first field,
-  // nullptr on the others)
-  const float* fo[kDfMaxFields];
-  int64_t fo_ld[kDfMaxFields];
   uint32_t dense_mask;
   int F, dim_shift;
   int64_t M;
@@ -55,9 +51,18 @@ struct DfArgs {
   float* fm2;
   uint32_t* flags;
 };
+// rk_deepfm_forward_fo: first-order weight of field f for row index r from fo[f][r * fo_ld[f]] (split
+// wire rows: the owner's per-sample partial sum on its first field, nullptr on the others).  A
+// separate kernel-argument type, so the packed path's arguments stay as small as before.
+struct DfArgsFo : DfArgs {
+  const float* fo[kDfMaxFields];
+  int64_t fo_ld[kDfMaxFields];
+};
 
-template <class P, int RT>
-__global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
+// FO: first-order weights from a.fo (rk_deepfm_forward_fo); otherwise from the packed row itself
+// (column dim, the address the row's own loads use: no per-field pointer loads)
+template <class P, int RT, bool FO>
+__global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(std::conditional_t<FO, DfArgsFo, DfArgs> a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
 #ifdef RK_MLP_PHASES
@@ -115,8 +120,12 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(DfArgs a) {
         const float* row = reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
         v[t][i] = *reinterpret_cast<const f32x4_t*>(row + 4 * (q & (G - 1)));
       }
-      const float* fop = a.fo[f_me];
-      fw[t] = fop ? fop[rr * a.fo_ld[f_me]] : 0.f;
+      if constexpr (FO) {
+        const float* fop = a.fo[f_me];
+        fw[t] = fop ? fop[rr * a.fo_ld[f_me]] : 0.f;
+      } else {
+        fw[t] = p[dim];
+      }
     }
   };
   // round 3: the row into buf0 (zeros for padding quads, out-of-range rows and rows past the batch)
@@ -209,7 +218,7 @@ static int deepfm_forward_impl(const rk_segment* fields, const float* const* fir
       batch < 0)
     return fail(RK_ERR_INVALID, "rk_deepfm_forward: bad arguments (head with final_w / final_b, fm1, fm2)");
   const int K0 = num_fields * dim;
-  DfArgs a = {};
+  DfArgsFo a = {};
   a.head = *head;
   a.head.fm1 = fm1;  // selects the FM combine; the values come from LDS
   a.head.fm2 = fm2;
@@ -238,9 +247,6 @@ static int deepfm_forward_impl(const rk_segment* fields, const float* const* fir
         return fail(RK_ERR_INVALID, "rk_deepfm_forward_fo: field %d first-order stride", f);
       a.fo[f] = first[f];
       a.fo_ld[f] = first[f] ? first_ld[f] : 0;
-    } else {
-      a.fo[f] = s.src + dim;  // packed layout: the weight follows the row's dim floats
-      a.fo_ld[f] = s.src_ld;
     }
     if (s.idx) {
       a.idx[f] = s.idx;
@@ -284,13 +290,16 @@ static int deepfm_forward_impl(const rk_segment* fields, const float* const* fir
   if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: widths need %zu B of LDS", shm);
   const int64_t blocks = (batch + kMlpRows * rt - 1) / (kMlpRows * rt);
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_deepfm_forward: batch too large");
-  if (rt == 2) {
-    raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960, 2>, 160 * 1024);
-    deepfm_fused_kernel<StreamPlanK960, 2><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
-  } else {
-    raise_lds_limit((const void*)deepfm_fused_kernel<StreamPlanK960, 1>, 160 * 1024);
-    deepfm_fused_kernel<StreamPlanK960, 1><<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
-  }
+  auto go = [&](auto kern, const auto& args) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(args);
+  };
+  const DfArgs& base = a;
+  if (first)
+    rt == 2 ? go(deepfm_fused_kernel<StreamPlanK960, 2, true>, a) : go(deepfm_fused_kernel<StreamPlanK960, 1, true>, a);
+  else
+    rt == 2 ? go(deepfm_fused_kernel<StreamPlanK960, 2, false>, base)
+            : go(deepfm_fused_kernel<StreamPlanK960, 1, false>, base);
   return check_launch("rk_deepfm_forward");
 }
 
