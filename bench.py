@@ -1024,12 +1024,12 @@ def main():
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "afm":
-                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_kernel<8,128>"])
+                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_kernel<8,2>"])
                 r["roofline"].update(counter_fields("afm_kernel", "afm"))
             if name == "deepcrossing":
                 r["roofline"] = small_forward_roofline(m2, "deepcrossing", inp2, batch, DEEPCROSSING_FLOP,
-                                                       DEEPCROSSING_BYTES, ["concat_gather_kernel", "mlp_stream_kernel"])
-                r["roofline"].update(counter_fields("mlp", "deepcrossing"))
+                                                       DEEPCROSSING_BYTES, ["concat_gather_kernel<1>", "mlp_kernel<1,false>"])
+                r["roofline"].update(counter_fields("mlp_kernel", "deepcrossing"))
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob
                 r["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * r["samples_per_s"] / 1e9, 1)
                 r["bytes_per_sample"] = FWFM_BYTES_PER_SAMPLE
