@@ -941,6 +941,13 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
         tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
         res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
         res["step"] = "prepared launch (%s)" % ("rk_dcn_forward" if model_name == "dcn" else "rk_deepfm_forward")
+    elif name == "bst_ref":
+        # at the reference script's d_model 16 the whole BST forward is one kernel too
+        # (rk_bst_small_forward): BSTModel.prepare binds it to the inputs; graph replay beside it
+        run = model.prepare(inp["dense"], inp["category"], inp["seq_feedid"], inp["seq_length"])
+        tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
+        res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
+        res["step"] = "prepared launch (rk_bst_small_forward)"
     else:
         run = g.replay
     t = time_replays(run, steps, warmup, world)

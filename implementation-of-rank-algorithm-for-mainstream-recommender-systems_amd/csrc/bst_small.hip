@@ -529,7 +529,9 @@ struct BstFwdArgs {
 };
 static_assert(sizeof(BstFwdArgs) <= 4096, "kernel arguments beyond 4 KiB");
 
-template <int NH>
+// P: the DNN tail's plan — StreamPlanK80 when the row (+ pooled columns) fits 80 columns (the
+// reference's 66: layer 0 streams 5 of its image's 8 K-chunks, the other 3 multiply zero columns)
+template <int NH, class P>
 __global__ __launch_bounds__(kMlpThreads) void bst_small_fwd_kernel(BstFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -563,11 +565,12 @@ __global__ __launch_bounds__(kMlpThreads) void bst_small_fwd_kernel(BstFwdArgs a
   }
   const float pooled = live ? bst_small_sample<NH>(a.s, b, kv, kv + kST * kSD, lane) : 0.f;
   if (lane < kSD) row[a.width + lane] = pooled;
-  mlp_stream_rows<StreamPlanK128, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
+  mlp_stream_rows<P, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
 }
 
 // The same forward with 4 heads on the matrix cores (bst_mfma_sample): no K / V slices in LDS; the
 // blocks' parameter image after buf1.
+template <class P>
 __global__ __launch_bounds__(kMlpThreads) void bst_mfma_fwd_kernel(BstFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -606,7 +609,7 @@ __global__ __launch_bounds__(kMlpThreads) void bst_mfma_fwd_kernel(BstFwdArgs a)
   } else if (lane < kSD) {
     row[a.width + lane] = 0.f;
   }
-  mlp_stream_rows<StreamPlanK128, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
+  mlp_stream_rows<P, kEpiRegs>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid);
 }
 
 static bool bst_use_mfma(int heads) {
@@ -697,16 +700,26 @@ RK_API int rk_bst_small_forward(const rk_segment* row_segs, int32_t nseg, int32_
     raise_lds_limit((const void*)kern, 160 * 1024);
     kern<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(a);
   };
-  if (mfma) {
-    go(bst_mfma_fwd_kernel);
-    return check_launch("rk_bst_small_forward");
-  }
-  switch (heads) {
-    case 1: go(bst_small_fwd_kernel<1>); break;
-    case 2: go(bst_small_fwd_kernel<2>); break;
-    case 4: go(bst_small_fwd_kernel<4>); break;
-    default: go(bst_small_fwd_kernel<8>); break;
-  }
+  // the tail's K chunks: 5 when the row fits 80 columns (RANKOPS_BST_K80=0: all 8, A/B)
+  static const bool k80_on = [] {
+    const char* e = getenv("RANKOPS_BST_K80");
+    return !(e && e[0] == '0');
+  }();
+  const bool k80 = k80_on && K0 <= StreamPlanK80::KC0 * 16;
+  auto launch = [&](auto plan) {
+    using P = decltype(plan);
+    if (mfma) return go(bst_mfma_fwd_kernel<P>);
+    switch (heads) {
+      case 1: go(bst_small_fwd_kernel<1, P>); break;
+      case 2: go(bst_small_fwd_kernel<2, P>); break;
+      case 4: go(bst_small_fwd_kernel<4, P>); break;
+      default: go(bst_small_fwd_kernel<8, P>); break;
+    }
+  };
+  if (k80)
+    launch(StreamPlanK80{});
+  else
+    launch(StreamPlanK128{});
   return check_launch("rk_bst_small_forward");
 }
 

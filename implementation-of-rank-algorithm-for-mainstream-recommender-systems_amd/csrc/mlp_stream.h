@@ -608,6 +608,7 @@ __device__ __forceinline__ void mlp_stream_rows(const rk_mlp_layer* __restrict__
 // DCN / DIN / BST / DeepFM): by the input's K chunks.  DeepFM's tail after its tiled first layer
 // is [256, 128] over K0 = 512.
 using StreamPlanK64 = StreamPlan<4, 32, 16, 8>;    // DCN (width 50)
+using StreamPlanK80 = StreamPlan<5, 32, 16, 8>;    // BST d 16 DNN (16 + 34 + 16 = 66; K chunks past 80 all zero)
 using StreamPlanK128 = StreamPlan<8, 32, 16, 8>;   // DIN (16 + 34 + 2H <= 128)
 using StreamPlanK192 = StreamPlan<12, 32, 16, 8>;  // BST DNN (16 + 34 + d = 178 at d 128)
 using StreamPlanK256 = StreamPlan<16, 32, 16, 8>;

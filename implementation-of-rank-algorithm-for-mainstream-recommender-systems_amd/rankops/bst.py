@@ -270,6 +270,55 @@ class BSTModel(EngineModule):
         run_tail(row, self._tail, self.dnn[-1], {}, logits, probs)
         return probs, logits
 
+    def prepare(self, dense, category, seq_feedid, seq_length):
+        """An eval forward bound to these input tensors (as DIN.prepare / DCNModel.prepare: the
+        single-kernel analogue of capturing the forward in a hipGraph) at the reference script's
+        d_model 16: returns `run()` that recomputes the whole forward from the current contents of
+        the inputs with one rk_bst_small_forward launch and returns the same (prob, logit) tensors
+        each time.  Binds the current weights (repack-free: the packed tail images are pinned)."""
+        if self.training:
+            raise RuntimeError("BSTModel.prepare: eval mode only (call .eval() first)")
+        dense = ops.as_f32(dense, "dense")
+        seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
+        seq_length = ops.as_index(seq_length, "seq_length")
+        B, T = seq_feedid.shape
+        dev = dense.device
+        blocks = self._fused_blocks(T) if self.transformer_blocks else None
+        if blocks is None or self.d_model != 16 or not common.FUSED_BST_FWD:
+            raise RuntimeError("BSTModel.prepare: configuration outside rk_bst_small_forward's envelope")
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col = self.num_dense_features
+        idx_keep = []
+        for name, emb in self.embeddings.items():
+            if name in category:
+                idx = ops.as_index(category[name], f"category[{name!r}]")
+                idx_keep.append(idx)
+                segs.append(ops.table_segment(emb.weight, idx, col))
+                col += emb.embedding_dim
+        logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        probs = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        packed = [common.PACKED(l.linear.weight) for l in self._tail]
+        for l in self._tail:  # the images the launch binds are never rewritten in place under it
+            common.PACKED.pin(l.linear.weight)
+        epis = [l.epilogue_kwargs() for l in self._tail]  # folded BatchNorm tensors: kept alive below
+        mls = [ops.make_mlp_layer(l.linear.weight, pk, **ek) for l, pk, ek in zip(self._tail, packed, epis)]
+        head = ops.make_epilogue(head_w=self.dnn[-1].weight, head_b=self.dnn[-1].bias, head_logit=logits,
+                                 head_prob=probs)
+        args = ops.bst_small_forward_args(segs, col, self.embeddings['feedid'].weight, seq_feedid, seq_length,
+                                          self.transformer_blocks[0].nhead, blocks, self.pooling_method != 'sum',
+                                          mls, head)
+        fn, out = ops._lib.load().rk_bst_small_forward, (probs, logits)
+        rc = fn(*args)
+        if rc == ops._lib.RK_ERR_UNSUPPORTED:
+            raise RuntimeError("BSTModel.prepare: configuration outside rk_bst_small_forward's envelope")
+        ops.check(rc, "rk_bst_small_forward")
+
+        def run():
+            ops.check(fn(*args), "rk_bst_small_forward")
+            return out
+        run.keep = (args, head, mls, packed, epis, blocks, segs, idx_keep, dense, seq_feedid, seq_length, category)
+        return run
+
     def blocks_kernel_launcher(self, seq_feedid, seq_length):
         """Zero-argument re-launch of this forward's rk_bst_forward_blocks kernel (every block +
         pooling) into a scratch DNN row, for kernel-level timing (bench.py BST roofline)."""

@@ -333,10 +333,9 @@ def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr
                                     ld_pool, 1 if pool_mean else 0, _lib.stream_of(table)), "rk_bst_forward_blocks")
 
 
-def bst_small_forward(segs, width, table, seq, seq_len, heads, blocks, pool_mean, layers, head: Epilogue) -> bool:
-    """rk_bst_small_forward: the whole BST eval forward at d_model 16 in one launch.  False (nothing
-    launched) outside its envelope (RK_ERR_UNSUPPORTED), for the three-launch path."""
-    lib = _lib.load()
+def bst_small_forward_args(segs, width, table, seq, seq_len, heads, blocks, pool_mean, layers, head: Epilogue):
+    """The argument tuple of one rk_bst_small_forward call (every array it points into is part of
+    the tuple, so holding the tuple keeps them alive; the tensors stay the caller's)."""
     B, T = seq.shape
     params = (ctypes.c_void_p * (BST_BLOCK_PARAMS * len(blocks)))()
     scalars = (ctypes.c_float * (3 * len(blocks)))()
@@ -347,9 +346,16 @@ def bst_small_forward(segs, width, table, seq, seq_len, heads, blocks, pool_mean
             scalars[3 * i + k] = float(sc[k])
     arr = _seg_array(segs)
     larr = (_lib.MlpLayer * max(1, len(layers)))(*layers)
-    rc = lib.rk_bst_small_forward(arr, len(segs), width, ptr(table), table.shape[0], table.stride(0), ptr(seq),
-                                  seq.stride(0), T, ptr(seq_len), B, heads, len(blocks), params, scalars,
-                                  1 if pool_mean else 0, larr, len(layers), ctypes.byref(head), _lib.stream_of(table))
+    return (arr, len(segs), width, ptr(table), table.shape[0], table.stride(0), ptr(seq), seq.stride(0), T,
+            ptr(seq_len), B, heads, len(blocks), params, scalars, 1 if pool_mean else 0, larr, len(layers),
+            ctypes.byref(head), _lib.stream_of(table))
+
+
+def bst_small_forward(segs, width, table, seq, seq_len, heads, blocks, pool_mean, layers, head: Epilogue) -> bool:
+    """rk_bst_small_forward: the whole BST eval forward at d_model 16 in one launch.  False (nothing
+    launched) outside its envelope (RK_ERR_UNSUPPORTED), for the three-launch path."""
+    rc = _lib.load().rk_bst_small_forward(*bst_small_forward_args(segs, width, table, seq, seq_len, heads, blocks,
+                                                                  pool_mean, layers, head))
     if rc == _lib.RK_ERR_UNSUPPORTED:
         return False
     check(rc, "rk_bst_small_forward")

@@ -121,3 +121,49 @@ def test_small_bst_mfma_equals_valu_kernel(monkeypatch, cfg):
     torch.cuda.synchronize()
     for a, b in zip(mf, va):
         torch.testing.assert_close(a, b, atol=ATOL, rtol=RTOL, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_small_bst_prepare_equals_forward():
+    """BSTModel.prepare: the bound one-launch forward (rk_bst_small_forward) equals the module's
+    forward bit for bit, recomputes from the inputs' current contents, and keeps reading live
+    images after a generation bump and a normal forward rebuild the caches (folded BatchNorm)."""
+    cfg = {"T": 50, "heads": 4, "vocab": H.WECHAT_VOCAB}
+    model = H.build("bst", cfg)
+    H.randomize_eval_stats(model, 7)
+    model = model.cuda().eval()
+    d = H.to_device(H.make_inputs("bst", cfg, 3000, seed=11), "cuda")
+    run = model.prepare(d["dense"], d["category"], d["seq_feedid"], d["seq_length"])
+    with torch.no_grad():
+        first = tuple(o.clone() for o in run())
+        ref = H.as_tuple(H.call_model(model, "bst", d))
+    for a, b in zip(first, ref):
+        assert torch.equal(a, b)
+    e = H.to_device(H.make_inputs("bst", cfg, 3000, seed=12), "cuda")
+    d["dense"].copy_(e["dense"])
+    d["seq_feedid"].copy_(e["seq_feedid"])
+    d["seq_length"].copy_(e["seq_length"])
+    for k in d["category"]:
+        d["category"][k].copy_(e["category"][k])
+    with torch.no_grad():
+        b = tuple(o.clone() for o in run())
+        ref = H.as_tuple(H.call_model(model, "bst", e))
+    for x, y in zip(b, ref):
+        assert torch.equal(x, y)
+    model.eval()  # generation bump: the next forward refolds BatchNorm
+    with torch.no_grad():
+        H.call_model(model, "bst", e)
+        scratch = [torch.randn(1 << 20, device="cuda") for _ in range(32)]  # reuse freed blocks
+        again = run()
+    torch.cuda.synchronize()
+    for x, y in zip(b, again):
+        assert torch.equal(x, y)
+    del scratch
+
+
+def test_small_bst_prepare_rejects_train_mode():
+    """(CPU) prepare() is an eval-only binding."""
+    model = H.build("bst", {"T": 8, "heads": 4})
+    d = H.make_inputs("bst", {"T": 8, "heads": 4}, 16, seed=1)
+    with pytest.raises(RuntimeError):
+        model.train().prepare(d["dense"], d["category"], d["seq_feedid"], d["seq_length"])
