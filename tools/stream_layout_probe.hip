@@ -1,0 +1,102 @@
+// Weight-image layout probe (tools only, not part of the library): does the ORDER in which the 16
+// waves of every CU walk a shared L2-resident image change the intake rate?  256 workgroups x 16
+// waves, R = 8 register ring of 1 KiB fragments, each fragment optionally feeding 4
+// v_mfma_f32_16x16x4_f32 (one tile-chunk of the streamed tails, mlp_stream.h).
+//   contiguous : step i, wave w reads fragment 16 i + w (the 16 waves read 16 adjacent KiB)
+//   tile-major : wave w reads fragments w n + i (its own tile's chunks, n = fragments per wave):
+//                the packed-weight layout the tails use, tiles n KiB apart
+//   tile-major+pad : the same with tiles n + 1 KiB apart (breaks the common stride)
+//   tile-major+xor : the same fragments, the tile base permuted per CU (blockIdx-dependent
+//                rotation of the wave -> tile map), so CUs in lockstep read different tiles
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/bin/stream_layout_probe tools/stream_layout_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kWaves = 16, R = 8;
+
+template <int MODE, int MF>
+__global__ __launch_bounds__(1024) void walk(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  const int tile = MODE == 3 ? (wave + blockIdx.x) & (kWaves - 1) : wave;
+  auto frag = [&](int i) -> int64_t {
+    if (MODE == 0) return (int64_t)kWaves * i + wave;
+    if (MODE == 2) return (int64_t)tile * (n + 1) + i;
+    return (int64_t)tile * n + i;
+  };
+  f4 ring[R];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[frag(i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (MF == 0) {
+        acc += ring[j];
+      } else {
+#pragma unroll
+        for (int m = 0; m < MF; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j][m & 3], acc, 0, 0, 0);
+      }
+      if (i + j + R < n) ring[j] = base[frag(i + j + R) * 64];
+    }
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
+int main() {
+  float* img;
+  float* out;
+  const int max_kb = 4096;
+  hipMalloc(&img, (size_t)max_kb * 1024);
+  hipMalloc(&out, 1024 * sizeof(float));
+  std::vector<float> h((size_t)max_kb * 256, 0.5f);
+  hipMemcpy(img, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  const char* names[] = {"contiguous", "tile-major", "tile-major+pad", "tile-major+rot"};
+  for (int mf : {0, 4}) {
+    for (int kb : {512, 896, 2560}) {  // per-layer image sizes: DCN/DIN 512->256 layer, DIN fcn, DeepFM
+      const int n = kb / kWaves;
+      for (int round = 0; round < 2; ++round) {
+        for (int mode = 0; mode < 4; ++mode) {
+          auto launch = [&]() {
+            if (mf == 0) {
+              switch (mode) {
+                case 0: walk<0, 0><<<256, 1024>>>(img, n, out); break;
+                case 1: walk<1, 0><<<256, 1024>>>(img, n, out); break;
+                case 2: walk<2, 0><<<256, 1024>>>(img, n, out); break;
+                default: walk<3, 0><<<256, 1024>>>(img, n, out); break;
+              }
+            } else {
+              switch (mode) {
+                case 0: walk<0, 4><<<256, 1024>>>(img, n, out); break;
+                case 1: walk<1, 4><<<256, 1024>>>(img, n, out); break;
+                case 2: walk<2, 4><<<256, 1024>>>(img, n, out); break;
+                default: walk<3, 4><<<256, 1024>>>(img, n, out); break;
+              }
+            }
+          };
+          for (int w = 0; w < 5; ++w) launch();
+          hipEventRecord(a);
+          const int it = 50;
+          for (int w = 0; w < it; ++w) launch();
+          hipEventRecord(b);
+          hipEventSynchronize(b);
+          float ms;
+          hipEventElapsedTime(&ms, a, b);
+          const double us = 1e3 * ms / it;
+          printf("mf %d image %5d KiB  %-16s %8.2f us  %7.1f GB/s per CU%s\n", mf, kb, names[mode], us,
+                 kb * 1024.0 / (us * 1e-6) / 1e9, mf ? "  (MFMA floor: n x 4 x 32 cycles x 4 waves per SIMD)" : "");
+        }
+      }
+    }
+  }
+  hipError_t e = hipGetLastError();
+  printf("status: %s\n", hipGetErrorString(e));
+  return e == hipSuccess ? 0 : 1;
+}
