@@ -96,6 +96,25 @@ int main() {
       }
     }
   }
+  // the same walk (tile-major, MFMA) on fewer workgroups: one workgroup per CU, dispatched round-robin
+  // over the 8 XCDs, so grid g puts g / 8 CUs on each XCD's L2.  A per-CU intake limit keeps the time;
+  // a shared per-XCD L2 limit shortens it as the CUs per XCD drop.
+  for (int round = 0; round < 2; ++round) {
+    for (int grid : {256, 192, 128, 64, 32, 8}) {
+      const int kb = 896, n = kb / kWaves;
+      for (int w = 0; w < 5; ++w) walk<1, 4><<<grid, 1024>>>(img, n, out);
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) walk<1, 4><<<grid, 1024>>>(img, n, out);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      const double us = 1e3 * ms / it;
+      printf("grid %3d (%2d CUs per XCD) image 896 KiB tile-major mf 4  %8.2f us  %7.1f GB/s per CU\n", grid, grid / 8,
+             us, kb * 1024.0 / (us * 1e-6) / 1e9);
+    }
+  }
   hipError_t e = hipGetLastError();
   printf("status: %s\n", hipGetErrorString(e));
   return e == hipSuccess ? 0 : 1;
