@@ -81,8 +81,15 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # one GPU per rank; modulo the visible devices only so that a one-GPU box can rehearse the
+        # N > 1 path with every rank on its single GPU (timings then meaningless)
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("RANKOPS_BENCH_BACKEND") == "gloo":
+            # rehearsal only (RCCL refuses two ranks on one GPU): gloo with the tensors on the GPU
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -155,7 +162,9 @@ def graph_of(fn):
             fn()
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.no_grad(), torch.cuda.graph(g):
+    # thread_local: with a process group up, RCCL's watchdog thread keeps querying its events
+    # during a capture; only this thread's calls are restricted
+    with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
         out = fn()
     return g, out
 
@@ -688,7 +697,7 @@ def bench_train(batch, steps, warmup, name="dcn"):
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
             opt.zero_grad(set_to_none=True)
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 step()
             run = g.replay
         for _ in range(warmup):

@@ -463,7 +463,9 @@ def _graph_of(fn):
             fn()
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.no_grad(), torch.cuda.graph(g):
+    # thread_local: RCCL's watchdog thread queries its events during the capture (only this
+    # thread's calls are restricted)
+    with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
         out = fn()
     return g, out
 
