@@ -364,8 +364,8 @@ def bench_sharded(world, rank, steps, warmup):
         step = g0.replay
     else:
         # the cross-batch exchange pipeline (ShardedDeepFM.pipeline, captured): per step the index
-        # all-to-all of batch i, the gather + row all-to-all of batch i-1 (side stream, RCCL async)
-        # and the one-launch forward of batch i-2 (compute stream); three local batches bound to
+        # all-to-all of batch i, the gather + row all-to-all of batch i-1 (RCCL async) and the
+        # one-launch forward of batch i-2; three local batches bound to
         # the pipeline's slots.  Warm-up fills the pipeline; every timed step completes one batch.
         cats = [cat] + [{f: torch.from_numpy(rng.integers(0, SHARDED_ROWS_PER_FIELD, B_l, dtype=np.int64)).to(dev)
                          for f in fields} for _ in range(2)]
@@ -382,9 +382,10 @@ def bench_sharded(world, rank, steps, warmup):
             "wire_format": "split" if model.split_wire() else "packed",
             "scaling": "strong",
             "mode": ("one hipGraph (packed FM gather + tail, no exchange at P=1)" if world == 1 else
-                     "cross-batch pipeline (ShardedDeepFM.pipeline): per step pack + index all_to_all_single of "
-                     "batch i, gather + row all_to_all_single of batch i-1 on a side stream, the one-launch "
-                     "forward of batch i-2; local segments as hipGraphs, RCCL async between them")}
+                     "cross-batch pipeline (ShardedDeepFM.pipeline, side_stream=False): per step pack + index "
+                     "all_to_all_single of batch i, gather + row all_to_all_single of batch i-1, the one-launch "
+                     "forward of batch i-2, local steps in stream order as hipGraphs, the all-to-alls async on "
+                     "RCCL's stream between them")}
 
 
 XGMI_LINK_BPS = 153e9   # MI355X: 7 xGMI links x ~153 GB/s per GPU, point to point (fully connected node)
