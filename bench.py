@@ -951,6 +951,12 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
         tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
         res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
         res["step"] = "prepared launch (%s)" % ("rk_dcn_forward" if model_name == "dcn" else "rk_deepfm_forward")
+    elif name == "afm":
+        # one kernel (rk_afm_forward): AFM.prepare binds it to the inputs; graph replay beside it
+        run = model.prepare(inp["dense_input"], inp["category_input"])
+        tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
+        res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
+        res["step"] = "prepared launch (rk_afm_forward)"
     elif name == "bst_ref":
         # at the reference script's d_model 16 the whole BST forward is one kernel too
         # (rk_bst_small_forward): BSTModel.prepare binds it to the inputs; graph replay beside it
@@ -1041,7 +1047,7 @@ def main():
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "afm":
-                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_kernel<8,2>"])
+                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_mfma_kernel<2,8>"])
                 r["roofline"].update(counter_fields("afm_kernel", "afm"))
             if name == "deepcrossing":
                 r["roofline"] = small_forward_roofline(m2, "deepcrossing", inp2, batch, DEEPCROSSING_FLOP,

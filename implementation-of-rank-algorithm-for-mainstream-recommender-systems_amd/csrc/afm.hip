@@ -9,7 +9,10 @@
 // One wave per sample.  The field embeddings of the wave's sample are staged in LDS; lane a
 // owns attention units a, a+64, ... (their W_a rows live in registers) and accumulates its
 // share of every pair score; one wave reduction per pair finishes the score.
+#include <cstdlib>
+
 #include "common.h"
+#include "mlp_core.h"
 
 namespace rk {
 
@@ -114,6 +117,142 @@ __global__ __launch_bounds__(256) void afm_kernel(AfmFields fields, int F, int64
   }
 }
 
+// The same forward with the attention MLP on the matrix cores (round 5): per sample the pair
+// products form a [P x D] matrix and the attention layer is [P x D] . W_a^T ([D x A]) — P = 28 pairs,
+// D = 8, A = 128 at afm.py's defaults — so one wave runs it as ceil(P/16) x NT tiles of
+// v_mfma_f32_16x16x4_f32 over D/4 K-steps: lane l feeds pair 16 mt + l % 16, dims 4 s + l / 16 (the
+// A operand, products formed from the LDS-staged embeddings) and holds W_a's fragments (the B
+// operand: unit 16 t + l % 16, dims 4 s + l / 16) in registers for the whole launch.  Each output
+// register is relu(. + b_a) * h, summed over the lane's unit tiles, then over the row's 16 units
+// (row16_transpose_sum): the pair scores.  Softmax and the weighted sum run one pair per lane:
+// afm = sum_p w_p (pair_p . p_w) + p_b, the weighted pair vector contracted with p first (the same
+// value as p(sum_p w_p pair_p), reassociated).  KS = D / 4 (D in {4, 8, 16}), NT = unit tiles of 16
+// (A <= 128, rounded up to 2 / 4 / 8: the extra units have zero weights).
+constexpr int kAfmMfmaMaxPairs = 120;  // F <= 16
+template <int KS, int NT>
+__global__ __launch_bounds__(256) void afm_mfma_kernel(AfmFields fields, int F, int64_t batch,
+                                                       const float* __restrict__ dense, int64_t ld_dense, int nd,
+                                                       const float* __restrict__ dense_w,
+                                                       const float* __restrict__ dense_b,
+                                                       const float* __restrict__ att_w, const float* __restrict__ att_b,
+                                                       int A, const float* __restrict__ att_h,
+                                                       const float* __restrict__ att_hb, const float* __restrict__ p_w,
+                                                       const float* __restrict__ p_b, float* __restrict__ logit_out,
+                                                       float* __restrict__ prob_out, uint32_t* flags) {
+  constexpr int D = 4 * KS;
+  __shared__ float emb[4][kAfmMaxFields * D];
+  __shared__ float score[4][kAfmMfmaMaxPairs];
+  __shared__ uint8_t pfi[kAfmMfmaMaxPairs], pfj[kAfmMfmaMaxPairs];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, p16 = lane & 15, grp = lane >> 4;
+  float* e = emb[wave];
+  float* sc = score[wave];
+  const int P = F * (F - 1) / 2;
+  // pair p -> (i, j), i < j in field order (afm.py:101-108)
+  if ((int)threadIdx.x < P) {
+    int p = threadIdx.x, i = 0;
+    while (p >= F - 1 - i) {
+      p -= F - 1 - i;
+      ++i;
+    }
+    pfi[threadIdx.x] = (uint8_t)i;
+    pfj[threadIdx.x] = (uint8_t)(i + 1 + p);
+  }
+  // W_a fragments, b_a and h of this lane's unit columns 16 t + p16
+  float bw[NT][KS], ba[NT], hh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int a = 16 * t + p16;
+    const bool on = a < A;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bw[t][s] = on ? att_w[(int64_t)a * D + 4 * s + grp] : 0.f;
+    ba[t] = on ? att_b[a] : 0.f;
+    hh[t] = on ? att_h[a] : 0.f;
+  }
+  float pw[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) pw[d] = p_w[d];
+  const float hb = att_hb[0], pb = p_b[0];
+  __syncthreads();  // the pair tables
+  const int MT = (P + 15) >> 4;
+
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < batch; b += (int64_t)gridDim.x * 4) {
+    for (int i = lane; i < F * D; i += 64) {
+      const int f = i / D, d = i % D;
+      const float* row = segment_row(fields.s[f], b, flags);
+      e[i] = row ? row[d] : 0.f;
+    }
+    float dl = 0.f;
+    for (int k = lane; k < nd; k += 64) dl = fmaf(dense[b * ld_dense + k], dense_w[k], dl);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+
+    for (int mt = 0; mt < kAfmMfmaMaxPairs / 16 + 1; ++mt) {
+      if (mt >= MT) break;
+      const int p = 16 * mt + p16;
+      const bool pv = p < P;
+      const int fi = pv ? pfi[p] : 0, fj = pv ? pfj[p] : 0;
+      float a[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int d = 4 * s + grp;
+        a[s] = pv ? e[fi * D + d] * e[fj * D + d] : 0.f;
+      }
+      f32x4_t acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc[t] = mfma16(a[s], bw[t][s], acc[t]);
+      }
+      // lane l, register r: pair 16 mt + 4 grp + r, unit 16 t + p16
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float z = acc[t][r] + ba[t];
+          z = z < 0.f ? 0.f : z;  // relu (NaN propagates, as torch.relu)
+          part[r] = fmaf(z, hh[t], part[r]);
+        }
+      const float sum = row16_transpose_sum<4>(part, p16);  // pair 16 mt + 4 grp + p16 / 4
+      const int q = 16 * mt + 4 * grp + (p16 >> 2);
+      if ((p16 & 3) == 0 && q < P) sc[q] = sum + hb;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+
+    // softmax over the pairs and the contracted weighted sum, pairs lane and lane + 64
+    float sp[2], tp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = lane + 64 * k;
+      const bool pv = p < P;
+      sp[k] = pv ? sc[p] : -INFINITY;
+      float t = 0.f;
+      if (pv) {
+        const int fi = pfi[p], fj = pfj[p];
+#pragma unroll
+        for (int d = 0; d < D; ++d) t = fmaf(e[fi * D + d] * e[fj * D + d], pw[d], t);
+      }
+      tp[k] = t;
+    }
+    const float mx = wave_max(fmaxf(sp[0], sp[1]));
+    float ex[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) ex[k] = lane + 64 * k < P ? expf(sp[k] - mx) : 0.f;
+    const float den = wave_sum(ex[0] + ex[1]);
+    const float afm = wave_sum((ex[0] / den) * tp[0] + (ex[1] / den) * tp[1]) + pb;
+    dl = wave_sum(dl) + dense_b[0];
+    if (lane == 0) {
+      const float t = dl + afm;
+      logit_out[b] = t;
+      prob_out[b] = 1.0f / (1.0f + expf(-t));
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -139,6 +278,33 @@ RK_API int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t 
   const unsigned blocks = (unsigned)std::min<int64_t>((batch + 3) / 4, (int64_t)num_cus() * 8);
   hipStream_t st = (hipStream_t)stream;
   uint32_t* fl = device_flags();
+  static const bool mfma_on = [] {  // RANKOPS_AFM_MFMA=0: the VALU kernel (A/B)
+    const char* e = getenv("RANKOPS_AFM_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  if (mfma_on && (dim == 4 || dim == 8 || dim == 16) && att_factor <= 128) {
+    const int nt = (att_factor + 15) / 16;
+    auto go = [&](auto kern) {
+      kern<<<blocks, 256, 0, st>>>(t, num_fields, batch, dense, ld_dense, num_dense, dense_w, dense_b, att_w, att_b,
+                                   att_factor, att_h, att_hb, p_w, p_b, logit, prob, fl);
+    };
+    auto by_nt = [&](auto ks) {
+      constexpr int KS = decltype(ks)::value;
+      if (nt <= 2)
+        go(afm_mfma_kernel<KS, 2>);
+      else if (nt <= 4)
+        go(afm_mfma_kernel<KS, 4>);
+      else
+        go(afm_mfma_kernel<KS, 8>);
+    };
+    if (dim == 4)
+      by_nt(std::integral_constant<int, 1>{});
+    else if (dim == 8)
+      by_nt(std::integral_constant<int, 2>{});
+    else
+      by_nt(std::integral_constant<int, 4>{});
+    return check_launch("rk_afm_forward");
+  }
   const int upl = (att_factor + 63) / 64;
 #define RK_AFM_LAUNCH(DD, UU)                                                                                    \
   afm_kernel<DD, UU><<<blocks, 256, 0, st>>>(t, num_fields, batch, dense, ld_dense, num_dense, dense_w, dense_b, \

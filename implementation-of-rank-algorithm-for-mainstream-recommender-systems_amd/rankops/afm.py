@@ -81,3 +81,30 @@ class AFM(EngineModule):
         ops.afm_forward(fields, self.embedding_dim, B, dense_input, self.dense_layer.weight, self.dense_layer.bias,
                         att1.weight, att1.bias, att2.weight, att2.bias, self.p.weight, self.p.bias, logit, pred)
         return pred, logit
+
+    def prepare(self, dense_input, category_input):
+        """An eval forward bound to these input tensors (as DCNModel.prepare: the single-kernel analogue
+        of capturing the forward in a hipGraph): returns `run()` that recomputes the forward from the
+        current contents of the inputs with one rk_afm_forward launch and returns the same
+        (pred, logit) tensors each time.  The launch reads the parameters in place, so later weight
+        updates are seen."""
+        if self.training:
+            raise RuntimeError("AFM.prepare: eval mode only (call .eval() first)")
+        dense_input = ops.as_f32(dense_input, "dense_input")
+        B, dev = dense_input.shape[0], dense_input.device
+        idxs = [ops.as_index(category_input[col], f"category_input[{col!r}]") for col in self.category_features]
+        fields = [ops.table_segment(self.embeddings[col].weight, idx, 0)
+                  for col, idx in zip(self.category_features, idxs)]
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        pred = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        att1, att2 = self.attention[0], self.attention[2]
+        args = ops.afm_forward_args(fields, self.embedding_dim, B, dense_input, self.dense_layer.weight,
+                                    self.dense_layer.bias, att1.weight, att1.bias, att2.weight, att2.bias,
+                                    self.p.weight, self.p.bias, logit, pred)
+        fn, out = ops._lib.load().rk_afm_forward, (pred, logit)
+
+        def run():
+            ops.check(fn(*args), "rk_afm_forward")
+            return out
+        run.keep = (args, fields, idxs, dense_input, category_input)
+        return run

@@ -275,15 +275,19 @@ def row_l2norm_mean(x: torch.Tensor, col0: int, ncols: int, scale: float, out: t
     return out
 
 
-def afm_forward(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h, att_hb, p_w, p_b, logit, prob):
-    lib = _lib.load()
+def afm_forward_args(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h, att_hb, p_w, p_b, logit, prob):
+    """The argument tuple of one rk_afm_forward call (the segment array is part of it)."""
     _lib.ensure_device(logit.device)
     arr = _seg_array(fields)
     nd = dense.shape[1] if dense is not None else 0
-    check(lib.rk_afm_forward(arr, len(fields), dim, batch, ptr(dense), dense.stride(0) if dense is not None else 0,
-                             nd, ptr(dense_w), ptr(dense_b), ptr(att_w), ptr(att_b), att_w.shape[0], ptr(att_h),
-                             ptr(att_hb), ptr(p_w), ptr(p_b), ptr(logit), ptr(prob), _lib.stream_of(logit)),
-          "rk_afm_forward")
+    return (arr, len(fields), dim, batch, ptr(dense), dense.stride(0) if dense is not None else 0, nd, ptr(dense_w),
+            ptr(dense_b), ptr(att_w), ptr(att_b), att_w.shape[0], ptr(att_h), ptr(att_hb), ptr(p_w), ptr(p_b),
+            ptr(logit), ptr(prob), _lib.stream_of(logit))
+
+
+def afm_forward(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h, att_hb, p_w, p_b, logit, prob):
+    check(_lib.load().rk_afm_forward(*afm_forward_args(fields, dim, batch, dense, dense_w, dense_b, att_w, att_b, att_h,
+                                                       att_hb, p_w, p_b, logit, prob)), "rk_afm_forward")
 
 
 def _as_seg_array(segs):

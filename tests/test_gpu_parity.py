@@ -28,7 +28,9 @@ CASES = [
     ("din", {"T": 77}),  # more than two 32-position tiles
     ("afm", {}),
     ("afm", {"dim": 32, "att": 64}),
-    ("afm", {"dim": 16, "att": 200}),
+    ("afm", {"dim": 16, "att": 200}),  # > 128 units: the VALU kernel (as dim 32)
+    ("afm", {"dim": 4, "att": 100}),    # the MFMA kernel with a partial unit tile
+    ("afm", {"dim": 16, "att": 128}),
     ("deepcrossing", {}),
     ("deepcrossing", {"units": 3, "internal": 64}),
     ("bst", {"T": 50}),
@@ -333,3 +335,27 @@ def test_linear_tiled_direct():
         z = (x.double() @ w.double().T + b.double()) * sc.double() + sh.double()
         ref = torch.where(z > 0, z, 0.01 * z).float()
         torch.testing.assert_close(y, ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_afm_prepare_equals_forward():
+    """AFM.prepare: the bound one-launch forward equals the module's forward bit for bit and
+    recomputes from the inputs' current contents."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8, "att": 128}
+    model = H.build("afm", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("afm", cfg, 3000, seed=21), "cuda")
+    run = model.prepare(d["dense_input"], d["category_input"])
+    with torch.no_grad():
+        a = tuple(o.clone() for o in run())
+        ref = H.as_tuple(H.call_model(model, "afm", d))
+    for x, y in zip(a, ref):
+        assert torch.equal(x, y)
+    e = H.to_device(H.make_inputs("afm", cfg, 3000, seed=22), "cuda")
+    d["dense_input"].copy_(e["dense_input"])
+    for k in d["category_input"]:
+        d["category_input"][k].copy_(e["category_input"][k])
+    with torch.no_grad():
+        b = run()
+        ref = H.as_tuple(H.call_model(model, "afm", e))
+    for x, y in zip(b, ref):
+        assert torch.equal(x, y)
