@@ -68,6 +68,73 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_kernel(MlpArgs a) {
   MLP_FLUSH(tid);
 }
 
+// The generic tail with its input row gathered in the stage (round 5, rk_mlp_forward_gather): wave w
+// of the 16-row workgroup reads sample m0 + w's columns straight from the segments (a dense block or
+// a table row at the sample's index, rk_concat_gather's column map: the last covering segment wins,
+// uncovered columns and out-of-range rows are zero, the latter flagged) into the layer-0 buffer, so
+// the [M, width] row never goes through HBM.  DeepCrossing's forward (deepcrossing.py:146-163): the
+// residual units and output_layer run on mlp_rows as in mlp_kernel.
+constexpr int kMgSegs = 16;
+constexpr int kMgCols = 256;
+struct MlpGatherArgs {
+  MlpArgs m;
+  rk_segment segs[kMgSegs];
+  uint8_t col_seg[kMgCols], col_off[kMgCols];  // 255: no segment
+  uint32_t* flags;
+};
+static_assert(sizeof(MlpGatherArgs) <= 4096, "kernel arguments beyond 4 KiB");
+
+__global__ __launch_bounds__(kMlpThreads) void mlp_gather_kernel(MlpGatherArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
+  float* const buf0 = sm;
+  float* const buf1 = sm + a.m.off1;
+  const int K0p = pad64(a.m.K0);
+  const bool live = wave < rows;
+  const int64_t b = m0 + wave;
+  // the row's index in every column's segment first (one dependent round trip), the values after
+  float v[kMgCols / 64];
+  int64_t r[kMgCols / 64];
+  int sg[kMgCols / 64];
+  auto stage_issue = [&]() {
+#pragma unroll
+    for (int i = 0; i < kMgCols / 64; ++i) {
+      const int c = lane + 64 * i;
+      sg[i] = live && c < a.m.K0 ? a.col_seg[c] : 255;
+      r[i] = b;
+      if (sg[i] != 255) {
+        const rk_segment& g = a.segs[sg[i]];
+        if (g.idx) {
+          r[i] = g.idx[b * g.idx_stride];
+          if (r[i] < 0 || r[i] >= g.rows) {
+            flag_oob(a.flags);
+            r[i] = -1;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kMgCols / 64; ++i) {
+      v[i] = 0.f;
+      if (sg[i] != 255 && r[i] >= 0) {
+        const rk_segment& g = a.segs[sg[i]];
+        v[i] = g.src[r[i] * g.src_ld + a.col_off[lane + 64 * i]];
+      }
+    }
+  };
+  auto stage_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < kMgCols / 64; ++i) {
+      const int c = lane + 64 * i;
+      if (c < K0p) buf0[wave * a.m.ld0 + c] = v[i];
+    }
+  };
+  mlp_rows<1, false>(a.m.L, a.m.nl, a.m.K0, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, a.m.y, a.m.ldy, tid,
+                     two_phase(stage_issue, stage_store));
+}
+
 // The same tail on a compiled layer plan (mlp_stream.h): one weight stream across the layers.
 // RT = 2 (large batches): 32 rows per workgroup, each weight float4 feeding both 16-row tiles.
 template <class P, int RT>
@@ -574,6 +641,53 @@ RK_API int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, co
   else
     store ? go(mlp_kernel<1, true>, shm) : go(mlp_kernel<1, false>, shm);
   return check_launch("rk_mlp_forward");
+}
+
+RK_API int rk_mlp_forward_gather(const rk_segment* segs, int32_t nseg, int32_t width, int64_t batch,
+                                 const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, void* stream) {
+  if (!segs || nseg <= 0 || nseg > kMgSegs || width <= 0 || width > kMgCols || batch < 0 || !head || !head->head_w)
+    return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward_gather: %d segments (<= %d) over %d columns (<= %d), with a head",
+                nseg, kMgSegs, width, kMgCols);
+  MlpGatherArgs g = {};
+  MlpArgs& a = g.m;
+  a.head = *head;
+  int need0 = 0, need1 = 0;
+  if (int e = mlp_validate(layers, nlayers, width, a.head, &need0, &need1, "rk_mlp_forward_gather")) return e;
+  for (int l = 0; l < nlayers; ++l) {
+    if (layers[l].store) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward_gather: eval only (layer %d stores)", l);
+    a.L[l] = layers[l];
+  }
+  a.nl = nlayers;
+  a.ld0 = need0 + kMlpLdPad;
+  a.ld1 = need1 + kMlpLdPad;
+  a.off1 = kMlpRows * a.ld0;
+  const size_t shm = (size_t)kMlpRows * (a.ld0 + a.ld1) * sizeof(float);
+  if (shm > 160 * 1024) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward_gather: widths need %zu B of LDS", shm);
+  a.M = batch;
+  a.K0 = width;
+  for (int c = 0; c < kMgCols; ++c) {
+    g.col_seg[c] = 255;
+    g.col_off[c] = 0;
+  }
+  for (int i = 0; i < nseg; ++i) {
+    const rk_segment& sg = segs[i];
+    if (!sg.src || sg.dim <= 0 || sg.out_col < 0 || sg.out_col + sg.dim > width || (sg.idx && sg.rows <= 0) ||
+        sg.dim > 255)
+      return fail(RK_ERR_INVALID, "rk_mlp_forward_gather: segment %d invalid", i);
+    g.segs[i] = sg;
+    for (int c = sg.out_col; c < sg.out_col + sg.dim; ++c) {  // the last covering segment wins
+      g.col_seg[c] = (uint8_t)i;
+      g.col_off[c] = (uint8_t)(c - sg.out_col);
+    }
+  }
+  g.flags = device_flags();
+  if (!g.flags) return fail(RK_ERR_RUNTIME, "rk_mlp_forward_gather: device not initialised (rk_init)");
+  if (batch == 0) return RK_OK;
+  const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
+  if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward_gather: batch too large");
+  raise_lds_limit((const void*)mlp_gather_kernel, 160 * 1024);
+  mlp_gather_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(g);
+  return check_launch("rk_mlp_forward_gather");
 }
 
 #ifdef RK_MLP_PHASES

@@ -197,6 +197,8 @@ SIGNATURES = {
     "rk_mlp_pack_weight": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "rk_mlp_forward": (
         ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, _MLP_P, c_int32, _EPI_P, c_void_p, c_int64, c_void_p]),
+    "rk_mlp_forward_gather": (ctypes.c_int, [POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64, _MLP_P,
+                                             ctypes.c_int32, _EPI_P, c_void_p]),
     "rk_fwfm_forward": (ctypes.c_int, [POINTER(Segment), POINTER(Segment), ctypes.c_int32, ctypes.c_int32, c_int64,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_gemm": (ctypes.c_int, [c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p,

@@ -381,6 +381,7 @@ class Layer:
 
 EAGER_CACHE = True  # eval forwards reuse their marshalled launches (EagerCalls); False: rebuild per call
 FUSED_MLP = True  # one rk_mlp_forward launch per tail when the widths fit (see fused_mlp_fits)
+FUSED_GATHER_MLP = True  # DeepCrossing: the row gather inside that launch (rk_mlp_forward_gather)
 FUSED_DIN = True  # DIN: gather + attention + fcn tail + head in one rk_din_forward launch
 FUSED_BST = True  # BST: all transformer blocks + pooling in one rk_bst_forward_blocks launch
 FUSED_BST_FWD = True  # BST at d_model 16: row gather + blocks + pooling + DNN tail in one rk_bst_small_forward

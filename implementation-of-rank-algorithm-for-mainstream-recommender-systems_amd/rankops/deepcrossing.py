@@ -61,6 +61,60 @@ class DeepCrossingModel(common.EngineModule):
     def _load_vocabulary(self, vocab_dir, filename):
         return load_vocabulary(vocab_dir, filename)
 
+    def _mlp_layers(self, units):
+        """rk_mlp_layer records of the residual units (packed images from common.PACKED)."""
+        layers = []
+        for w1, b1, w2, b2 in units:
+            layers.append(ops.make_mlp_layer(w1, common.PACKED(w1), bias=b1, act="relu"))
+            layers.append(ops.make_mlp_layer(w2, common.PACKED(w2), bias=b2, act="relu", residual=1))
+        return layers
+
+    def prepare(self, dense, category):
+        """An eval forward bound to these input tensors (as DCNModel.prepare): returns `run()` that
+        recomputes the forward from the current contents of the inputs with one
+        rk_mlp_forward_gather launch (row gather + every residual unit + output_layer + sigmoid) and
+        returns the same (prob, logit) tensors each time.  Frozen residual weights only (per-call
+        mode redraws them every forward)."""
+        if self.training:
+            raise RuntimeError("DeepCrossingModel.prepare: eval mode only (call .eval() first)")
+        if self.residual_weights.mode != "frozen":
+            raise RuntimeError("DeepCrossingModel.prepare: per-call residual weights are redrawn every forward; "
+                               "use interaction_weights='frozen'")
+        dense = ops.as_f32(dense, "dense")
+        B, dev = dense.shape[0], dense.device
+        segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
+        col, idxs = self.num_dense_features, []
+        for name, emb in self.embeddings.items():
+            idx = ops.as_index(category[name], f"category[{name!r}]")
+            idxs.append(idx)
+            segs.append(ops.table_segment(emb.weight, idx, col))
+            col += emb.embedding_dim
+        units = self.residual_weights.get(dev)
+        widths = [w for _ in units for w in (self.residual_internal_dim, self.input_dim)]
+        if not (units and common.FUSED_MLP and fused_mlp_fits(self.input_dim, widths) and len(segs) <= 16
+                and self.input_dim <= 256):
+            raise RuntimeError("DeepCrossingModel.prepare: configuration outside rk_mlp_forward_gather's envelope")
+        logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
+        head = ops.make_epilogue(head_w=self.output_layer.weight, head_b=self.output_layer.bias, head_logit=logit,
+                                 head_prob=prob)
+        for w1, _, w2, _ in units:  # the images the launch binds are never rewritten in place under it
+            common.PACKED.pin(w1)
+            common.PACKED.pin(w2)
+        packed = [common.PACKED(w) for w1, _, w2, _ in units for w in (w1, w2)]
+        layers = self._mlp_layers(units)
+        ops._lib.ensure_device(dev)
+        larr = (ops._lib.MlpLayer * len(layers))(*layers)
+        args = (ops._seg_array(segs), len(segs), self.input_dim, B, larr, len(layers), ops.ctypes.byref(head),
+                ops._lib.stream_of(prob))
+        fn, out = ops._lib.load().rk_mlp_forward_gather, (prob, logit)
+
+        def run():
+            ops.check(fn(*args), "rk_mlp_forward_gather")
+            return out
+        run.keep = (args, head, packed, units, segs, idxs, dense, category)
+        return run
+
     def forward(self, dense, category):
         # no BatchNorm / Dropout: train mode computes the eval forward; with autograd recording it
         # runs under rankops.train._DeepCrossingTrain (HIP backward)
@@ -78,8 +132,6 @@ class DeepCrossingModel(common.EngineModule):
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             idx = [ops.as_index(category[name], f"category[{name!r}]") for name in self.embeddings]
             return train.deepcrossing_train_forward(self, dense, idx, self.residual_weights.get(dev))
-        x = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
-        ops.concat_gather(segs, B, x)
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)
         prob = torch.empty(B, 1, device=dev, dtype=torch.float32)
         head = dict(head_w=self.output_layer.weight, head_b=self.output_layer.bias, head_logit=logit,
@@ -87,7 +139,19 @@ class DeepCrossingModel(common.EngineModule):
         units = self.residual_weights.get(dev)
         I = self.residual_internal_dim
         widths = [w for _ in units for w in (I, self.input_dim)]
-        if units and common.FUSED_MLP and fused_mlp_fits(self.input_dim, widths):
+        fused = units and common.FUSED_MLP and fused_mlp_fits(self.input_dim, widths)
+        if fused and common.FUSED_GATHER_MLP and len(segs) <= 16 and self.input_dim <= 256:
+            # the row gather, every residual unit, output_layer and sigmoid in one launch
+            layers = self._mlp_layers(units)
+            ops._lib.ensure_device(dev)
+            ops.check(ops._lib.load().rk_mlp_forward_gather(ops._seg_array(segs), len(segs), self.input_dim, B,
+                                                            (ops._lib.MlpLayer * len(layers))(*layers), len(layers),
+                                                            ops.ctypes.byref(ops.make_epilogue(**head)),
+                                                            ops._lib.stream_of(prob)), "rk_mlp_forward_gather")
+            return prob, logit
+        x = torch.empty(B, self.input_dim, device=dev, dtype=torch.float32)
+        ops.concat_gather(segs, B, x)
+        if fused:
             # all residual units + output_layer + sigmoid in one launch
             layers = []
             for w1, b1, w2, b2 in units:

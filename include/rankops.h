@@ -384,6 +384,15 @@ int rk_mlp_pack_epilogue(const rk_mlp_layer* layers, int32_t nlayers, int32_t K0
 int rk_mlp_forward(const float* x, int64_t ldx, int64_t M, int32_t K0, const rk_mlp_layer* layers,
                    int32_t nlayers, const rk_epilogue* head, float* y, int64_t ldy, void* stream);
 
+/* rk_concat_gather + rk_mlp_forward in one launch (eval, generic tail with residual layers, a head):
+ * each 16-row workgroup gathers its rows' `width` columns from the segments (rk_concat_gather's
+ * column map: the last covering segment wins, uncovered columns are zero, out-of-range rows are
+ * zero and raise RK_FLAG_INDEX_OOB) straight into the first layer's LDS buffer.  nseg <= 16,
+ * width <= 256, head->head_w required, no layer stores.  Replaces the reference's
+ * torch.cat(dense, embeddings) + residual stack + output layer (deepcrossing.py:146-163).       */
+int rk_mlp_forward_gather(const rk_segment* segs, int32_t nseg, int32_t width, int64_t batch,
+                          const rk_mlp_layer* layers, int32_t nlayers, const rk_epilogue* head, void* stream);
+
 /* Whole DCN eval forward in one launch (DCNModel.forward, dcn.py:161-180): gather of the row from
  * segs (out_col ascending from 0, at most 8 segments, width <= 256), num_layers cross layers
  * (weights [L, width] as rk_dcn_cross), the MLP tail as rk_mlp_forward (layers packed) and the head:

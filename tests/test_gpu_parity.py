@@ -359,3 +359,48 @@ def test_afm_prepare_equals_forward():
         ref = H.as_tuple(H.call_model(model, "afm", e))
     for x, y in zip(b, ref):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_deepcrossing_prepare_equals_forward():
+    """DeepCrossingModel.prepare: the bound gather + residual-MLP launches equal the module's forward
+    bit for bit and recompute from the inputs' current contents."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "internal": 128, "units": 1, "interaction_weights": "frozen"}
+    model = H.build("deepcrossing", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("deepcrossing", cfg, 3000, seed=23), "cuda")
+    run = model.prepare(d["dense"], d["category"])
+    with torch.no_grad():
+        a = tuple(o.clone() for o in run())
+        ref = H.as_tuple(H.call_model(model, "deepcrossing", d))
+    for x, y in zip(a, ref):
+        assert torch.equal(x, y)
+    e = H.to_device(H.make_inputs("deepcrossing", cfg, 3000, seed=24), "cuda")
+    d["dense"].copy_(e["dense"])
+    for k in d["category"]:
+        d["category"][k].copy_(e["category"][k])
+    with torch.no_grad():
+        b = run()
+        ref = H.as_tuple(H.call_model(model, "deepcrossing", e))
+    for x, y in zip(b, ref):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_deepcrossing_fused_gather_equals_two_launches(monkeypatch):
+    """rk_mlp_forward_gather (the row gather inside the residual MLP's launch) against
+    rk_concat_gather + rk_mlp_forward: bit-identical outputs (same staged values, same tail), and an
+    out-of-range index reads a zero row and raises RK_FLAG_INDEX_OOB in both."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "internal": 64, "units": 2, "interaction_weights": "frozen"}
+    model = H.build("deepcrossing", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("deepcrossing", cfg, 1037, seed=25), "cuda")
+    name = next(iter(d["category"]))
+    d["category"][name][7] = model.embeddings[name].num_embeddings  # one past the table
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(rankops.common, "FUSED_GATHER_MLP", fused)
+        rankops.error_flags(reset=True)
+        with torch.no_grad():
+            outs[fused] = tuple(o.clone() for o in H.as_tuple(H.call_model(model, "deepcrossing", d)))
+        assert rankops.error_flags(reset=True) & 1
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
