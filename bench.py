@@ -963,6 +963,12 @@ def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
         tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
         res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
         res["step"] = "prepared launch (rk_mlp_forward_gather)"
+    elif name == "fwfm":
+        # one kernel (rk_fwfm_forward): FwFM.prepare binds it to the inputs; graph replay beside it
+        run = model.prepare(inp["x"])
+        tg = max_over_ranks(world, time_replays(g.replay, steps, warmup, world))
+        res["graph_replay_ms_per_step"] = round(1e3 * tg / steps, 4)
+        res["step"] = "prepared launch (rk_fwfm_forward)"
     elif name == "bst_ref":
         # at the reference script's d_model 16 the whole BST forward is one kernel too
         # (rk_bst_small_forward): BSTModel.prepare binds it to the inputs; graph replay beside it

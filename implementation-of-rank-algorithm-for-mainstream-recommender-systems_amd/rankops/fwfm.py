@@ -73,6 +73,30 @@ class FwFM(EngineModule):
         ops.check(ops._lib.load().rk_fwfm_forward(*args), "rk_fwfm_forward")
         return (prob, logit) if return_logit else prob
 
+    def prepare(self, x):
+        """An eval forward bound to these index tensors (as DCNModel.prepare): returns `run()` that
+        recomputes (prob, logit) [B] from the indices' current contents with one rk_fwfm_forward
+        launch, into the same tensors each time.  The launch reads the parameters in place."""
+        if self.training:
+            raise RuntimeError("FwFM.prepare: eval mode only (call .eval() first)")
+        idxs = [ops.as_index(x[name], f"x[{name!r}]") for name in self.field_names]
+        B, dev = idxs[0].shape[0], idxs[0].device
+        emb = ops._seg_array([ops.table_segment(self.embedding[f].weight, idx, 0) for f, idx in enumerate(idxs)])
+        lin = ops._seg_array([ops.table_segment(self.linear[f].weight, idx, 0) for f, idx in enumerate(idxs)])
+        prob = torch.empty(B, device=dev, dtype=torch.float32)
+        logit = torch.empty(B, device=dev, dtype=torch.float32)
+        fw, bias = ops.as_f32(self.field_weight, "field_weight"), ops.as_f32(self.bias, "bias")
+        ops._lib.ensure_device(dev)
+        args = (emb, lin, len(idxs), self.embed_dim, B, fw.data_ptr(), bias.data_ptr(), logit.data_ptr(),
+                prob.data_ptr(), ops._lib.stream_of(prob))
+        fn, out = ops._lib.load().rk_fwfm_forward, (prob, logit)
+
+        def run():
+            ops.check(fn(*args), "rk_fwfm_forward")
+            return out
+        run.keep = (args, idxs, fw, bias, x)
+        return run
+
     def forward(self, x, *, return_logit=False):
         """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit).
         Under .train() with autograd on, the probabilities carry the HIP backward (rankops.train)."""

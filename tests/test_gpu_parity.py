@@ -404,3 +404,24 @@ def test_deepcrossing_fused_gather_equals_two_launches(monkeypatch):
         assert rankops.error_flags(reset=True) & 1
     for a, b in zip(outs[True], outs[False]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_fwfm_prepare_equals_forward():
+    """FwFM.prepare: the bound launch equals the module's forward bit for bit, and recomputes from
+    the indices' current contents."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8}
+    model = H.build("fwfm", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("fwfm", cfg, 3000, seed=26), "cuda")
+    run = model.prepare(d["x"])
+    with torch.no_grad():
+        prob, logit = (o.clone() for o in run())
+        ref_p, ref_l = model(d["x"], return_logit=True)
+    assert torch.equal(prob, ref_p) and torch.equal(logit, ref_l)
+    e = H.to_device(H.make_inputs("fwfm", cfg, 3000, seed=27), "cuda")
+    for k in d["x"]:
+        d["x"][k].copy_(e["x"][k])
+    with torch.no_grad():
+        prob, logit = run()
+        ref_p, ref_l = model(e["x"], return_logit=True)
+    assert torch.equal(prob, ref_p) and torch.equal(logit, ref_l)
