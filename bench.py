@@ -1060,7 +1060,7 @@ def main():
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "afm":
                 r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_mfma_kernel<2,8>"])
-                r["roofline"].update(counter_fields("afm_kernel", "afm"))
+                r["roofline"].update(counter_fields("afm_mfma_kernel", "afm"))
             if name == "deepcrossing":
                 r["roofline"] = small_forward_roofline(m2, "deepcrossing", inp2, batch, DEEPCROSSING_FLOP,
                                                        DEEPCROSSING_BYTES, ["mlp_gather_kernel"])
