@@ -47,6 +47,55 @@ __global__ __launch_bounds__(1024) void walk(const float* __restrict__ img, int 
   if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
 }
 
+// Two 16-row tiles per fragment (RT = 2, or two CUs splitting a layer's columns for 32 rows): 8 MFMAs
+// per fragment on two accumulator chains, over half the image
+__global__ __launch_bounds__(1024) void walk_rt2(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[R];
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const float a0 = 1.0f + lane, a1 = 2.0f - lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, ring[j][m], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, ring[j][m], acc1, 0, 0, 0);
+      }
+      if (i + j + R < n) ring[j] = base[((int64_t)wave * n + i + j + R) * 64];
+    }
+  }
+  acc0 += acc1;
+  if (acc0[0] + acc0[1] + acc0[2] + acc0[3] == 12345.f) out[threadIdx.x] = acc0[0];
+}
+
+// walk<1, 4> with the accumulator held in AGPRs (the MFMA's C / D in the accumulation registers, as
+// inline asm; the compiler's own choice is the VGPR form): does keeping the 4-register accumulator
+// out of the VGPR file leave the load returns their write bandwidth?
+__global__ __launch_bounds__(1024) void walk_agpr(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[R];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(ring[j][m]));
+      if (i + j + R < n) ring[j] = base[((int64_t)wave * n + i + j + R) * 64];
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 2" ::: "memory");
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
 int main() {
   float* img;
   float* out;
@@ -113,6 +162,61 @@ int main() {
       const double us = 1e3 * ms / it;
       printf("grid %3d (%2d CUs per XCD) image 896 KiB tile-major mf 4  %8.2f us  %7.1f GB/s per CU\n", grid, grid / 8,
              us, kb * 1024.0 / (us * 1e-6) / 1e9);
+    }
+  }
+  // the same MFMA count per CU from half the bytes: 896 KiB x 4 MFMAs per fragment against 448 KiB x 8
+  for (int round = 0; round < 2; ++round) {
+    for (int mode = 0; mode < 2; ++mode) {
+      const int kb = mode ? 448 : 896, n = kb / kWaves;
+      auto launch = [&]() {
+        if (mode) walk_rt2<<<256, 1024>>>(img, n, out);
+        else walk<1, 4><<<256, 1024>>>(img, n, out);
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      printf("%s  %8.2f us (MFMA floor 13.7 us at 2.1 GHz)\n",
+             mode ? "448 KiB, 8 MFMAs per fragment on 2 chains (32 rows per fragment)"
+                  : "896 KiB, 4 MFMAs per fragment on 1 chain (16 rows per fragment) ", 1e3 * ms / it);
+    }
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int mode = 0; mode < 2; ++mode) {
+      const int kb = 896, n = kb / kWaves;
+      auto launch = [&]() {
+        if (mode) walk_agpr<<<256, 1024>>>(img, n, out);
+        else walk<1, 4><<<256, 1024>>>(img, n, out);
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      printf("896 KiB mf 4, accumulator in %s  %8.2f us\n", mode ? "AGPRs" : "VGPRs", 1e3 * ms / it);
+    }
+  }
+  // more waves per SIMD: two 16-wave workgroups per CU (grid 512: 8 waves per SIMD), each walking
+  // the whole image — twice the work of grid 256; 2x the time means no gain from the extra waves
+  for (int round = 0; round < 2; ++round) {
+    for (int grid : {256, 512}) {
+      const int kb = 896, n = kb / kWaves;
+      for (int w = 0; w < 5; ++w) walk<1, 4><<<grid, 1024>>>(img, n, out);
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) walk<1, 4><<<grid, 1024>>>(img, n, out);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      printf("896 KiB mf 4, grid %d (%d waves per SIMD)  %8.2f us\n", grid, grid / 64, 1e3 * ms / it);
     }
   }
   hipError_t e = hipGetLastError();
