@@ -75,6 +75,12 @@ namespace rk {
 #ifndef RK_STREAM_NT
 #define RK_STREAM_NT 0
 #endif
+// Single-tile layers refill their ring slots two chunks at a time (two loads back to back after
+// every second chunk's MFMAs) instead of one load after each chunk: the same loads, issued in pairs.
+// A probe of the pattern (tools/stream_layout_probe.hip, "loads in pairs") runs 4 % faster.
+#ifndef RK_STREAM_PAIR_REFILL
+#define RK_STREAM_PAIR_REFILL 1
+#endif
 // Ring loads issued ahead of a kEarly stage's dependent loads (the rest right after them).  A/B
 // over two interleaved runs (profiles/r04/ab_re*.json): DCN 176.0 / 179.8 M with the whole ring
 // ahead (8), 181.0 / 183.0 M at 2, 181.4 / 179.5 at 0, 179.0 / 180.6 at 4; DeepFM within noise.
@@ -450,11 +456,20 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           });
         });
         // refill the slots just read with the stream's next loads (past this layer: the next
-        // layer's first chunks)
-        static_for<0, T>([&](auto JI) {
-          constexpr int j = JI;
-          issue(std::integral_constant<int, B0 + c * T + j + R>{});
-        });
+        // layer's first chunks); single-tile layers: in pairs, after every second chunk
+        if constexpr (RK_STREAM_PAIR_REFILL && T == 1) {
+          if constexpr ((c - CB) % 2 == 1) {
+            issue(std::integral_constant<int, B0 + c - 1 + R>{});
+            issue(std::integral_constant<int, B0 + c + R>{});
+          } else if constexpr (c + 1 == KC) {
+            issue(std::integral_constant<int, B0 + c + R>{});
+          }
+        } else {
+          static_for<0, T>([&](auto JI) {
+            constexpr int j = JI;
+            issue(std::integral_constant<int, B0 + c * T + j + R>{});
+          });
+        }
         __builtin_amdgcn_sched_barrier(0);
         // the stage's side work, once, beside the MFMAs of layer kSideL (default: the second),
         // staggered over the SIMD's four waves (wave w sits at position w / 4 of SIMD w % 4): wave

@@ -96,6 +96,51 @@ __global__ __launch_bounds__(1024) void walk_agpr(const float* __restrict__ img,
   if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
 }
 
+// The same MFMA stream with its B fragments read from LDS (a 64-KiB resident image, ds_read_b128)
+// instead of global memory: the cost of the VMEM instructions themselves
+__global__ __launch_bounds__(1024) void walk_lds(const float* __restrict__ img, int n, float* out) {
+  __shared__ f4 lds[64 * 64];  // 64 fragments of 1 KiB
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 64 * 64; i += 1024) lds[i] = reinterpret_cast<const f4*>(img)[i];
+  __syncthreads();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+  f4 cur = lds[((wave * 4) & 63) * 64 + lane];
+  for (int i = 0; i < n; ++i) {
+    const f4 nxt = lds[((wave * 4 + i + 1) & 63) * 64 + lane];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, cur[m], acc, 0, 0, 0);
+    cur = nxt;
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
+// walk<1, 4> with the ring refilled two fragments at a time (two loads back to back, then their 8
+// MFMAs): the same instruction counts, a different issue pattern
+__global__ __launch_bounds__(1024) void walk_pairs(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[R];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; j += 2) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j][m], acc, 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j + 1][m], acc, 0, 0, 0);
+      if (i + j + R < n) {
+        ring[j] = base[((int64_t)wave * n + i + j + R) * 64];
+        ring[j + 1] = base[((int64_t)wave * n + i + j + 1 + R) * 64];
+      }
+    }
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
 int main() {
   float* img;
   float* out;
@@ -217,6 +262,27 @@ int main() {
       float ms;
       hipEventElapsedTime(&ms, a, b);
       printf("896 KiB mf 4, grid %d (%d waves per SIMD)  %8.2f us\n", grid, grid / 64, 1e3 * ms / it);
+    }
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int mode = 0; mode < 3; ++mode) {
+      const int kb = 896, n = kb / kWaves;
+      auto launch = [&]() {
+        if (mode == 0) walk<1, 4><<<256, 1024>>>(img, n, out);
+        else if (mode == 1) walk_lds<<<256, 1024>>>(img, n, out);
+        else walk_pairs<<<256, 1024>>>(img, n, out);
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      const char* nm[] = {"global fragments, one load per 4 MFMAs", "LDS fragments (ds_read_b128)",
+                          "global fragments, loads in pairs"};
+      printf("896-KiB walk mf 4: %-40s %8.2f us\n", nm[mode], 1e3 * ms / it);
     }
   }
   hipError_t e = hipGetLastError();
