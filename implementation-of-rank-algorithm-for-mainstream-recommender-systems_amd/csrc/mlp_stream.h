@@ -75,11 +75,13 @@ namespace rk {
 #ifndef RK_STREAM_NT
 #define RK_STREAM_NT 0
 #endif
-// Single-tile layers refill their ring slots two chunks at a time (two loads back to back after
-// every second chunk's MFMAs) instead of one load after each chunk: the same loads, issued in pairs.
-// A probe of the pattern (tools/stream_layout_probe.hip, "loads in pairs") runs 4 % faster.
-#ifndef RK_STREAM_PAIR_REFILL
-#define RK_STREAM_PAIR_REFILL 1
+// Ring refills in groups: a layer's chunks refill their slots RK_STREAM_REFILL_GROUP loads at a time
+// (the loads of max(1, GROUP / T) consecutive chunks back to back after the last of them's MFMAs)
+// instead of T loads after every chunk: the same loads, issued in bursts.  The layout probe
+// (tools/stream_layout_probe.hip, a 1-KiB load per 4 MFMAs) runs 19.6 / 18.7 / 18.1 / 20.9 µs
+// refilling 1 / 2 / 4 / 8 at a time; 1 is the round-4 order.
+#ifndef RK_STREAM_REFILL_GROUP
+#define RK_STREAM_REFILL_GROUP 4
 #endif
 // Ring loads issued ahead of a kEarly stage's dependent loads (the rest right after them).  A/B
 // over two interleaved runs (profiles/r04/ab_re*.json): DCN 176.0 / 179.8 M with the whole ring
@@ -456,19 +458,16 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
           });
         });
         // refill the slots just read with the stream's next loads (past this layer: the next
-        // layer's first chunks); single-tile layers: in pairs, after every second chunk
-        if constexpr (RK_STREAM_PAIR_REFILL && T == 1) {
-          if constexpr ((c - CB) % 2 == 1) {
-            issue(std::integral_constant<int, B0 + c - 1 + R>{});
-            issue(std::integral_constant<int, B0 + c + R>{});
-          } else if constexpr (c + 1 == KC) {
-            issue(std::integral_constant<int, B0 + c + R>{});
+        // layer's first chunks), CG chunks' loads at a time
+        {
+          constexpr int CG = RK_STREAM_REFILL_GROUP / T > 1 ? RK_STREAM_REFILL_GROUP / T : 1;
+          if constexpr ((c - CB + 1) % CG == 0 || c + 1 == KC) {
+            constexpr int c0 = c - (c - CB) % CG;
+            static_for<c0 * T, (c + 1) * T>([&](auto GI) {
+              constexpr int g = GI;
+              issue(std::integral_constant<int, B0 + g + R>{});
+            });
           }
-        } else {
-          static_for<0, T>([&](auto JI) {
-            constexpr int j = JI;
-            issue(std::integral_constant<int, B0 + c * T + j + R>{});
-          });
         }
         __builtin_amdgcn_sched_barrier(0);
         // the stage's side work, once, beside the MFMAs of layer kSideL (default: the second),

@@ -141,6 +141,32 @@ __global__ __launch_bounds__(1024) void walk_pairs(const float* __restrict__ img
   if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
 }
 
+// walk<1, 4> with the ring refilled G fragments at a time (G loads back to back after G fragments' MFMAs)
+template <int G>
+__global__ __launch_bounds__(1024) void walk_groups(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[R];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; j += G) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j + g][m], acc, 0, 0, 0);
+      if (i + j + R < n) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) ring[j + g] = base[((int64_t)wave * n + i + j + g + R) * 64];
+      }
+    }
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
 int main() {
   float* img;
   float* out;
@@ -283,6 +309,26 @@ int main() {
       const char* nm[] = {"global fragments, one load per 4 MFMAs", "LDS fragments (ds_read_b128)",
                           "global fragments, loads in pairs"};
       printf("896-KiB walk mf 4: %-40s %8.2f us\n", nm[mode], 1e3 * ms / it);
+    }
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int g : {1, 2, 4, 8}) {
+      const int kb = 896, n = kb / kWaves;
+      auto launch = [&]() {
+        if (g == 1) walk_groups<1><<<256, 1024>>>(img, n, out);
+        else if (g == 2) walk_groups<2><<<256, 1024>>>(img, n, out);
+        else if (g == 4) walk_groups<4><<<256, 1024>>>(img, n, out);
+        else walk_groups<8><<<256, 1024>>>(img, n, out);
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      printf("896-KiB walk mf 4: ring refilled %d at a time  %8.2f us\n", g, 1e3 * ms / it);
     }
   }
   hipError_t e = hipGetLastError();
