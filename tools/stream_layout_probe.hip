@@ -167,6 +167,38 @@ __global__ __launch_bounds__(1024) void walk_groups(const float* __restrict__ im
   if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
 }
 
+// walk_groups<4> with the wave's priority raised around its MFMA burst (P = 1) or around its load
+// burst (P = 2)
+template <int P>
+__global__ __launch_bounds__(1024) void walk_prio(const float* __restrict__ img, int n, float* out) {
+  constexpr int G = 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[R];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < R; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; j += G) {
+      if (P == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j + g][m], acc, 0, 0, 0);
+      if (P == 1) __builtin_amdgcn_s_setprio(0);
+      if (P == 2) __builtin_amdgcn_s_setprio(1);
+      if (i + j + R < n) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) ring[j + g] = base[((int64_t)wave * n + i + j + g + R) * 64];
+      }
+      if (P == 2) __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
 int main() {
   float* img;
   float* out;
@@ -329,6 +361,26 @@ int main() {
       float ms;
       hipEventElapsedTime(&ms, a, b);
       printf("896-KiB walk mf 4: ring refilled %d at a time  %8.2f us\n", g, 1e3 * ms / it);
+    }
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int pm = 0; pm < 3; ++pm) {
+      const int kb = 896, n = kb / kWaves;
+      auto launch = [&]() {
+        if (pm == 0) walk_groups<4><<<256, 1024>>>(img, n, out);
+        else if (pm == 1) walk_prio<1><<<256, 1024>>>(img, n, out);
+        else walk_prio<2><<<256, 1024>>>(img, n, out);
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      const char* nm[] = {"refill 4, no priority", "refill 4, setprio 1 over the MFMAs", "refill 4, setprio 1 over the loads"};
+      printf("896-KiB walk mf 4: %-36s %8.2f us\n", nm[pm], 1e3 * ms / it);
     }
   }
   hipError_t e = hipGetLastError();
