@@ -199,6 +199,32 @@ __global__ __launch_bounds__(1024) void walk_prio(const float* __restrict__ img,
   if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
 }
 
+// walk_groups with an RR-deep ring
+template <int RR, int G>
+__global__ __launch_bounds__(1024) void walk_ring(const float* __restrict__ img, int n, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = reinterpret_cast<const f4*>(img) + lane;
+  f4 ring[RR];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float a = 1.0f + lane;
+#pragma unroll
+  for (int i = 0; i < RR; ++i) ring[i] = base[((int64_t)wave * n + i) * 64];
+  for (int i = 0; i < n; i += RR) {
+#pragma unroll
+    for (int j = 0; j < RR; j += G) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          if (i + j + g < n) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ring[j + g][m], acc, 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (i + j + g + RR < n) ring[j + g] = base[((int64_t)wave * n + i + j + g + RR) * 64];
+    }
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.f) out[threadIdx.x] = acc[0];
+}
+
 int main() {
   float* img;
   float* out;
@@ -381,6 +407,31 @@ int main() {
       hipEventElapsedTime(&ms, a, b);
       const char* nm[] = {"refill 4, no priority", "refill 4, setprio 1 over the MFMAs", "refill 4, setprio 1 over the loads"};
       printf("896-KiB walk mf 4: %-36s %8.2f us\n", nm[pm], 1e3 * ms / it);
+    }
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int v = 0; v < 5; ++v) {
+      const int kb = 896, n = kb / kWaves;
+      auto launch = [&]() {
+        switch (v) {
+          case 0: walk_ring<8, 4><<<256, 1024>>>(img, n, out); break;
+          case 1: walk_ring<12, 4><<<256, 1024>>>(img, n, out); break;
+          case 2: walk_ring<16, 4><<<256, 1024>>>(img, n, out); break;
+          case 3: walk_ring<12, 6><<<256, 1024>>>(img, n, out); break;
+          default: walk_ring<16, 8><<<256, 1024>>>(img, n, out); break;
+        }
+      };
+      for (int w = 0; w < 5; ++w) launch();
+      hipEventRecord(a);
+      const int it = 50;
+      for (int w = 0; w < it; ++w) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      const char* nm[] = {"ring 8, bursts of 4", "ring 12, bursts of 4", "ring 16, bursts of 4", "ring 12, bursts of 6",
+                          "ring 16, bursts of 8"};
+      printf("896-KiB walk mf 4: %-22s %8.2f us\n", nm[v], 1e3 * ms / it);
     }
   }
   hipError_t e = hipGetLastError();
