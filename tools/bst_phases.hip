@@ -1,7 +1,8 @@
 // Per-phase cycle breakdown of bst_block_kernel (rk_bst_forward_blocks) on random data.
 // Build + run on the GPU box:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRK_BST_PHASES -I include \
-//     -I <pkg>/csrc tools/bst_phases.hip <pkg>/csrc/runtime.hip -o /tmp/bst_phases && /tmp/bst_phases
+//     -I <pkg>/csrc tools/bst_phases.hip <pkg>/csrc/runtime.hip <pkg>/csrc/bst_small.hip <pkg>/csrc/mlp.hip \
+//     -o tools/bin/bst_phases && tools/bin/bst_phases
 // Phases (thread 0, cycles between consecutive barriers, summed over workgroups):
 //   0 gather | 1 V | 2 Q/K | 3 attention | 4 O-proj | 5 LN1 | 6 FFN1 | 7 FFN2 | 8 LN2 + pooling
 #include <hip/hip_runtime.h>
