@@ -237,7 +237,7 @@ def load_traffic(kernel: str, workload_name: str):
     e = load_counters(kernel, workload_name)
     if not e or "traffic" not in e:
         return None
-    return dict(e["traffic"], file=COUNTERS_FILE, session=e.get("session"))
+    return dict(e["traffic"], file=COUNTERS_FILE, session=e["traffic"].get("session", e.get("session")))
 
 
 def counter_fields(kernel: str, workload_name: str, flop_per_launch: float = None):
