@@ -31,6 +31,11 @@
 namespace rk {
 
 constexpr int kDfMaxFields = 32;
+// weight-ring loads issued ahead of the 30-field row gather (mlp_stream.h RingEarly): 4 against the
+// default 2 measured 54.6 / 55.0 vs 55.6 / 55.9 and 55.8 / 56.5 vs 56.7 / 56.4 us per forward (profiles/r05/ab_early/)
+#ifndef RK_DEEPFM_RING_EARLY
+#define RK_DEEPFM_RING_EARLY 4
+#endif
 constexpr int kDfLayers = 3;
 
 struct DfArgs {
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(kMlpThreads) void deepfm_fused_kernel(std::conditio
     }
   };
   mlp_stream_rows<P, RK_STREAM_EPI, RT, (RT > 1)>(a.L, buf0, a.ld0, buf1, a.ld1, nullptr, m0, rows, a.head, tid,
-                                    side_at<0>(staged(st_index, st_issue, st_store, st_fm)), nullptr, nullptr,
+                                    ring_early<RK_DEEPFM_RING_EARLY>(side_at<0>(staged(st_index, st_issue, st_store, st_fm))), nullptr, nullptr,
                                     fm_lds);
   MLP_MARK(4 * RK_MLP_MAX_LAYERS + 1, k_t0);
   MLP_WALL(4 * RK_MLP_MAX_LAYERS + 3);

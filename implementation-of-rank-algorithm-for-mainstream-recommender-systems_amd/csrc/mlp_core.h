@@ -484,6 +484,24 @@ template <int KS, class S>
 struct PreChunks : S {
   static constexpr int kPreChunks = KS;
 };
+// Ring loads a kEarly stage lets out ahead of its dependent loads (mlp_stream.h), when the stage
+// names a count: RingEarly<N, S> (DeepFM's 30-field row gather: 4; default RK_STREAM_RING_EARLY).
+template <class T, class = void>
+struct stage_ring_early {
+  static constexpr int value = -1;
+};
+template <class T>
+struct stage_ring_early<T, std::void_t<decltype(T::kRingEarly)>> {
+  static constexpr int value = T::kRingEarly;
+};
+template <int N, class S>
+struct RingEarly : S {
+  static constexpr int kRingEarly = N;
+};
+template <int N, class S>
+__device__ __forceinline__ RingEarly<N, S> ring_early(S s) {
+  return RingEarly<N, S>{s};
+}
 template <int L, class S>
 struct SideAt : S {
   static constexpr int kSideLayer = L;

@@ -315,7 +315,8 @@ __device__ __forceinline__ void mlp_stream_class(const rk_mlp_layer* __restrict_
   // kEarly stages: only the first R0 ring loads go out before the stage's dependent loads (DCN /
   // DeepFM: the row gather), so those queue behind R0 KiB per wave in the CU's memory pipe instead
   // of the whole ring (16 waves x 8 KiB); the rest of the ring follows them
-  constexpr int R0 = kEarly ? (RK_STREAM_RING_EARLY < R ? RK_STREAM_RING_EARLY : R) : R;
+  constexpr int kRE = stage_ring_early<Stage>::value >= 0 ? stage_ring_early<Stage>::value : RK_STREAM_RING_EARLY;
+  constexpr int R0 = kEarly ? (kRE < R ? kRE : R) : R;
   static_for<0, R0>([&](auto G) {
     issue(G);
     __builtin_amdgcn_sched_barrier(0);
