@@ -72,6 +72,8 @@ def parse():
                                         "din_per_call,din_zipf,dcn_eager,din_eager,deepfm_eager,bst_eager")
     ap.add_argument("--no-loader", action="store_true", help="skip the host input-path (bucketing) leg")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step legs")
+    ap.add_argument("--details", default=DEFAULT_DETAILS,
+                    help="file for the full result (every leg); the stdout line is the compact summary")
     return ap.parse_args()
 
 
@@ -219,6 +221,19 @@ def graph_kernel_avg_ms(launch, per_graph=20, iters=10):
 COUNTERS_FILE = os.path.join("profiles", "counters.json")  # tools/r04_counters.sh -> tools/pmc_counters.py
 
 
+_LIB_SRC = None  # the loaded librankops.so's source hash (rk_build_info), set in main()
+
+
+def counter_staleness(e: dict) -> str:
+    """Whether a committed counter entry was collected on the library now loaded: "current" when
+    the entry's `src` (the tree source hash at collection, tools/pmc_counters.py) equals the
+    loaded library's, "stale (<src>)" when it differs, "unknown" for entries that predate the tag."""
+    src = e.get("src")
+    if not src or not _LIB_SRC:
+        return "unknown"
+    return "current" if src == _LIB_SRC else f"stale ({src})"
+
+
 def load_counters(kernel: str, workload_name: str):
     """The committed counter digest of `kernel` under `workload_name` (profiles/counters.json: SQ
     MFMA-busy and wait counters, the profiled average duration, PMC HBM bytes), or None."""
@@ -228,7 +243,7 @@ def load_counters(kernel: str, workload_name: str):
     except (OSError, ValueError):
         return None
     if e is not None:
-        e = dict(e, file=COUNTERS_FILE)
+        e = dict(e, file=COUNTERS_FILE, staleness=counter_staleness(e))
     return e
 
 
@@ -237,7 +252,8 @@ def load_traffic(kernel: str, workload_name: str):
     e = load_counters(kernel, workload_name)
     if not e or "traffic" not in e:
         return None
-    return dict(e["traffic"], file=COUNTERS_FILE, session=e["traffic"].get("session", e.get("session")))
+    return dict(e["traffic"], file=COUNTERS_FILE, session=e["traffic"].get("session", e.get("session")),
+                staleness=e["staleness"])
 
 
 def counter_fields(kernel: str, workload_name: str, flop_per_launch: float = None):
@@ -247,8 +263,8 @@ def counter_fields(kernel: str, workload_name: str, flop_per_launch: float = Non
     if not e:
         return {"mfma_busy_frac": None, "counters": None}
     out = {"mfma_busy_frac": e.get("mfma_busy_frac"),
-           "counters": {k: e.get(k) for k in ("file", "session", "mfma_busy_cycles_per_simd", "busy_cycles_per_se",
-                                              "clock_ghz", "trace_avg_ns")}}
+           "counters": {k: e.get(k) for k in ("file", "session", "staleness", "mfma_busy_cycles_per_simd",
+                                              "busy_cycles_per_se", "clock_ghz", "trace_avg_ns")}}
     if flop_per_launch and e.get("trace_avg_ns"):
         out["frac_at_profiled_duration"] = round(flop_per_launch / (e["trace_avg_ns"] * 1e-9) / PEAK_FP32_MFMA, 4)
     return out
@@ -890,6 +906,95 @@ def workload_cfg(name):
                              "interaction_weights": "frozen"}}[name]
 
 
+# ------------------------------------------------------------------ the driver's line
+
+FINAL_LINE_MAX = 8192  # the driver parses the last stdout line out of a tail of ~8 KB
+DEFAULT_DETAILS = os.path.join("gpurun_out", "bench_details.json")
+
+
+def _frac_of(leg: dict):
+    r = leg.get("roofline") or {}
+    if "frac" in r:
+        return r["frac"]
+    b = r.get("batch_4096") or {}
+    return b.get("frac_flop")
+
+
+def models_summary(models: dict) -> dict:
+    """Per extra model leg: samples/s, ms per step and (where it has one) the roofline fraction."""
+    out = {}
+    for k, v in (models or {}).items():
+        if not isinstance(v, dict) or "samples_per_s" not in v:
+            continue
+        e = {"sps": v["samples_per_s"], "ms": v.get("ms_per_step")}
+        f = _frac_of(v)
+        if f is not None:
+            e["frac"] = f
+        if k == "deepfm" and isinstance(v.get("gather_roofline"), dict):
+            g = v["gather_roofline"]
+            e["gather_frac"] = {kk: g[kk]["frac"] for kk in g if isinstance(g[kk], dict) and "frac" in g[kk]}
+        out[k] = e
+    return out
+
+
+def compact_result(full: dict, details_path: str = None) -> dict:
+    """The driver's line: the contract keys, `roofline` with a numeric `traffic`, `cpu_baseline` with
+    its legs reduced to {value, cores, gpu_over_cpu}, and one-line summaries of the extra legs; the
+    full result (every leg's detail) is in `details_path` (bench_details.json)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "build")
+    out = {k: full[k] for k in keep if k in full}
+    r = full.get("roofline")
+    if r:
+        tr = r.get("traffic")
+        ctr = r.get("counters") or {}
+        out["roofline"] = {
+            "kernel": r["kernel"], "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"],
+            "unit": r["unit"], "frac": r["frac"],
+            "traffic": tr["bytes_per_launch"] if isinstance(tr, dict) else tr,
+            "avg_launch_ms": r.get("avg_launch_ms"), "flop_per_launch": r.get("flop_per_launch"),
+            "flop_basis": "reference formulation, SURVEY §8d (1,478,272 flop/sample)",
+            "frac_executed": r.get("frac_executed"), "mfma_busy_frac": r.get("mfma_busy_frac"),
+            "counters": {"session": ctr.get("session"), "staleness": ctr.get("staleness"),
+                         "traffic_session": tr.get("session") if isinstance(tr, dict) else None,
+                         "traffic_staleness": tr.get("staleness") if isinstance(tr, dict) else None,
+                         "file": COUNTERS_FILE}}
+    cb = full.get("cpu_baseline")
+    if cb:
+        c = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "gpu_over_cpu") if k in cb}
+        c["legs"] = {k: {kk: v[kk] for kk in ("value", "cores", "gpu_over_cpu") if kk in v}
+                     for k, v in (cb.get("legs") or {}).items()}
+        out["cpu_baseline"] = c
+    if full.get("models"):
+        out["models"] = models_summary(full["models"])
+    sh = full.get("sharded_deepfm")
+    if isinstance(sh, dict):
+        s = {k: sh[k] for k in ("samples_per_s", "ms_per_step", "scaling", "wire_format", "error") if k in sh}
+        mc = (sh.get("model_curve") or {}).get("curve")
+        if mc:
+            s["model_speedup_pipelined"] = {p: (v.get("speedup_vs_p1") or {}).get("pipelined")
+                                            for p, v in mc.items() if p != "1"}
+        out["sharded_deepfm"] = s
+    if details_path:
+        out["details"] = details_path
+    return out
+
+
+def emit(result: dict, details_path: str):
+    """Write the full result to `details_path`, print a summary of the extras, then the compact
+    line last (asserted under FINAL_LINE_MAX bytes)."""
+    if details_path:
+        os.makedirs(os.path.dirname(os.path.abspath(details_path)), exist_ok=True)
+        with open(details_path, "w") as f:
+            json.dump(result, f, indent=1)
+    line = json.dumps(compact_result(result, details_path))
+    if len(line.encode()) > FINAL_LINE_MAX:  # never let the headline grow past what the driver parses
+        slim = compact_result({k: v for k, v in result.items() if k not in ("models", "sharded_deepfm")},
+                              details_path)
+        line = json.dumps(slim)
+    print(line, flush=True)
+
+
 # ------------------------------------------------------------------ main
 
 def bench_one(name, batch, steps, warmup, world, rank, zipf=None, streams=1):
@@ -1018,6 +1123,8 @@ def main():
     }
     from rankops import _lib as rk_lib
     bi = rk_lib.build_info()
+    global _LIB_SRC
+    _LIB_SRC = bi.get("src")
     result["build"] = {"lib_src_hash": bi.get("src"), "tree_src_hash": bi.get("tree_src"), "arch": bi.get("arch"),
                        "extra_flags": bi.get("extra"),
                        "lib_matches_tree": bi.get("tree_src") is not None and bi.get("src") == bi.get("tree_src")}
@@ -1109,7 +1216,7 @@ def main():
         result["cpu_baseline"] = cpu_baselines(model.cpu(), cfg, result["value"], result.get("models", {}),
                                                args.batch, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(result))
+        emit(result, args.details)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
