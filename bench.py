@@ -390,8 +390,8 @@ def bench_sharded(world, rank, steps, warmup):
         step = model.pipeline(B_l, capture=cats, side_stream=False).step
 
     t = max_over_ranks(world, time_replays(step, steps, max(warmup, 3), world))
-    # bytes this rank sends per step (indices + rows), (P-1)/P of them to peers
-    wire = (B_l * SHARDED_FIELDS * model.index_dtype.itemsize + sum(model.row_splits(B_l)[0]) * 4) * (world - 1) / world
+    # bytes this rank sends per step (indices + rows: row_splits' input splits), (P-1)/P of them to peers
+    wire = (B_l * SHARDED_FIELDS * model.index_dtype.itemsize + sum(model.row_splits(B_l)[1]) * 4) * (world - 1) / world
     return {"samples_per_s": round(SHARDED_GLOBAL_BATCH * steps / t, 1), "ms_per_step": round(1e3 * t / steps, 4),
             "global_batch": SHARDED_GLOBAL_BATCH, "rows_total": SHARDED_FIELDS * SHARDED_ROWS_PER_FIELD,
             "fields_per_rank": len(model.local_fields), "wire_bytes_per_rank_step": int(wire),

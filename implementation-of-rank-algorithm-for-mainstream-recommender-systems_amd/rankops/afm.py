@@ -87,12 +87,12 @@ class AFM(EngineModule):
         of capturing the forward in a hipGraph): returns `run()` that recomputes the forward from the
         current contents of the inputs with one rk_afm_forward launch and returns the same
         (pred, logit) tensors each time.  The launch reads the parameters in place, so later weight
-        updates are seen."""
+        updates are seen.  Index tensors must be int64 (bound by address, never copied)."""
         if self.training:
             raise RuntimeError("AFM.prepare: eval mode only (call .eval() first)")
         dense_input = ops.as_f32(dense_input, "dense_input")
         B, dev = dense_input.shape[0], dense_input.device
-        idxs = [ops.as_index(category_input[col], f"category_input[{col!r}]") for col in self.category_features]
+        idxs = [ops.bound_index(category_input[col], f"category_input[{col!r}]") for col in self.category_features]
         fields = [ops.table_segment(self.embeddings[col].weight, idx, 0)
                   for col, idx in zip(self.category_features, idxs)]
         logit = torch.empty(B, 1, device=dev, dtype=torch.float32)

@@ -275,12 +275,13 @@ class BSTModel(EngineModule):
         single-kernel analogue of capturing the forward in a hipGraph) at the reference script's
         d_model 16: returns `run()` that recomputes the whole forward from the current contents of
         the inputs with one rk_bst_small_forward launch and returns the same (prob, logit) tensors
-        each time.  Binds the current weights (repack-free: the packed tail images are pinned)."""
+        each time.  Binds the current weights (repack-free: the packed tail images are pinned).  Index
+        tensors must be int64 and seq_feedid contiguous (bound by address, never copied)."""
         if self.training:
             raise RuntimeError("BSTModel.prepare: eval mode only (call .eval() first)")
         dense = ops.as_f32(dense, "dense")
-        seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
-        seq_length = ops.as_index(seq_length, "seq_length")
+        seq_feedid = ops.bound_index(seq_feedid, "seq_feedid", contiguous=True)
+        seq_length = ops.bound_index(seq_length, "seq_length")
         B, T = seq_feedid.shape
         dev = dense.device
         blocks = self._fused_blocks(T) if self.transformer_blocks else None
@@ -291,7 +292,7 @@ class BSTModel(EngineModule):
         idx_keep = []
         for name, emb in self.embeddings.items():
             if name in category:
-                idx = ops.as_index(category[name], f"category[{name!r}]")
+                idx = ops.bound_index(category[name], f"category[{name!r}]")
                 idx_keep.append(idx)
                 segs.append(ops.table_segment(emb.weight, idx, col))
                 col += emb.embedding_dim
@@ -322,8 +323,8 @@ class BSTModel(EngineModule):
     def blocks_kernel_launcher(self, seq_feedid, seq_length):
         """Zero-argument re-launch of this forward's rk_bst_forward_blocks kernel (every block +
         pooling) into a scratch DNN row, for kernel-level timing (bench.py BST roofline)."""
-        seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
-        seq_length = ops.as_index(seq_length, "seq_length")
+        seq_feedid = ops.bound_index(seq_feedid, "seq_feedid", contiguous=True)
+        seq_length = ops.bound_index(seq_length, "seq_length")
         B, T = seq_feedid.shape
         blocks = self._fused_blocks(T)
         if blocks is None or not self.transformer_blocks:

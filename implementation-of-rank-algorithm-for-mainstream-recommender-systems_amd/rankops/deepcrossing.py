@@ -73,8 +73,10 @@ class DeepCrossingModel(common.EngineModule):
         """An eval forward bound to these input tensors (as DCNModel.prepare): returns `run()` that
         recomputes the forward from the current contents of the inputs with one
         rk_mlp_forward_gather launch (row gather + every residual unit + output_layer + sigmoid) and
-        returns the same (prob, logit) tensors each time.  Frozen residual weights only (per-call
-        mode redraws them every forward)."""
+        returns the same (prob, logit) tensors each time.  Binds the current weights: the residual
+        units' and the output layer's packed images are pinned, so a later weight update is not seen
+        by run() (prepare again after an update).  Frozen residual weights only (per-call mode redraws
+        them every forward).  Index tensors must be int64 (bound by address, never copied)."""
         if self.training:
             raise RuntimeError("DeepCrossingModel.prepare: eval mode only (call .eval() first)")
         if self.residual_weights.mode != "frozen":
@@ -85,7 +87,7 @@ class DeepCrossingModel(common.EngineModule):
         segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
         col, idxs = self.num_dense_features, []
         for name, emb in self.embeddings.items():
-            idx = ops.as_index(category[name], f"category[{name!r}]")
+            idx = ops.bound_index(category[name], f"category[{name!r}]")
             idxs.append(idx)
             segs.append(ops.table_segment(emb.weight, idx, col))
             col += emb.embedding_dim

@@ -76,10 +76,11 @@ class FwFM(EngineModule):
     def prepare(self, x):
         """An eval forward bound to these index tensors (as DCNModel.prepare): returns `run()` that
         recomputes (prob, logit) [B] from the indices' current contents with one rk_fwfm_forward
-        launch, into the same tensors each time.  The launch reads the parameters in place."""
+        launch, into the same tensors each time.  The launch reads the parameters in place.  Index
+        tensors must be int64 (bound by address, never copied)."""
         if self.training:
             raise RuntimeError("FwFM.prepare: eval mode only (call .eval() first)")
-        idxs = [ops.as_index(x[name], f"x[{name!r}]") for name in self.field_names]
+        idxs = [ops.bound_index(x[name], f"x[{name!r}]") for name in self.field_names]
         B, dev = idxs[0].shape[0], idxs[0].device
         emb = ops._seg_array([ops.table_segment(self.embedding[f].weight, idx, 0) for f, idx in enumerate(idxs)])
         lin = ops._seg_array([ops.table_segment(self.linear[f].weight, idx, 0) for f, idx in enumerate(idxs)])

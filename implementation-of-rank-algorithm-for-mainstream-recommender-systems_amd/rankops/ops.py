@@ -39,6 +39,19 @@ def as_index(t: torch.Tensor, what: str) -> torch.Tensor:
     return t
 
 
+def bound_index(t: torch.Tensor, what: str, contiguous: bool = False) -> torch.Tensor:
+    """An index tensor a prepared launch binds by address (Model.prepare): it must be the caller's
+    own int64 tensor (and contiguous where the kernel reads it as a dense block), since a converted
+    copy would silently stop following later writes to the caller's tensor."""
+    require_gpu(t, what)
+    if t.dtype != torch.int64:
+        raise TypeError(f"rankops: prepare() binds {what} by address; it must be int64 (got {t.dtype}): "
+                        "convert it once and pass the converted tensor")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"rankops: prepare() binds {what} by address; it must be contiguous")
+    return t
+
+
 def as_f32(t: torch.Tensor, what: str) -> torch.Tensor:
     require_gpu(t, what)
     if t.dtype != torch.float32:

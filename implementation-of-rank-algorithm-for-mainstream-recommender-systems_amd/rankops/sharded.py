@@ -160,7 +160,10 @@ class ShardedDeepFM(EngineModule):
                 and 4 <= D <= 256 and D & (D - 1) == 0 and ops.deepfm_whole_plan(len(self.fields) * D, widths))
 
     def _block(self, B: int, F_r: int) -> int:
-        """Floats of one owner's row block for B samples of F_r of its fields."""
+        """Floats of one owner's row block for B samples of F_r of its fields (an owner with no
+        fields, world > fields, sends nothing: no receiver reads an empty owner's partials)."""
+        if F_r == 0:
+            return 0
         if self.split_wire():
             return B * F_r * self.embedding_dim + (B + 3) // 4 * 4
         return B * F_r * row_stride(self.embedding_dim)

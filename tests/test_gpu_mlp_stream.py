@@ -196,6 +196,47 @@ def test_dcn_stream_equals_generic(B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B", [8197, 8192 + 31])
+def test_dcn_row_tiles_ragged(B, monkeypatch):
+    """dcn_fused_kernel's 32-row workgroups (RT = 2, the default from 8,192 rows) at a
+    ragged batch — the last workgroup's second 16-row tile partly or wholly dead, its side waves'
+    cross rows past `rows` — against the 16-row form bit for bit, with an out-of-range index in the
+    second row tile of a workgroup (flagged, a zero row in both), and against the oracle."""
+    import rankops
+    cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
+    model = H.build("dcn", cfg)
+    p = H.cpu_params(model)
+    inp = H.make_inputs("dcn", cfg, B, seed=31)
+    inp["category"]["userid"][32 * 7 + 16 + 5] = model.embeddings["userid"].num_embeddings  # one past the table
+    model = model.cuda().eval()
+    d = H.to_device(inp, "cuda")
+    outs = {}
+    torch.manual_seed(0)  # the frozen cross weights are drawn at the first forward, as the oracle's
+    for rt in ("1", "2", None):
+        if rt is None:
+            monkeypatch.delenv("RANKOPS_DCN_ROW_TILES", raising=False)
+        else:
+            monkeypatch.setenv("RANKOPS_DCN_ROW_TILES", rt)
+        rankops.error_flags(reset=True)
+        with torch.no_grad():
+            outs[rt] = tuple(o.clone() for o in H.as_tuple(H.call_model(model, "dcn", d)) if isinstance(o, torch.Tensor))
+        torch.cuda.synchronize()
+        assert rankops.error_flags(reset=True) & 1, rt
+    for rt in ("2", None):
+        for a, b in zip(outs[rt], outs["1"]):
+            assert torch.equal(a, b), rt
+    # the oracle on the same inputs with the out-of-range row read as zeros (the kernel's contract)
+    emb = p["embeddings.userid.weight"]
+    p["embeddings.userid.weight"] = torch.cat([emb, torch.zeros(1, emb.shape[1])], 0)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        ref = H.as_tuple(H.call_oracle("dcn", cfg, p, inp))
+    for o, r in zip(outs[None], ref):
+        if isinstance(r, torch.Tensor):
+            torch.testing.assert_close(o.cpu(), r, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
 def test_dcn_stream_matches_oracle():
     cfg = {"vocab": H.WECHAT_VOCAB, "interaction_weights": "frozen"}
     model = H.build("dcn", cfg)

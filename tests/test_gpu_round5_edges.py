@@ -84,3 +84,25 @@ def test_mlp_forward_gather_edges():
     want = y @ hw.T + hb
     torch.testing.assert_close(logit, want, atol=ATOL, rtol=RTOL)
     torch.testing.assert_close(prob, torch.sigmoid(want), atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+def test_prepare_rejects_converted_index_copies():
+    """prepare() binds its index tensors by address, so an input that would need a
+    converted copy (int32 indices, a non-contiguous sequence) is refused instead of silently bound
+    to a copy that stops following the caller's tensor."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "dim": 8, "att": 128}
+    model = H.build("afm", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("afm", cfg, 64, seed=3), "cuda")
+    model.prepare(d["dense_input"], d["category_input"])  # int64: bound
+    name = next(iter(d["category_input"]))
+    d["category_input"][name] = d["category_input"][name].int()
+    with pytest.raises(TypeError):
+        model.prepare(d["dense_input"], d["category_input"])
+    cfg = {"vocab": H.WECHAT_VOCAB, "T": 50, "dim": 16, "heads": 4, "max_len": 50}
+    model = H.build("bst", cfg).cuda().eval()
+    d = H.to_device(H.make_inputs("bst", cfg, 64, seed=4), "cuda")
+    wide = torch.zeros(64, 100, dtype=torch.int64, device="cuda")
+    wide[:, ::2] = d["seq_feedid"]
+    with pytest.raises(ValueError):
+        model.prepare(d["dense"], d["category"], wide[:, ::2], d["seq_length"])

@@ -461,3 +461,52 @@ def test_split_and_packed_wire_agree(world):
         _check(outs["packed"][r], expect, r * B_l, (r + 1) * B_l, 1e-4)
         for a, b in zip(outs["split"][r], outs["packed"][r]):
             torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+FIELDS15 = {f"field_{i:02d}": 200 + 11 * i for i in range(15)}
+CFG15 = {"dim": 64, "fields": FIELDS15, "hidden": [512, 256, 128]}
+
+
+@pytest.mark.parametrize("world", [8, 15, 16, 20])
+def test_split_wire_splits_agree_across_ranks(world):
+    """every rank's row all-to-all splits pair up (rank r's receive split from s equals
+    s's send split to r), including owners with no fields when world > fields (15 fields at D = 64,
+    the split format's shape), whose blocks are empty."""
+    shards = [sharded.ShardedDeepFM(FIELDS15, 64, [512, 256, 128], rank=r, world_size=world) for r in range(world)]
+    for B in (1, 7, 300):
+        splits = [sh.row_splits(B) for sh in shards]
+        for r in range(world):
+            assert shards[r].split_wire()
+            for s in range(world):
+                assert splits[r][0][s] == splits[s][1][r], (world, B, r, s)
+            if not shards[r].local_fields:
+                assert sum(splits[r][1]) == 0
+
+
+@pytest.mark.gpu
+def test_split_wire_world_above_fields_on_gpu():
+    """15 fields at D = 64 on 16 emulated ranks (one owns nothing): run_steps and the cross-batch
+    pipeline with the split wire format against the oracle."""
+    full = H.build("deepfm", CFG15, seed=42).cuda()
+    world, B_l = 16, 40
+    shards, emu = _shards(full, world)
+    assert all(sh.split_wire() for sh in shards) and not shards[15].local_fields
+    batches = [H.to_device(H.make_inputs("deepfm", CFG15, B_l * world, seed=5100 + i), "cuda")["category"]
+               for i in range(3)]
+
+    def rank_fn(r):
+        mine = {f: v[r * B_l:(r + 1) * B_l].contiguous() for f, v in batches[0].items()}
+        with torch.no_grad():
+            out = shards[r].run_steps(mine, chunks=1)
+        torch.cuda.synchronize()
+        return tuple(o.cpu() for o in out)
+
+    outs = run_ranks(world, rank_fn, on_error=emu.abort)
+    expect = _oracle(full, CFG15, batches[0])
+    for r in range(world):
+        _check(outs[r], expect, r * B_l, (r + 1) * B_l, 1e-4)
+    piped = _pipe_run(shards, emu, batches, B_l)
+    for i, cat in enumerate(batches):
+        expect = _oracle(full, CFG15, cat)
+        for r in range(world):
+            _check(piped[r][i], expect, r * B_l, (r + 1) * B_l, 1e-4)
