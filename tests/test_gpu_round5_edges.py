@@ -7,6 +7,7 @@ out-of-range index (zero row, flagged)."""
 import pytest
 import torch
 
+import helpers as H
 import rankops
 from rankops import ops
 
