@@ -743,14 +743,17 @@ def bench_train(batch, steps, warmup, name="dcn"):
 # ------------------------------------------------------------------ embedding-gather roofline (DeepFM configs[1])
 
 def gather_roofline(model, inp, cfg, batch, big_batch=65536):
-    """rk_fm_gather alone (fm_gather_kernel: 30 second-order rows of 128 B + 30 first-order
-    weights + 30 indices read, the 3,840 B deep-input row + fm1/fm2 written per sample) over
-    configs[1]'s 30 x 1e6-row tables, timed with HIP events around hipGraph replays of back-to-back
-    launches (graph_kernel_avg_ms: host launch cost excluded), at the config's batch
-    and at a larger batch over the same tables (steady-state rate, launch ramp amortised)."""
+    """rk_fm_gather alone (30 second-order rows of 128 B + 30 first-order weights + 30 indices read,
+    the 3,840-B deep-input row + fm1/fm2 written per sample: 8,048 algorithmic B) over configs[1]'s
+    30 x 1e6-row tables, timed with HIP events around hipGraph replays of back-to-back launches
+    (graph_kernel_avg_ms: host launch cost excluded), at the config's batch and at 65,536 (steady
+    state).  The primary legs read the nn.Embedding weights as they are ([V, 32] rows, one 128-B line
+    each, and the [V, 1] first-order table): fm_gather_kernel (sample-major) at 4,096,
+    fm_gather_fmaj_kernel (field-major, round 6) from 16,384.  `packed_*`: the rk_fm_pack_table
+    layout (one [V, 36] row per index: two 128-B lines), kept for comparison."""
     import helpers as H
-    out = {"kernel": "fm_gather_kernel<8>", "bound": "hbm", "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-           "bytes_per_sample": DEEPFM_GATHER_BYTES,
+    out = {"kernel": "fm_gather_kernel<8, kFmPacked> (4,096) / fm_gather_fmaj_kernel<8, kFmPacked, 6, nt> (65,536)",
+           "bound": "hbm", "peak": PEAK_HBM / 1e9, "unit": "GB/s", "bytes_per_sample": DEEPFM_GATHER_BYTES,
            "tables": "30 fields x 1,000,000 rows x 32 fp32 (3.84 GB) + 30 x 1e6 x 1 (beyond the 256 MiB MALL)"}
     dev = torch.device("cuda", torch.cuda.current_device())
     legs = [(f"batch_{batch}", batch, inp["category"]),
@@ -759,28 +762,20 @@ def gather_roofline(model, inp, cfg, batch, big_batch=65536):
     for b in (batch, big_batch):  # SURVEY §8d cache-sensitivity variant: Zipf(1.1) row popularity
         legs.append((f"zipf_{ZIPF_A}_batch_{b}", b,
                      H.to_device(H.make_inputs("deepfm", dict(cfg, zipf=ZIPF_A), b, seed=4321 + b), dev)["category"]))
-    # the alternative layout: line-aligned [V, 32] second-order rows (one 128-B line
-    # each) and the first-order weights in their own [V, 1] table, i.e. the nn.Embedding weights as
-    # they are (fm_gather_kernel<8, kFmTables>)
-    legs += [(f"tables_batch_{b}", b, c) for (_, b, c) in legs[:2]]
+    legs += [(f"packed_batch_{b}", b, c) for (_, b, c) in legs[:2]]
     for key, b, cat in legs:
-        ms = graph_kernel_avg_ms(model.gather_launcher(cat, packed=not key.startswith("tables")))
+        packed = key.startswith("packed")
+        ms = graph_kernel_avg_ms(model.gather_launcher(cat, packed=packed))
         achieved = DEEPFM_GATHER_BYTES * b / (ms * 1e-3)
-        # (tools/r04_counters.sh: workloads deepfm_gather at the config's batch, deepfm_gather65536)
-        wl = ("deepfm_gather_tables" if key.startswith("tables") else "deepfm_gather") + ("" if b == batch else str(b))
-        tr = load_traffic("fm_gather_kernel", wl) if not key.startswith("zipf") else None
+        # (tools/sessions/r06_counters.sh: workloads deepfm_gather_tables / deepfm_gather at 4,096 and 65,536)
+        wl = ("deepfm_gather" if packed else "deepfm_gather_tables") + ("" if b == batch else str(b))
+        kern = "fm_gather_fmaj_kernel" if b >= 16384 else "fm_gather_kernel"
+        tr = load_traffic(kern, wl) if not key.startswith("zipf") else None
         out[key] = {"avg_launch_ms": round(ms, 5), "achieved": round(achieved / 1e9, 1),
                     "frac": round(achieved / PEAK_HBM, 4), "traffic": tr}
-        if tr:  # PMC-measured HBM bytes at the same launch time
+        if tr:  # PMC-measured HBM bytes (2 x FETCH_SIZE + WRITE_SIZE: every L2 read request is 128 B)
             out[key]["hbm_gb_per_s"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
             out[key]["hbm_frac"] = round(tr["bytes_per_launch"] / (ms * 1e-3) / PEAK_HBM, 4)
-    # the calibrated physical ceiling: a 144-B packed row spans two 128-B lines, so
-    # the gather moves ~30 x 256 B + indices + the 3,848-B write = 11.8 KB per 8,048 algorithmic
-    # bytes; at the guide's ~6.3 TB/s achievable HBM rate the algorithmic fraction tops out at
-    # 6.3 / 8.0 x 8,048 / 11,848 = 0.54
-    out["physical_ceiling_frac"] = round(6.3 / 8.0 * DEEPFM_GATHER_BYTES / (30 * (256 + 8) + 3848 + 8), 3)
-    out["physical_ceiling_basis"] = ("2 x 128-B lines per 144-B packed row + 8-B index per field + 3,848-B "
-                                     "write per sample, at 6.3 TB/s achievable (MI355X_MICROARCH.md)")
     return out
 
 

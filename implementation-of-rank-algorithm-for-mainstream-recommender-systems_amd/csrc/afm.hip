@@ -253,6 +253,185 @@ __global__ __launch_bounds__(256) void afm_mfma_kernel(AfmFields fields, int F, 
   }
 }
 
+// Round 6: the same forward with S samples per wave and their pair rows packed into shared MFMA
+// tiles.  Per wave: lanes (s, f), s < S, f < F, load sample b0 + s's index of field f and its
+// D-float row (float4s) — every load of the S samples issued before the one wait — and stage the
+// rows in LDS; lanes s < S form the dense dot of sample b0 + s meanwhile.  The S x P pair rows
+// (row r = s P + p) fill ceil(S P / 16) tiles of v_mfma_f32_16x16x4_f32 (7 fields, S = 2: 42 rows =
+// 3 tiles, 88 % full, instead of 2 tiles at 66 % per sample), each tile NT independent accumulator
+// chains of depth KS, the W_a fragments in registers as in afm_mfma_kernel.  Scores go to LDS; then
+// LPS = 16 / 32 / 64 lanes per sample (P <= LPS) run the softmax and the contracted weighted sum
+// with segment reductions on DPP and the cross-row permlane swaps.  One wait after the staging and
+// one LDS hand-off per phase for all S samples (afm_mfma_kernel: two per sample, and one for the
+// outputs' stores).  Same arithmetic per pair as afm_mfma_kernel; the per-sample sums run in a
+// different (fixed) order.
+constexpr int kAfmTileMaxRows = 256;  // S * P
+template <int LPS>
+__device__ __forceinline__ float seg_sum(float v) {
+  v = row16_sum(v);
+  if constexpr (LPS >= 32) v = xor16_sum(v);
+  if constexpr (LPS >= 64) v = xor32_sum(v);
+  return v;
+}
+template <int LPS>
+__device__ __forceinline__ float seg_max(float v) {
+  v = row16_max(v);
+  if constexpr (LPS >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  if constexpr (LPS >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  return v;
+}
+
+// softmax + contracted weighted sum of the wave's S samples, LPS lanes per sample (P <= LPS)
+template <int D, int S, int LPS>
+__device__ __forceinline__ void afm_tiles_softmax(const float* e, const float* sc, const uint32_t* rinfo, int P,
+                                                  int64_t b0, int64_t batch, float dl, float db, float pb,
+                                                  const float (&pw)[D], float* __restrict__ logit_out,
+                                                  float* __restrict__ prob_out) {
+  constexpr int SPP = 64 / LPS;  // samples per pass
+  const int lane = threadIdx.x & 63, sl = lane / LPS, p = lane % LPS;
+#pragma unroll
+  for (int s0 = 0; s0 < S; s0 += SPP) {
+    const int s = s0 + sl;
+    const bool v = s < S && p < P && b0 + s < batch;
+    float scr = -INFINITY, tp = 0.f;
+    if (v) {
+      scr = sc[s * P + p];
+      const uint32_t ri = rinfo[s * P + p];
+      const int oi = (int)(ri & 0xffffu) * D, oj = (int)(ri >> 16) * D;
+#pragma unroll
+      for (int d = 0; d < D; ++d) tp = fmaf(e[oi + d] * e[oj + d], pw[d], tp);
+    }
+    const float mx = seg_max<LPS>(scr);
+    const float ex = v ? expf(scr - mx) : 0.f;
+    const float den = seg_sum<LPS>(ex);
+    const float afm = seg_sum<LPS>(v ? (ex / den) * tp : 0.f) + pb;
+    const float dls = __shfl(dl, s < S ? s : 0, kWave) + db;
+    if (p == 0 && s < S && b0 + s < batch) {
+      const float t = dls + afm;
+      logit_out[b0 + s] = t;
+      prob_out[b0 + s] = 1.0f / (1.0f + expf(-t));
+    }
+  }
+}
+
+template <int KS, int NT, int S>
+__global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F, int64_t batch,
+                                                        const float* __restrict__ dense, int64_t ld_dense, int nd,
+                                                        const float* __restrict__ dense_w,
+                                                        const float* __restrict__ dense_b,
+                                                        const float* __restrict__ att_w, const float* __restrict__ att_b,
+                                                        int A, const float* __restrict__ att_h,
+                                                        const float* __restrict__ att_hb, const float* __restrict__ p_w,
+                                                        const float* __restrict__ p_b, float* __restrict__ logit_out,
+                                                        float* __restrict__ prob_out, uint32_t* flags) {
+  constexpr int D = 4 * KS;
+  __shared__ __attribute__((aligned(16))) float emb[4][64 * D];  // S * F <= 64 staged rows per wave
+  __shared__ float score[4][kAfmTileMaxRows];
+  __shared__ uint32_t rinfo[kAfmTileMaxRows];  // pair row r -> staged rows (s F + i) | (s F + j) << 16
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, p16 = lane & 15, grp = lane >> 4;
+  const int P = F * (F - 1) / 2, R = S * P;
+  for (int r = threadIdx.x; r < R; r += 256) {
+    const int s = r / P;
+    int p = r - s * P, i = 0;
+    while (p >= F - 1 - i) {  // pair p -> (i, j), i < j in field order (afm.py:101-108)
+      p -= F - 1 - i;
+      ++i;
+    }
+    rinfo[r] = (uint32_t)(s * F + i) | (uint32_t)(s * F + i + 1 + p) << 16;
+  }
+  const int64_t b0 = ((int64_t)blockIdx.x * 4 + wave) * S;
+  float* e = emb[wave];
+  float* sc = score[wave];
+  // stage: lane (s, f) loads sample b0 + s's row of field f (all loads in flight together)
+  f32x4_t rv[KS];
+  const int SF = S * F;
+  {
+    const float* row = nullptr;
+    if (lane < SF) {
+      const int s = lane / F, f = lane - s * F;
+      const int64_t b = b0 + s;
+      if (b < batch) row = segment_row(fields.s[f], b, flags);
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+      rv[k] = row ? *reinterpret_cast<const f32x4_t*>(row + 4 * k) : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  }
+  float dl = 0.f;
+  if (lane < S && b0 + lane < batch) {
+    const float* x = dense + (b0 + lane) * ld_dense;
+    for (int k = 0; k < nd; ++k) dl = fmaf(x[k], dense_w[k], dl);
+  }
+  // W_a fragments, b_a and h of this lane's unit columns 16 t + p16 (as afm_mfma_kernel)
+  float bw[NT][KS], ba[NT], hh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int a = 16 * t + p16;
+    const bool on = a < A;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bw[t][s] = on ? att_w[(int64_t)a * D + 4 * s + grp] : 0.f;
+    ba[t] = on ? att_b[a] : 0.f;
+    hh[t] = on ? att_h[a] : 0.f;
+  }
+  const float hb = att_hb[0], pb = p_b[0], db = dense_b[0];
+  if (lane < SF) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) *reinterpret_cast<f32x4_t*>(e + lane * D + 4 * k) = rv[k];
+  }
+  __syncthreads();  // rinfo (whole workgroup) and this wave's staged rows
+  if (b0 >= batch) return;
+
+  const int MT = (R + 15) >> 4;
+  for (int mt = 0; mt < MT; ++mt) {
+    const int r = 16 * mt + p16;
+    const bool rvld = r < R;
+    const uint32_t ri = rvld ? rinfo[r] : 0u;
+    const int oi = (int)(ri & 0xffffu) * D, oj = (int)(ri >> 16) * D;
+    float a[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int d = 4 * s + grp;
+      a[s] = rvld ? e[oi + d] * e[oj + d] : 0.f;
+    }
+    f32x4_t acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc[t] = mfma16(a[s], bw[t][s], acc[t]);
+    }
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float z = acc[t][q] + ba[t];
+        z = z < 0.f ? 0.f : z;  // relu (NaN propagates, as torch.relu)
+        part[q] = fmaf(z, hh[t], part[q]);
+      }
+    const float sum = row16_transpose_sum<4>(part, p16);  // pair row 16 mt + 4 grp + p16 / 4
+    const int q = 16 * mt + 4 * grp + (p16 >> 2);
+    if ((p16 & 3) == 0 && q < R) sc[q] = sum + hb;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the scores are in LDS
+  __builtin_amdgcn_wave_barrier();
+
+  float pw[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) pw[d] = p_w[d];
+  if (P <= 16)
+    afm_tiles_softmax<D, S, 16>(e, sc, rinfo, P, b0, batch, dl, db, pb, pw, logit_out, prob_out);
+  else if (P <= 32)
+    afm_tiles_softmax<D, S, 32>(e, sc, rinfo, P, b0, batch, dl, db, pb, pw, logit_out, prob_out);
+  else
+    afm_tiles_softmax<D, S, 64>(e, sc, rinfo, P, b0, batch, dl, db, pb, pw, logit_out, prob_out);
+}
+
 }  // namespace rk
 
 using namespace rk;
@@ -282,6 +461,47 @@ RK_API int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t 
     const char* e = getenv("RANKOPS_AFM_MFMA");
     return !(e && e[0] == '0');
   }();
+  // samples per wave of afm_tiles_kernel (RANKOPS_AFM_S: 0 = afm_mfma_kernel, one sample per wave)
+  const int tile_s = [] {  // read per call (tests switch it)
+    const char* e = getenv("RANKOPS_AFM_S");
+    const int v = e ? atoi(e) : 2;
+    return v == 0 || v == 2 || v == 4 ? v : 2;
+  }();
+  const int P = num_fields * (num_fields - 1) / 2;
+  bool rows16 = true;  // float4 row loads: 16-B aligned rows
+  for (int f = 0; f < num_fields; ++f)
+    rows16 = rows16 && aligned16(fields[f].src) && fields[f].src_ld % 4 == 0;
+  if (mfma_on && tile_s && (dim == 4 || dim == 8 || dim == 16) && att_factor <= 128 && P <= 64 && rows16 &&
+      tile_s * num_fields <= 64 && tile_s * P <= kAfmTileMaxRows) {
+    const int nt = (att_factor + 15) / 16;
+    const unsigned tblocks = (unsigned)((batch + 4 * tile_s - 1) / (4 * tile_s));
+    auto go = [&](auto kern) {
+      kern<<<tblocks, 256, 0, st>>>(t, num_fields, batch, dense, ld_dense, num_dense, dense_w, dense_b, att_w, att_b,
+                                    att_factor, att_h, att_hb, p_w, p_b, logit, prob, fl);
+    };
+    auto by_s = [&](auto ks, auto ntc) {
+      constexpr int KS = decltype(ks)::value, NT = decltype(ntc)::value;
+      if (tile_s == 4)
+        go(afm_tiles_kernel<KS, NT, 4>);
+      else
+        go(afm_tiles_kernel<KS, NT, 2>);
+    };
+    auto by_nt = [&](auto ks) {
+      if (nt <= 2)
+        by_s(ks, std::integral_constant<int, 2>{});
+      else if (nt <= 4)
+        by_s(ks, std::integral_constant<int, 4>{});
+      else
+        by_s(ks, std::integral_constant<int, 8>{});
+    };
+    if (dim == 4)
+      by_nt(std::integral_constant<int, 1>{});
+    else if (dim == 8)
+      by_nt(std::integral_constant<int, 2>{});
+    else
+      by_nt(std::integral_constant<int, 4>{});
+    return check_launch("rk_afm_forward");
+  }
   if (mfma_on && (dim == 4 || dim == 8 || dim == 16) && att_factor <= 128) {
     const int nt = (att_factor + 15) / 16;
     auto go = [&](auto kern) {

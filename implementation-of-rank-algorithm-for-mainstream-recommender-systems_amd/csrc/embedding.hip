@@ -5,6 +5,8 @@
 //   cross:   x_{l+1} = x0 * (x_l @ w_l) + b_l^T + x_l                       dcn.py:47-49
 //   FM:      fm1 = sum_f w_f[idx_f]; fm2 = 0.5*sum_d((sum_f e)^2 - sum_f e^2) deepfm.py:122-140
 //   l2:      lambda * mean_b ||[cat_emb, target, att]_b||_2                 din.py:318-322
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rk {
@@ -150,18 +152,41 @@ __global__ __launch_bounds__(256) void dcn_cross_kernel(SegTable segs, int nseg,
 // batch 65536 over 30 x 1e6-row tables (tools/gather_probe.hip).
 // ------------------------------------------------------------------------------------
 constexpr int kFmMaxFields = 32;
+constexpr int kFmjU = 6;  // fields per round of the field-major kernel
+// descriptor slots: the field-major kernel's fully unrolled rounds read slots up to the next
+// multiple of kFmjU (36); slots past the last field repeat it (filled on the host)
+constexpr int kFmSlots = (kFmMaxFields + kFmjU - 1) / kFmjU * kFmjU;
 // Per-field descriptors as arrays (one pointer/stride per field), so that every lane's loads of
 // its field's descriptor, index and row are branch-free and all issue before the first wait.
 struct FmTables {
-  const float* src2[kFmMaxFields];
-  const float* src1[kFmMaxFields];
-  const int64_t* idx2[kFmMaxFields];
-  const int64_t* idx1[kFmMaxFields];
-  int64_t istride2[kFmMaxFields], istride1[kFmMaxFields];
-  int64_t ld2[kFmMaxFields], ld1[kFmMaxFields];
-  int64_t rows2[kFmMaxFields], rows1[kFmMaxFields];
-  int32_t col[kFmMaxFields];
+  const float* src2[kFmSlots];
+  const float* src1[kFmSlots];
+  const int64_t* idx2[kFmSlots];
+  const int64_t* idx1[kFmSlots];
+  int64_t istride2[kFmSlots], istride1[kFmSlots];
+  int64_t ld2[kFmSlots], ld1[kFmSlots];
+  int64_t rows2[kFmSlots], rows1[kFmSlots];
+  int32_t col[kFmSlots];
 };
+static_assert(sizeof(FmTables) + 64 <= 4096, "kernel arguments beyond 4 KiB");
+
+// Slots [F, kFmSlots) repeat field F - 1 (the field-major kernel's rounds past the last field read
+// a valid descriptor and discard the values).
+inline void fm_fill_slots(FmTables& t, int F) {
+  for (int f = F; f < kFmSlots; ++f) {
+    t.src2[f] = t.src2[F - 1];
+    t.src1[f] = t.src1[F - 1];
+    t.idx2[f] = t.idx2[F - 1];
+    t.idx1[f] = t.idx1[F - 1];
+    t.istride2[f] = t.istride2[F - 1];
+    t.istride1[f] = t.istride1[F - 1];
+    t.ld2[f] = t.ld2[F - 1];
+    t.ld1[f] = t.ld1[F - 1];
+    t.rows2[f] = t.rows2[F - 1];
+    t.rows1[f] = t.rows1[F - 1];
+    t.col[f] = t.col[F - 1];
+  }
+}
 
 // Modes: kFmTables — embedding tables, any index/row strides; kFmPacked — embedding tables with
 // one shared unit-stride index array per field (first- and second-order) and contiguous rows
@@ -250,6 +275,108 @@ __global__ __launch_bounds__(256) void fm_gather_kernel(FmTables t, int F, int64
 #pragma unroll
   for (int o = G / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
   if (lane == 0) {
+    fm2[b] = 0.5f * part;
+    fm1[b] = fo;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// The same gather FIELD-MAJOR (round 6, large batches): a wave owns J = 64 / G samples (lane =
+// sample slot j, quad q) and walks the fields in order, U fields' rows in flight per round, the
+// next round's indices issued before this round's rows are consumed.  What it buys: on gfx950
+// every random access costs one 128-B L2-to-memory request whatever its width (a 4-B first-order
+// weight as much as a 128-B row: tools/gather_probe2.hip, profiles/r06/gather_calib), and the
+// request rate bounds the gather.  Swept field by field by every resident wave at about the same
+// time, field f's first-order table (4 MB at 1e6 rows) is re-read from the on-die caches while the
+// field is being swept, instead of costing a request per lookup as in the sample-major walk.
+// The deep-input rows go out as nontemporal stores (streamed past L2, which then keeps the
+// first-order and index lines).  At batch 65,536 over configs[1]'s tables: 109 us (U = 6) against
+// 131 us with ordinary stores and no index prefetch, and 138 us for the sample-major walk.
+// Per sample the sums run over the fields in order (a different association from
+// fm_gather_kernel's slot-then-shuffle order: the two agree to fp32 rounding, not bit for bit).
+// ------------------------------------------------------------------------------------
+template <int G, int MODE, int U, bool NTS, bool PF_FIRST = true>
+__global__ __launch_bounds__(256) void fm_gather_fmaj_kernel(FmTables t, int F, int64_t batch,
+                                                             float* __restrict__ deep_in, int64_t ld_deep,
+                                                             float* __restrict__ fm1, float* __restrict__ fm2,
+                                                             uint32_t* flags) {
+  static_assert(kFmSlots % U == 0, "rounds must tile the descriptor slots");
+  constexpr int J = 64 / G;
+  constexpr bool kDense = MODE == kFmDense, kPacked = MODE == kFmPacked, kRow = MODE == kFmRowPacked;
+  const int lane = threadIdx.x & 63, q = lane % G, j = lane / G;
+  const int64_t b = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * J + j;
+  const bool live = b < batch;
+  const int64_t bb = live ? b : 0;  // dead slots re-read sample 0 and write nothing
+  f32x4 s = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
+  float fo = 0.f;
+  bool oob = false;
+  int64_t r2[U], r1[U];
+  // the rounds are unrolled over every descriptor slot, so each field's descriptor sits at a
+  // constant kernel-argument offset (one batch of scalar loads per round, no dependent address
+  // arithmetic); rounds past the last field are skipped by a wave-uniform branch
+  auto load_idx = [&](int f0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = f0 + u;
+      if constexpr (kDense) {
+        r2[u] = r1[u] = bb;
+      } else if constexpr (kPacked || kRow) {
+        r2[u] = r1[u] = t.idx2[f][bb];
+      } else {
+        r2[u] = t.idx2[f][bb * t.istride2[f]];
+        r1[u] = t.idx1[f][bb * t.istride1[f]];
+      }
+    }
+  };
+  load_idx(0);
+#pragma unroll
+  for (int f0 = 0; f0 < kFmSlots; f0 += U) {
+    if (f0 >= F) break;
+    f32x4 v[U];
+    float w1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = f0 + u;
+      const bool lf = f < F;
+      const bool ok2 = kDense || (uint64_t)r2[u] < (uint64_t)t.rows2[f];
+      const bool ok1 = kDense || kPacked || kRow ? ok2 : (uint64_t)r1[u] < (uint64_t)t.rows1[f];
+      oob |= live && lf && !(ok2 && ok1);
+      const int64_t ld2 = kPacked ? 4 * G : t.ld2[f], ld1 = kPacked ? 1 : t.ld1[f];
+      const float* row = t.src2[f] + (ok2 ? r2[u] : 0) * ld2;
+      v[u] = *reinterpret_cast<const f32x4*>(row + 4 * q);
+      if constexpr (kRow)
+        w1[u] = row[4 * G];
+      else
+        w1[u] = t.src1[f][(ok1 ? r1[u] : 0) * ld1];
+      if (!ok2) v[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (!(lf && ok1) || q != 0) w1[u] = 0.f;
+    }
+    if (PF_FIRST && f0 + U < kFmSlots && f0 + U < F) load_idx(f0 + U);
+    // straight-line stores (no branch: a join would make the compiler drain the whole vmcnt queue,
+    // the next round's index loads included, behind the stores): a slot past the last field
+    // repeats field F - 1 (descriptor, index, value) and rewrites its bytes; a dead sample slot
+    // carries sample 0's values and rewrites sample 0's row — identical bytes either way.  The
+    // sums take those slots with weight 0.
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row_b = live ? b : 0;
+      f32x4* o = reinterpret_cast<f32x4*>(deep_in + row_b * ld_deep + t.col[f0 + u] + 4 * q);
+      if constexpr (NTS)
+        __builtin_nontemporal_store(v[u], o);
+      else
+        *o = v[u];
+      const float m = f0 + u < F ? 1.f : 0.f;
+      s += v[u] * m;
+      sq += (v[u] * v[u]) * m;
+      fo += w1[u];
+    }
+    if (!PF_FIRST && f0 + U < kFmSlots && f0 + U < F) load_idx(f0 + U);
+  }
+  if (!kDense && oob) flag_oob(flags);
+  float part = (s.x * s.x - sq.x) + (s.y * s.y - sq.y) + (s.z * s.z - sq.z) + (s.w * s.w - sq.w);
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) part += __shfl_xor(part, o, kWave);
+  if (live && q == 0) {
     fm2[b] = 0.5f * part;
     fm1[b] = fo;
   }
@@ -487,10 +614,64 @@ RK_API int rk_fm_gather_packed(const rk_segment* fields, int32_t num_fields, int
 }
 
 namespace rk {
-int launch_fm_gather(const FmTables& t, int mode, int num_fields, int G, int64_t batch, float* deep_in,
+int launch_fm_gather(const FmTables& t0, int mode, int num_fields, int G, int64_t batch, float* deep_in,
                      int64_t ld_deep, float* fm1, float* fm2, hipStream_t st) {
-  const int64_t blocks = (batch + 3) / 4;  // one wave per sample, 4 waves per workgroup
+  FmTables t = t0;
+  fm_fill_slots(t, num_fields);
   uint32_t* fl = device_flags();
+  // field-major from fmaj_min samples (RANKOPS_FM_FMAJ_MIN; 0 = never): at configs[1]'s 4,096 the
+  // sample-major form is the faster (more waves, no sweep to share), at 65,536 the field-major one
+  const int64_t fmaj_min = [] {
+    const char* e = getenv("RANKOPS_FM_FMAJ_MIN");
+    return e ? (int64_t)atoll(e) : (int64_t)16384;
+  }();
+  if (fmaj_min > 0 && batch >= fmaj_min) {
+    const int64_t waves = (batch + 64 / G - 1) / (64 / G);
+    const int64_t fblocks = (waves + 3) / 4;
+    if (fblocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: batch too large");
+    // A/B switch (per call): RANKOPS_FM_FMAJ_VARIANT=1 issues the next round's indices after the
+    // stores instead of before them; =2 also drops the nontemporal hint
+    const char* ve = getenv("RANKOPS_FM_FMAJ_VARIANT");
+    const int variant = ve ? atoi(ve) : 0;
+#define RK_FMJ_LAUNCH(GG, MM)                                                                                   \
+  do {                                                                                                          \
+    if (variant == 1)                                                                                           \
+      fm_gather_fmaj_kernel<GG, MM, kFmjU, true, false>                                                         \
+          <<<(unsigned)fblocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl);           \
+    else if (variant == 2)                                                                                      \
+      fm_gather_fmaj_kernel<GG, MM, kFmjU, false, true>                                                         \
+          <<<(unsigned)fblocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl);           \
+    else                                                                                                        \
+      fm_gather_fmaj_kernel<GG, MM, kFmjU, true, true>                                                          \
+          <<<(unsigned)fblocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl);           \
+  } while (0)
+#define RK_FMJ_CASE(GG)          \
+  case GG:                       \
+    if (mode == kFmDense)        \
+      RK_FMJ_LAUNCH(GG, kFmDense); \
+    else if (mode == kFmPacked)  \
+      RK_FMJ_LAUNCH(GG, kFmPacked); \
+    else if (mode == kFmRowPacked) \
+      RK_FMJ_LAUNCH(GG, kFmRowPacked); \
+    else                         \
+      RK_FMJ_LAUNCH(GG, kFmTables); \
+    break;
+    switch (G) {
+      RK_FMJ_CASE(1)
+      RK_FMJ_CASE(2)
+      RK_FMJ_CASE(4)
+      RK_FMJ_CASE(8)
+      RK_FMJ_CASE(16)
+      RK_FMJ_CASE(32)
+      RK_FMJ_CASE(64)
+      default:
+        return fail(RK_ERR_UNSUPPORTED, "rk_fm_gather: dim %d", 4 * G);
+    }
+#undef RK_FMJ_CASE
+#undef RK_FMJ_LAUNCH
+    return check_launch("rk_fm_gather");
+  }
+  const int64_t blocks = (batch + 3) / 4;  // one wave per sample, 4 waves per workgroup
 #define RK_FM_LAUNCH(GG, MM) \
   fm_gather_kernel<GG, MM><<<(unsigned)blocks, 256, 0, st>>>(t, num_fields, batch, deep_in, ld_deep, fm1, fm2, fl)
 #define RK_FM_CASE(GG)                                   \

@@ -176,12 +176,9 @@ __global__ __launch_bounds__(256) void shard_gather_split_kernel(ShardSplitArgs 
 // F first-order weights) in flight together; grid.y = the source, so no 64-bit divisions by runtime
 // sizes.  The first-order sum keeps the field order and skips out-of-range rows, as above.
 constexpr int kShardSplitU = 8;  // fields per pass
-// nontemporal row loads and send-buffer stores (experiment: each row is read once, the send buffer
-// is read next by the collective)
-#ifndef RK_SHARD_NT
-#define RK_SHARD_NT 0
-#endif
-template <int G>
+// NTS: the send-buffer rows go out as nontemporal stores (streamed past L2: each is read once,
+// next by the collective), so L2 keeps the index and first-order lines (RANKOPS_SHARD_NTS).
+template <int G, bool NTS>
 __global__ __launch_bounds__(256) void shard_gather_split_group_kernel(ShardSplitArgs a) {
   constexpr int S = 256 / G, D = 4 * G;
   const int tid = threadIdx.x, q = tid & (G - 1);
@@ -209,11 +206,7 @@ __global__ __launch_bounds__(256) void shard_gather_split_group_kernel(ShardSpli
         ok[u] = row[u] >= 0 && row[u] < a.rows[j];
         oob |= !ok[u];
         const int64_t r = ok[u] ? row[u] : 0;
-#if RK_SHARD_NT
-        v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.src2[j] + r * a.ld2[j] + 4 * q));
-#else
         v[u] = *reinterpret_cast<const f32x4*>(a.src2[j] + r * a.ld2[j] + 4 * q);
-#endif
         if (q == 0) w[u] = a.src1[j][r * a.ld1[j]];
       }
     }
@@ -222,11 +215,11 @@ __global__ __launch_bounds__(256) void shard_gather_split_group_kernel(ShardSpli
       const int j = j0 + u;
       if (j < F) {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#if RK_SHARD_NT
-        __builtin_nontemporal_store(ok[u] ? v[u] : z, reinterpret_cast<f32x4*>(out + (bp * F + j) * D + 4 * q));
-#else
-        *reinterpret_cast<f32x4*>(out + (bp * F + j) * D + 4 * q) = ok[u] ? v[u] : z;
-#endif
+        f32x4* o = reinterpret_cast<f32x4*>(out + (bp * F + j) * D + 4 * q);
+        if constexpr (NTS)
+          __builtin_nontemporal_store(ok[u] ? v[u] : z, o);
+        else
+          *o = ok[u] ? v[u] : z;
         if (ok[u]) acc += w[u];
       }
     }
@@ -279,12 +272,15 @@ RK_API int rk_shard_gather_rows_split(const rk_segment* second, const rk_segment
   if (!flat && num_sources <= 65535 && (a.G == 4 || a.G == 8 || a.G == 16)) {
     const int S = 256 / a.G;
     const dim3 grid((unsigned)((bc + S - 1) / S), (unsigned)num_sources);
+    const char* ne = getenv("RANKOPS_SHARD_NTS");  // per call (A/B)
+    const bool nts = !(ne && ne[0] == '0');
+    auto go = [&](auto kern) { kern<<<grid, 256, 0, (hipStream_t)stream>>>(a); };
     if (a.G == 8)
-      shard_gather_split_group_kernel<8><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+      nts ? go(shard_gather_split_group_kernel<8, true>) : go(shard_gather_split_group_kernel<8, false>);
     else if (a.G == 4)
-      shard_gather_split_group_kernel<4><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+      nts ? go(shard_gather_split_group_kernel<4, true>) : go(shard_gather_split_group_kernel<4, false>);
     else
-      shard_gather_split_group_kernel<16><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+      nts ? go(shard_gather_split_group_kernel<16, true>) : go(shard_gather_split_group_kernel<16, false>);
     return check_launch("rk_shard_gather_rows_split");
   }
   const int64_t n4 = nrows * num_fields * a.G;

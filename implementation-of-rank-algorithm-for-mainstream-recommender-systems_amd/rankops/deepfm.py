@@ -34,6 +34,8 @@ WECHAT_FIELDS = ("userid", "feedid", "device", "authorid", "bgm_song_id", "bgm_s
 # Eval gather from packed [V, pad4(D+1)] tables (one line pair per row instead of a row line plus
 # a separate line for the 4-B first-order weight; costs one extra table copy in HBM).
 PACKED_TABLES = True
+# rk_fm_gather's field-major switch point (csrc/embedding.hip launch_fm_gather, RANKOPS_FM_FMAJ_MIN)
+FIELD_MAJOR_MIN = 16384
 # Gather + FM + first deep layer in one rk_fm_linear_packed launch when that layer is tiled.
 FUSED_FRONT = True
 # The whole eval forward in one rk_deepfm_forward launch where a plan is compiled for the shape
@@ -92,7 +94,12 @@ class DeepFM(EngineModule):
         first = ops.as_index(category[names[0]], f"category[{names[0]!r}]")
         B, dev = first.shape[0], first.device
         fits = D % 4 == 0 and (D // 4) & (D // 4 - 1) == 0 and D <= 256
-        packed = (PACKED_TABLES if packed is None else packed) and fits
+        if packed is None:
+            # from FIELD_MAJOR_MIN samples the gather runs field-major (fm_gather_fmaj_kernel), where
+            # the [V, D] + [V, 1] weights as they are beat the packed rows (one 128-B request per
+            # row instead of two; the first-order lines are re-read on die): 109 vs 153 us at 65,536
+            packed = PACKED_TABLES and B < FIELD_MAJOR_MIN
+        packed = packed and fits
         second_segs, first_segs = [], []
         for f, name in enumerate(names):
             idx = ops.as_index(category[name], f"category[{name!r}]")

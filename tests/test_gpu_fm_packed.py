@@ -137,3 +137,74 @@ def test_sharded_gather_local_rows_are_packed_rows():
         want[:, :32] = full.second_order_embeddings[f].weight.detach().cpu()[idx]
         want[:, 32] = full.first_order_embeddings[f].weight.detach().cpu()[idx, 0]
         assert torch.equal(got[:, j], want), f
+
+
+def _fm64(tables2, tables1, idx, D):
+    """float64 FM sums and the deep-input row (deepfm.py:122-140), out-of-range rows as zeros."""
+    e, w = [], []
+    for t2, t1, i in zip(tables2, tables1, idx):
+        ok = (i >= 0) & (i < t2.shape[0])
+        ci = i.clamp(0, t2.shape[0] - 1)
+        e.append(t2[ci].double() * ok[:, None])
+        w.append(t1[ci, 0].double() * ok)
+    E = torch.stack(e, 1)
+    fm1 = torch.stack(w, 1).sum(1)
+    fm2 = 0.5 * (E.sum(1) ** 2 - (E ** 2).sum(1)).sum(1)
+    return E.reshape(E.shape[0], -1), fm1, fm2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["tables", "shared_idx", "packed", "dense"])
+@pytest.mark.parametrize("D,B", [(32, 16389), (8, 16400), (64, 16385), (4, 16391)])
+def test_field_major_gather_equals_sample_major(mode, D, B, monkeypatch):
+    """rk_fm_gather / rk_fm_gather_packed's field-major kernel (round 6, from 16,384 samples by
+    default; RANKOPS_FM_FMAJ_MIN) against the sample-major one (RANKOPS_FM_FMAJ_MIN=0) on the same
+    inputs: the deep-input rows bit-identical (copies), fm1 / fm2 within fp32 rounding of each other
+    and of a float64 restatement; ragged batches (the last wave's dead sample slots), 29 fields
+    (the last round of fields partial), an out-of-range index in each mode that takes indices."""
+    dev = "cuda"
+    F, V = 29, 3000
+    g = torch.Generator(device=dev).manual_seed(D + B)
+    t2 = [torch.randn(V, D, device=dev, generator=g) for _ in range(F)]
+    t1 = [torch.randn(V, 1, device=dev, generator=g) for _ in range(F)]
+    idx = [torch.randint(0, V, (B,), device=dev, generator=g) for _ in range(F)]
+    if mode != "dense":
+        idx[7][B - 3] = V  # one past the table: a zero row, flagged
+    E, f1, f2 = _fm64([t.cpu() for t in t2], [t.cpu() for t in t1], [i.cpu() for i in idx], D)
+    outs = {}
+    for fmaj in ("1", "0"):
+        monkeypatch.setenv("RANKOPS_FM_FMAJ_MIN", fmaj)
+        deep = torch.full((B, F * D + 4), float("nan"), device=dev)
+        fm1 = torch.empty(B, device=dev)
+        fm2 = torch.empty(B, device=dev)
+        rankops.error_flags(reset=True)
+        if mode == "packed":
+            packed = [ops.fm_pack_table(a, b, (D + 1 + 3) // 4 * 4) for a, b in zip(t2, t1)]
+            segs = [ops.packed_segment(p, i, D, f * D) for f, (p, i) in enumerate(zip(packed, idx))]
+            ops.fm_gather_packed(segs, D, B, deep, fm1, fm2)
+        elif mode == "dense":  # rows already gathered: row b of a [B, D] block per field
+            rows2 = [t[i] for t, i in zip(t2, idx)]
+            rows1 = [t[i] for t, i in zip(t1, idx)]
+            second = [ops.dense_segment(r, D, f * D) for f, r in enumerate(rows2)]
+            first = [ops.dense_segment(r, 1, f) for f, r in enumerate(rows1)]
+            ops.fm_gather(second, first, D, B, deep, fm1, fm2)
+        else:
+            second = [ops.table_segment(t, i, f * D) for f, (t, i) in enumerate(zip(t2, idx))]
+            if mode == "tables":  # first-order indices through their own (strided) view
+                first = [ops.table_segment(t, i, f) for f, (t, i) in enumerate(zip(t1, [x.clone() for x in idx]))]
+            else:
+                first = [ops.table_segment(t, i, f) for f, (t, i) in enumerate(zip(t1, idx))]
+            ops.fm_gather(second, first, D, B, deep, fm1, fm2)
+        torch.cuda.synchronize()
+        flagged = rankops.error_flags(reset=True) & 1
+        assert bool(flagged) == (mode != "dense"), (fmaj, mode)
+        outs[fmaj] = (deep.clone(), fm1.clone(), fm2.clone())
+    (d1, a1, b1), (d0, a0, b0) = outs["1"], outs["0"]
+    assert torch.equal(d1[:, :F * D], d0[:, :F * D])
+    assert torch.isnan(d1[:, F * D:]).all()  # columns past the fields untouched
+    torch.testing.assert_close(d1[:, :F * D].cpu().double(), E)
+    for got in ((a1, b1), (a0, b0)):
+        torch.testing.assert_close(got[0].cpu().double(), f1, atol=ATOL, rtol=RTOL)
+        torch.testing.assert_close(got[1].cpu().double(), f2, atol=1e-3, rtol=RTOL)
+    torch.testing.assert_close(a1, a0, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(b1, b0, atol=1e-3, rtol=1e-4)

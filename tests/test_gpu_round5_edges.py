@@ -24,8 +24,11 @@ def _afm_reference(tables, idx, dense, dw, db, aw, ab, ah, ahb, pw, pb):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,D,A,B", [(2, 8, 128, 100), (16, 4, 37, 257), (9, 16, 128, 64), (16, 16, 16, 33)])
-def test_afm_mfma_edges(F, D, A, B):
+@pytest.mark.parametrize("S", ["0", "2", "4"])  # afm_mfma_kernel (one sample per wave), afm_tiles_kernel S = 2 / 4
+@pytest.mark.parametrize("F,D,A,B", [(2, 8, 128, 100), (16, 4, 37, 257), (9, 16, 128, 64), (16, 16, 16, 33),
+                                     (7, 8, 128, 4099), (11, 4, 100, 37), (3, 16, 128, 1)])
+def test_afm_mfma_edges(F, D, A, B, S, monkeypatch):
+    monkeypatch.setenv("RANKOPS_AFM_S", S)
     g = torch.Generator(device="cuda").manual_seed(F * 100 + D)
     rows = 50
     tables = [torch.randn(rows, D, device="cuda", generator=g) * 0.5 for _ in range(F)]
@@ -107,3 +110,31 @@ def test_prepare_rejects_converted_index_copies():
     wide[:, ::2] = d["seq_feedid"]
     with pytest.raises(ValueError):
         model.prepare(d["dense"], d["category"], wide[:, ::2], d["seq_length"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", ["0", "2", "4"])
+def test_afm_out_of_range_index_zero_row(S, monkeypatch):
+    """An out-of-range index reads a zero embedding row (and raises RK_FLAG_INDEX_OOB) in every AFM
+    kernel: the outputs equal the reference with that row zeroed."""
+    monkeypatch.setenv("RANKOPS_AFM_S", S)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    F, D, A, B, rows = 7, 8, 128, 77, 40
+    tables = [torch.randn(rows, D, device="cuda", generator=g) * 0.5 for _ in range(F)]
+    idx = [torch.randint(0, rows, (B,), device="cuda", generator=g) for _ in range(F)]
+    idx[3][10] = rows  # one past the table
+    dense = torch.randn(B, 4, device="cuda", generator=g)
+    dw, db = torch.randn(1, 4, device="cuda", generator=g), torch.randn(1, device="cuda", generator=g)
+    aw, ab = torch.randn(A, D, device="cuda", generator=g) * 0.3, torch.randn(A, device="cuda", generator=g) * 0.1
+    ah, ahb = torch.randn(1, A, device="cuda", generator=g) * 0.3, torch.randn(1, device="cuda", generator=g)
+    pw, pb = torch.randn(1, D, device="cuda", generator=g), torch.randn(1, device="cuda", generator=g)
+    logit, prob = torch.empty(B, 1, device="cuda"), torch.empty(B, 1, device="cuda")
+    segs = [ops.table_segment(t, i, 0) for t, i in zip(tables, idx)]
+    rankops.error_flags(reset=True)
+    ops.afm_forward(segs, D, B, dense, dw, db, aw, ab, ah, ahb, pw, pb, logit, prob)
+    torch.cuda.synchronize()
+    assert rankops.error_flags(reset=True) & 1
+    padded = [torch.cat([t, torch.zeros(1, D, device="cuda")]) for t in tables]
+    want_p, want_l = _afm_reference(padded, idx, dense, dw, db, aw, ab, ah, ahb, pw, pb)
+    torch.testing.assert_close(logit, want_l, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(prob, want_p, atol=ATOL, rtol=RTOL)

@@ -49,12 +49,14 @@ def child(P, B, F):
 def main():
     P, B, F = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (8, 8192, 4)))
     res = {}
-    forms = [("grouped", "0", None), ("flat", "1", None)]
+    forms = [("grouped", "0", None), ("grouped_no_nts", "0", None), ("flat", "1", None)]
     for v in filter(None, os.environ.get("SPLIT_VARIANTS", "").split(",")):
         name, lib = v.split("=")
         forms.append((name, "0", os.path.join(ROOT, lib)))
     for form, flat, lib in forms:
         env = dict(os.environ, RANKOPS_SHARD_SPLIT_FLAT=flat)
+        if form == "grouped_no_nts":  # round 6: the grouped form with ordinary send-buffer stores
+            env["RANKOPS_SHARD_NTS"] = "0"
         if lib:
             env["RANKOPS_LIB"] = lib
         out = subprocess.run([sys.executable, __file__, "--child", str(P), str(B), str(F)], env=env,
