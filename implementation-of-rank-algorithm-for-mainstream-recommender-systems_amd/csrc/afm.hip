@@ -464,8 +464,8 @@ RK_API int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t 
   // samples per wave of afm_tiles_kernel (RANKOPS_AFM_S: 0 = afm_mfma_kernel, one sample per wave)
   const int tile_s = [] {  // read per call (tests switch it)
     const char* e = getenv("RANKOPS_AFM_S");
-    const int v = e ? atoi(e) : 2;
-    return v == 0 || v == 2 || v == 4 ? v : 2;
+    const int v = e ? atoi(e) : 4;  // S = 4: 10.97 us at 4,096 (S = 2: 11.18, S = 0: 15.63), profiles/r06/afm_ab.log
+    return v == 0 || v == 2 || v == 4 ? v : 4;
   }();
   const int P = num_fields * (num_fields - 1) / 2;
   bool rows16 = true;  // float4 row loads: 16-B aligned rows
