@@ -43,13 +43,26 @@ def kernel_avg_ns(session, workload, kernel):
     return None, None, 0
 
 
+def tree_src():
+    """The source hash of the library the session ran (rk_build_info's src: the tree's csrc/ and
+    include/ hash, rankops._lib.tree_source_hash), so bench.py can tell a stale counter entry."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "implementation-of-rank-algorithm-for-mainstream-recommender-systems_amd"))
+    try:
+        from rankops import _lib
+        return _lib.tree_source_hash()
+    except Exception:  # no torch here: leave the entry untagged
+        return None
+
+
 def main():
     session = sys.argv[1]
     out_path = os.path.join(session, "counters.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    src = tree_src()
     for spec in sys.argv[2:]:
         workload, kernel = spec.split(":", 1)
-        e = {"session": os.path.basename(os.path.normpath(session))}
+        e = {"session": os.path.basename(os.path.normpath(session)), "src": src}
         sq = {}
         for p in ("a", "b"):
             for k, v in per_dispatch(os.path.join(session, f"sq_{workload}", p), kernel).items():
