@@ -81,6 +81,7 @@ struct MlpGatherArgs {
   rk_segment segs[kMgSegs];
   uint8_t col_seg[kMgCols], col_off[kMgCols];  // 255: no segment
   uint32_t* flags;
+  int nseg;
 };
 static_assert(sizeof(MlpGatherArgs) <= 4096, "kernel arguments beyond 4 KiB");
 
@@ -133,6 +134,163 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_gather_kernel(MlpGatherArgs a
   };
   mlp_rows<1, false>(a.m.L, a.m.nl, a.m.K0, buf0, a.m.ld0, buf1, a.m.ld1, m0, rows, a.m.head, a.m.y, a.m.ldy, tid,
                      two_phase(stage_issue, stage_store));
+}
+
+// DeepCrossing's forward with every weight in registers (round 6): the residual units
+// (deepcrossing.py:25-42: x <- relu(x + W2 relu(W1 x + b1) + b2)) and output_layer over 16 rows per
+// workgroup of 16 waves.  mlp_gather_kernel streams each layer's weights through the 8-slot ring
+// and fetches the second layer's only after the first layer's MFMAs (an L2 round trip at every
+// layer boundary); here the whole image of the workgroup's tiles (50 -> 128 -> 50: 64 KiB, 16 or 48
+// VGPRs per wave) is loaded at entry, beside the row gather's index round trip, so the only
+// exposed latency is index -> row.  Work split as mlp_rows (wave w owns column tile w of a layer;
+// waves without a tile wait at the barrier); the MFMA order, the epilogue (col_apply) and the head
+// are mlp_rows', so the outputs are bit-identical to mlp_gather_kernel's.  IT: column tiles of the
+// internal layer (internal dim <= 16 IT), U residual units, K0 <= 64 input columns.
+constexpr int kDcMaxUnits = 2;
+template <int IT, int U>
+__global__ __launch_bounds__(kMlpThreads) void dc_forward_kernel(MlpGatherArgs a) {
+  static_assert(IT <= kMlpWaves && U <= kDcMaxUnits, "one tile per wave");
+  constexpr int KX = 64 + kMlpLdPad, KH = 16 * IT + kMlpLdPad;  // LDS row strides
+  __shared__ __attribute__((aligned(16))) float xs[kMlpRows * KX];
+  __shared__ __attribute__((aligned(16))) float hs[kMlpRows * KH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id(), li = lane & 15, kq = 4 * (lane >> 4);
+  const int64_t m0 = (int64_t)blockIdx.x * kMlpRows;
+  const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
+  const bool live = wave < rows;
+  const int64_t b = m0 + wave;
+  // one dependent round trip, index -> row: lane t loads the sample's index in segment t (its
+  // descriptor by uniform selects, lane_segment), then lane c takes the index of the segment that
+  // covers column c (the column map by a uniform walk over the segments: the last covering one wins,
+  // as mlp_gather_kernel's map) by a cross-lane read
+  const int c = lane;  // K0 <= 64: one column per lane
+  const int nseg = a.nseg;
+  int64_t mine = b;
+  if (lane < nseg && live) {
+    const rk_segment g = lane_segment(a.segs, lane);
+    if (g.idx) {
+      mine = g.idx[b * g.idx_stride];
+      if (mine < 0 || mine >= g.rows) {
+        flag_oob(a.flags);
+        mine = -1;
+      }
+    }
+  }
+  int sg = 255, off = 0;
+  const float* src = nullptr;
+  int64_t ld = 0;
+  for (int t = 0; t < nseg; ++t) {  // uniform loop: scalar loads of segment t's descriptor
+    const rk_segment& g = a.segs[t];
+    if (c >= g.out_col && c < g.out_col + g.dim) {
+      sg = t;
+      off = c - g.out_col;
+      src = g.src;
+      ld = g.src_ld;
+    }
+  }
+  if (!(live && c < a.m.K0)) sg = 255;
+  // every weight fragment of this wave's tiles (fragment-major packed images, mlp_core.h wfrag)
+  f32x4_t wa[U][4], wb[U][IT];
+  // per-column biases only: dc_plan admits no other epilogue parameter (col_apply reads only the
+  // bias of a ReLU layer without affines), so the rest of ColEpi is never live
+  float ea[U], eb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const rk_mlp_layer& LA = a.m.L[2 * u];
+    const rk_mlp_layer& LB = a.m.L[2 * u + 1];
+    if (wave < IT) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wa[u][k] = *reinterpret_cast<const f32x4_t*>(wfrag(LA, wave, lane) + kFragStep * k);
+      const int n = 16 * wave + li;
+      ea[u] = col_epi(LA, n < LA.n ? n : 0).bias;
+    }
+    if (wave < 4) {
+#pragma unroll
+      for (int k = 0; k < IT; ++k) wb[u][k] = *reinterpret_cast<const f32x4_t*>(wfrag(LB, wave, lane) + kFragStep * k);
+      const int n = 16 * wave + li;
+      eb[u] = col_epi(LB, n < LB.n ? n : 0).bias;
+    }
+  }
+  const float hw = lane < a.m.K0 ? a.m.head.head_w[lane] : 0.f;
+  const int64_t r = __shfl(mine, sg != 255 ? sg : 0, kWave);
+  float v = 0.f;
+  if (sg != 255 && r >= 0) v = src[r * ld + off];
+  xs[wave * KX + c] = v;  // dead rows and pad columns stage zeros (mlp_rows' zero K pad)
+  mlp_lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const rk_mlp_layer& LA = a.m.L[2 * u];
+    const rk_mlp_layer& LB = a.m.L[2 * u + 1];
+    if (wave < IT) {  // x [16 x 64] . W1^T -> relu(. + b1) into hs
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const float* arow = xs + li * KX + kq;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x4_t av = *reinterpret_cast<const f32x4_t*>(arow + 16 * k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = mfma16(av[e], wa[u][k][e], acc);
+      }
+      const int n = 16 * wave + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = (lane >> 4) * 4 + q;
+        const float z = col_apply(LA, ColEpi{ea[u], 1.f, 0.f, 0.f, 0.f, 0.f, 1.f, 0.f}, false, acc[q], false, 0.f);
+        hs[row * KH + n] = n < LA.n ? z : 0.f;
+      }
+    }
+    mlp_lds_barrier();
+    if (wave < 4) {  // h [16 x 16 IT] . W2^T -> relu(x + . + b2) over x in place
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const float* arow = hs + li * KH + kq;
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const f32x4_t av = *reinterpret_cast<const f32x4_t*>(arow + 16 * k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = mfma16(av[e], wb[u][k][e], acc);
+      }
+      const int n = 16 * wave + li;
+      float res[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) res[q] = xs[((lane >> 4) * 4 + q) * KX + n];  // read all, then write (same lane)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = (lane >> 4) * 4 + q;
+        const float z = col_apply(LB, ColEpi{eb[u], 1.f, 0.f, 0.f, 0.f, 0.f, 1.f, 0.f}, false, acc[q], true, res[q]);
+        xs[row * KX + n] = n < LB.n ? z : 0.f;
+      }
+    }
+    mlp_lds_barrier();
+  }
+  // head: one wave per row (mlp_rows' order: one fmaf per lane, then wave_sum)
+  if (live) {
+    float p = 0.f;
+    if (lane < a.m.K0) p = fmaf(xs[wave * KX + lane], hw, p);
+    p = wave_sum(p);
+    if (lane == 0) {
+      const float logit = p + a.m.head.head_b[0];
+      if (a.m.head.head_logit) a.m.head.head_logit[b] = logit;
+      if (a.m.head.head_prob) a.m.head.head_prob[b] = 1.0f / (1.0f + expf(-logit));
+    }
+  }
+}
+
+// The layer stacks dc_forward_kernel runs: U <= 2 residual units over K0 <= 64 input columns, each
+// (internal <= 128, ReLU, no residual) then (K0 wide, ReLU, residual), bias optional, nothing else
+// (no BatchNorm affines, Dice / PReLU, stores); a plain head.  Returns the internal tiles (0: no).
+static int dc_plan(const rk_mlp_layer* layers, int nlayers, int K0, const rk_epilogue& h) {
+  if (const char* e = getenv("RANKOPS_DC_KERNEL"))
+    if (e[0] == '0') return 0;
+  if (K0 > 64 || nlayers < 2 || nlayers > 2 * kDcMaxUnits || (nlayers & 1)) return 0;
+  if (h.head_partial || h.fm1 || h.head_aux || !h.head_w) return 0;
+  const int I = layers[0].n;
+  if (I > 128) return 0;
+  for (int l = 0; l < nlayers; ++l) {
+    const rk_mlp_layer& L = layers[l];
+    const bool second = l & 1;
+    if (L.act != RK_ACT_RELU || L.store || L.pre_scale || L.post_scale || L.n != (second ? K0 : I) ||
+        L.residual != (second ? 1 : 0))
+      return 0;
+  }
+  return I <= 64 ? 4 : 8;
 }
 
 // The same tail on a compiled layer plan (mlp_stream.h): one weight stream across the layers.
@@ -681,10 +839,19 @@ RK_API int rk_mlp_forward_gather(const rk_segment* segs, int32_t nseg, int32_t w
     }
   }
   g.flags = device_flags();
+  g.nseg = nseg;
   if (!g.flags) return fail(RK_ERR_RUNTIME, "rk_mlp_forward_gather: device not initialised (rk_init)");
   if (batch == 0) return RK_OK;
   const int64_t blocks = (batch + kMlpRows - 1) / kMlpRows;
   if (blocks > INT32_MAX) return fail(RK_ERR_UNSUPPORTED, "rk_mlp_forward_gather: batch too large");
+  if (const int it = dc_plan(layers, nlayers, width, a.head)) {  // DeepCrossing: weights in registers
+    auto go = [&](auto kern) { kern<<<(unsigned)blocks, kMlpThreads, 0, (hipStream_t)stream>>>(g); };
+    if (it == 4)
+      nlayers == 2 ? go(dc_forward_kernel<4, 1>) : go(dc_forward_kernel<4, 2>);
+    else
+      nlayers == 2 ? go(dc_forward_kernel<8, 1>) : go(dc_forward_kernel<8, 2>);
+    return check_launch("rk_mlp_forward_gather");
+  }
   raise_lds_limit((const void*)mlp_gather_kernel, 160 * 1024);
   mlp_gather_kernel<<<(unsigned)blocks, kMlpThreads, shm, (hipStream_t)stream>>>(g);
   return check_launch("rk_mlp_forward_gather");

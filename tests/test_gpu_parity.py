@@ -407,6 +407,40 @@ def test_deepcrossing_fused_gather_equals_two_launches(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("internal,units,B", [(128, 1, 4097), (64, 2, 1037), (100, 1, 33), (128, 2, 16)])
+def test_deepcrossing_register_kernel_equals_ring_kernel(internal, units, B, monkeypatch):
+    """dc_forward_kernel (round 6: every weight fragment in registers from entry) against
+    mlp_gather_kernel (RANKOPS_DC_KERNEL=0: the streamed ring) on the same inputs: bit-identical
+    (same MFMA order, epilogue and head), out-of-range index flagged in both, and the oracle."""
+    cfg = {"vocab": H.WECHAT_VOCAB, "internal": internal, "units": units, "interaction_weights": "frozen"}
+    model = H.build("deepcrossing", cfg)
+    p = H.cpu_params(model)
+    inp = H.make_inputs("deepcrossing", cfg, B, seed=41)
+    name = next(iter(inp["category"]))
+    inp["category"][name][B // 2] = model.embeddings[name].num_embeddings  # one past the table
+    model = model.cuda().eval()
+    d = H.to_device(inp, "cuda")
+    torch.manual_seed(0)
+    outs = {}
+    for k in ("1", "0"):
+        monkeypatch.setenv("RANKOPS_DC_KERNEL", k)
+        rankops.error_flags(reset=True)
+        with torch.no_grad():
+            outs[k] = tuple(o.clone() for o in H.as_tuple(H.call_model(model, "deepcrossing", d)))
+        torch.cuda.synchronize()
+        assert rankops.error_flags(reset=True) & 1
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b)
+    emb = p[f"embeddings.{name}.weight"]
+    p[f"embeddings.{name}.weight"] = torch.cat([emb, torch.zeros(1, emb.shape[1])], 0)
+    torch.manual_seed(0)  # the oracle draws the residual units as the frozen model did at its first forward
+    with torch.no_grad():
+        ref = H.as_tuple(H.call_oracle("deepcrossing", cfg, p, inp))
+    for o, r in zip(outs["1"], ref):
+        torch.testing.assert_close(o.cpu(), r, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
 def test_fwfm_prepare_equals_forward():
     """FwFM.prepare: the bound launch equals the module's forward bit for bit, and recomputes from
     the indices' current contents."""
