@@ -356,8 +356,7 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
     if (lane < SF) {
       const int s = lane / F, f = lane - s * F;
       const int64_t b = b0 + s;
-      const rk_segment sg = lane_segment(fields.s, f);
-      if (b < batch) row = segment_row(sg, b, flags);
+      if (b < batch) row = segment_row(fields.s[f], b, flags);
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k)

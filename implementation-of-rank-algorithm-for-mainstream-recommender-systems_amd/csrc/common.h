@@ -187,18 +187,6 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
   return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
 }
 
-// The descriptor of segment `t` (lane-varying, 0 <= t < N) of a kernel-argument array, by wave-
-// uniform scalar loads and selects: indexing the argument array with a lane-varying t is a per-lane
-// global load, one more dependent round trip in front of the index and row loads it feeds.
-template <int N>
-__device__ __forceinline__ rk_segment lane_segment(const rk_segment (&segs)[N], int t) {
-  rk_segment r = segs[0];
-#pragma unroll
-  for (int i = 1; i < N; ++i)
-    if (t == i) r = segs[i];
-  return r;
-}
-
 // Segment table passed by value as a kernel argument.
 struct SegTable {
   rk_segment s[RK_MAX_SEGMENTS];
