@@ -157,21 +157,37 @@ __global__ __launch_bounds__(kMlpThreads) void dc_forward_kernel(MlpGatherArgs a
   const int rows = (int)min<int64_t>(kMlpRows, a.m.M - m0);
   const bool live = wave < rows;
   const int64_t b = m0 + wave;
-  // the row's index in every column's segment first (one dependent round trip), as mlp_gather_kernel
-  // (selecting the descriptors by wave-uniform scalar loads instead measured slower: 7.2 vs 6.5 us)
+  // the row: lane t loads the sample's index in segment t (the descriptor fields picked by selects
+  // over constant-index argument reads, as dcn_fused_kernel), while the column -> segment map and
+  // the column's source are looked up per lane beside it; then each column takes its segment's index
+  // by a cross-lane read and loads its value — index -> value, one dependent round trip after the
+  // argument reads instead of map -> descriptor -> index -> value
   const int c = lane;  // K0 <= 64: one column per lane
-  const int sg = live && c < a.m.K0 ? a.col_seg[c] : 255;
-  int64_t r = b;
-  if (sg != 255) {
-    const rk_segment& g = a.segs[sg];
-    if (g.idx) {
-      r = g.idx[b * g.idx_stride];
-      if (r < 0 || r >= g.rows) {
-        flag_oob(a.flags);
-        r = -1;
-      }
+  const int64_t* ip = a.segs[0].idx;
+  int64_t ist = a.segs[0].idx_stride, irows = a.segs[0].rows;
+#pragma unroll
+  for (int t = 1; t < kMgSegs; ++t)
+    if (lane == t) {
+      ip = a.segs[t].idx;
+      ist = a.segs[t].idx_stride;
+      irows = a.segs[t].rows;
+    }
+  int64_t mine = b;
+  if (live && ip) {  // lanes past the segment count read a zeroed slot (idx null): nothing
+    mine = ip[b * ist];
+    if (mine < 0 || mine >= irows) {
+      flag_oob(a.flags);
+      mine = -1;
     }
   }
+  const int sg = live && c < a.m.K0 ? a.col_seg[c] : 255;
+  const float* csrc = nullptr;
+  int64_t cld = 0;
+  if (sg != 255) {
+    csrc = a.segs[sg].src + a.col_off[c];
+    cld = a.segs[sg].src_ld;
+  }
+  const int64_t r = __shfl(mine, sg != 255 ? sg : 0, kWave);
   // every weight fragment of this wave's tiles (fragment-major packed images, mlp_core.h wfrag)
   f32x4_t wa[U][4], wb[U][IT];
   // per-column biases only: dc_plan admits no other epilogue parameter (col_apply reads only the
@@ -196,10 +212,7 @@ __global__ __launch_bounds__(kMlpThreads) void dc_forward_kernel(MlpGatherArgs a
   }
   const float hw = lane < a.m.K0 ? a.m.head.head_w[lane] : 0.f;
   float v = 0.f;
-  if (sg != 255 && r >= 0) {
-    const rk_segment& g = a.segs[sg];
-    v = g.src[r * g.src_ld + a.col_off[c]];
-  }
+  if (sg != 255 && r >= 0) v = csrc[r * cld];
   xs[wave * KX + c] = v;  // dead rows and pad columns stage zeros (mlp_rows' zero K pad)
   mlp_lds_barrier();
 #pragma unroll
