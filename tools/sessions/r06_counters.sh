@@ -28,7 +28,7 @@ if [ -z "$NO_PMC" ]; then
   pmc deepfm_gather_tables --workload deepfm_gather_tables --iters 3 || { echo "pmc gather tables 4096 failed"; exit 1; }
 fi
 python3 tools/pmc_counters.py $O din:din_forward_kernel dcn:dcn_fused_kernel deepfm:deepfm_fused_kernel \
-  bst:bst_block_kernel bst:mlp_stream_kernel bst_ref:bst_mfma_fwd_kernel bst_ref_blocks:bst_mfma_kernel afm:afm_tiles_kernel deepcrossing:mlp_gather_kernel \
+  bst:bst_block_kernel bst:mlp_stream_kernel bst_ref:bst_mfma_fwd_kernel bst_ref_blocks:bst_mfma_kernel afm:afm_tiles_kernel deepcrossing:dc_forward_kernel \
   deepfm_gather:fm_gather_kernel deepfm_gather65536:fm_gather_fmaj_kernel deepfm_gather_tables65536:fm_gather_fmaj_kernel \
   deepfm_gather_tables:fm_gather_kernel \
   > $O/digest.log 2>&1 || { echo "digest failed"; tail $O/digest.log; exit 1; }
