@@ -874,7 +874,7 @@ DEEPCROSSING_BYTES = 16 * 4 + 6 * 8 + (16 + 2 + 4 * 4) * 4 + 2 * 4  # dense, 6 i
 
 def small_forward_roofline(model, name, inp, batch, flop_per_sample, bytes_per_sample, kernels, big_batch=65536):
     """AFM / DeepCrossing forward legs: the whole eval forward (AFM: one rk_afm_forward
-    launch; DeepCrossing: rk_concat_gather + the one-launch residual MLP) timed as 20 back-to-back
+    launch; DeepCrossing: one rk_mlp_forward_gather launch) timed as 20 back-to-back
     forwards in one hipGraph (HIP events on the replay stream), at the bench batch and at 65,536 rows
     (launch ramp amortised).  Both roofs are reported: FP32 matrix/vector peak for the flops, HBM for
     the bytes; at these per-sample sizes neither is close — the forwards are launch- and latency-bound."""
@@ -1161,12 +1161,13 @@ def main():
             if name == "deepfm":
                 r["gather_roofline"] = gather_roofline(m2, inp2, cfg2, batch)
             if name == "afm":
-                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES, ["afm_mfma_kernel<2,8>"])
-                r["roofline"].update(counter_fields("afm_mfma_kernel", "afm"))
+                r["roofline"] = small_forward_roofline(m2, "afm", inp2, batch, AFM_FLOP, AFM_BYTES,
+                                                       ["afm_tiles_kernel<2,8,4>"])
+                r["roofline"].update(counter_fields("afm_tiles_kernel", "afm"))
             if name == "deepcrossing":
                 r["roofline"] = small_forward_roofline(m2, "deepcrossing", inp2, batch, DEEPCROSSING_FLOP,
-                                                       DEEPCROSSING_BYTES, ["mlp_gather_kernel"])
-                r["roofline"].update(counter_fields("mlp_gather_kernel", "deepcrossing"))
+                                                       DEEPCROSSING_BYTES, ["dc_forward_kernel<8,1>"])
+                r["roofline"].update(counter_fields("dc_forward_kernel", "deepcrossing"))
             if name == "fwfm":  # 6 x (8 B index + 32 B embedding row + 4 B linear) + 4 B prob
                 r["gather_gb_per_s"] = round(FWFM_BYTES_PER_SAMPLE * r["samples_per_s"] / 1e9, 1)
                 r["bytes_per_sample"] = FWFM_BYTES_PER_SAMPLE
