@@ -674,29 +674,37 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
                                       PreChunks<KS, DinRowsReady<(NIT > 0 && KS > 0), true>>{}, nullptr,
                                       NIT > 0 ? s_rows : nullptr);
   DIN_TS(3);
-  // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off =
-  // MI355X_MICROARCH.md "inter-workgroup visibility", first row of the sc1 table (measured valid on
-  // gfx950 / ROCm 7.2, not an architectural guarantee): one lane per workgroup stores its partial
-  // sc1 (relaxed agent store), waits vmcnt(0), then adds to ONE counter (relaxed agent atomic);
-  // the workgroup whose add returns n-1 loads every partial with sc1 loads (relaxed agent loads)
-  // in the adding wave, after the add returned.  The memory-model form (release/acquire at agent
-  // scope) lowers to buffer_wbl2 / buffer_inv, ~1.7-3.5 us each on the critical path of a ~50 us
-  // kernel; tests/test_gpu_din_plan.py checks l2 against the deterministic host-order sum over
-  // repeated launches.  (The norms in LDS were ordered before this by mlp_rows' barriers.)
+  // l2 partials: the last workgroup to publish its partial finishes the mean.  Hand-off by atomic
+  // read-modify-writes only (round 6): one lane per workgroup publishes its
+  // partial with an agent-scope atomic exchange and waits for its return (the exchange is then
+  // performed at the location's coherence point), then adds to ONE counter (agent-scope atomic); the
+  // workgroup whose add returns n-1 reads every partial with an atomic fetch-add of 0.  Every access
+  // of the hand-off is an agent-scope RMW on a single location — coherent across the XCDs (the RMWs
+  // of one location are totally ordered at its coherence point) — and the order across locations is
+  // by completion: a partial's exchange has returned before its workgroup's add is issued, and the
+  // reader issues its partial RMWs after its own add returned n-1.  That is not a C++ happens-before
+  // (which would take a release / acquire pair: buffer_wbl2 / buffer_inv, 1.7-3.5 us each on the
+  // critical path), but unlike rounds 3-5's sc1 plain stores and loads it does not depend on how a
+  // cache treats non-atomic accesses.  The partials are non-negative sums of norms, so adding 0
+  // returns them unchanged.
+  // tests/test_gpu_din_plan.py checks l2 against the deterministic host-order sum over repeated
+  // launches.  (The norms in LDS were ordered before this by mlp_rows' barriers.)
   if (a.l2_part && tid < 64) {
     unsigned prev = 0;
     if (tid == 0) {
       float t = 0.f;
       for (int w = 0; w < kMlpRows; ++w) t += sm[Ly::NORM + w];
-      __hip_atomic_store(a.l2_part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      prev = __hip_atomic_fetch_add(a.l2_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float old = __hip_atomic_exchange(a.l2_part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the counter's add waits for the exchange to return (a use of its result orders it after)
+      unsigned one = 1u;
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(one) : "v"(old) : "memory");
+      prev = __hip_atomic_fetch_add(a.l2_count, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     prev = __builtin_amdgcn_readfirstlane(prev);
     if (prev == gridDim.x - 1) {
       float t = 0.f;
       for (int i = tid; i < (int)gridDim.x; i += 64)
-        t += __hip_atomic_load(a.l2_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t += __hip_atomic_fetch_add(a.l2_part + i, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       t = wave_sum(t);  // the order of row_l2norm_final_kernel (embedding.hip)
       if (tid == 0) {
         a.l2_out[0] = a.l2_scale * (t / (float)a.batch);
