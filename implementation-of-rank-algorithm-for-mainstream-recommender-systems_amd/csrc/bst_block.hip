@@ -19,6 +19,7 @@
 // are -inf like bst.py:80; an all-masked row gives NaN exactly as torch's softmax.
 #include "common.h"
 
+
 namespace rk {
 
 constexpr int kBD = 128;       // d_model
@@ -89,20 +90,23 @@ __device__ unsigned long long g_bst_wave[10][8];  // [mark][wave]
 #define BST_RING 2
 #endif
 constexpr int kRing = BST_RING;  // super-chunk buffers
-template <int TT>
+// PK: the tile stored in that order (rk_bst_pack_block_weight), each load one contiguous 1 KiB.
+template <int TT, bool PK>
 struct WStream {
   const float* wrow[TT];
   f4 bq[kRing][4];
   __device__ __forceinline__ void start(const float* const (&W)[TT], int lane) {
 #pragma unroll
-    for (int j = 0; j < TT; ++j) wrow[j] = W[j] + (int64_t)(lane & 31) * kBD + 4 * (lane >> 5);
+    for (int j = 0; j < TT; ++j)
+      wrow[j] = PK ? W[j] + 4 * lane : W[j] + (int64_t)(lane & 31) * kBD + 4 * (lane >> 5);
 #pragma unroll
     for (int g = 0; g + 1 < kRing; ++g) issue(g);
   }
   __device__ __forceinline__ void issue(int g) {
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      bq[g % kRing][c] = *reinterpret_cast<const f4*>(wrow[g / 4] + 32 * (g % 4) + 8 * c);
+      bq[g % kRing][c] = *reinterpret_cast<const f4*>(PK ? wrow[g / 4] + 1024 * (g % 4) + 256 * c
+                                                         : wrow[g / 4] + 32 * (g % 4) + 8 * c);
   }
 };
 
@@ -111,8 +115,8 @@ struct WStream {
 // the MFMAs (one dependent accumulator chain at a time: 32x32x2_f32 accumulates back to back at the
 // full 64-cycle issue rate), the next A float4 one chunk ahead; sched_barrier keeps the compiler
 // from sinking the loads next to their use.
-template <int TT>
-__device__ __forceinline__ void gemm128(const float* __restrict__ A, WStream<TT>& ws, f32x16 (&acc)[TT], int rt,
+template <int TT, bool PK>
+__device__ __forceinline__ void gemm128(const float* __restrict__ A, WStream<TT, PK>& ws, f32x16 (&acc)[TT], int rt,
                                         int lane) {
   constexpr int NG = TT * (kBD / 32);
   const float* arow = A + (rt * 32 + (lane & 31)) * kBLD + 4 * (lane >> 5);
@@ -279,6 +283,7 @@ __device__ __forceinline__ void zero(f32x16& a) {
   for (int r = 0; r < 16; ++r) a[r] = 0.f;
 }
 
+template <bool PK>
 __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Xs = sm;
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
   unsigned long long t_phase = clock64();
 #endif
   int64_t b = blockIdx.x;
-  WStream<1> ws1;
+  WStream<1, PK> ws1;
   {
     const float* W[1] = {a.blk[0].wv + q4 * 32 * kBD};
     ws1.start(W, lane);
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
       const BstBlockW& P = a.blk[blk];
       const bool last = blk + 1 == a.nblocks;
       // ---- 1a. V = x . Wv^T + bv -> Vs
-      WStream<2> ws2;
+      WStream<2, PK> ws2;
       {
         f32x16 acc[1];
         const float bb = P.bv[c32];
@@ -494,27 +499,23 @@ __global__ __launch_bounds__(512) void bst_block_kernel(BstArgs a) {
   }
 }
 
-}  // namespace rk
-
-using namespace rk;
-
-RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq,
-                                 int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t d_model,
-                                 int32_t heads, int32_t nblocks, const float* const* block_params,
-                                 const float* block_scalars, float* pool_out, int64_t ld_pool, int32_t pool_mean,
-                                 void* stream) {
-  if (d_model == 16)  // the reference script's own width (bst.py:192): bst_small.hip
+static int bst_forward_blocks(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq,
+                              int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t d_model,
+                              int32_t heads, int32_t nblocks, const float* const* block_params,
+                              const float* block_scalars, float* pool_out, int64_t ld_pool, int32_t pool_mean,
+                              hipStream_t stream, bool packed, const char* what) {
+  if (d_model == 16 && !packed)  // the reference script's own width (bst.py:192): bst_small.hip
     return bst_small_forward(table, table_rows, ld_table, seq, ld_seq, T, seq_len, batch, heads, nblocks, block_params,
-                             block_scalars, pool_out, ld_pool, pool_mean, (hipStream_t)stream);
+                             block_scalars, pool_out, ld_pool, pool_mean, stream);
   if (d_model != kBD || heads != 4)
-    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: d_model=%d heads=%d (fused paths: 128/4, 16/1-8)", d_model,
-                heads);
-  if (T <= 0 || T > kBT) return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: T=%d outside [1, %d]", T, kBT);
+    return fail(RK_ERR_UNSUPPORTED, "%s: d_model=%d heads=%d (fused paths: 128/4%s)", what, d_model, heads,
+                packed ? "" : ", 16/1-8");
+  if (T <= 0 || T > kBT) return fail(RK_ERR_UNSUPPORTED, "%s: T=%d outside [1, %d]", what, T, kBT);
   if (nblocks <= 0 || nblocks > kBMaxBlocks)
-    return fail(RK_ERR_UNSUPPORTED, "rk_bst_forward_blocks: %d blocks (max %d)", nblocks, kBMaxBlocks);
+    return fail(RK_ERR_UNSUPPORTED, "%s: %d blocks (max %d)", what, nblocks, kBMaxBlocks);
   if (!table || !seq || !seq_len || !block_params || !block_scalars || !pool_out || ld_table % 4 ||
       ((uintptr_t)table & 15u) || ld_seq < T || ld_pool < kBD || table_rows <= 0)
-    return fail(RK_ERR_INVALID, "rk_bst_forward_blocks: bad arguments");
+    return fail(RK_ERR_INVALID, "%s: bad arguments", what);
   BstArgs a = {};
   a.table = table;
   a.rows = table_rows;
@@ -547,7 +548,7 @@ RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t
     w.be2 = p[16];
     for (int k = 0; k < 17; ++k)
       if (!p[k] || ((uintptr_t)p[k] & 15u))
-        return fail(RK_ERR_INVALID, "rk_bst_forward_blocks: block %d parameter %d null or misaligned", i, k);
+        return fail(RK_ERR_INVALID, "%s: block %d parameter %d null or misaligned", what, i, k);
     w.eps1 = block_scalars[3 * i];
     w.eps2 = block_scalars[3 * i + 1];
     w.slope = block_scalars[3 * i + 2];
@@ -556,11 +557,54 @@ RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t
   a.ld_pool = ld_pool;
   a.pool_mean = pool_mean;
   a.flags = device_flags();
-  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "rk_bst_forward_blocks: negative batch");
+  if (batch <= 0) return batch == 0 ? RK_OK : fail(RK_ERR_INVALID, "%s: negative batch", what);
   const size_t shm = (size_t)(4 * kBT * kBLD + 4 * kBD) * sizeof(float);
-  raise_lds_limit((const void*)bst_block_kernel, 160 * 1024);
   // one resident workgroup per CU (LDS-bound); each walks samples blockIdx.x + k * gridDim.x
   const int64_t grid = std::min<int64_t>(batch, num_cus());
-  bst_block_kernel<<<(unsigned)grid, 512, shm, (hipStream_t)stream>>>(a);
-  return check_launch("rk_bst_forward_blocks");
+  auto go = [&](auto kern) {
+    raise_lds_limit((const void*)kern, 160 * 1024);
+    kern<<<(unsigned)grid, 512, shm, stream>>>(a);
+  };
+  packed ? go(bst_block_kernel<true>) : go(bst_block_kernel<false>);
+  return check_launch(what);
+}
+
+// [128 n, 128 k] nn.Linear weight -> the WStream<PK = true> order: float 4096 j + 1024 g + 256 c + 4 l + e
+// = W[32 j + l % 32][32 g + 8 c + 4 (l / 32) + e]; thread i moves float4 i
+__global__ __launch_bounds__(256) void bst_pack_block_weight_kernel(const float* __restrict__ w, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // < 4096
+  const int l = i & 63, c = (i >> 6) & 3, g = (i >> 8) & 3, j = i >> 10;
+  const f4 v = *reinterpret_cast<const f4*>(w + (32 * j + (l & 31)) * kBD + 32 * g + 8 * c + 4 * (l >> 5));
+  *reinterpret_cast<f4*>(out + 4 * i) = v;
+}
+
+}  // namespace rk
+
+using namespace rk;
+
+RK_API int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq,
+                                 int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch, int32_t d_model,
+                                 int32_t heads, int32_t nblocks, const float* const* block_params,
+                                 const float* block_scalars, float* pool_out, int64_t ld_pool, int32_t pool_mean,
+                                 void* stream) {
+  return bst_forward_blocks(table, table_rows, ld_table, seq, ld_seq, T, seq_len, batch, d_model, heads, nblocks,
+                            block_params, block_scalars, pool_out, ld_pool, pool_mean, (hipStream_t)stream, false,
+                            "rk_bst_forward_blocks");
+}
+
+RK_API int rk_bst_forward_blocks_packed(const float* table, int64_t table_rows, int64_t ld_table, const int64_t* seq,
+                                        int64_t ld_seq, int32_t T, const int64_t* seq_len, int64_t batch,
+                                        int32_t d_model, int32_t heads, int32_t nblocks,
+                                        const float* const* block_params, const float* block_scalars,
+                                        float* pool_out, int64_t ld_pool, int32_t pool_mean, void* stream) {
+  return bst_forward_blocks(table, table_rows, ld_table, seq, ld_seq, T, seq_len, batch, d_model, heads, nblocks,
+                            block_params, block_scalars, pool_out, ld_pool, pool_mean, (hipStream_t)stream, true,
+                            "rk_bst_forward_blocks_packed");
+}
+
+RK_API int rk_bst_pack_block_weight(const float* w, float* out, void* stream) {
+  if (!w || !out || ((uintptr_t)w & 15u) || ((uintptr_t)out & 15u) || w == out)
+    return fail(RK_ERR_INVALID, "rk_bst_pack_block_weight: null, misaligned or in-place operands");
+  bst_pack_block_weight_kernel<<<16, 256, 0, (hipStream_t)stream>>>(w, out);
+  return check_launch("rk_bst_pack_block_weight");
 }

@@ -165,6 +165,11 @@ SIGNATURES = {
         ctypes.c_int,
         [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32, c_int32,
          POINTER(c_void_p), POINTER(ctypes.c_float), c_void_p, c_int64, c_int32, c_void_p]),
+    "rk_bst_forward_blocks_packed": (
+        ctypes.c_int,
+        [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32, c_int32,
+         POINTER(c_void_p), POINTER(ctypes.c_float), c_void_p, c_int64, c_int32, c_void_p]),
+    "rk_bst_pack_block_weight": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
     "rk_linear": (
         ctypes.c_int,
         [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, _EPI_P, c_void_p,

@@ -260,9 +260,10 @@ class BSTModel(EngineModule):
         ops.concat_gather(segs, B, row)
         if blocks is not None:
             # every block + pooling in one launch, activations in LDS (rk_bst_forward_blocks)
+            packed = d == 128
             ops.bst_forward_blocks(self.embeddings['feedid'].weight, seq_feedid, seq_length, d,
-                                   self.transformer_blocks[0].nhead, blocks, ops._lib.fptr(row, col), width,
-                                   self.pooling_method != 'sum')
+                                   self.transformer_blocks[0].nhead, self._packed_blocks(blocks) if packed else blocks,
+                                   ops._lib.fptr(row, col), width, self.pooling_method != 'sum', packed=packed)
         else:
             self._run_blocks(row, col, width, seq_feedid, seq_length, B, T)
         logits = torch.empty(B, 1, device=dev, dtype=torch.float32)
@@ -331,9 +332,24 @@ class BSTModel(EngineModule):
             raise RuntimeError("BST configuration outside rk_bst_forward_blocks' envelope")
         d = self.d_model
         row = torch.empty(B, d, device=seq_feedid.device, dtype=torch.float32)
+        packed = d == 128
+        if packed:
+            blocks = self._packed_blocks(blocks)
         return lambda: ops.bst_forward_blocks(self.embeddings['feedid'].weight, seq_feedid, seq_length, d,
                                               self.transformer_blocks[0].nhead, blocks, ops._lib.fptr(row, 0), d,
-                                              self.pooling_method != 'sum')
+                                              self.pooling_method != 'sum', packed=packed)
+
+    @staticmethod
+    def _packed_blocks(blocks):
+        """_fused_blocks' parameters with the six d-128 projection weights (wq, wk, wv, wo, ffn.0,
+        ffn.3) replaced by their rk_bst_pack_block_weight images (cached per weight version)."""
+        out = []
+        for ts, sc in blocks:
+            ts = list(ts)
+            for k in (1, 3, 5, 7, 9, 11):
+                ts[k] = common.BST_PACKED(ts[k])
+            out.append((tuple(ts), sc))
+        return out
 
     def _fused_blocks(self, T):
         """Parameters for rk_bst_forward_blocks, or None outside its envelope: d_model 128 with 4

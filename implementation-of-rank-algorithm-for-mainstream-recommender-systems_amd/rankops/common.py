@@ -414,16 +414,17 @@ def fused_mlp_fits(k0: int, widths) -> bool:
 
 
 class PackedWeights:
-    """rk_mlp_pack_weight images, held weakly per weight tensor object and rebuilt when its
-    storage or version changes (load_state_dict, .to(), optimizer steps).  Keying on the
-    object — not the address — keeps a freed model's packed image from being served to a new
-    tensor that reuses its memory.  After an optimizer step the image is rewritten in place, on
+    """Packed weight images (rk_mlp_pack_weight, or the `pack` given), held weakly per weight
+    tensor object and rebuilt when its storage or version changes (load_state_dict, .to(),
+    optimizer steps).  Keying on the object — not the address — keeps a freed model's packed
+    image from being served to a new tensor that reuses its memory.  After an optimizer step the image is rewritten in place, on
     the current stream, unless a prepared forward (DIN / DCN / DeepFM .prepare) pinned it: such a
     plan keeps the image it was prepared with (it binds the weights of that moment; prepare again
     after changing them), and its launches on other streams never see a half-rewritten image."""
 
-    def __init__(self):
+    def __init__(self, pack=None):
         self._d = {}  # id(tensor) -> (weakref, key, packed, pinned); the weakref callback drops the entry
+        self._pack = pack or (lambda w, out=None: ops.pack_mlp_weight(w, out=out))
 
     def __call__(self, w: torch.Tensor) -> torch.Tensor:
         key = (_GENERATION[0], w.data_ptr(), w._version, tuple(w.shape), w.device)
@@ -434,10 +435,10 @@ class PackedWeights:
                     and not hit[3] and not torch.cuda.is_current_stream_capturing():
                 # only the version moved (an optimizer step): rewrite the image in place, on the
                 # stream, behind every launch already reading it
-                hit = (hit[0], key, ops.pack_mlp_weight(w, out=hit[2]), False)
+                hit = (hit[0], key, self._pack(w, out=hit[2]), False)
             else:
                 ref = weakref.ref(w, lambda _r, d=d, i=i: d.pop(i, None) if d.get(i, (None,))[0] is _r else None)
-                hit = (ref, key, ops.pack_mlp_weight(w), False)
+                hit = (ref, key, self._pack(w), False)
             self._d[i] = hit
         return hit[2]
 
@@ -451,6 +452,7 @@ class PackedWeights:
 
 
 PACKED = PackedWeights()
+BST_PACKED = PackedWeights(lambda w, out=None: ops.pack_bst_weight(w, out=out))  # bst_block_kernel's projections
 
 
 def tiled_layer(K: int, B: int, device, ml) -> bool:

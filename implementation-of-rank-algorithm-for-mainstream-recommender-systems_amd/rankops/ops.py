@@ -332,10 +332,14 @@ def bst_attention_masked(qkv, batch, T, d_model, heads, key_mask, ctx):
 BST_BLOCK_PARAMS = 17
 
 
-def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr, ld_pool, pool_mean):
+def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr, ld_pool, pool_mean,
+                       packed=False):
     """rk_bst_forward_blocks: `blocks` = list of (17 device tensors in the header's order,
-    (ln1_eps, ln2_eps, slope))."""
+    (ln1_eps, ln2_eps, slope)); packed: the six projection weights in rk_bst_pack_block_weight's
+    layout (rk_bst_forward_blocks_packed)."""
     lib = _lib.load()
+    fn, name = ((lib.rk_bst_forward_blocks_packed, "rk_bst_forward_blocks_packed") if packed else
+                (lib.rk_bst_forward_blocks, "rk_bst_forward_blocks"))
     B, T = seq.shape
     params = (ctypes.c_void_p * (BST_BLOCK_PARAMS * len(blocks)))()
     scalars = (ctypes.c_float * (3 * len(blocks)))()
@@ -345,9 +349,22 @@ def bst_forward_blocks(table, seq, seq_len, d_model, heads, blocks, pool_out_ptr
             params[BST_BLOCK_PARAMS * i + k] = ptr(t)
         for k in range(3):
             scalars[3 * i + k] = float(sc[k])
-    check(lib.rk_bst_forward_blocks(ptr(table), table.shape[0], table.stride(0), ptr(seq), seq.stride(0), T,
-                                    ptr(seq_len), B, d_model, heads, len(blocks), params, scalars, pool_out_ptr,
-                                    ld_pool, 1 if pool_mean else 0, _lib.stream_of(table)), "rk_bst_forward_blocks")
+    check(fn(ptr(table), table.shape[0], table.stride(0), ptr(seq), seq.stride(0), T, ptr(seq_len), B, d_model, heads,
+             len(blocks), params, scalars, pool_out_ptr, ld_pool, 1 if pool_mean else 0, _lib.stream_of(table)), name)
+
+
+def pack_bst_weight(weight: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """[128, 128] BST projection weight -> rk_bst_pack_block_weight's MFMA load order (into `out`
+    when given: a previous image, rewritten in place)."""
+    lib = _lib.load()
+    require_gpu(weight, "bst weight")
+    if tuple(weight.shape) != (128, 128) or weight.dtype != torch.float32:
+        raise ValueError(f"pack_bst_weight: expected a float32 [128, 128] weight, got {tuple(weight.shape)}")
+    w = weight.detach().contiguous()
+    if out is None:
+        out = torch.empty(128, 128, device=w.device, dtype=torch.float32)
+    check(lib.rk_bst_pack_block_weight(w.data_ptr(), out.data_ptr(), _lib.stream_of(out)), "rk_bst_pack_block_weight")
+    return out
 
 
 def bst_small_forward_args(segs, width, table, seq, seq_len, heads, blocks, pool_mean, layers, head: Epilogue):

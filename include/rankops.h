@@ -31,6 +31,7 @@
  *   rk_bst_attention   BSTTransformer scores/mask/softmax/AV bst.py:73-84 (mask from seq_length, bst.py:228-229)
  *   rk_bst_attention_masked  the same with BSTTransformer.forward's key_padding_mask  bst.py:66-84
  *   rk_bst_forward_blocks  all BSTTransformer blocks + pooling, fused bst.py:66-91,224-241
+ *   rk_bst_forward_blocks_packed  the same on pre-packed projection weights
  *   rk_linear_tiled    one wide MLP layer (2D-tiled)          deepfm.py:100-112 (first deep layer)
  *   rk_fm_linear_packed  the DeepFM front end in one launch: packed-table gather, fm1, fm2 and the
  *                      first deep layer (the deep input never reaches HBM)  deepfm.py:100-112,122-142
@@ -356,6 +357,18 @@ int rk_bst_forward_blocks(const float* table, int64_t table_rows, int64_t ld_tab
                           int64_t batch, int32_t d_model, int32_t heads, int32_t nblocks,
                           const float* const* block_params, const float* block_scalars,
                           float* pool_out, int64_t ld_pool, int32_t pool_mean, void* stream);
+/* rk_bst_forward_blocks (d_model 128 only) with the six projection weights of every block (wq, wk,
+ * wv, wo, w1, w2) in rk_bst_pack_block_weight's layout; same outputs, bit for bit.            */
+int rk_bst_forward_blocks_packed(const float* table, int64_t table_rows, int64_t ld_table,
+                                 const int64_t* seq, int64_t ld_seq, int32_t T,
+                                 const int64_t* seq_len, int64_t batch, int32_t d_model,
+                                 int32_t heads, int32_t nblocks, const float* const* block_params,
+                                 const float* block_scalars, float* pool_out, int64_t ld_pool,
+                                 int32_t pool_mean, void* stream);
+/* A [128, 128] projection weight (nn.Linear [out, in], contiguous) in the order the block kernel's
+ * 32x32x2 MFMA lanes load it: float 4096 j + 1024 g + 256 c + 4 l + e of `out` (16384 floats) is
+ * W[32 j + l % 32][32 g + 8 c + 4 (l / 32) + e] — each wave load one contiguous 1 KiB.  Not in place. */
+int rk_bst_pack_block_weight(const float* w, float* out, void* stream);
 
 /* ---- dense layers ---- */
 int rk_linear(const float* x, int64_t ldx, const float* x_periodic, int32_t x_period,
