@@ -22,6 +22,7 @@ eval batches on the device (rankops.EvalAccumulator) against the reference's hos
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -87,11 +88,14 @@ def dist_setup(args):
         # N > 1 path with every rank on its single GPU (timings then meaningless)
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
+        # a bounded collective timeout: a rank that fails between collectives ends the job within
+        # minutes instead of leaving the others blocked until the driver's limit
+        timeout = datetime.timedelta(seconds=int(os.environ.get("RANKOPS_BENCH_PG_TIMEOUT", "300")))
         if os.environ.get("RANKOPS_BENCH_BACKEND") == "gloo":
             # rehearsal only (RCCL refuses two ranks on one GPU): gloo with the tensors on the GPU
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     else:
         torch.cuda.set_device(0)
     return world, rank, local

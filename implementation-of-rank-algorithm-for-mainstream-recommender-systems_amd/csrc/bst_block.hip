@@ -82,36 +82,35 @@ __device__ unsigned long long g_bst_wave[10][8];  // [mark][wave]
 
 // Weight stream over TT 32-row W tiles in 32x32x2 B-operand order, consumed one tile after the
 // other: super-chunk g (tile g/4, k = 32*(g%4) .. +31, one 128-B line of each W row) gives lane
-// (n = lane%32, half h) W_tile[n][32*(g%4) + 8c + 4h + e], c < 4, e < 4.  kRing buffers: start()
-// issues the first kRing-1 super-chunks before the barrier that opens the phase, gemm128() keeps
-// kRing-1 in flight.  Measured at batch 2048 (tools/bst_phases.hip): 2 buffers 328 us, 3 345 us,
-// 4 372 us -- deeper rings cost more in register pressure and VMEM queueing than they hide.
-#ifndef BST_RING
-#define BST_RING 2
-#endif
-constexpr int kRing = BST_RING;  // super-chunk buffers
-// PK: the tile stored in that order (rk_bst_pack_block_weight), each load one contiguous 1 KiB.
+// (n = lane%32, half h) W_tile[n][32*(g%4) + 8c + 4h + e], c < 4, e < 4.  R buffers: start()
+// issues the first R-1 super-chunks before the barrier that opens the phase, gemm128() keeps R-1
+// in flight.  nn.Linear order (PK false), measured at batch 2048 (tools/bst_phases.hip): 2 buffers
+// 328 us, 3 345 us, 4 372 us -- deeper rings cost more in register pressure and VMEM queueing than
+// they hide.  PK: the tile stored in that order (rk_bst_pack_block_weight), each load one
+// contiguous 1 KiB; there 3 buffers beat 2 in each of three interleaved rounds (279-283 vs
+// 282-287 us, profiles/r06/bst_lib_ab.log), at the same 256 VGPRs.
 template <int TT, bool PK>
 struct WStream {
+  static constexpr int R = PK ? 3 : 2;  // super-chunk buffers
   const float* wrow[TT];
-  f4 bq[kRing][4];
+  f4 bq[R][4];
   __device__ __forceinline__ void start(const float* const (&W)[TT], int lane) {
 #pragma unroll
     for (int j = 0; j < TT; ++j)
       wrow[j] = PK ? W[j] + 4 * lane : W[j] + (int64_t)(lane & 31) * kBD + 4 * (lane >> 5);
 #pragma unroll
-    for (int g = 0; g + 1 < kRing; ++g) issue(g);
+    for (int g = 0; g + 1 < R; ++g) issue(g);
   }
   __device__ __forceinline__ void issue(int g) {
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      bq[g % kRing][c] = *reinterpret_cast<const f4*>(PK ? wrow[g / 4] + 1024 * (g % 4) + 256 * c
-                                                         : wrow[g / 4] + 32 * (g % 4) + 8 * c);
+      bq[g % R][c] = *reinterpret_cast<const f4*>(PK ? wrow[g / 4] + 1024 * (g % 4) + 256 * c
+                                                     : wrow[g / 4] + 32 * (g % 4) + 8 * c);
   }
 };
 
-// acc[j] = A[rt*32.., :] . W_j[0..32, :]^T over K = 128 for the TT tiles of `ws` (super-chunks 0
-// and 1 already in flight), A in LDS.  Fully unrolled; super-chunk g + 2 is loaded while g feeds
+// acc[j] = A[rt*32.., :] . W_j[0..32, :]^T over K = 128 for the TT tiles of `ws` (its first R - 1
+// super-chunks already in flight), A in LDS.  Fully unrolled; super-chunk g + R - 1 is loaded while g feeds
 // the MFMAs (one dependent accumulator chain at a time: 32x32x2_f32 accumulates back to back at the
 // full 64-cycle issue rate), the next A float4 one chunk ahead; sched_barrier keeps the compiler
 // from sinking the loads next to their use.
@@ -125,17 +124,18 @@ __device__ __forceinline__ void gemm128(const float* __restrict__ A, WStream<TT,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   f4 a_cur = *reinterpret_cast<const f4*>(arow);
+  constexpr int R = WStream<TT, PK>::R;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     __builtin_amdgcn_sched_barrier(0);
-    if (g + kRing - 1 < NG) ws.issue(g + kRing - 1);
+    if (g + R - 1 < NG) ws.issue(g + R - 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int cc = 4 * (g % 4) + c, cn = (cc + 1) % 16;
       const f4 a_next = g + 1 < NG || c < 3 ? *reinterpret_cast<const f4*>(arow + 8 * cn) : a_cur;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[g / 4] = mfma32(a_cur[e], ws.bq[g % kRing][c][e], acc[g / 4]);
+      for (int e = 0; e < 4; ++e) acc[g / 4] = mfma32(a_cur[e], ws.bq[g % R][c][e], acc[g / 4]);
       a_cur = a_next;
     }
   }
