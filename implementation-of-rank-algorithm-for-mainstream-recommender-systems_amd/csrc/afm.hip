@@ -392,25 +392,23 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
     return;
   }
 
+  // the pair tiles two at a time: both tiles' products, then their 2 NT independent accumulator
+  // chains interleaved, then both epilogues — one wave per SIMD at 4,096 samples, so only a
+  // wave's own independent work hides the MFMA and LDS latencies.  A second tile past MT reads as
+  // zero rows and stores nothing (its rows are >= R); per-tile arithmetic as one tile at a time.
   const int MT = (R + 15) >> 4;
-  for (int mt = 0; mt < MT; ++mt) {
+  auto tile_in = [&](int mt, float (&a)[KS]) {
     const int r = 16 * mt + p16;
     const bool rvld = r < R;
     const uint32_t ri = rvld ? rinfo[r] : 0u;
     const int oi = (int)(ri & 0xffffu) * D, oj = (int)(ri >> 16) * D;
-    float a[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int d = 4 * s + grp;
       a[s] = rvld ? e[oi + d] * e[oj + d] : 0.f;
     }
-    f32x4_t acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) acc[t] = mfma16(a[s], bw[t][s], acc[t]);
-    }
+  };
+  auto tile_out = [&](int mt, const f32x4_t (&acc)[NT]) {
     float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -423,6 +421,24 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
     const float sum = row16_transpose_sum<4>(part, p16);  // pair row 16 mt + 4 grp + p16 / 4
     const int q = 16 * mt + 4 * grp + (p16 >> 2);
     if ((p16 & 3) == 0 && q < R) sc[q] = sum + hb;
+  };
+  for (int mt = 0; mt < MT; mt += 2) {
+    float a0[KS], a1[KS];
+    tile_in(mt, a0);
+    tile_in(mt + 1, a1);
+    f32x4_t acc0[NT], acc1[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc0[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      acc1[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        acc0[t] = mfma16(a0[s], bw[t][s], acc0[t]);
+        acc1[t] = mfma16(a1[s], bw[t][s], acc1[t]);
+      }
+    }
+    tile_out(mt, acc0);
+    tile_out(mt + 1, acc1);
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the scores are in LDS
   __builtin_amdgcn_wave_barrier();

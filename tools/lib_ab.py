@@ -26,6 +26,17 @@ def child(what, batch):
         torch.cuda.synchronize()
         ts = [bench.kernel_avg_ms(launch, 20) for _ in range(3)]
         print(f"RESULT {min(ts) * 1e3:.2f} {sum(ts) / len(ts) * 1e3:.2f}", flush=True)
+    elif what in ("afm", "deepcrossing"):
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from env_ab import prepared
+        model, inp, fn, cfg, name = bench.workload(what, batch, 0)
+        run = prepared(model, what, inp)
+        with torch.no_grad():
+            out = run()
+        torch.cuda.synchronize()
+        ts = [bench.kernel_avg_ms(run) for _ in range(3)]
+        print(f"RESULT {min(ts) * 1e3:.2f} {sum(ts) / len(ts) * 1e3:.2f} {float(out[0].double().sum()):.9e}",
+              flush=True)
     else:
         raise ValueError(what)
 
@@ -58,7 +69,8 @@ def main():
                 sys.exit(1)
             mn, mean = map(float, line[0].split()[1:3])
             res[lab].append(mn)
-            print(f"round {rnd} {lab:8s}: {mn:8.2f} us min {mean:8.2f} us mean", flush=True)
+            extra = " ".join(line[0].split()[3:])
+            print(f"round {rnd} {lab:8s}: {mn:8.2f} us min {mean:8.2f} us mean {extra}", flush=True)
     for lab, ts in res.items():
         print(f"{args.what} B {args.batch} {lab:8s}: best {min(ts):8.2f} us, mean of mins {sum(ts) / len(ts):8.2f} us")
 
