@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
                                                         int A, const float* __restrict__ att_h,
                                                         const float* __restrict__ att_hb, const float* __restrict__ p_w,
                                                         const float* __restrict__ p_b, float* __restrict__ logit_out,
-                                                        float* __restrict__ prob_out, uint32_t* flags, int dbg) {
+                                                        float* __restrict__ prob_out, uint32_t* flags) {
   constexpr int D = 4 * KS;
   __shared__ __attribute__((aligned(16))) float emb[4][64 * D];  // S * F <= 64 staged rows per wave
   __shared__ float score[4][kAfmTileMaxRows];
@@ -387,10 +387,10 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
   }
   __syncthreads();  // rinfo (whole workgroup) and this wave's staged rows
   if (b0 >= batch) return;
-  if (dbg == 1) {  // timing experiment (RANKOPS_AFM_DEBUG): staging only
-    if (lane < S && b0 + lane < batch) logit_out[b0 + lane] = e[lane] + dl;
-    return;
-  }
+#if defined(RK_AFM_PHASE) && RK_AFM_PHASE == 1  // timing builds only (wrong outputs): staging only
+  if (lane < S && b0 + lane < batch) logit_out[b0 + lane] = e[lane] + dl;
+  return;
+#endif
 
   // the pair tiles two at a time: both tiles' products, then their 2 NT independent accumulator
   // chains interleaved, then both epilogues — one wave per SIMD at 4,096 samples, so only a
@@ -443,10 +443,10 @@ __global__ __launch_bounds__(256) void afm_tiles_kernel(AfmFields fields, int F,
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the scores are in LDS
   __builtin_amdgcn_wave_barrier();
 
-  if (dbg == 2) {  // timing experiment: staging + the pair-score MFMAs
-    if (lane < S && b0 + lane < batch) logit_out[b0 + lane] = sc[lane] + dl;
-    return;
-  }
+#if defined(RK_AFM_PHASE) && RK_AFM_PHASE == 2  // timing builds only: staging + the pair-score MFMAs
+  if (lane < S && b0 + lane < batch) logit_out[b0 + lane] = sc[lane] + dl;
+  return;
+#endif
   float pw[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) pw[d] = p_w[d];
@@ -502,11 +502,9 @@ RK_API int rk_afm_forward(const rk_segment* fields, int32_t num_fields, int32_t 
       tile_s * num_fields <= 64 && tile_s * P <= kAfmTileMaxRows) {
     const int nt = (att_factor + 15) / 16;
     const unsigned tblocks = (unsigned)((batch + 4 * tile_s - 1) / (4 * tile_s));
-    const char* de = getenv("RANKOPS_AFM_DEBUG");  // timing experiments only (wrong outputs when set)
-    const int dbg = de ? atoi(de) : 0;
     auto go = [&](auto kern) {
       kern<<<tblocks, 256, 0, st>>>(t, num_fields, batch, dense, ld_dense, num_dense, dense_w, dense_b, att_w, att_b,
-                                    att_factor, att_h, att_hb, p_w, p_b, logit, prob, fl, dbg);
+                                    att_factor, att_h, att_hb, p_w, p_b, logit, prob, fl);
     };
     auto by_s = [&](auto ks, auto ntc) {
       constexpr int KS = decltype(ks)::value, NT = decltype(ntc)::value;
