@@ -16,7 +16,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import ops, train
+from . import common, ops, train
 from .common import DENSE_FEATURES, EngineModule, check_eval
 
 
@@ -68,6 +68,8 @@ class AFM(EngineModule):
         dense_input = ops.as_f32(dense_input, "dense_input")
         B = dense_input.shape[0]
         dev = dense_input.device
+        if B == 0 and not self.training:
+            return common.empty_rows(dev, 2)
         fields, idxs = [], []
         for col in self.category_features:
             idx = ops.as_index(category_input[col], f"category_input[{col!r}]")

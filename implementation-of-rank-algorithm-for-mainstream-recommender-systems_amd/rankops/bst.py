@@ -205,6 +205,8 @@ class BSTModel(EngineModule):
         dense = ops.as_f32(dense, "dense")
         seq_feedid = ops.as_index(seq_feedid, "seq_feedid").contiguous()
         seq_length = ops.as_index(seq_length, "seq_length")
+        if not self.training and seq_feedid.shape[0] == 0:
+            return common.empty_rows(dense.device, 2)
         if self.training:  # Dropout in the blocks and the dnn, BatchNorm batch statistics, HIP backward
             for blk in self.transformer_blocks:
                 if seq_feedid.shape[1] > blk.position_embedding.num_embeddings:

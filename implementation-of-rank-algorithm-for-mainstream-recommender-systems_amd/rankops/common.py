@@ -417,10 +417,11 @@ class PackedWeights:
     """Packed weight images (rk_mlp_pack_weight, or the `pack` given), held weakly per weight
     tensor object and rebuilt when its storage or version changes (load_state_dict, .to(),
     optimizer steps).  Keying on the object — not the address — keeps a freed model's packed
-    image from being served to a new tensor that reuses its memory.  After an optimizer step the image is rewritten in place, on
-    the current stream, unless a prepared forward (DIN / DCN / DeepFM .prepare) pinned it: such a
-    plan keeps the image it was prepared with (it binds the weights of that moment; prepare again
-    after changing them), and its launches on other streams never see a half-rewritten image."""
+    image from being served to a new tensor that reuses its memory.  After an optimizer step the
+    image is rewritten in place, on the current stream, unless a prepared forward (DIN / DCN /
+    DeepFM .prepare) pinned it: such a plan keeps the image it was prepared with (it binds the
+    weights of that moment; prepare again after changing them), and its launches on other streams
+    never see a half-rewritten image."""
 
     def __init__(self, pack=None):
         self._d = {}  # id(tensor) -> (weakref, key, packed, pinned); the weakref callback drops the entry
@@ -453,6 +454,13 @@ class PackedWeights:
 
 PACKED = PackedWeights()
 BST_PACKED = PackedWeights(lambda w, out=None: ops.pack_bst_weight(w, out=out))  # bst_block_kernel's projections
+
+
+def empty_rows(device, n: int, shape=(0, 1)):
+    """The outputs of an eval forward over an empty batch: n empty float32 tensors of the model's
+    output shape.  The reference's torch ops return empty outputs there; the engine launches no
+    kernel (an empty tensor's data pointer may be null, which the C ABI rejects)."""
+    return tuple(torch.empty(shape, device=device, dtype=torch.float32) for _ in range(n))
 
 
 def tiled_layer(K: int, B: int, device, ml) -> bool:

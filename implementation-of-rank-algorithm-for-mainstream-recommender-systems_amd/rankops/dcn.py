@@ -159,6 +159,9 @@ class DCNModel(EngineModule):
         return run
 
     def forward(self, dense, category):
+        if not self.training and ops.as_f32(dense, "dense").shape[0] == 0:
+            self.cross_weights.get(dense.device)  # per-call mode draws every forward, as dcn.py:37-41 does
+            return common.empty_rows(dense.device, 2)
         if not self.training:
             out = self._eager_eval(dense, category)
             if out is not None:

@@ -123,6 +123,10 @@ class DeepCrossingModel(common.EngineModule):
         dense = ops.as_f32(dense, "dense")
         B = dense.shape[0]
         dev = dense.device
+        recording = self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if B == 0 and not recording:
+            self.residual_weights.get(dev)  # per-call mode draws every forward (deepcrossing.py:25-42)
+            return common.empty_rows(dev, 2)
         segs = [ops.dense_segment(dense, self.num_dense_features, 0)]
         col = self.num_dense_features
         for name, emb in self.embeddings.items():

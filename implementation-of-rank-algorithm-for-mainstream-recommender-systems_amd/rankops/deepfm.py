@@ -281,6 +281,9 @@ class DeepFM(EngineModule):
         return run
 
     def forward(self, category):
+        first = category.get(next(iter(self.second_order_embeddings)), None) if isinstance(category, dict) else None
+        if not self.training and isinstance(first, torch.Tensor) and first.shape[0] == 0:
+            return common.empty_rows(ops.require_gpu(first, "category").device, 5)
         if not self.training:
             out = self._eager_eval(category)
             if out is not None:

@@ -364,6 +364,15 @@ class DIN(EngineModule):
         return calls.put(key, (list(args) + [ops.ptr(epi)], head, B, want_l2, H, (keep, packed, layers, epi)))
 
     def forward(self, dense, category, sequence, target):
+        tgt = target.get("feedid", None) if isinstance(target, dict) else None
+        if not self.training and isinstance(tgt, torch.Tensor) and tgt.shape[0] == 0:
+            # an empty batch: the reference still draws its attention MLP (din.py:61-67), and its l2
+            # term is l2_lambda times the mean of no norms, NaN (din.py:319-322)
+            dev = ops.require_gpu(tgt, "target['feedid']").device
+            self.att_weights.get(dev)
+            prob, logit = common.empty_rows(dev, 2)
+            want_l2 = self.mini_batch_aware_regularization and self.l2_lambda > 0
+            return prob, logit, (torch.full((), float("nan"), device=dev) if want_l2 else 0.0)
         if not self.training:
             out = self._eager_eval(dense, category, sequence, target)
             if out is not None:

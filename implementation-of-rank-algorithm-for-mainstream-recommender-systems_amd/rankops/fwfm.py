@@ -101,6 +101,10 @@ class FwFM(EngineModule):
     def forward(self, x, *, return_logit=False):
         """x: {field: int64 [B]} -> probabilities [B] (and the logits [B] with return_logit).
         Under .train() with autograd on, the probabilities carry the HIP backward (rankops.train)."""
+        first = x.get(self.field_names[0], None) if isinstance(x, dict) else None
+        if not self.training and isinstance(first, torch.Tensor) and first.shape[0] == 0:
+            prob, logit = common.empty_rows(ops.require_gpu(first, "x").device, 2, shape=(0,))
+            return (prob, logit) if return_logit else prob
         if not self.training:
             out = self._eager_eval(x, return_logit)
             if out is not None:
