@@ -109,14 +109,20 @@ __device__ __forceinline__ void din_marks_flush(int tid) {
   } while (0)
 #endif
 
-// Balanced assignment (NIT > 0: batch <= NIT * 1024).  The attention cost of a sample is its tile
-// count, and with one workgroup per CU the kernel ends with the workgroup whose SIMDs carry the
-// most tiles (tools/din_phases.py: phase-A time tracks the 2-tile samples per workgroup, corr 0.91).
-// Every workgroup ranks the whole batch by descending tile count (stable in the batch order) and
-// takes ranks blockIdx.x + G * j, j = 0..15 (G workgroups): each workgroup gets the same mix of
-// long and short samples, within one, and wave j gets the j-th longest of its 16.  The ranking is
-// a counting sort over the ceil(T/32) + 1 tile classes: per 64-sample block a ballot mask per
-// class in LDS, then each wave finds its rank's sample by a prefix over the blocks' popcounts.
+// Balanced assignment (NIT > 0).  The attention cost of a sample is its tile count, and with one
+// workgroup per CU the kernel ends with the workgroup whose SIMDs carry the most tiles
+// (tools/din_phases.py: phase-A time tracks the 2-tile samples per workgroup, corr 0.91).  The
+// workgroups rank their samples by descending tile count (stable in the batch order) and take
+// ranks g + G * j, j = 0..15 (G workgroups): each workgroup gets the same mix of long and short
+// samples, within one, and wave j gets the j-th longest of its 16.  The ranking is a counting sort
+// over the ceil(T/16) + 1 tile classes: per 64-sample block a ballot mask per class in LDS, then
+// each wave finds its rank's sample by a prefix over the blocks' popcounts.  NIT == 1 (round 6,
+// the default): the ranking runs per 1,024-sample universe, the 64 workgroups of universe j
+// serving samples 1024 j ..: one length load per thread instead of the whole batch per
+// workgroup (NIT 4 / 8: batch <= 8,192), and any batch size.  The per-universe deal leaves the
+// most-loaded SIMD within a tile of the whole-batch one (a simulation at T = 50: 9.01 against 9.00
+// tiles) and takes the kernel 40.3 -> 38.5 us at 4,096 (568.6 -> 553.6 us at 65,536 against
+// contiguous samples), outputs bit-identical (profiles/r06/din_uni_ab.log).
 constexpr int kDinBalMax = 8;  // NIT <= 8: batch <= 8192
 constexpr int kDinBalClasses = 17;  // T <= 256 (16-position tiles)
 
@@ -211,11 +217,21 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   int rows;
   int my_tiles = -1;  // NIT == 0, lanes 0..15: tiles of sample m0 + lane (-1: past the batch)
   int64_t my_len = 0;
-  int64_t lv[NIT > 0 ? NIT : 1];  // NIT > 0: lengths of samples tid + 1024 r (clamped index)
+  int64_t lv[NIT > 0 ? NIT : 1];  // NIT > 0: lengths of samples u0 + tid + 1024 r (clamped index)
+  // NIT == 1: the ranking runs per 1,024-sample universe (samples u0 .. u0 + UB - 1, served by the
+  // UG workgroups 64 j ..): one length per thread instead of the whole batch per workgroup
+  int u0 = 0, UB = (int)a.batch, UG = (int)gridDim.x, ugl = (int)blockIdx.x;
+  if constexpr (NIT == 1) {
+    const int j = (int)blockIdx.x / (kMlpThreads / kMlpRows);
+    u0 = j * kMlpThreads;
+    UB = min(kMlpThreads, (int)(a.batch - u0));
+    UG = (UB + kMlpRows - 1) / kMlpRows;
+    ugl = (int)blockIdx.x - j * (kMlpThreads / kMlpRows);
+  }
   if constexpr (NIT > 0) {
 #pragma unroll
     for (int r = 0; r < NIT; ++r) {
-      const int i = tid + kMlpThreads * r;
+      const int64_t i = u0 + tid + kMlpThreads * r;
       lv[r] = a.seq_len[i < a.batch ? i : a.batch - 1];
     }
   } else {
@@ -333,10 +349,10 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   }
   DIN_TS(5);
   if constexpr (NIT > 0) {  // class masks of the 64-sample blocks (block 16 r + wave holds sample tid + 1024 r)
-    const int nblk = (int)((a.batch + 63) / 64);
+    const int nblk = (UB + 63) / 64;
 #pragma unroll
     for (int r = 0; r < NIT; ++r) {
-      const int cls = tid + kMlpThreads * r < a.batch ? tiles_of(clamp_len(lv[r])) : -1;
+      const int cls = tid + kMlpThreads * r < UB ? tiles_of(clamp_len(lv[r])) : -1;
       // class c's mask lands in lane c; lanes 0 .. nb-1 store them
       unsigned long long mk = 0;
 #pragma unroll 1
@@ -367,9 +383,9 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
   int64_t len, b;
   bool live;
   if constexpr (NIT > 0) {
-    const int G = gridDim.x, B = (int)a.batch;  // batch <= 8192 here: 32-bit index math
-    const int p = blockIdx.x + G * rho;  // this wave's rank
-    rows = min(kMlpRows, (B - (int)blockIdx.x + G - 1) / G);
+    const int G = UG, B = UB;  // the universe (NIT == 1) or the whole batch (<= 8192): 32-bit index math
+    const int p = ugl + G * rho;  // this wave's rank
+    rows = min(kMlpRows, (B - ugl + G - 1) / G);
     loc = rho;
     live = p < B;
     int cls = 0;
@@ -408,7 +424,7 @@ __global__ __launch_bounds__(kMlpThreads) void din_forward_kernel(DinArgs a) {
       }
       const int below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
       const int pos = __builtin_ctzll(__ballot(((m >> lane) & 1ull) && below == kk));
-      b = __builtin_amdgcn_readfirstlane(64 * blk + pos);
+      b = __builtin_amdgcn_readfirstlane(u0 + 64 * blk + pos);
     }
     ntiles = __builtin_amdgcn_readfirstlane(cls);
     // the length rides with phase A.1's loads (only the tile masks need it) — as a vector load: a
@@ -872,8 +888,9 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   size_t shm = (base + (size_t)kMlpRows * (a.ld0 + a.ld1)) * sizeof(float) + kDinSegLdsOff +
                sizeof(rk_segment) * kDinSegs + sizeof(int64_t) * 64 * kMlpRows;
   if (shm > 160 * 1024 - kStreamStaticLds) return fail(RK_ERR_UNSUPPORTED, "rk_din_forward: %zu B of LDS needed", shm);
-  // balanced assignment (see din_forward_kernel) for one or two workgroup rounds' worth of batch,
-  // by default when the histories span three or more 16-position tile counts (T > 32).  Measured
+  // balanced assignment (see din_forward_kernel): per 1,024-sample universe at any batch (NIT 1),
+  // or (RANKOPS_DIN_UNI=0) over the whole batch up to 8,192 samples (NIT 4 / 8), by default when
+  // the histories span three or more 16-position tile counts (T > 32).  Measured
   // (round 3, 32-position tiles, graph replays, batch 4096, lengths uniform in 1..T): T = 128
   // 74.7 -> 68.9 us, T = 256 100.9 -> 91.9 us; round 4 (16-position tiles) at T = 50, kernel averages
   // over two interleaved A/B pairs: 45.18 / 44.22 -> 44.05 / 43.59 us (profiles/r04/ab_bal_*).
@@ -882,10 +899,13 @@ static int din_prepare(const rk_segment* row_segs, int32_t nseg, int32_t width, 
   const char* env = getenv("RANKOPS_DIN_BALANCE");
   a.bal_nb = (T + 15) / 16 + 1;  // tile-count classes 0 .. ceil(T / 16)
   const bool want_bal = env && env[0] ? env[0] != '0' : T > 32;
-  if (want_bal && batch > kMlpRows && batch <= kDinBalMax * kMlpThreads && a.bal_nb <= kDinBalClasses) {
-    const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((batch + 63) / 64) * a.bal_nb;
+  const char* uni_env = getenv("RANKOPS_DIN_UNI");  // 0: rank the whole batch (NIT 4 / 8, A/B)
+  const bool uni = !(uni_env && uni_env[0] == '0');
+  if (want_bal && batch > kMlpRows && (uni || batch <= kDinBalMax * kMlpThreads) && a.bal_nb <= kDinBalClasses) {
+    const int64_t ranked = uni ? std::min<int64_t>(batch, kMlpThreads) : batch;
+    const size_t extra = sizeof(int64_t) * kMlpRows + sizeof(unsigned long long) * ((ranked + 63) / 64) * a.bal_nb;
     if (shm + extra <= 160 * 1024 - kStreamStaticLds) {
-      plan->nit = batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
+      plan->nit = uni ? 1 : batch <= 4 * kMlpThreads ? 4 : kDinBalMax;
       shm += extra;
     }
   }
@@ -924,12 +944,15 @@ static int din_launch(const DinPlan& p, hipStream_t st) {
     using S = StreamPlanK128;
     switch (p.H * 16 + p.nit) {
       case 8 * 16: go(din_forward_kernel<8, 0, S, din_pre_chunks<8>()>); break;
+      case 8 * 16 + 1: go(din_forward_kernel<8, 1, S, din_pre_chunks<8>()>); break;
       case 8 * 16 + 4: go(din_forward_kernel<8, 4, S, din_pre_chunks<8>()>); break;
       case 8 * 16 + 8: go(din_forward_kernel<8, 8, S, din_pre_chunks<8>()>); break;
       case 16 * 16: go(din_forward_kernel<16, 0, S, din_pre_chunks<16>()>); break;
+      case 16 * 16 + 1: go(din_forward_kernel<16, 1, S, din_pre_chunks<16>()>); break;
       case 16 * 16 + 4: go(din_forward_kernel<16, 4, S, din_pre_chunks<16>()>); break;
       case 16 * 16 + 8: go(din_forward_kernel<16, 8, S, din_pre_chunks<16>()>); break;
       case 32 * 16: go(din_forward_kernel<32, 0, S, din_pre_chunks<32>()>); break;
+      case 32 * 16 + 1: go(din_forward_kernel<32, 1, S, din_pre_chunks<32>()>); break;
       case 32 * 16 + 4: go(din_forward_kernel<32, 4, S, din_pre_chunks<32>()>); break;
       default: go(din_forward_kernel<32, 8, S, din_pre_chunks<32>()>); break;
     }
@@ -939,12 +962,15 @@ static int din_launch(const DinPlan& p, hipStream_t st) {
     using S = StreamPlanK128;
     switch (p.H * 16 + p.nit) {
       case 8 * 16: go(din_forward_kernel<8, 0, S>); break;
+      case 8 * 16 + 1: go(din_forward_kernel<8, 1, S>); break;
       case 8 * 16 + 4: go(din_forward_kernel<8, 4, S>); break;
       case 8 * 16 + 8: go(din_forward_kernel<8, 8, S>); break;
       case 16 * 16: go(din_forward_kernel<16, 0, S>); break;
+      case 16 * 16 + 1: go(din_forward_kernel<16, 1, S>); break;
       case 16 * 16 + 4: go(din_forward_kernel<16, 4, S>); break;
       case 16 * 16 + 8: go(din_forward_kernel<16, 8, S>); break;
       case 32 * 16: go(din_forward_kernel<32, 0, S>); break;
+      case 32 * 16 + 1: go(din_forward_kernel<32, 1, S>); break;
       case 32 * 16 + 4: go(din_forward_kernel<32, 4, S>); break;
       default: go(din_forward_kernel<32, 8, S>); break;
     }
@@ -952,12 +978,15 @@ static int din_launch(const DinPlan& p, hipStream_t st) {
   }
   switch (p.H * 16 + p.nit) {
     case 8 * 16: go(din_forward_kernel<8, 0, void>); break;
+    case 8 * 16 + 1: go(din_forward_kernel<8, 1, void>); break;
     case 8 * 16 + 4: go(din_forward_kernel<8, 4, void>); break;
     case 8 * 16 + 8: go(din_forward_kernel<8, 8, void>); break;
     case 16 * 16: go(din_forward_kernel<16, 0, void>); break;
+    case 16 * 16 + 1: go(din_forward_kernel<16, 1, void>); break;
     case 16 * 16 + 4: go(din_forward_kernel<16, 4, void>); break;
     case 16 * 16 + 8: go(din_forward_kernel<16, 8, void>); break;
     case 32 * 16: go(din_forward_kernel<32, 0, void>); break;
+    case 32 * 16 + 1: go(din_forward_kernel<32, 1, void>); break;
     case 32 * 16 + 4: go(din_forward_kernel<32, 4, void>); break;
     default: go(din_forward_kernel<32, 8, void>); break;
   }

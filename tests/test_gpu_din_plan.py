@@ -139,27 +139,34 @@ def test_l2_hand_off_stable_over_repeated_launches():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("softmax", [False, True])
-@pytest.mark.parametrize("batch,T", [(17, 50), (1000, 50), (4096, 50), (5000, 50), (8192, 50), (3000, 160), (8192, 256)])
+@pytest.mark.parametrize("batch,T", [(17, 50), (1000, 50), (1025, 50), (4096, 50), (5000, 50), (8192, 50), (3000, 160),
+                                     (8192, 256), (10000, 50), (33 * 1024 + 5, 64)])
 def test_balanced_assignment_matches_contiguous_blocks(monkeypatch, softmax, batch, T):
-    """Batches of 17..8192 rows rank the samples by attention tile count inside the kernel and
+    """Batches of 17..33,797 rows rank the samples by attention tile count inside the kernel and
     deal them round-robin to the workgroups (din_fused.hip, balanced assignment: the default for
-    T > 64, forced here with RANKOPS_DIN_BALANCE=1); every output row
-    must equal the contiguous-block launch (RANKOPS_DIN_BALANCE=0) bit for bit — zero, short and
-    full-length histories mixed, all tile classes present — and the l2 mean within fp32 rounding."""
+    T > 32, forced here with RANKOPS_DIN_BALANCE=1), per 1,024-sample universe (the default, round
+    6) or over the whole batch (RANKOPS_DIN_UNI=0, batches up to 8,192; beyond, contiguous blocks);
+    every output row must equal the contiguous-block launch (RANKOPS_DIN_BALANCE=0) bit for bit —
+    zero, short and full-length histories mixed, all tile classes present, a partial last universe
+    — and the l2 mean within fp32 rounding."""
     cfg = _cfg(softmax=softmax, T=T)
     model = H.build("din", cfg).cuda().eval()
     inp = H.make_inputs("din", cfg, batch, seed=batch)
     L = inp["sequence"]["his_read_comment_7d_seq_length"]
     L[: min(batch, 9)] = torch.tensor([0, 1, 31, 32, 33, T, 0, T + 14, -3])[: min(batch, 9)]
     d = H.to_device(inp, "cuda")
+    outs = {}
     with torch.no_grad():
-        monkeypatch.setenv("RANKOPS_DIN_BALANCE", "1")
-        bal = H.as_tuple(H.call_model(model, "din", d))
-        monkeypatch.setenv("RANKOPS_DIN_BALANCE", "0")
-        ctg = H.as_tuple(H.call_model(model, "din", d))
+        for mode, bal, uni in (("universe", "1", "1"), ("whole", "1", "0"), ("contiguous", "0", "1")):
+            monkeypatch.setenv("RANKOPS_DIN_BALANCE", bal)
+            monkeypatch.setenv("RANKOPS_DIN_UNI", uni)
+            outs[mode] = H.as_tuple(H.call_model(model, "din", d))
     torch.cuda.synchronize()
-    assert torch.equal(bal[0], ctg[0]) and torch.equal(bal[1], ctg[1])
-    torch.testing.assert_close(bal[2], ctg[2], rtol=1e-6, atol=0)
+    ctg = outs["contiguous"]
+    for mode in ("universe", "whole"):
+        bal = outs[mode]
+        assert torch.equal(bal[0], ctg[0]) and torch.equal(bal[1], ctg[1]), mode
+        torch.testing.assert_close(bal[2], ctg[2], rtol=1e-6, atol=0)
 
 
 @pytest.mark.gpu
